@@ -1,0 +1,400 @@
+// eps-neighbourhoods for DBSCAN / OPTICS over 2-D pixel points.
+//
+// Reference: DBSCANSimpleCluster::radiusSearch (PCC/DBSCAN_simple.h:118-142, O(N) per query,
+// d^2 <= eps^2 in double, self first), DBSCANPrecompCluster::precomp (PCC/DBSCAN_precomp.h:
+// 22-44, O(N^2) adjacency), kdt::KDTree::radius_search (OPT/include/optics/kdTree.hpp:307-422)
+// and optics::compute_core_dist (OPT/include/optics/optics.hpp:286-299: nth_element of the
+// squared distances at min_pts-1, self included).
+//
+// MI355X design: one workgroup per segment (<= 8192 points, e.g. one downsample window).  The
+// segment is binned in LDS into a uniform grid of cell size >= eps (counting sort with LDS
+// atomics; each cell's index list is then sorted so lists come out ascending), and every lane
+// answers one query from the 3x3 surrounding cells: exact integer d^2 compared against eps^2
+// in fp64, the count, and the (min_pts-1)-th smallest d^2 kept in a register insertion network
+// (no runtime-indexed arrays), so core distance = sqrt of an exact integer (fp64, correctly
+// rounded — bit-exact vs the oracle).  The list kernel emits each query's neighbours with a
+// 9-way merge of the cells' sorted lists, i.e. ascending segment-local indices (the order of
+// DBSCAN_precomp's adjacency lists), at offsets from a device exclusive scan of the counts.
+// Algorithmic bytes: 4 B/point in + 4 B/point (count) [+ 8 B core distance] out.
+#include "ecc_internal.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxPts = 8192;
+constexpr int kMaxCells = 8192;
+
+struct SegView {
+    const int32_t *counts;
+    int64_t n_segs, stride;
+};
+
+struct Grid {
+    int xmin, ymin, cs, gx, gy;
+};
+
+// Loads segment s into LDS, bins it and sorts each cell's list. Returns m (points) and grid.
+__device__ int bin_segment(const uint32_t *__restrict__ xy, const SegView &sv, int64_t s,
+                           double eps, uint32_t *pxy, uint16_t *sorted, uint32_t *cend,
+                           int *red, Grid &g) {
+    const int tid = threadIdx.x;
+    int m = sv.counts ? sv.counts[s] : (int)sv.stride;
+    if (m > kMaxPts) m = kMaxPts;  // validated on the host
+    const int64_t base = s * sv.stride;
+    int xmn = 0x7fffffff, ymn = 0x7fffffff, xmx = -1, ymx = -1;
+    for (int i = tid; i < m; i += kThreads) {
+        const uint32_t v = xy[base + i];
+        pxy[i] = v;
+        const int x = ecc::xy_x(v), y = ecc::xy_y(v);
+        xmn = min(xmn, x); ymn = min(ymn, y); xmx = max(xmx, x); ymx = max(ymx, y);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        xmn = min(xmn, __shfl_xor(xmn, o)); ymn = min(ymn, __shfl_xor(ymn, o));
+        xmx = max(xmx, __shfl_xor(xmx, o)); ymx = max(ymx, __shfl_xor(ymx, o));
+    }
+    if ((tid & 63) == 0) {
+        red[4 * (tid >> 6) + 0] = xmn; red[4 * (tid >> 6) + 1] = ymn;
+        red[4 * (tid >> 6) + 2] = xmx; red[4 * (tid >> 6) + 3] = ymx;
+    }
+    for (int c = tid; c < kMaxCells; c += kThreads) cend[c] = 0;
+    __syncthreads();
+    xmn = red[0]; ymn = red[1]; xmx = red[2]; ymx = red[3];
+    for (int w = 1; w < kThreads / 64; ++w) {
+        xmn = min(xmn, red[4 * w]); ymn = min(ymn, red[4 * w + 1]);
+        xmx = max(xmx, red[4 * w + 2]); ymx = max(ymx, red[4 * w + 3]);
+    }
+    if (m == 0) { xmn = ymn = 0; xmx = ymx = 0; }
+    int cs = (int)ceil(eps);
+    if (cs < 1) cs = 1;
+    while ((int64_t)((xmx - xmn) / cs + 1) * ((ymx - ymn) / cs + 1) > kMaxCells) cs *= 2;
+    g = Grid{xmn, ymn, cs, (xmx - xmn) / cs + 1, (ymx - ymn) / cs + 1};
+    __syncthreads();
+    // counting sort by cell (cend[] ends as the END of each cell's range)
+    for (int i = tid; i < m; i += kThreads) {
+        const uint32_t v = pxy[i];
+        const int c = ((ecc::xy_y(v) - g.ymin) / g.cs) * g.gx + (ecc::xy_x(v) - g.xmin) / g.cs;
+        atomicAdd(&cend[c], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of the cell counts (kMaxCells / kThreads values per thread)
+    {
+        constexpr int per = kMaxCells / kThreads;
+        uint32_t loc[per];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < per; ++k) { loc[k] = cend[tid * per + k]; sum += loc[k]; }
+        // inclusive wave scan of sum
+        uint32_t inc = sum;
+        const int lane = tid & 63;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+        }
+        __syncthreads();
+        if (lane == 63) red[16 + (tid >> 6)] = (int)inc;
+        __syncthreads();
+        uint32_t off = inc - sum;
+        for (int w = 0; w < (tid >> 6); ++w) off += (uint32_t)red[16 + w];
+#pragma unroll
+        for (int k = 0; k < per; ++k) { cend[tid * per + k] = off; off += loc[k]; }
+    }
+    __syncthreads();
+    for (int i = tid; i < m; i += kThreads) {
+        const uint32_t v = pxy[i];
+        const int c = ((ecc::xy_y(v) - g.ymin) / g.cs) * g.gx + (ecc::xy_x(v) - g.xmin) / g.cs;
+        const uint32_t pos = atomicAdd(&cend[c], 1u);
+        sorted[pos] = (uint16_t)i;
+    }
+    __syncthreads();
+    // sort each cell's index list ascending (cells are small: insertion sort per thread)
+    for (int c = tid; c < g.gx * g.gy; c += kThreads) {
+        const int lo = c == 0 ? 0 : (int)cend[c - 1], hi = (int)cend[c];
+        for (int a = lo + 1; a < hi; ++a) {
+            const uint16_t key = sorted[a];
+            int b = a - 1;
+            while (b >= lo && sorted[b] > key) { sorted[b + 1] = sorted[b]; --b; }
+            sorted[b + 1] = key;
+        }
+    }
+    __syncthreads();
+    return m;
+}
+
+__device__ __forceinline__ void cell_range(const Grid &g, const uint32_t *cend, int cx, int cy,
+                                           int &lo, int &hi) {
+    if (cx < 0 || cy < 0 || cx >= g.gx || cy >= g.gy) { lo = hi = 0; return; }
+    const int c = cy * g.gx + cx;
+    lo = c == 0 ? 0 : (int)cend[c - 1];
+    hi = (int)cend[c];
+}
+
+template <int K>
+__global__ void __launch_bounds__(kThreads)
+eps_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, double eps, int min_pts,
+                  int32_t *__restrict__ counts, double *__restrict__ core) {
+    __shared__ uint32_t pxy[kMaxPts];
+    __shared__ uint16_t sorted[kMaxPts];
+    __shared__ uint32_t cend[kMaxCells];
+    __shared__ int red[32];
+    const double r2 = eps * eps;
+    for (int64_t s = blockIdx.x; s < sv.n_segs; s += gridDim.x) {
+        Grid g;
+        const int m = bin_segment(xy, sv, s, eps, pxy, sorted, cend, red, g);
+        const int64_t base = s * sv.stride;
+        for (int i = threadIdx.x; i < sv.stride; i += kThreads) {
+            if (i >= m) {
+                counts[base + i] = 0;
+                if (core) core[base + i] = -1.0;
+                continue;
+            }
+            const uint32_t v = pxy[i];
+            const int x = ecc::xy_x(v), y = ecc::xy_y(v);
+            const int cx = (x - g.xmin) / g.cs, cy = (y - g.ymin) / g.cs;
+            int cnt = 0;
+            int best[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) best[k] = 0x7fffffff;
+            for (int dy = -1; dy <= 1; ++dy) {
+                for (int dx = -1; dx <= 1; ++dx) {
+                    int lo, hi;
+                    cell_range(g, cend, cx + dx, cy + dy, lo, hi);
+                    for (int a = lo; a < hi; ++a) {
+                        const uint32_t w = pxy[sorted[a]];
+                        const int ex = ecc::xy_x(w) - x, ey = ecc::xy_y(w) - y;
+                        const int d2 = ex * ex + ey * ey;
+                        if ((double)d2 <= r2) {
+                            ++cnt;
+                            if (core) {
+                                int val = d2;  // insertion network keeps the K smallest, sorted
+#pragma unroll
+                                for (int k = 0; k < K; ++k) {
+                                    const int lo2 = min(best[k], val);
+                                    val = max(best[k], val);
+                                    best[k] = lo2;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            counts[base + i] = cnt;
+            if (core) {
+                double cd = -1.0;
+                if (cnt >= min_pts && min_pts >= 1) {
+                    int sel = 0;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) sel = (k == min_pts - 1) ? best[k] : sel;
+                    cd = sqrt((double)sel);
+                }
+                core[base + i] = cd;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+eps_lists_kernel(const uint32_t *__restrict__ xy, SegView sv, double eps,
+                 const int64_t *__restrict__ offsets, int32_t *__restrict__ nbr, int64_t nbr_cap,
+                 int32_t *__restrict__ err) {
+    __shared__ uint32_t pxy[kMaxPts];
+    __shared__ uint16_t sorted[kMaxPts];
+    __shared__ uint32_t cend[kMaxCells];
+    __shared__ int red[32];
+    const double r2 = eps * eps;
+    for (int64_t s = blockIdx.x; s < sv.n_segs; s += gridDim.x) {
+        Grid g;
+        const int m = bin_segment(xy, sv, s, eps, pxy, sorted, cend, red, g);
+        const int64_t base = s * sv.stride;
+        for (int i = threadIdx.x; i < m; i += kThreads) {
+            const uint32_t v = pxy[i];
+            const int x = ecc::xy_x(v), y = ecc::xy_y(v);
+            const int cx = (x - g.xmin) / g.cs, cy = (y - g.ymin) / g.cs;
+            int lo[9], hi[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) cell_range(g, cend, cx + (k % 3) - 1, cy + (k / 3) - 1, lo[k], hi[k]);
+            int64_t out = offsets[base + i];
+            const int64_t end = offsets[base + i + 1];
+            // 9-way merge of ascending cell lists
+            for (;;) {
+                int bestk = -1, besti = 0x7fffffff;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    if (lo[k] < hi[k]) {
+                        const int idx = sorted[lo[k]];
+                        if (idx < besti) { besti = idx; bestk = k; }
+                    }
+                }
+                if (bestk < 0) break;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) lo[k] += (k == bestk) ? 1 : 0;
+                const uint32_t w = pxy[besti];
+                const int ex = ecc::xy_x(w) - x, ey = ecc::xy_y(w) - y;
+                if ((double)(ex * ex + ey * ey) <= r2) {
+                    if (out < end && out < nbr_cap) nbr[out] = besti;
+                    else *err = 1;
+                    ++out;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- exclusive scan int32 -> int64 (3 kernels: block sums, scan of sums, finish) ----------
+constexpr int kScanBlock = 1024;  // elements per block (4 per thread)
+
+__global__ void __launch_bounds__(kThreads)
+scan_block_sums(const int32_t *__restrict__ in, int64_t n, int64_t *__restrict__ bsum) {
+    __shared__ int64_t red[kThreads / 64];
+    const int64_t b0 = (int64_t)blockIdx.x * kScanBlock;
+    int64_t s = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = b0 + threadIdx.x * 4 + k;
+        if (i < n) s += in[i];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(kThreads)
+scan_sums(int64_t *__restrict__ bsum, int64_t nb) {
+    // single workgroup: exclusive scan in place, chunks of kThreads
+    __shared__ int64_t wtot[kThreads / 64];
+    int64_t carry = 0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t c0 = 0; c0 < nb; c0 += kThreads) {
+        const int64_t i = c0 + threadIdx.x;
+        const int64_t v = i < nb ? bsum[i] : 0;
+        int64_t inc = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wtot[wave] = inc;
+        __syncthreads();
+        int64_t off = carry + inc - v, tot = 0;
+        for (int w = 0; w < kThreads / 64; ++w) {
+            if (w < wave) off += wtot[w];
+            tot += wtot[w];
+        }
+        if (i < nb) bsum[i] = off;
+        carry += tot;
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+scan_finish(const int32_t *__restrict__ in, int64_t n, const int64_t *__restrict__ bsum,
+            int64_t *__restrict__ out) {
+    __shared__ int64_t wtot[kThreads / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t b0 = (int64_t)blockIdx.x * kScanBlock;
+    int64_t v[4], s = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = b0 + threadIdx.x * 4 + k;
+        v[k] = i < n ? in[i] : 0;
+        s += v[k];
+    }
+    int64_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wtot[wave] = inc;
+    __syncthreads();
+    int64_t off = bsum[blockIdx.x] + inc - s;
+    for (int w = 0; w < wave; ++w) off += wtot[w];
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = b0 + threadIdx.x * 4 + k;
+        if (i < n) out[i] = off;
+        off += v[k];
+        if (i == n - 1) out[n] = off;  // total
+    }
+}
+
+int check_segs(const ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t stride,
+               double eps) {
+    if (!ctx || n_segs < 0 || stride < 1 || !(eps >= 0.0) || eps > 32767.0) return ECC_ERR_INVALID;
+    if (n_segs > 0 && !xy) return ECC_ERR_INVALID;
+    if (stride > kMaxPts) return ECC_ERR_INVALID;  // segments hold <= 8192 points
+    return ECC_OK;
+}
+
+}  // namespace
+
+ECC_API int ecc_eps_counts(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                           const int32_t *seg_counts, double eps, int32_t min_pts,
+                           int32_t *counts, double *core_dist, ecc_stream_t stream) {
+    int rc = check_segs(ctx, xy, n_segs, seg_stride, eps);
+    if (rc) return rc;
+    if (!counts || (core_dist && (min_pts < 1 || min_pts > 64))) return ECC_ERR_INVALID;
+    if (n_segs == 0) return ECC_OK;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    SegView sv{seg_counts, n_segs, seg_stride};
+    const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 4096);
+    auto kern = (!core_dist || min_pts <= 8) ? eps_counts_kernel<8> : eps_counts_kernel<64>;
+    {
+        ECC_TIMED(ctx, ecc::as_stream(stream), "eps_counts_kernel");
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, ecc::as_stream(stream), xy, sv, eps,
+                           min_pts, counts, core_dist);
+    }
+    ECC_CHECK_LAUNCH(ctx, "eps_counts_kernel");
+    return ECC_OK;
+}
+
+ECC_API int ecc_eps_lists(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                          const int32_t *seg_counts, double eps, const int32_t *counts,
+                          int64_t *offsets, int32_t *nbr, int64_t nbr_cap, ecc_stream_t stream) {
+    int rc = check_segs(ctx, xy, n_segs, seg_stride, eps);
+    if (rc) return rc;
+    if (!counts || !offsets || (nbr_cap > 0 && !nbr) || nbr_cap < 0) return ECC_ERR_INVALID;
+    if (n_segs == 0) return ECC_OK;
+    const int64_t n = n_segs * seg_stride;
+    const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
+    rc = ecc::ws_reserve(ctx, (size_t)nb * 8 + 256);
+    if (rc) return rc;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    auto *bsum = reinterpret_cast<int64_t *>(ctx->ws);
+    {
+        ECC_TIMED(ctx, s, "scan_block_sums");
+        hipLaunchKernelGGL(scan_block_sums, dim3((unsigned)nb), dim3(kThreads), 0, s, counts, n, bsum);
+    }
+    {
+        ECC_TIMED(ctx, s, "scan_sums");
+        hipLaunchKernelGGL(scan_sums, dim3(1), dim3(kThreads), 0, s, bsum, nb);
+    }
+    {
+        ECC_TIMED(ctx, s, "scan_finish");
+        hipLaunchKernelGGL(scan_finish, dim3((unsigned)nb), dim3(kThreads), 0, s, counts, n, bsum, offsets);
+    }
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + 2, 0, 4, s), "memset(eps err)");
+    SegView sv{seg_counts, n_segs, seg_stride};
+    const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 4096);
+    {
+        ECC_TIMED(ctx, s, "eps_lists_kernel");
+        hipLaunchKernelGGL(eps_lists_kernel, dim3(grid), dim3(kThreads), 0, s, xy, sv, eps,
+                           (const int64_t *)offsets, nbr, nbr_cap, ctx->flags + 2);
+    }
+    ECC_CHECK_LAUNCH(ctx, "eps_lists_kernel");
+    return ECC_OK;
+}
+
+ECC_API int ecc_eps_total(ecc_ctx *ctx, const int64_t *offsets, int64_t n, int64_t *total,
+                          ecc_stream_t stream) {
+    if (!ctx || !offsets || !total || n < 0) return ECC_ERR_INVALID;
+    hipStream_t s = ecc::as_stream(stream);
+    int32_t err = 0;
+    ECC_CHECK_HIP(ctx, hipMemcpyAsync(total, offsets + n, 8, hipMemcpyDeviceToHost, s), "read total");
+    ECC_CHECK_HIP(ctx, hipMemcpyAsync(&err, ctx->flags + 2, 4, hipMemcpyDeviceToHost, s), "read err");
+    ECC_CHECK_HIP(ctx, hipStreamSynchronize(s), "sync");
+    return err ? ECC_ERR_CAPACITY : ECC_OK;
+}

@@ -1,0 +1,333 @@
+// k-means over 2-D event points.
+//
+// Reference: KM/assign_to_centers.cl — assign_to_centers (:1-34: nearest of 8 centres by
+// length((cx-x, cy-y, 0)), strict `<` from threshold 50, uchar 255 = none),
+// assign_data_cluster (:36-119: atomic scatter into 8 bins of 2048), reduction_scalar
+// (:121-140: 1024-wide tree sums), and the host loop KM/assign_to_centers2.c:184-548
+// (buffers re-created every pass, blocking reads, goto restart).
+//
+// MI355X design ("fixed" mode, Appendix A Q7-Q10):
+//   * one fused kernel per iteration: 16-B loads of 4 packed-u16 points per lane, centroids in
+//     LDS (broadcast reads), assignment, and per-wave LDS accumulators updated with 64-bit LDS
+//     atomics — no scatter pass, no bins, no host round trip;
+//   * partial sums are INTEGERS (pixel coordinates): count<<40 | sum_x and sum_y per cluster,
+//     flushed with one 64-bit global atomic per (WG, cluster, field) — exact, so the result is
+//     independent of reduction order and bit-identical to the fp64 oracle;
+//   * a 1-wave update kernel computes c = (float)(sum/n) in fp64, the max shift, and a
+//     device-side `done` flag that makes the remaining queued iterations no-ops (no host
+//     sync per iteration).
+// Assignment arithmetic (canonical, shared with oracle/oracle.cpp assign_one): fp32
+// d2 = dx*dx + dy*dy (no FMA contraction), argmin over sqrtf(d2) with the reference's
+// first-minimum rule.  sqrtf is taken once for the minimum and only re-evaluated for the
+// (rare) centres whose d2 lies within 2^-20 relative of it, which yields exactly the index
+// the reference's per-centre sqrt loop selects.
+// Algorithmic bytes: 4 B/point/iteration (packed u16 xy) + 1 B/point for the final labels.
+#include "ecc_internal.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kMaxK = 64;
+constexpr int kMaxGrid = 2048;
+
+struct KmState {
+    int32_t done;
+    int32_t iters;
+};
+
+// first-minimum argmin over sqrtf(d2) with threshold; c in LDS as (x,y) pairs.
+__device__ __forceinline__ uint32_t assign_point(float px, float py, const float2 *__restrict__ c,
+                                                 int k, float thr) {
+    float m = __builtin_inff();
+    for (int i = 0; i < k; ++i) {
+        const float2 ci = c[i];
+        const float dx = __fsub_rn(ci.x, px), dy = __fsub_rn(ci.y, py);
+        const float d2 = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+        m = fminf(m, d2);
+    }
+    const float s = __fsqrt_rn(m);
+    if (!(s < thr)) return 255u;
+    const float bound = __fadd_rn(m, __fmul_rn(m, 0x1p-20f));
+    for (int i = 0; i < k; ++i) {
+        const float2 ci = c[i];
+        const float dx = __fsub_rn(ci.x, px), dy = __fsub_rn(ci.y, py);
+        const float d2 = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+        if (d2 <= bound && __fsqrt_rn(d2) == s) return (uint32_t)i;
+    }
+    return 255u;  // unreachable: the minimum itself satisfies the test
+}
+
+// Segment geometry: segment s holds cnt(s) points at base s*stride.
+struct Segs {
+    const int32_t *counts;  // nullable
+    int64_t n_segs, stride, n_dense;
+    __device__ __forceinline__ int64_t count(int64_t s) const {
+        if (counts) return counts[s];
+        const int64_t r = n_dense - s * stride;
+        return r < stride ? r : stride;
+    }
+};
+
+template <bool kAccumulate>
+__global__ void __launch_bounds__(kThreads)
+kmeans_xy16_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__restrict__ cent,
+                   int k, float thr, unsigned long long *__restrict__ acc,
+                   const KmState *__restrict__ st, uint8_t *__restrict__ labels) {
+    if (kAccumulate && st->done) return;
+    __shared__ float2 c_lds[kMaxK];
+    __shared__ unsigned long long a_xc[kWaves][kMaxK];
+    __shared__ unsigned long long a_y[kWaves][kMaxK];
+    const int tid = threadIdx.x, wave = tid >> 6;
+    if (tid < k) c_lds[tid] = make_float2(cent[2 * tid], cent[2 * tid + 1]);
+    if (kAccumulate) {
+        for (int i = tid; i < kWaves * kMaxK; i += kThreads) {
+            (&a_xc[0][0])[i] = 0ull;
+            (&a_y[0][0])[i] = 0ull;
+        }
+    }
+    __syncthreads();
+    const bool vec_ok = (segs.stride & 3) == 0;
+    for (int64_t s = blockIdx.x; s < segs.n_segs; s += gridDim.x) {
+        const int64_t cnt = segs.count(s);
+        const int64_t base = s * segs.stride;
+        for (int64_t j = 4 * tid; j < cnt; j += 4 * kThreads) {
+            uint32_t v[4];
+            if (vec_ok && j + 3 < cnt) {
+                const uint4 q = *reinterpret_cast<const uint4 *>(xy + base + j);
+                v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (j + e < cnt) ? xy[base + j + e] : 0u;
+            }
+            uint32_t lab[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool ok = j + e < cnt;
+                const int x = ecc::xy_x(v[e]), y = ecc::xy_y(v[e]);
+                lab[e] = ok ? assign_point((float)x, (float)y, c_lds, k, thr) : 255u;
+                if (kAccumulate && lab[e] != 255u) {
+                    atomicAdd(&a_xc[wave][lab[e]], (1ull << 40) | (unsigned long long)x);
+                    atomicAdd(&a_y[wave][lab[e]], (unsigned long long)y);
+                }
+            }
+            if (labels) {
+                if (j + 3 < cnt && ((base + j) & 3) == 0) {
+                    const uint32_t pk = lab[0] | (lab[1] << 8) | (lab[2] << 16) | (lab[3] << 24);
+                    *reinterpret_cast<uint32_t *>(labels + base + j) = pk;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (j + e < cnt) labels[base + j + e] = (uint8_t)lab[e];
+                }
+            }
+        }
+    }
+    if (kAccumulate) {
+        __syncthreads();
+        if (tid < k) {
+            unsigned long long xc = 0, ys = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) { xc += a_xc[w][tid]; ys += a_y[w][tid]; }
+            const unsigned long long n_pts = xc >> 40;
+            if (n_pts) {
+                atomicAdd(&acc[3 * tid + 0], n_pts);
+                atomicAdd(&acc[3 * tid + 1], xc & ((1ull << 40) - 1));
+                atomicAdd(&acc[3 * tid + 2], ys);
+            }
+        }
+    }
+}
+
+// float-input variant (reference data layout: interleaved float x,y): fp64 LDS + global
+// atomics (order-dependent only at the 1e-16 relative level).
+template <bool kAccumulate>
+__global__ void __launch_bounds__(kThreads)
+kmeans_f32_kernel(const float *__restrict__ xy, int64_t n, const float *__restrict__ cent, int k,
+                  float thr, double *__restrict__ acc, const KmState *__restrict__ st,
+                  uint8_t *__restrict__ labels) {
+    if (kAccumulate && st->done) return;
+    __shared__ float2 c_lds[kMaxK];
+    __shared__ double a_s[kMaxK * 3];
+    const int tid = threadIdx.x;
+    if (tid < k) c_lds[tid] = make_float2(cent[2 * tid], cent[2 * tid + 1]);
+    if (kAccumulate)
+        for (int i = tid; i < kMaxK * 3; i += kThreads) a_s[i] = 0.0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + tid; i < n; i += (int64_t)gridDim.x * kThreads) {
+        const float2 p = reinterpret_cast<const float2 *>(xy)[i];
+        const uint32_t lab = assign_point(p.x, p.y, c_lds, k, thr);
+        if (labels) labels[i] = (uint8_t)lab;
+        if (kAccumulate && lab != 255u) {
+            atomicAdd(&a_s[3 * lab + 0], 1.0);
+            atomicAdd(&a_s[3 * lab + 1], (double)p.x);
+            atomicAdd(&a_s[3 * lab + 2], (double)p.y);
+        }
+    }
+    if (kAccumulate) {
+        __syncthreads();
+        if (tid < 3 * k && a_s[tid] != 0.0) atomicAdd(&acc[tid], a_s[tid]);
+    }
+}
+
+// Centroid update, one wave: c = (float)(sum / n) (fp64), shift = max |new - old|.
+template <typename AccT>
+__global__ void __launch_bounds__(64)
+kmeans_update_kernel(AccT *__restrict__ acc, float *__restrict__ cent, int k, float tol,
+                     KmState *__restrict__ st) {
+    if (st->done) return;
+    const int lane = threadIdx.x;
+    float shift = 0.f;
+    if (lane < k) {
+        const double n_pts = (double)acc[3 * lane + 0];
+        if (n_pts > 0.0) {
+            const float nx = (float)((double)acc[3 * lane + 1] / n_pts);
+            const float ny = (float)((double)acc[3 * lane + 2] / n_pts);
+            shift = fmaxf(fabsf(nx - cent[2 * lane]), fabsf(ny - cent[2 * lane + 1]));
+            cent[2 * lane] = nx;
+            cent[2 * lane + 1] = ny;
+        }
+        acc[3 * lane + 0] = 0;
+        acc[3 * lane + 1] = 0;
+        acc[3 * lane + 2] = 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) shift = fmaxf(shift, __shfl_xor(shift, o));
+    if (lane == 0) {
+        st->iters += 1;
+        if (tol >= 0.f && shift <= tol) st->done = 1;
+    }
+}
+
+int grid_for(int64_t units) {
+    int64_t g = units < kMaxGrid ? units : kMaxGrid;
+    return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace
+
+ECC_API void ecc_kmeans_cfg_default(ecc_kmeans_cfg *cfg) {
+    if (!cfg) return;
+    cfg->k = 16;            // BASELINE.json C3 (the reference hard-codes 8, assign_to_centers.cl:14)
+    cfg->max_iters = 20;
+    cfg->threshold = 50.f;  // assign_to_centers.cl:11
+    cfg->tol = 1e-3f;
+}
+
+static int kmeans_check(const ecc_ctx *ctx, const ecc_kmeans_cfg *cfg, const float *centroids) {
+    if (!ctx || !cfg || !centroids) return ECC_ERR_INVALID;
+    if (cfg->k < 1 || cfg->k > kMaxK || cfg->max_iters < 0) return ECC_ERR_INVALID;
+    return ECC_OK;
+}
+
+ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs,
+                                int64_t seg_stride, const int32_t *seg_counts,
+                                const ecc_kmeans_cfg *cfg, float *centroids, uint8_t *labels,
+                                int32_t *iters_out, ecc_stream_t stream) {
+    int rc = kmeans_check(ctx, cfg, centroids);
+    if (rc) return rc;
+    if (n_segs < 0 || seg_stride < 1) return ECC_ERR_INVALID;
+    Segs segs{seg_counts, n_segs, seg_stride, n_segs * seg_stride};
+    if (!seg_counts) {
+        // dense array of n_segs*seg_stride points: re-cut into 16384-point segments
+        const int64_t n = n_segs * seg_stride;
+        segs.stride = 16384;
+        segs.n_segs = (n + segs.stride - 1) / segs.stride;
+        segs.n_dense = n;
+    }
+    if (segs.n_segs > 0 && !xy) return ECC_ERR_INVALID;
+    // per-WG packed counts must stay < 2^24 points (sum_x < 2^40)
+    const int grid = grid_for(segs.n_segs);
+    if (segs.n_segs * segs.stride / grid >= (1ll << 24)) return ECC_ERR_INVALID;
+    rc = ecc::ws_reserve(ctx, 4096);
+    if (rc) return rc;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    auto *acc = reinterpret_cast<unsigned long long *>(ctx->ws);
+    auto *st = reinterpret_cast<KmState *>(reinterpret_cast<char *>(ctx->ws) + 3 * kMaxK * 8);
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, 3 * kMaxK * 8 + 64, s), "memset(kmeans acc)");
+    for (int it = 0; it < cfg->max_iters; ++it) {
+        {
+            ECC_TIMED(ctx, s, "kmeans_xy16_kernel");
+            hipLaunchKernelGGL(kmeans_xy16_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
+                               centroids, cfg->k, cfg->threshold, acc, st, (uint8_t *)nullptr);
+        }
+        {
+            ECC_TIMED(ctx, s, "kmeans_update_kernel");
+            hipLaunchKernelGGL(kmeans_update_kernel<unsigned long long>, dim3(1), dim3(64), 0, s, acc,
+                               centroids, cfg->k, cfg->tol, st);
+        }
+    }
+    ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 iteration");
+    if (labels && segs.n_segs > 0) {
+        {
+            ECC_TIMED(ctx, s, "kmeans_xy16_labels");
+            hipLaunchKernelGGL(kmeans_xy16_kernel<false>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
+                               centroids, cfg->k, cfg->threshold, acc, st, labels);
+        }
+        ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 labels");
+    }
+    if (iters_out)
+        ECC_CHECK_HIP(ctx, hipMemcpyAsync(iters_out, &st->iters, 4, hipMemcpyDeviceToDevice, s),
+                      "copy iters");
+    return ECC_OK;
+}
+
+ECC_API int ecc_kmeans_run_f32(ecc_ctx *ctx, const float *xy, int64_t n_points,
+                               const ecc_kmeans_cfg *cfg, float *centroids, uint8_t *labels,
+                               int32_t *iters_out, ecc_stream_t stream) {
+    int rc = kmeans_check(ctx, cfg, centroids);
+    if (rc) return rc;
+    if (n_points < 0 || (n_points > 0 && !xy)) return ECC_ERR_INVALID;
+    rc = ecc::ws_reserve(ctx, 4096);
+    if (rc) return rc;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    auto *acc = reinterpret_cast<double *>(ctx->ws);
+    auto *st = reinterpret_cast<KmState *>(reinterpret_cast<char *>(ctx->ws) + 3 * kMaxK * 8);
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, 3 * kMaxK * 8 + 64, s), "memset(kmeans acc)");
+    const int grid = grid_for((n_points + kThreads - 1) / kThreads);
+    for (int it = 0; it < cfg->max_iters && n_points > 0; ++it) {
+        {
+            ECC_TIMED(ctx, s, "kmeans_f32_kernel");
+            hipLaunchKernelGGL(kmeans_f32_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, n_points,
+                               centroids, cfg->k, cfg->threshold, acc, st, (uint8_t *)nullptr);
+        }
+        {
+            ECC_TIMED(ctx, s, "kmeans_update_kernel");
+            hipLaunchKernelGGL(kmeans_update_kernel<double>, dim3(1), dim3(64), 0, s, acc, centroids,
+                               cfg->k, cfg->tol, st);
+        }
+    }
+    ECC_CHECK_LAUNCH(ctx, "kmeans_f32 iteration");
+    if (labels && n_points > 0) {
+        {
+            ECC_TIMED(ctx, s, "kmeans_f32_labels");
+            hipLaunchKernelGGL(kmeans_f32_kernel<false>, dim3(grid), dim3(kThreads), 0, s, xy, n_points,
+                               centroids, cfg->k, cfg->threshold, acc, st, labels);
+        }
+        ECC_CHECK_LAUNCH(ctx, "kmeans_f32 labels");
+    }
+    if (iters_out)
+        ECC_CHECK_HIP(ctx, hipMemcpyAsync(iters_out, &st->iters, 4, hipMemcpyDeviceToDevice, s),
+                      "copy iters");
+    return ECC_OK;
+}
+
+ECC_API int ecc_kmeans_assign_f32(ecc_ctx *ctx, const float *xy, int64_t n_points,
+                                  const float *centroids, int32_t k, float threshold,
+                                  uint8_t *labels, ecc_stream_t stream) {
+    if (!ctx || !centroids || !labels || k < 1 || k > kMaxK || n_points < 0) return ECC_ERR_INVALID;
+    if (n_points == 0) return ECC_OK;
+    if (!xy) return ECC_ERR_INVALID;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    const int grid = grid_for((n_points + kThreads - 1) / kThreads);
+    {
+        ECC_TIMED(ctx, ecc::as_stream(stream), "kmeans_f32_kernel");
+        hipLaunchKernelGGL(kmeans_f32_kernel<false>, dim3(grid), dim3(kThreads), 0,
+                           ecc::as_stream(stream), xy, n_points, centroids, k, threshold,
+                           (double *)nullptr, (const KmState *)nullptr, labels);
+    }
+    ECC_CHECK_LAUNCH(ctx, "kmeans assign");
+    return ECC_OK;
+}

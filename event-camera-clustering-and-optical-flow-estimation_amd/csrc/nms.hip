@@ -1,0 +1,166 @@
+// Greedy box NMS per slice.
+//
+// Reference: CornerFilter::filterCorners, FCT/…group_track.cpp:81-152 — a H×W u8 mask
+// (cv::Mat::zeros per call), corners visited in detection order, a corner is kept iff no mask
+// pixel inside its clipped box [x±7]×[y±7] is set, and a kept corner paints its box
+// (cv::rectangle filled).  Called once per 16384-event slice (:832-837).
+//
+// MI355X design: one workgroup per slice, every slice of a batch in ONE launch.  The slice's
+// corner flags (16 KiB) are read with 16-B loads and compacted in event order into LDS; the
+// greedy pass then runs on one wave without any mask image: "box touches a painted pixel"
+// == "box intersects the box of an earlier kept corner" (kept boxes are the painted set).
+// Candidates are processed 64 at a time: each lane tests its candidate against the kept list
+// (LDS broadcast reads), then the within-chunk order dependency is resolved on a 64x64
+// overlap bitmask with scalar bit logic.  Output label = rank in the kept list (:140).
+#include "ecc_internal.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxCand = 16384;  // LDS candidate list (64 KiB)
+constexpr int kMaxKept = 8192;   // LDS kept list (boxes are disjoint => <= W*H/144)
+
+struct Box { int16_t x0, x1, y0, y1; };
+
+__device__ __forceinline__ Box make_box(uint32_t v, int half, int W, int H) {
+    const int x = ecc::xy_x(v), y = ecc::xy_y(v);
+    Box b;
+    b.x0 = (int16_t)max(0, x - half);     // :114-117
+    b.x1 = (int16_t)min(W - 1, x + half);
+    b.y0 = (int16_t)max(0, y - half);
+    b.y1 = (int16_t)min(H - 1, y + half);
+    return b;
+}
+
+__device__ __forceinline__ bool overlap(const Box &a, const Box &b) {
+    return a.x0 <= b.x1 && b.x0 <= a.x1 && a.y0 <= b.y1 && b.y0 <= a.y1;
+}
+
+__global__ void __launch_bounds__(kThreads)
+nms_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ flags, int64_t n, int S,
+           int W, int H, int half, int cap, ecc_corner *__restrict__ out,
+           int32_t *__restrict__ out_count, int32_t *__restrict__ err) {
+    __shared__ uint32_t cand[kMaxCand];
+    __shared__ Box kept[kMaxKept];
+    __shared__ int wave_tot[kThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t s = blockIdx.x;
+    const int64_t lo = s * (int64_t)S;
+    const int64_t hi = (lo + S < n) ? lo + S : n;
+    const int64_t len = hi - lo;
+
+    // 1. compaction of flagged events in event order, in chunks of 256*16 events
+    int n_cand = 0;
+    for (int64_t c0 = 0; c0 < len; c0 += kThreads * 16) {
+        const int64_t my0 = c0 + (int64_t)tid * 16;
+        uint32_t bits = 0;
+        if (my0 + 15 < len && ((lo + my0) & 15) == 0) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(flags + lo + my0);
+            const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) bits |= (((w4[k >> 2] >> (8 * (k & 3))) & 0xffu) ? 1u : 0u) << k;
+        } else {
+            for (int k = 0; k < 16; ++k)
+                if (my0 + k < len && flags[lo + my0 + k]) bits |= 1u << k;
+        }
+        const int cntv = __popc(bits);
+        // wave inclusive scan of cntv
+        int incl = cntv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wave_tot[wave] = incl;
+        __syncthreads();
+        int off = n_cand + incl - cntv, tot = 0;
+        for (int w = 0; w < kThreads / 64; ++w) {
+            if (w < wave) off += wave_tot[w];
+            tot += wave_tot[w];
+        }
+        while (bits) {
+            const int k = __ffs(bits) - 1;
+            bits &= bits - 1;
+            if (off < kMaxCand) cand[off] = xy[lo + my0 + k];
+            ++off;
+        }
+        n_cand += tot;
+        __syncthreads();
+    }
+    if (n_cand > kMaxCand) n_cand = kMaxCand;  // cannot happen when S <= kMaxCand
+    __syncthreads();
+    // 2. greedy NMS on wave 0 (the other waves only keep the barriers uniform)
+    int n_kept = 0;
+    bool overflow = false;
+    for (int c0 = 0; c0 < n_cand; c0 += 64) {
+        if (wave == 0) {
+            const int ci = c0 + lane;
+            const bool valid = ci < n_cand;
+            const uint32_t v = valid ? cand[ci] : 0u;
+            const Box b = make_box(v, half, W, H);
+            bool alive = valid;
+            for (int k = 0; k < n_kept && alive; ++k)
+                if (overlap(b, kept[k])) alive = false;
+            // within-chunk dependency: ov = lanes j < lane whose box overlaps mine
+            uint64_t ov = 0;
+            for (int j = 0; j < 64; ++j) {
+                const int x0 = __shfl((int)b.x0, j), x1 = __shfl((int)b.x1, j);
+                const int y0 = __shfl((int)b.y0, j), y1 = __shfl((int)b.y1, j);
+                const bool o = (j < lane) && x0 <= b.x1 && b.x0 <= x1 && y0 <= b.y1 && b.y0 <= y1;
+                ov |= (uint64_t)o << j;
+            }
+            uint64_t alive_m = __ballot(alive);
+            uint64_t acc = 0;
+            while (alive_m) {
+                const int i = __ffsll((unsigned long long)alive_m) - 1;
+                alive_m &= alive_m - 1;
+                const uint64_t ov_i = __shfl(ov, i);
+                if ((ov_i & acc) == 0) acc |= 1ull << i;
+            }
+            const bool keep = (acc >> lane) & 1ull;
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            const int rank = n_kept + __popcll(acc & lt);
+            if (keep) {
+                if (rank < kMaxKept) kept[rank] = b;
+                else overflow = true;
+                if (rank < cap) out[s * (int64_t)cap + rank] = ecc_corner{ecc::xy_x(v), ecc::xy_y(v), rank};
+                else overflow = true;
+            }
+            n_kept += __popcll(acc);
+            if (n_kept > kMaxKept) n_kept = kMaxKept;
+        }
+        __syncthreads();  // orders the kept[] LDS writes before the next chunk's reads
+    }
+    if (wave != 0) return;
+    overflow = __any(overflow);
+    if (lane == 0) {
+        out_count[s] = n_kept < cap ? n_kept : cap;
+        if (overflow) *err = 1;
+    }
+}
+
+}  // namespace
+
+ECC_API int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corner_flags,
+                           int64_t n, int32_t slice_events, int32_t width, int32_t height,
+                           int32_t box_size, int32_t cap, ecc_corner *out, int32_t *out_count,
+                           ecc_stream_t stream) {
+    if (!ctx || n < 0 || slice_events < 1 || slice_events > kMaxCand || width < 1 ||
+        height < 1 || width > 32767 || height > 32767 || box_size < 1 || cap < 0)
+        return ECC_ERR_INVALID;
+    if (n == 0) return ECC_OK;
+    if (!xy || !corner_flags || !out_count || (cap > 0 && !out)) return ECC_ERR_INVALID;
+    const int64_t n_slices = (n + slice_events - 1) / slice_events;
+    if (n_slices > INT32_MAX) return ECC_ERR_INVALID;
+    hipStream_t s = ecc::as_stream(stream);
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + 1, 0, 4, s), "memset(nms err)");
+    {
+        ECC_TIMED(ctx, s, "nms_kernel");
+        hipLaunchKernelGGL(nms_kernel, dim3((unsigned)n_slices), dim3(kThreads), 0, s, xy,
+                           corner_flags, n, slice_events, width, height, box_size / 2, cap, out,
+                           out_count, ctx->flags + 1);
+    }
+    ECC_CHECK_LAUNCH(ctx, "nms_kernel");
+    return ECC_OK;
+}

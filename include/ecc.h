@@ -1,0 +1,309 @@
+/*
+ * ecc.h — C ABI of the MI355X-native event-camera clustering / corner pipeline.
+ *
+ * Drop-in boundary for the hot path of
+ * LogicTronixInc/Event-Camera-Clustering-and-Optical-Flow-Estimation:
+ *
+ *   hash-map downsample -> k-means / DBSCAN / OPTICS eps-neighbour -> SAE + FAST arc corners
+ *   -> box NMS -> predictor-corrector corner tracker
+ *
+ * Every compute entry point takes DEVICE pointers (hipMalloc'd memory on the context's GPU)
+ * plus an opaque stream (a hipStream_t passed as void*, NULL = default stream) and enqueues
+ * work asynchronously, mirroring the OpenCL clEnqueueNDRangeKernel boundary the reference
+ * uses.  Return value: ECC_OK (0) or a negative ecc_status, mirroring the reference's
+ * `if (err < 0) { perror(...); exit(1); }` convention (SMP/…opencl_store.cpp:256-260).
+ *
+ * Canonical data layout in HBM (SoA): xy = packed u32 (x | y << 16), t = int64 µs,
+ * p = u8.  The reference copies EventCD{u16 x,u16 y,i16 p,i64 t} into int arrays.
+ *
+ * Reference interface each entry point replaces is cited on the declaration.
+ * Quirk decisions (ref_compat vs fixed) follow SURVEY.md Appendix A.
+ */
+#ifndef ECC_H
+#define ECC_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ECC_VERSION 1
+
+typedef void *ecc_stream_t; /* hipStream_t */
+
+typedef enum ecc_status {
+    ECC_OK = 0,
+    ECC_ERR_INVALID = -1,       /* bad argument / shape */
+    ECC_ERR_HIP = -2,           /* HIP runtime error (launch, memcpy, malloc) */
+    ECC_ERR_UNSORTED_TIME = -3, /* event timestamps decrease inside a batch */
+    ECC_ERR_CAPACITY = -4,      /* an output capacity was exceeded (result truncated) */
+    ECC_ERR_NOMEM = -5,         /* host / device allocation failed */
+    ECC_ERR_NO_DEVICE = -6      /* no GPU visible */
+} ecc_status;
+
+typedef struct ecc_ctx ecc_ctx; /* per-stream context: device id + scratch workspace */
+
+/* Reference: create_device()/clCreateContext (SMP/…opencl_store.cpp:51-79, 233-240). */
+int ecc_ctx_create(ecc_ctx **out, int device);
+int ecc_ctx_destroy(ecc_ctx *ctx);
+const char *ecc_status_string(int status);
+int ecc_version(void);
+/* Last HIP error string recorded by this context (for ECC_ERR_HIP). */
+const char *ecc_ctx_last_error(const ecc_ctx *ctx);
+/* Blocks until all work queued by this library on `stream` has finished. */
+int ecc_stream_sync(ecc_stream_t stream);
+
+/* Runtime plumbing (the reference's clCreateBuffer / clEnqueueRead/WriteBuffer /
+ * clGetEventProfilingInfo, SMP/…opencl_store.cpp:264-268, 406-422) so hosts and tests need
+ * no other GPU runtime.  Copies are stream-ordered; *_sync variants block. */
+int ecc_device_count(int *n);
+int ecc_set_device(int device);
+int ecc_dev_alloc(void **ptr, size_t bytes);
+int ecc_dev_free(void *ptr);
+int ecc_memset_async(void *dst, int value, size_t bytes, ecc_stream_t stream);
+int ecc_memcpy_h2d(void *dst, const void *src, size_t bytes, ecc_stream_t stream);
+int ecc_memcpy_d2h(void *dst, const void *src, size_t bytes, ecc_stream_t stream);
+int ecc_memcpy_d2d(void *dst, const void *src, size_t bytes, ecc_stream_t stream);
+int ecc_stream_create(ecc_stream_t *stream);
+int ecc_stream_destroy(ecc_stream_t stream);
+int ecc_event_create(void **event);
+int ecc_event_destroy(void *event);
+int ecc_event_record(void *event, ecc_stream_t stream);
+int ecc_event_elapsed_ms(float *ms, void *start, void *stop); /* synchronises `stop` */
+
+/* Per-kernel timing (the reference's CL_QUEUE_PROFILING_ENABLE + clGetEventProfilingInfo,
+ * SMP/…opencl_store.cpp:263-264, 406-412): when enabled, every kernel this context launches
+ * is bracketed by HIP events on its stream.  The report (JSON object
+ * {"<kernel>": {"launches": n, "total_ms": t}, ...}) synchronises the device first. */
+int ecc_ctx_set_timing(ecc_ctx *ctx, int enable);
+int ecc_ctx_timing_reset(ecc_ctx *ctx);
+int ecc_ctx_timing_report(ecc_ctx *ctx, char *buf, size_t cap);
+
+/* ---------------------------------------------------------------------------------------
+ * 1. Hash-map downsample
+ * Reference: __kernel process_coordinates(input_coords, repeated_coords, unique_coords,
+ *            repeated_count, unique_count, total_coords, width, height)
+ *            SMP/build/coordinate_processor.cl:3-14 (hash), :16-89 (kernel);
+ *            host launch SMP/…opencl_store.cpp:250-312, DSA/…opencl_store.cpp:370-445.
+ * Events are cut into contiguous windows of `window` events (reference ring: 8192 pairs).
+ * Per window: bucket h = (x*mult_x + y*mult_y) % n_buckets for events with
+ * 0<=x<=x_max && 0<=y<=y_max (inclusive, coordinate_processor.cl:56); the first hit of a
+ * bucket (canonical: LOWEST event index, Appendix A Q2) is the representative; a bucket's
+ * second hit increments `repeated`.  Outputs (any may be NULL):
+ *   rep_xy [n_windows*window]  packed xy of representatives of window w at w*window + k,
+ *                              k < win_unique[w], ascending event index;
+ *   rep_idx[n_windows*window]  global event index of the same representatives;
+ *   win_unique[n_windows], win_repeated[n_windows] per-window counts (Q4: not cumulative).
+ * n_windows = ceil(n / window).  Bit-exact vs oracle/ and the reference kernel's counts.
+ * ------------------------------------------------------------------------------------- */
+typedef struct ecc_hash_cfg {
+    int32_t window;    /* events per window, 1..16384 (reference 8192) */
+    int32_t x_max;     /* inclusive bound (reference 1280) */
+    int32_t y_max;     /* inclusive bound (reference 720) */
+    int32_t mult_x;    /* 1619 */
+    int32_t mult_y;    /* 31 */
+    int32_t n_buckets; /* 8192 (fixed: LDS table size) */
+} ecc_hash_cfg;
+
+void ecc_hash_cfg_default(ecc_hash_cfg *cfg);
+int ecc_downsample_hash(ecc_ctx *ctx, const uint32_t *xy, int64_t n, const ecc_hash_cfg *cfg,
+                        uint32_t *rep_xy, uint32_t *rep_idx, int32_t *win_unique,
+                        int32_t *win_repeated, ecc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * 2. k-means (2-D, k <= 64)
+ * Reference: __kernel assign_to_centers / assign_data_cluster / reduction_scalar
+ *            KM/assign_to_centers.cl:1-34, :36-119, :121-140; host loop
+ *            KM/assign_to_centers2.c:184-548.
+ * Assignment (a5, Q10): d_c = sqrtf(dx*dx + dy*dy) in fp32 with dx = cx - px, first
+ * minimum with strict `<` starting from `threshold` (50); no centre closer => label 255.
+ * Update ("fixed" mode, Q7-Q9): c = (sum x / n, sum y / n) over assigned points (exact
+ * integer / fp64 sums), unchanged when n == 0; stop after `max_iters` updates or once the
+ * largest per-coordinate centroid shift <= tol (tol < 0: never).  After the loop, labels
+ * (if non-NULL) are the assignment against the FINAL centroids.
+ * Points: packed u16 xy (the downsample output) or interleaved float xy.
+ * Segmented input (downsample layout): point j of segment s is at s*seg_stride + j,
+ * j < seg_counts[s] (device int32[n_segs]); pass seg_counts = NULL for a dense array of
+ * n_points (= n_segs*seg_stride is then ignored; use n_segs = 1, seg_stride = n_points).
+ * centroids: DEVICE float[2k] (x0,y0,x1,y1,...) in/out.  iters_out: DEVICE int32[1] or NULL.
+ * ------------------------------------------------------------------------------------- */
+typedef struct ecc_kmeans_cfg {
+    int32_t k;         /* number of centres, 1..64 */
+    int32_t max_iters; /* >= 0 */
+    float threshold;   /* 50.0f */
+    float tol;         /* convergence tolerance on centroid shift; < 0 disables */
+} ecc_kmeans_cfg;
+
+void ecc_kmeans_cfg_default(ecc_kmeans_cfg *cfg);
+int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                        const int32_t *seg_counts, const ecc_kmeans_cfg *cfg, float *centroids,
+                        uint8_t *labels, int32_t *iters_out, ecc_stream_t stream);
+int ecc_kmeans_run_f32(ecc_ctx *ctx, const float *xy, int64_t n_points, const ecc_kmeans_cfg *cfg,
+                       float *centroids, uint8_t *labels, int32_t *iters_out, ecc_stream_t stream);
+/* One assignment pass only (assign_to_centers): labels[i] in [0,k) or 255. */
+int ecc_kmeans_assign_f32(ecc_ctx *ctx, const float *xy, int64_t n_points, const float *centroids,
+                          int32_t k, float threshold, uint8_t *labels, ecc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * 3. SAE (time surface) + FAST/arc corner detection
+ * Reference: FCT/metavision_time_surface_periodic_group_track.cpp:884-1063 (aggregate lambda:
+ *            batch SAE update :900-923, arc test :948-1063, circles :44-45), slices of
+ *            16384 events (make_n_events, :772-774), detection from the 2nd slice on (:926).
+ * Semantics per slice s (events [s*slice, (s+1)*slice)): first ALL events of the slice write
+ * sae[y][x] = t (Q14, batch), then every event is tested: border events
+ * (x<m || x>=W-m || y<m || y>=H-m, m = margin 4, W/H = sensor size: Q12) are skipped
+ * (border_mode 0 = fixed) or end the slice's tests (border_mode 1 = ref_compat `break`,
+ * Q11); corner = circle3 streak (len 3..6 of 16) AND circle4 streak (len 4..8 of 20).
+ * Slices with global index < first_detect_slice are not tested (Q15: pass 1 for a fresh
+ * stream, 0 when continuing a stream).
+ * sae: DEVICE int64[H*W], row-major, holds the initial SAE on entry and the final SAE on
+ * exit (stream continuation / multi-GPU hand-off).  Timestamps must be non-decreasing
+ * (Metavision stream order) -> ECC_ERR_UNSORTED_TIME otherwise (flag checked on device,
+ * reported by ecc_fast_detect_status()).
+ * corner_flags: DEVICE uint8[n], 1 = corner.  Bit-exact vs oracle/.
+ * ------------------------------------------------------------------------------------- */
+typedef struct ecc_corner_cfg {
+    int32_t width, height;      /* sensor size */
+    int32_t slice_events;       /* 16384 */
+    int32_t margin;             /* 4 */
+    int32_t border_mode;        /* 0 fixed (continue), 1 ref_compat (break) */
+    int32_t first_detect_slice; /* 1 */
+} ecc_corner_cfg;
+
+void ecc_corner_cfg_default(ecc_corner_cfg *cfg);
+int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                    const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
+                    ecc_stream_t stream);
+/* Synchronises `stream` and reports ECC_ERR_UNSORTED_TIME if the last ecc_fast_detect on
+ * this context saw decreasing timestamps, else ECC_OK. */
+int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream);
+/* Final-SAE-only pass (used for the multi-GPU hand-off: per-shard local SAE). */
+int ecc_sae_scatter(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n, int32_t width,
+                    int32_t height, int64_t *sae, ecc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * 4. Greedy box NMS per slice
+ * Reference: CornerFilter::filterCorners(corners, W, H, box_size=15, threshold)
+ *            FCT/…group_track.cpp:69-153, called per slice at :832-837.
+ * Corners of slice s are the events with corner_flags==1 in event order; a corner is kept
+ * iff its clipped box [x±box/2]×[y±box/2] touches no box of an earlier kept corner; kept
+ * corner label = its rank in the kept list (":140").  out: DEVICE ecc_corner[n_slices*cap],
+ * slice s at s*cap; out_count: DEVICE int32[n_slices] (ECC_ERR_CAPACITY if a slice
+ * overflows: counts are clamped to cap).
+ * ------------------------------------------------------------------------------------- */
+typedef struct ecc_corner { int32_t x, y, label; } ecc_corner; /* reference struct Corner */
+
+int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corner_flags, int64_t n,
+                   int32_t slice_events, int32_t width, int32_t height, int32_t box_size,
+                   int32_t cap, ecc_corner *out, int32_t *out_count, ecc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * 5. Corner tracker (damped predictor-corrector + grouping)
+ * Reference: class CornerTracker FCT/…group_track.cpp:163-537 (updateTrackedCorners
+ *            :421-530, predictPosition :304-319, calculateDirection :233-271,
+ *            estimateVelocity :273-302, updateCornerGroups :321-398), constructed with
+ *            (30, 30, 10, 5, 0.8, 0.3, 100) at :805-813.  fp32 arithmetic in the
+ *            reference's operation order; miss path truncates to int (Q16).
+ * A tracker lives on the device; ecc_tracker_update consumes n_slices NMS outputs in order
+ * (one updateTrackedCorners call per slice) in a single launch.
+ * ------------------------------------------------------------------------------------- */
+#define ECC_TRACK_HIST_MAX 16
+
+typedef struct ecc_tracker_cfg {
+    float max_distance;     /* 30 */
+    int32_t max_frames;     /* 30 */
+    int32_t history_size;   /* 10 (<= ECC_TRACK_HIST_MAX) */
+    int32_t frames_to_skip; /* 5 */
+    float damping;          /* 0.8 */
+    float smoothing;        /* 0.3 */
+    float group_radius;     /* 100 */
+} ecc_tracker_cfg;
+
+typedef struct ecc_track { /* reference struct TrackedCorner (:177-190) */
+    int32_t x, y, label, frame_count;
+    int32_t is_matched, frames_since_last_detection;
+    int32_t hist_len;
+    int32_t hist_x[ECC_TRACK_HIST_MAX], hist_y[ECC_TRACK_HIST_MAX]; /* [0] = most recent */
+    float vx, vy;
+    float dir_cur_x, dir_cur_y, dir_tgt_x, dir_tgt_y;
+    int32_t group_id;
+} ecc_track;
+
+typedef struct ecc_group { /* reference struct CornerGroup (:193-199), keyed by group id */
+    int32_t id, n_labels, first_label_offset; /* labels in ecc_tracker_get_groups' label array */
+    float avg_vx, avg_vy, cx, cy, radius;
+} ecc_group;
+
+typedef struct ecc_tracker ecc_tracker;
+
+void ecc_tracker_cfg_default(ecc_tracker_cfg *cfg);
+int ecc_tracker_create(ecc_ctx *ctx, const ecc_tracker_cfg *cfg, int32_t max_tracks,
+                       int32_t max_detections, ecc_tracker **out);
+int ecc_tracker_destroy(ecc_tracker *tr);
+int ecc_tracker_update(ecc_tracker *tr, const ecc_corner *corners, const int32_t *counts,
+                       int32_t n_slices, int32_t cap, ecc_stream_t stream);
+/* Host copies of the current state (synchronises stream). */
+int ecc_tracker_get_tracks(ecc_tracker *tr, ecc_track *out, int32_t cap, int32_t *n_out,
+                           ecc_stream_t stream);
+int ecc_tracker_get_groups(ecc_tracker *tr, ecc_group *out, int32_t cap, int32_t *n_out,
+                           int32_t *labels, int32_t labels_cap, ecc_stream_t stream);
+/* 0 = OK, otherwise an ecc_status (capacity overflow inside the device loop). */
+int ecc_tracker_status(ecc_tracker *tr, ecc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * 6. eps-neighbourhoods for DBSCAN / OPTICS over 2-D integer points (pixels)
+ * Reference: DBSCANSimpleCluster::radiusSearch PCC/DBSCAN_simple.h:118-142 and
+ *            DBSCANPrecompCluster::precomp PCC/DBSCAN_precomp.h:22-44 (d^2 <= eps^2 in double,
+ *            self included); kdt::KDTree::radius_search OPT/include/optics/kdTree.hpp:307-422;
+ *            optics::compute_core_dist OPT/include/optics/optics.hpp:286-299.
+ * Points are packed u16 xy, segmented like ecc_kmeans_run_xy16 (one independent
+ * neighbourhood problem per segment, <= 8192 points each, e.g. one downsample window);
+ * duplicates allowed.  Arrays are indexed by the flattened point index p = s*seg_stride + j
+ * (entries with j >= seg_counts[s] are left untouched, except offsets which stay monotone).
+ *   counts[p]    = |{j in seg : (xi-xj)^2 + (yi-yj)^2 <= eps^2}| (self included);
+ *   core_dist[p] = sqrt of the (min_pts-1)-th smallest d^2 of that set (fp64), or -1 when
+ *                  counts[p] < min_pts (optics.hpp:292-298).  NULL to skip.
+ * ecc_eps_lists: offsets[n_segs*seg_stride + 1] = exclusive scan of counts (computed here);
+ *   nbr[offsets[p] .. offsets[p+1]) = segment-local neighbour indices in ascending order
+ *   (the order of DBSCAN_precomp.h's adjacency lists).  ECC_ERR_CAPACITY if nbr_cap is too
+ *   small (call ecc_eps_counts + read offsets' last entry to size it).
+ * ------------------------------------------------------------------------------------- */
+int ecc_eps_counts(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                   const int32_t *seg_counts, double eps, int32_t min_pts, int32_t *counts,
+                   double *core_dist, ecc_stream_t stream);
+int ecc_eps_lists(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                  const int32_t *seg_counts, double eps, const int32_t *counts, int64_t *offsets,
+                  int32_t *nbr, int64_t nbr_cap, ecc_stream_t stream);
+/* Host helper: synchronises `stream`, returns offsets[n] (total list length) via *total. */
+int ecc_eps_total(ecc_ctx *ctx, const int64_t *offsets, int64_t n, int64_t *total,
+                  ecc_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * 7. Host-side helpers (no GPU): synthetic event streams and event-file I/O.
+ * Reference ingress is Metavision's Camera::from_file(argv[1]) (FCT/…group_track.cpp:756-760);
+ * here: CSV "x,y,t,p" (OPT/test/event_raw_data8.csv layout) or the binary SoA .ecc file.
+ * ------------------------------------------------------------------------------------- */
+typedef struct ecc_gen_cfg {
+    uint64_t seed;
+    int32_t width, height;
+    double rate_mev_s;     /* events per µs of sensor time (10 = 10 Mev/s) */
+    int64_t t0;            /* first timestamp (µs) */
+    int32_t n_polygons;    /* 8 moving convex polygons (70 % of events) */
+    int32_t n_blobs;       /* 16 Gaussian blobs sigma 4 (20 %) */
+    float frac_edges, frac_blobs; /* remaining = uniform noise */
+} ecc_gen_cfg;
+
+void ecc_gen_cfg_default(ecc_gen_cfg *cfg);
+/* Fills host arrays (any may be NULL) with events [first, first+n) of the stream. */
+int ecc_gen_events(const ecc_gen_cfg *cfg, int64_t first, int64_t n, uint32_t *xy, int64_t *t,
+                   uint8_t *p);
+/* CSV reader: returns the number of events read (<= cap) or a negative status. */
+int64_t ecc_read_csv(const char *path, uint32_t *xy, int64_t *t, uint8_t *p, int64_t cap);
+int64_t ecc_count_csv(const char *path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ECC_H */

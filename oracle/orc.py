@@ -1,0 +1,222 @@
+"""ctypes wrapper of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+The oracle is the CPU restatement of the reference algorithms (oracle/oracle.cpp).  Only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and
+only as the checker / the CPU baseline.  It never backs a product code path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB_PATH = ORACLE_DIR / "liboracle.so"
+
+
+def build() -> None:
+    import subprocess
+    subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, stdout=subprocess.DEVNULL)
+
+
+if not LIB_PATH.exists():
+    build()
+lib = C.CDLL(str(LIB_PATH))
+
+P = C.c_void_p
+i64, i32, f32, f64 = C.c_int64, C.c_int32, C.c_float, C.c_double
+_sigs = {
+    "orc_downsample_hash": (C.c_int, [P, i64, i32, i32, i32, i32, i32, i32, P, P, P, P]),
+    "orc_kmeans_assign_f32": (C.c_int, [P, i64, P, i32, f32, P]),
+    "orc_kmeans_run_f32": (C.c_int, [P, i64, P, i32, i32, f32, f32, P, P]),
+    "orc_kmeans_run_xy16": (C.c_int, [P, i64, P, i32, i32, f32, f32, P, P]),
+    "orc_kmeans_refcompat": (C.c_int, [P, i64, P, i32, P, P]),
+    "orc_arc_test": (C.c_int, [P, i32, i32, i32]),
+    "orc_fast_detect": (C.c_int, [P, P, i64, i32, i32, i32, i32, i32, i32, P, P]),
+    "orc_filter_corners": (C.c_int, [P, i32, i32, i32, i32, P, i32]),
+    "orc_corner_nms": (C.c_int, [P, P, i64, i32, i32, i32, i32, i32, P, P]),
+    "orc_tracker_create": (P, [P]),
+    "orc_tracker_destroy": (None, [P]),
+    "orc_tracker_update": (C.c_int, [P, P, i32]),
+    "orc_tracker_get_tracks": (C.c_int, [P, P, i32]),
+    "orc_tracker_get_groups": (C.c_int, [P, P, i32, P, i32]),
+    "orc_eps_neighbours": (C.c_int, [P, i64, i64, P, f64, i32, P, P, P, P, i64]),
+    "orc_dbscan": (C.c_int, [P, i32, f64, i32, i32, i32, P]),
+    "orc_epsilon_estimation": (f64, [P, i32, i32, i32]),
+    "orc_optics": (C.c_int, [P, i32, i32, i32, f64, P, P]),
+    "orc_get_cluster_indices": (C.c_int, [P, i32, f64, P]),
+    "orc_radius_search": (C.c_int, [P, i32, i32, P, f64, P, i32]),
+}
+for _n, (_r, _a) in _sigs.items():
+    f = getattr(lib, _n)
+    f.restype = _r
+    f.argtypes = _a
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def downsample_hash(xy, window=8192, x_max=1280, y_max=720, mult_x=1619, mult_y=31, nb=8192):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    n = len(xy)
+    nw = (n + window - 1) // window
+    rep_xy = np.zeros(nw * window, np.uint32)
+    rep_idx = np.zeros(nw * window, np.uint32)
+    u = np.zeros(nw, np.int32)
+    r = np.zeros(nw, np.int32)
+    rc = lib.orc_downsample_hash(_p(xy), n, window, x_max, y_max, mult_x, mult_y, nb, _p(rep_xy),
+                                 _p(rep_idx), _p(u), _p(r))
+    assert rc == 0
+    return rep_xy, rep_idx, u, r
+
+
+def kmeans_assign_f32(xy2, centroids, thr=50.0):
+    xy2 = np.ascontiguousarray(xy2, np.float32)
+    c = np.ascontiguousarray(centroids, np.float32)
+    n = xy2.size // 2
+    lab = np.zeros(n, np.uint8)
+    lib.orc_kmeans_assign_f32(_p(xy2), n, _p(c), c.size // 2, thr, _p(lab))
+    return lab
+
+
+def kmeans_run_xy16(xy, centroids, max_iters, thr=50.0, tol=-1.0):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    c = np.array(centroids, np.float32).copy()
+    lab = np.zeros(len(xy), np.uint8)
+    it = np.zeros(1, np.int32)
+    lib.orc_kmeans_run_xy16(_p(xy), len(xy), _p(c), c.size // 2, max_iters, thr, tol, _p(lab), _p(it))
+    return c, lab, int(it[0])
+
+
+def kmeans_run_f32(xy2, centroids, max_iters, thr=50.0, tol=-1.0):
+    xy2 = np.ascontiguousarray(xy2, np.float32)
+    c = np.array(centroids, np.float32).copy()
+    n = xy2.size // 2
+    lab = np.zeros(n, np.uint8)
+    it = np.zeros(1, np.int32)
+    lib.orc_kmeans_run_f32(_p(xy2), n, _p(c), c.size // 2, max_iters, thr, tol, _p(lab), _p(it))
+    return c, lab, int(it[0])
+
+
+def fast_detect(xy, t, W, H, slice_events=16384, margin=4, border_mode=0, first_detect=1, sae=None):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    t = np.ascontiguousarray(t, np.int64)
+    sae = np.zeros(W * H, np.int64) if sae is None else np.array(sae, np.int64).copy()
+    flags = np.zeros(len(xy), np.uint8)
+    rc = lib.orc_fast_detect(_p(xy), _p(t), len(xy), W, H, slice_events, margin, border_mode,
+                             first_detect, _p(sae), _p(flags))
+    assert rc == 0
+    return flags, sae
+
+
+def arc_test(sae, W, x, y):
+    sae = np.ascontiguousarray(sae, np.int64)
+    return lib.orc_arc_test(_p(sae), W, x, y)
+
+
+CORNER_DTYPE = np.dtype([("x", np.int32), ("y", np.int32), ("label", np.int32)])
+
+
+def filter_corners(corners_xy, W, H, box=15):
+    c = np.zeros(len(corners_xy), CORNER_DTYPE)
+    if len(corners_xy):
+        c["x"] = [p[0] for p in corners_xy]
+        c["y"] = [p[1] for p in corners_xy]
+    out = np.zeros(max(len(corners_xy), 1), CORNER_DTYPE)
+    k = lib.orc_filter_corners(_p(c), len(c), W, H, box, _p(out), len(out))
+    return out[:k]
+
+
+def corner_nms(xy, flags, W, H, slice_events=16384, box=15, cap=4096):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    flags = np.ascontiguousarray(flags, np.uint8)
+    ns = (len(xy) + slice_events - 1) // slice_events
+    out = np.zeros(ns * cap, CORNER_DTYPE)
+    counts = np.zeros(ns, np.int32)
+    rc = lib.orc_corner_nms(_p(xy), _p(flags), len(xy), slice_events, W, H, box, cap, _p(out), _p(counts))
+    return out, counts, rc
+
+
+class OracleTracker:
+    def __init__(self, cfg):
+        self.h = lib.orc_tracker_create(C.byref(cfg))
+
+    def update(self, corners: np.ndarray):
+        corners = np.ascontiguousarray(corners, CORNER_DTYPE)
+        lib.orc_tracker_update(self.h, _p(corners), len(corners))
+
+    def tracks(self, track_type, cap=65536):
+        buf = (track_type * cap)()
+        n = lib.orc_tracker_get_tracks(self.h, buf, cap)
+        return [buf[i] for i in range(min(n, cap))]
+
+    def groups(self, group_type, cap=65536):
+        buf = (group_type * cap)()
+        labels = np.zeros(cap, np.int32)
+        n = lib.orc_tracker_get_groups(self.h, buf, cap, _p(labels), cap)
+        return [buf[i] for i in range(min(n, cap))], labels
+
+    def __del__(self):
+        try:
+            lib.orc_tracker_destroy(self.h)
+        except Exception:
+            pass
+
+
+def eps_neighbours(xy, n_segs, stride, seg_counts, eps, min_pts, want_lists=True):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    total = n_segs * stride
+    counts = np.zeros(total, np.int32)
+    core = np.zeros(total, np.float64)
+    offsets = np.zeros(total + 1, np.int64)
+    sc = None if seg_counts is None else np.ascontiguousarray(seg_counts, np.int32)
+    # first pass for the list size
+    lib.orc_eps_neighbours(_p(xy), n_segs, stride, _p(sc), eps, min_pts, _p(counts), _p(core),
+                           _p(offsets), None, 0)
+    nbr = None
+    if want_lists:
+        nbr = np.zeros(max(int(offsets[-1]), 1), np.int32)
+        lib.orc_eps_neighbours(_p(xy), n_segs, stride, _p(sc), eps, min_pts, None, None,
+                               _p(offsets), _p(nbr), len(nbr))
+    return counts, core, offsets, nbr
+
+
+def dbscan(pts3, eps, min_pts, min_size=1, max_size=2**31 - 1):
+    pts3 = np.ascontiguousarray(pts3, np.float32)
+    n = pts3.shape[0]
+    lab = np.zeros(n, np.int32)
+    k = lib.orc_dbscan(_p(pts3), n, eps, min_pts, min_size, max_size, _p(lab))
+    return k, lab
+
+
+def epsilon_estimation(pts, min_pts):
+    pts = np.ascontiguousarray(pts, np.float64)
+    n, d = pts.shape
+    return lib.orc_epsilon_estimation(_p(pts), n, d, min_pts)
+
+
+def optics(pts, min_pts, eps=-1.0):
+    pts = np.ascontiguousarray(pts, np.float64)
+    n, d = pts.shape
+    order = np.zeros(n, np.int64)
+    reach = np.zeros(n, np.float64)
+    lib.orc_optics(_p(pts), n, d, min_pts, eps, _p(order), _p(reach))
+    return order, reach
+
+
+def get_cluster_indices(order, reach, thr):
+    reach = np.ascontiguousarray(reach, np.float64)
+    cl = np.zeros(len(reach), np.int32)
+    k = lib.orc_get_cluster_indices(_p(reach), len(reach), thr, _p(cl))
+    return [list(np.asarray(order)[cl == c]) for c in range(k)]
+
+
+def radius_search(pts, q, r):
+    pts = np.ascontiguousarray(pts, np.float64)
+    q = np.ascontiguousarray(q, np.float64)
+    n, d = pts.shape
+    out = np.zeros(n, np.int64)
+    k = lib.orc_radius_search(_p(pts), n, d, _p(q), r, _p(out), n)
+    return list(out[:k])

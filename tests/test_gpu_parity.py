@@ -1,0 +1,382 @@
+"""GPU parity tests: every HIP entry point through the C ABI against the oracle (CPU restatement)
+on the same seeded inputs.  Bar: bit-exact for integer / index / label work and for the fp32
+tracker (identical operation order), 1e-4 for float-input k-means centroids."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+W_SMALL, H_SMALL = 346, 260
+
+
+def dev(ecc, a):
+    return ecc.DeviceArray.from_numpy(np.ascontiguousarray(a))
+
+
+# ------------------------------------------------------------------------------ downsample
+@pytest.mark.parametrize("n,window,seed,wh", [
+    (200_000, 8192, 1, (346, 260)),
+    (123_457, 8192, 2, (1280, 720)),
+    (50_001, 1000, 3, (1280, 720)),      # ragged last window, window not a multiple of 1024
+    (70_000, 16384, 4, (346, 260)),
+    (8192, 8192, 5, (1400, 800)),        # coordinates beyond the inclusive 1280/720 bounds (:56)
+    (1, 8192, 6, (346, 260)),
+])
+def test_downsample_matches_oracle(ecc, orc, gpu, n, window, seed, wh):
+    xy, _, _ = ecc.gen_events(n, seed=seed, width=wh[0], height=wh[1])
+    cfg = ecc.hash_cfg(window=window)
+    d_xy = dev(ecc, xy)
+    rep_xy, rep_idx, uniq, rep, nw = gpu.downsample_hash(d_xy, n, cfg)
+    gpu.sync()
+    o_xy, o_idx, o_u, o_r = orc.downsample_hash(xy, window=window)
+    g_u, g_r = uniq.numpy()[:nw], rep.numpy()[:nw]
+    assert (g_u == o_u).all() and (g_r == o_r).all()
+    gx, gi = rep_xy.numpy(), rep_idx.numpy()
+    for w in range(nw):
+        k = o_u[w]
+        sl = slice(w * window, w * window + k)
+        assert (gx[sl] == o_xy[sl]).all(), f"window {w} representatives differ"
+        assert (gi[sl] == o_idx[sl]).all(), f"window {w} representative indices differ"
+
+
+def test_downsample_full_size_properties(ecc, gpu):
+    """10 M events (BASELINE config C2) — size-independent properties: every representative is
+    the first event of its bucket, buckets are distinct, counts agree with the outputs."""
+    n = 10_000_000
+    xy, _, _ = ecc.gen_events(n, seed=11, width=1280, height=720)
+    d_xy = dev(ecc, xy)
+    rep_xy, rep_idx, uniq, rep, nw = gpu.downsample_hash(d_xy, n)
+    gpu.sync()
+    u, r, rx, ri = uniq.numpy(), rep.numpy(), rep_xy.numpy(), rep_idx.numpy()
+    assert nw == 1221 and (u <= 8192).all() and (r <= u).all()
+    rng = np.random.default_rng(0)
+    for w in rng.choice(nw, 24, replace=False):
+        lo = w * 8192
+        ev = xy[lo:lo + 8192]
+        x, y = ev & 0xFFFF, ev >> 16
+        h = (x.astype(np.int64) * 1619 + y.astype(np.int64) * 31) % 8192
+        first = {}
+        cnt = {}
+        for i, b in enumerate(h):
+            first.setdefault(int(b), i)
+            cnt[int(b)] = cnt.get(int(b), 0) + 1
+        k = u[w]
+        assert k == len(first) and r[w] == sum(1 for c in cnt.values() if c >= 2)
+        exp_idx = np.array(sorted(first.values()), np.int64) + lo
+        assert (ri[lo:lo + k] == exp_idx).all()
+        assert (rx[lo:lo + k] == xy[exp_idx]).all()
+
+
+# ------------------------------------------------------------------------------ k-means
+def _reps(ecc, orc, n=400_000, seed=7):
+    xy, _, _ = ecc.gen_events(n, seed=seed)
+    o_xy, _, o_u, _ = orc.downsample_hash(xy)
+    return xy, o_xy, o_u
+
+
+def _init_centroids(k, seed=0, w=W_SMALL, h=H_SMALL):
+    rng = np.random.default_rng(seed)
+    return np.stack([rng.uniform(0, w, k), rng.uniform(0, h, k)], 1).astype(np.float32).ravel()
+
+
+@pytest.mark.parametrize("k,iters,tol", [(16, 10, -1.0), (8, 20, 1e-3), (64, 3, -1.0), (1, 4, -1.0)])
+def test_kmeans_xy16_segmented_matches_oracle(ecc, orc, gpu, k, iters, tol):
+    xy, rep_xy, u = _reps(ecc, orc)
+    nw = len(u)
+    dense = np.concatenate([rep_xy[w * 8192: w * 8192 + u[w]] for w in range(nw)])
+    c0 = _init_centroids(k)
+    o_c, o_lab, o_it = orc.kmeans_run_xy16(dense, c0, iters, 50.0, tol)
+    d_rep = dev(ecc, rep_xy)
+    d_cnt = dev(ecc, u)
+    d_c = dev(ecc, c0)
+    d_lab = ecc.DeviceArray(len(rep_xy), np.uint8)
+    d_it = ecc.DeviceArray(1, np.int32)
+    cfg = ecc.kmeans_cfg(k=k, max_iters=iters, tol=tol)
+    gpu.kmeans_xy16(d_rep, nw, 8192, d_cnt, d_c, cfg, d_lab, d_it)
+    gpu.sync()
+    g_c = d_c.numpy()
+    assert d_it.numpy()[0] == o_it
+    assert np.array_equal(g_c.view(np.uint32), o_c.view(np.uint32)), (g_c, o_c)
+    g_lab = d_lab.numpy()
+    g_dense = np.concatenate([g_lab[w * 8192: w * 8192 + u[w]] for w in range(nw)])
+    assert (g_dense == o_lab).all()
+
+
+def test_kmeans_xy16_dense_matches_oracle(ecc, orc, gpu):
+    xy, _, _ = ecc.gen_events(300_001, seed=9)
+    c0 = _init_centroids(16, 3)
+    o_c, o_lab, o_it = orc.kmeans_run_xy16(xy, c0, 6)
+    d_c = dev(ecc, c0)
+    d_lab = ecc.DeviceArray(len(xy), np.uint8)
+    gpu.kmeans_xy16(dev(ecc, xy), 1, len(xy), None, d_c, ecc.kmeans_cfg(k=16, max_iters=6, tol=-1.0), d_lab)
+    gpu.sync()
+    assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
+    assert (d_lab.numpy() == o_lab).all()
+
+
+def test_kmeans_f32_matches_oracle(ecc, orc, gpu):
+    rng = np.random.default_rng(5)
+    pts = np.concatenate([rng.normal(m, 6.0, (20000, 2)) for m in ([40, 40], [120, 60], [200, 180], [300, 90])])
+    pts = pts.astype(np.float32).ravel()
+    c0 = np.array([30, 30, 110, 70, 210, 170, 290, 100], np.float32)
+    o_c, o_lab, _ = orc.kmeans_run_f32(pts, c0, 8)
+    d_c = dev(ecc, c0)
+    d_lab = ecc.DeviceArray(len(pts) // 2, np.uint8)
+    gpu.kmeans_f32(dev(ecc, pts), len(pts) // 2, d_c, ecc.kmeans_cfg(k=4, max_iters=8, tol=-1.0), d_lab)
+    gpu.sync()
+    assert np.allclose(d_c.numpy(), o_c, atol=1e-4, rtol=0)   # north_star tolerance for centroids
+    assert (d_lab.numpy() != o_lab).mean() < 1e-4
+
+
+def test_kmeans_assign_ties_and_threshold(ecc, orc, gpu):
+    """assign_to_centers semantics: first minimum wins, strict < threshold 50, 255 = none."""
+    c = np.array([10, 10, 20, 10, 10, 10, 100, 100], np.float32)  # centres 0 and 2 coincide
+    pts = np.array([[15, 10], [10, 10], [60, 10], [59.99, 10], [100, 149.99], [100, 150], [17.5, 10]], np.float32)
+    rng = np.random.default_rng(1)
+    pts = np.concatenate([pts, rng.uniform(-20, 200, (100000, 2)).astype(np.float32)]).ravel()
+    o = orc.kmeans_assign_f32(pts, c)
+    d_lab = ecc.DeviceArray(len(pts) // 2, np.uint8)
+    gpu.kmeans_assign_f32(dev(ecc, pts), len(pts) // 2, dev(ecc, c), 4, 50.0, d_lab)
+    gpu.sync()
+    g = d_lab.numpy()
+    assert (g == o).all()
+    assert list(g[:7]) == [0, 0, 255, 1, 3, 255, 1]
+
+
+# ------------------------------------------------------------------------------ SAE + arc corners
+def _fast_gpu(ecc, gpu, xy, t, W, H, border_mode=0, first_detect=1, sae0=None, slice_events=16384):
+    cfg = ecc.corner_cfg(width=W, height=H, border_mode=border_mode, first_detect_slice=first_detect,
+                         slice_events=slice_events)
+    sae = dev(ecc, np.zeros(W * H, np.int64) if sae0 is None else sae0)
+    flags = ecc.DeviceArray(len(xy), np.uint8)
+    gpu.fast_detect(dev(ecc, xy), dev(ecc, t), len(xy), cfg, sae, flags)
+    assert gpu.fast_detect_status() == 0
+    return flags.numpy(), sae.numpy()
+
+
+@pytest.mark.parametrize("n,wh,mode,seed,slice_events", [
+    (600_000, (346, 260), 0, 1, 16384),
+    (600_000, (346, 260), 1, 2, 16384),
+    (700_000, (1280, 720), 0, 3, 16384),
+    (300_000, (640, 480), 1, 4, 16384),
+    (100_000, (346, 260), 0, 5, 1000),   # many slices per group, ragged tail
+])
+def test_fast_detect_matches_oracle(ecc, orc, gpu, n, wh, mode, seed, slice_events):
+    W, H = wh
+    xy, t, _ = ecc.gen_events(n, seed=seed, width=W, height=H)
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H, slice_events=slice_events, border_mode=mode)
+    g_flags, g_sae = _fast_gpu(ecc, gpu, xy, t, W, H, border_mode=mode, slice_events=slice_events)
+    assert o_flags.sum() > 0, "synthetic stream should contain corners"
+    assert (g_flags == o_flags).all(), f"{(g_flags != o_flags).sum()} corner labels differ"
+    assert (g_sae == o_sae).all()
+
+
+def test_fast_detect_stream_continuation(ecc, orc, gpu):
+    """Two batches with the SAE carried over == one batch (stream hand-off / sharding)."""
+    W, H = W_SMALL, H_SMALL
+    xy, t, _ = ecc.gen_events(32768 * 9, seed=8)
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H)
+    cut = 32768 * 5
+    f1, s1 = _fast_gpu(ecc, gpu, xy[:cut], t[:cut], W, H)
+    f2, s2 = _fast_gpu(ecc, gpu, xy[cut:], t[cut:], W, H, first_detect=0, sae0=s1)
+    assert (np.concatenate([f1, f2]) == o_flags).all()
+    assert (s2 == o_sae).all()
+
+
+def test_fast_detect_rejects_decreasing_time(ecc, gpu):
+    xy, t, _ = ecc.gen_events(40000, seed=2)
+    t = t.copy()
+    t[20000] = t[19999] - 5
+    cfg = ecc.corner_cfg(width=W_SMALL, height=H_SMALL)
+    sae = ecc.DeviceArray.zeros(W_SMALL * H_SMALL, np.int64)
+    flags = ecc.DeviceArray(len(xy), np.uint8)
+    gpu.fast_detect(dev(ecc, xy), dev(ecc, t), len(xy), cfg, sae, flags)
+    assert gpu.fast_detect_status() == ecc.ERR_UNSORTED_TIME
+
+
+def test_arc_test_known_patterns(ecc, orc, gpu):
+    """Hand-built SAE patterns around one event (checked by the literal reference loop in the
+    oracle): a contiguous fresh arc on both circles is a corner; gaps / ties / too long are not."""
+    W, H = 64, 64
+    c3 = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3), (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+    c4 = [(0, 4), (1, 4), (2, 3), (3, 2), (4, 1), (4, 0), (4, -1), (3, -2), (2, -3), (1, -4), (0, -4), (-1, -4), (-2, -3), (-3, -2), (-4, -1), (-4, 0), (-4, 1), (-3, 2), (-2, 3), (-1, 4)]
+    cx, cy = 20, 20
+    cases = []
+    for arc3, arc4, expect in [(range(0, 4), range(0, 5), 1), (range(2, 8), range(3, 11), 1),
+                               ([0, 1, 3, 4], range(0, 5), 0), (range(0, 7), range(0, 5), 0),
+                               (range(0, 2), range(0, 5), 0), (range(14, 18), range(18, 23), 1),
+                               (range(0, 4), range(0, 9), 0)]:
+        cases.append((arc3, arc4, expect))
+    xs, ts = [], []
+    tbase = 1000
+    for ci, (arc3, arc4, expect) in enumerate(cases):
+        sae = np.zeros((H, W), np.int64)
+        for k in arc3:
+            dy, dx = c3[k % 16]
+            sae[cy + dy, cx + dx] = 500
+        for k in arc4:
+            dy, dx = c4[k % 20]
+            sae[cy + dy, cx + dx] = 500
+        assert orc.arc_test(sae.ravel(), W, cx, cy) == expect, ci
+    # same patterns through the GPU pipeline: slice 0 paints the pattern, slice 1 holds the event
+    for ci, (arc3, arc4, expect) in enumerate(cases):
+        pts = set()
+        for k in arc3:
+            dy, dx = c3[k % 16]
+            pts.add((cx + dx, cy + dy))
+        for k in arc4:
+            dy, dx = c4[k % 20]
+            pts.add((cx + dx, cy + dy))
+        pts = sorted(pts)
+        S = 64
+        ev_xy = [ecc.pack_xy(x, y) for x, y in pts] + [ecc.pack_xy(60, 60)] * (S - len(pts))
+        ev_t = [500] * S
+        ev_xy += [ecc.pack_xy(cx, cy)] + [ecc.pack_xy(2, 2)] * (S - 1)
+        ev_t += [600] * S
+        xy = np.array(ev_xy, np.uint32)
+        t = np.array(ev_t, np.int64)
+        o_flags, _ = orc.fast_detect(xy, t, W, H, slice_events=S)
+        g_flags, _ = _fast_gpu(ecc, gpu, xy, t, W, H, slice_events=S)
+        assert (g_flags == o_flags).all()
+        # the centre event itself sees its own pixel as the newest value, not on either circle
+        assert g_flags[S] == expect, ci
+
+
+# ------------------------------------------------------------------------------ NMS
+def test_nms_matches_oracle(ecc, orc, gpu):
+    W, H = W_SMALL, H_SMALL
+    xy, t, _ = ecc.gen_events(1_000_000, seed=21)
+    o_flags, _ = orc.fast_detect(xy, t, W, H)
+    o_out, o_cnt, rc = orc.corner_nms(xy, o_flags, W, H)
+    assert rc == 0 and o_cnt.sum() > 0
+    ns = len(o_cnt)
+    cap = 4096
+    d_out = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE)
+    d_cnt = ecc.DeviceArray(ns, np.int32)
+    gpu.corner_nms(dev(ecc, xy), dev(ecc, o_flags), len(xy), 16384, W, H, 15, cap, d_out, d_cnt)
+    gpu.sync()
+    g_cnt = d_cnt.numpy()
+    assert (g_cnt == o_cnt).all()
+    g_out = d_out.numpy()
+    for s in range(ns):
+        k = o_cnt[s]
+        assert (g_out[s * cap: s * cap + k] == o_out[s * cap: s * cap + k]).all(), s
+
+
+def test_nms_dense_candidates(ecc, orc, gpu):
+    """Many overlapping candidates in one slice (within-chunk dependency resolution)."""
+    W, H = 200, 200
+    rng = np.random.default_rng(4)
+    n = 16384
+    x = rng.integers(4, 196, n)
+    y = rng.integers(4, 196, n)
+    xy = ecc.pack_xy(x, y)
+    flags = (rng.random(n) < 0.7).astype(np.uint8)
+    o_out, o_cnt, _ = orc.corner_nms(xy, flags, W, H, slice_events=n)
+    d_out = ecc.DeviceArray(4096, ecc.CORNER_DTYPE)
+    d_cnt = ecc.DeviceArray(1, np.int32)
+    gpu.corner_nms(dev(ecc, xy), dev(ecc, flags), n, n, W, H, 15, 4096, d_out, d_cnt)
+    gpu.sync()
+    k = o_cnt[0]
+    assert d_cnt.numpy()[0] == k
+    assert (d_out.numpy()[:k] == o_out[:k]).all()
+
+
+# ------------------------------------------------------------------------------ tracker
+def _track_key(tr):
+    return (tr.x, tr.y, tr.label, tr.frame_count, tr.is_matched, tr.frames_since_last_detection,
+            tr.hist_len, tuple(tr.hist_x[:tr.hist_len]), tuple(tr.hist_y[:tr.hist_len]),
+            np.float32(tr.vx).view(np.uint32), np.float32(tr.vy).view(np.uint32),
+            np.float32(tr.dir_cur_x).view(np.uint32), np.float32(tr.dir_cur_y).view(np.uint32),
+            tr.group_id)
+
+
+def test_tracker_matches_oracle(ecc, orc, gpu):
+    W, H = W_SMALL, H_SMALL
+    xy, t, _ = ecc.gen_events(16384 * 48, seed=31)
+    o_flags, _ = orc.fast_detect(xy, t, W, H)
+    cap = 4096
+    o_out, o_cnt, _ = orc.corner_nms(xy, o_flags, W, H, cap=cap)
+    ns = len(o_cnt)
+    otr = orc.OracleTracker(ecc.tracker_cfg())
+    gtr = ecc.Tracker(gpu)
+    d_out, d_cnt = dev(ecc, o_out), dev(ecc, o_cnt)
+    # feed in two device launches (16 + rest slices) to exercise state carry-over
+    for s in range(ns):
+        otr.update(o_out[s * cap: s * cap + o_cnt[s]])
+    sub = 16
+    gtr.update(d_out, d_cnt, sub, cap)
+    rest_out = dev(ecc, o_out[sub * cap:])
+    rest_cnt = dev(ecc, o_cnt[sub:])
+    gtr.update(rest_out, rest_cnt, ns - sub, cap)
+    gpu.sync()
+    assert gtr.status() == 0
+    o_tr = otr.tracks(ecc.Track)
+    g_tr = gtr.tracks()
+    assert len(o_tr) > 0 and len(g_tr) == len(o_tr)
+    for a, b in zip(g_tr, o_tr):
+        assert _track_key(a) == _track_key(b)
+    og, ol = otr.groups(ecc.Group)
+    gg, gl = gtr.groups()
+    assert len(gg) == len(og)
+    for a, b in zip(gg, og):
+        assert (a.id, a.n_labels, a.first_label_offset) == (b.id, b.n_labels, b.first_label_offset)
+        for f in ("avg_vx", "avg_vy", "cx", "cy", "radius"):
+            assert np.float32(getattr(a, f)) == np.float32(getattr(b, f)), f
+    nl = sum(g.n_labels for g in og)
+    assert (gl[:nl] == ol[:nl]).all()
+
+
+# ------------------------------------------------------------------------------ eps-neighbourhoods
+@pytest.mark.parametrize("eps,min_pts", [(10.0, 2), (20.0, 20), (1.01, 1), (3.5, 64)])
+def test_eps_neighbourhoods_match_oracle(ecc, orc, gpu, eps, min_pts):
+    xy, _, _ = ecc.gen_events(60_000, seed=41)
+    rep_xy, _, u, _ = orc.downsample_hash(xy)
+    nw = len(u)
+    o_cnt, o_core, o_off, o_nbr = orc.eps_neighbours(rep_xy, nw, 8192, u, eps, min_pts)
+    d_xy, d_u = dev(ecc, rep_xy), dev(ecc, u)
+    d_cnt = ecc.DeviceArray(nw * 8192, np.int32)
+    d_core = ecc.DeviceArray(nw * 8192, np.float64)
+    gpu.eps_counts(d_xy, nw, 8192, d_u, eps, min_pts, d_cnt, d_core)
+    d_off = ecc.DeviceArray(nw * 8192 + 1, np.int64)
+    cap = int(o_off[-1]) + 16
+    d_nbr = ecc.DeviceArray(cap, np.int32)
+    gpu.eps_lists(d_xy, nw, 8192, d_u, eps, d_cnt, d_off, d_nbr, cap)
+    gpu.sync()
+    g_cnt, g_core, g_off = d_cnt.numpy(), d_core.numpy(), d_off.numpy()
+    for w in range(nw):
+        sl = slice(w * 8192, w * 8192 + u[w])
+        assert (g_cnt[sl] == o_cnt[sl]).all()
+        assert np.array_equal(g_core[sl], o_core[sl])
+    assert (g_off == o_off).all()
+    assert (d_nbr.numpy()[:o_off[-1]] == o_nbr[:o_off[-1]]).all()
+
+
+def test_eps_duplicates_and_kdtree_kat(ecc, gpu):
+    """kd-tree KATs of OPT/test/test_main.cpp:595-720 (radius 1.01), 1-D cases mapped onto the
+    x axis (+4), including the duplicate-point case."""
+    import json
+    from pathlib import Path
+    kat = json.loads((Path(__file__).parent / "golden" / "optics_kat.json").read_text())
+    for name, shift in (("kdtree_1d", 4), ("kdtree_1d_dup", 1), ("kdtree_2d", 0)):
+        case = kat[name]
+        pts = np.array(case["points"], np.float64)
+        if pts.shape[1] == 1:
+            pts = np.concatenate([pts + shift, np.zeros_like(pts)], 1)
+        xy = ecc.pack_xy(pts[:, 0].astype(np.int64), pts[:, 1].astype(np.int64))
+        n = len(xy)
+        d_cnt = ecc.DeviceArray(n, np.int32)
+        gpu.eps_counts(dev(ecc, xy), 1, n, None, case["radius"], 1, d_cnt, None)
+        d_off = ecc.DeviceArray(n + 1, np.int64)
+        d_nbr = ecc.DeviceArray(n * n, np.int32)
+        gpu.eps_lists(dev(ecc, xy), 1, n, None, case["radius"], d_cnt, d_off, d_nbr, n * n)
+        gpu.sync()
+        off, nbr = d_off.numpy(), d_nbr.numpy()
+        for q, expected in case["queries"]:
+            q = np.array(q, np.float64)
+            if len(q) == 1:
+                q = np.array([q[0] + shift, 0.0])
+            i = int(np.where((pts == q).all(1))[0][0])
+            assert list(nbr[off[i]:off[i + 1]]) == expected, (name, q)
