@@ -217,3 +217,20 @@ ECC_API int ecc_event_elapsed_ms(float *ms, void *start, void *stop) {
     if (hipEventSynchronize(reinterpret_cast<hipEvent_t>(stop)) != hipSuccess) return ECC_ERR_HIP;
     ECC_RT(hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(start), reinterpret_cast<hipEvent_t>(stop)));
 }
+
+namespace {
+__global__ void util_sqrt_kernel(const float *__restrict__ in, float *__restrict__ out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = ecc::sqrt_rn(in[i]);
+}
+}  // namespace
+
+ECC_API int ecc_util_sqrt_f32(ecc_ctx *ctx, const float *in, float *out, int64_t n, ecc_stream_t stream) {
+    if (!ctx || n < 0 || (n > 0 && (!in || !out))) return ECC_ERR_INVALID;
+    if (n == 0) return ECC_OK;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(util_sqrt_kernel, dim3((unsigned)blocks), dim3(256), 0, ecc::as_stream(stream), in, out, n);
+    ECC_CHECK_LAUNCH(ctx, "util_sqrt_kernel");
+    return ECC_OK;
+}

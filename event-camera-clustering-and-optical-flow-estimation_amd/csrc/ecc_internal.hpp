@@ -78,6 +78,25 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 __host__ __device__ inline int xy_x(uint32_t v) { return (int)(v & 0xffffu); }
 __host__ __device__ inline int xy_y(uint32_t v) { return (int)(v >> 16); }
 
+// Correctly rounded fp32 square root.  On gfx950 `__fsqrt_rn` may lower to the bare
+// v_sqrt_f32 (<= 1 ulp), which breaks bit-exactness against IEEE sqrtf on the host.  This is
+// the hardware approximation followed by the exact one-ulp correction with FMA residuals
+// (x - r'*r for the two neighbours r' of r), with scaling for tiny inputs.
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const bool tiny = x < 0x1p-96f;
+    const float xs = tiny ? x * 0x1p+32f : x;
+    float r = __builtin_amdgcn_sqrtf(xs);
+    const float rm = __int_as_float(__float_as_int(r) - 1);
+    const float rp = __int_as_float(__float_as_int(r) + 1);
+    const float em = __builtin_fmaf(-rm, r, xs);
+    const float ep = __builtin_fmaf(-rp, r, xs);
+    r = (em <= 0.0f) ? rm : r;
+    r = (ep > 0.0f) ? rp : r;
+    r = tiny ? r * 0x1p-16f : r;
+    // +-0, +inf and NaN: IEEE results
+    return (xs == 0.0f || !(xs < __builtin_inff())) ? __builtin_amdgcn_sqrtf(x) : r;
+}
+
 // Wave64 helpers (gfx950: wavefront = 64 lanes).
 __device__ inline int lane_id() { return (int)__lane_id(); }
 

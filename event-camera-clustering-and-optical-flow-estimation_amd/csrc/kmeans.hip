@@ -17,10 +17,8 @@
 //     device-side `done` flag that makes the remaining queued iterations no-ops (no host
 //     sync per iteration).
 // Assignment arithmetic (canonical, shared with oracle/oracle.cpp assign_one): fp32
-// d2 = dx*dx + dy*dy (no FMA contraction), argmin over sqrtf(d2) with the reference's
-// first-minimum rule.  sqrtf is taken once for the minimum and only re-evaluated for the
-// (rare) centres whose d2 lies within 2^-20 relative of it, which yields exactly the index
-// the reference's per-centre sqrt loop selects.
+// d2 = dx*dx + dy*dy (no FMA contraction), correctly rounded sqrt (ecc::sqrt_rn), the
+// reference's first-minimum rule; sqrt only where d2 improves (see assign_point).
 // Algorithmic bytes: 4 B/point/iteration (packed u16 xy) + 1 B/point for the final labels.
 #include "ecc_internal.hpp"
 
@@ -36,26 +34,26 @@ struct KmState {
     int32_t iters;
 };
 
-// first-minimum argmin over sqrtf(d2) with threshold; c in LDS as (x,y) pairs.
+// assign_to_centers (KM/assign_to_centers.cl:10-27): the FIRST centre whose fp32 distance
+// sqrtf(dx*dx + dy*dy) is strictly below the running best (initially the threshold).  The
+// sqrt is only evaluated when d2 drops below the pruning bound pb (a centre with d2 >= pb has
+// sqrt >= the current best, so it can never be strictly closer) — about ln(k)+1 square roots
+// per point instead of k, with exactly the reference's selection.
 __device__ __forceinline__ uint32_t assign_point(float px, float py, const float2 *__restrict__ c,
                                                  int k, float thr) {
-    float m = __builtin_inff();
+    uint32_t best = 255u;
+    float best_s = thr, pb = __builtin_inff();
     for (int i = 0; i < k; ++i) {
         const float2 ci = c[i];
         const float dx = __fsub_rn(ci.x, px), dy = __fsub_rn(ci.y, py);
         const float d2 = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
-        m = fminf(m, d2);
+        if (d2 < pb) {
+            pb = d2;
+            const float s = ecc::sqrt_rn(d2);
+            if (s < best_s) { best_s = s; best = (uint32_t)i; }
+        }
     }
-    const float s = __fsqrt_rn(m);
-    if (!(s < thr)) return 255u;
-    const float bound = __fadd_rn(m, __fmul_rn(m, 0x1p-20f));
-    for (int i = 0; i < k; ++i) {
-        const float2 ci = c[i];
-        const float dx = __fsub_rn(ci.x, px), dy = __fsub_rn(ci.y, py);
-        const float d2 = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
-        if (d2 <= bound && __fsqrt_rn(d2) == s) return (uint32_t)i;
-    }
-    return 255u;  // unreachable: the minimum itself satisfies the test
+    return best;
 }
 
 // Segment geometry: segment s holds cnt(s) points at base s*stride.

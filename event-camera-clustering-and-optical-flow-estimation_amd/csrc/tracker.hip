@@ -53,10 +53,10 @@ __device__ __forceinline__ F2 add(F2 a, F2 b) { return F2{__fadd_rn(a.x, b.x), _
 __device__ __forceinline__ F2 mul(F2 a, float s) { return F2{__fmul_rn(a.x, s), __fmul_rn(a.y, s)}; }
 __device__ __forceinline__ float dist(F2 a, F2 b) {  // :217-222
     const float dx = __fsub_rn(a.x, b.x), dy = __fsub_rn(a.y, b.y);
-    return __fsqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
+    return ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
 }
 __device__ __forceinline__ float norm(F2 a) {
-    return __fsqrt_rn(__fadd_rn(__fmul_rn(a.x, a.x), __fmul_rn(a.y, a.y)));
+    return ecc::sqrt_rn(__fadd_rn(__fmul_rn(a.x, a.x), __fmul_rn(a.y, a.y)));
 }
 
 __device__ __forceinline__ void push_hist(DevTrack &t, int history) {  // :224-231

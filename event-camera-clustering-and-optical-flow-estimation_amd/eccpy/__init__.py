@@ -113,6 +113,10 @@ _sigs = {
     "ecc_event_destroy": (C.c_int, [P]),
     "ecc_event_record": (C.c_int, [P, P]),
     "ecc_event_elapsed_ms": (C.c_int, [C.POINTER(C.c_float), P, P]),
+    "ecc_ctx_set_timing": (C.c_int, [P, C.c_int]),
+    "ecc_ctx_timing_reset": (C.c_int, [P]),
+    "ecc_ctx_timing_report": (C.c_int, [P, C.c_char_p, C.c_size_t]),
+    "ecc_util_sqrt_f32": (C.c_int, [P, P, P, i64, P]),
     "ecc_hash_cfg_default": (None, [C.POINTER(HashCfg)]),
     "ecc_downsample_hash": (C.c_int, [P, P, i64, C.POINTER(HashCfg), P, P, P, P, P]),
     "ecc_kmeans_cfg_default": (None, [C.POINTER(KmeansCfg)]),
@@ -136,13 +140,12 @@ _sigs = {
     "ecc_eps_total": (C.c_int, [P, P, i64, C.POINTER(i64), P]),
     "ecc_gen_cfg_default": (None, [C.POINTER(GenCfg)]),
     "ecc_gen_events": (C.c_int, [C.POINTER(GenCfg), i64, i64, P, P, P]),
+    "ecc_fast_detect_status": (C.c_int, [P, P]),
     "ecc_read_csv": (i64, [C.c_char_p, P, P, P, i64]),
     "ecc_count_csv": (i64, [C.c_char_p]),
 }
 for _name, (_res, _args) in _sigs.items():
-    _f = getattr(lib, _name, None)
-    if _f is None:
-        continue
+    _f = getattr(lib, _name)  # every bound symbol must exist (fail loudly on a stale build)
     _f.restype = _res
     _f.argtypes = _args
 

@@ -81,6 +81,11 @@ int ecc_ctx_set_timing(ecc_ctx *ctx, int enable);
 int ecc_ctx_timing_reset(ecc_ctx *ctx);
 int ecc_ctx_timing_report(ecc_ctx *ctx, char *buf, size_t cap);
 
+/* Numerics self-check: out[i] = correctly rounded fp32 sqrt(in[i]) as used by every bit-exact
+ * kernel of this library (device pointers).  Lets tests pin the device arithmetic against
+ * IEEE sqrtf on the host. */
+int ecc_util_sqrt_f32(ecc_ctx *ctx, const float *in, float *out, int64_t n, ecc_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * 1. Hash-map downsample
  * Reference: __kernel process_coordinates(input_coords, repeated_coords, unique_coords,

@@ -15,6 +15,27 @@ def dev(ecc, a):
     return ecc.DeviceArray.from_numpy(np.ascontiguousarray(a))
 
 
+# ------------------------------------------------------------------------------ numerics
+def test_device_sqrt_is_correctly_rounded(ecc, gpu):
+    """ecc::sqrt_rn (used by k-means, tracker) == IEEE sqrtf for random and edge inputs."""
+    rng = np.random.default_rng(0)
+    parts = [rng.uniform(0, 1e5, 2_000_000), rng.integers(0, 1 << 20, 1_000_000),
+             np.exp(rng.uniform(-80, 80, 1_000_000)), (np.arange(1, 200000) ** 2),
+             np.array([0.0, np.inf, 1e-40, 1e-45, 2.0 ** -100, 3.4e38])]
+    x = np.concatenate([p.astype(np.float32) for p in parts])
+    # also the neighbours of exact squares (where rounding decisions are tight)
+    sq = (np.arange(1, 100000, dtype=np.float32) ** 2)
+    x = np.concatenate([x, np.nextafter(sq, np.float32(np.inf)), np.nextafter(sq, np.float32(0))]).astype(np.float32)
+    d_in = dev(ecc, x)
+    d_out = ecc.DeviceArray(len(x), np.float32)
+    ecc.check(ecc.lib.ecc_util_sqrt_f32(gpu.ctx, d_in.ptr, d_out.ptr, len(x), gpu.stream))
+    gpu.sync()
+    got = d_out.numpy()
+    ref = np.sqrt(x)
+    bad = np.nonzero(got.view(np.uint32) != ref.view(np.uint32))[0]
+    assert len(bad) == 0, (x[bad[:5]], got[bad[:5]], ref[bad[:5]])
+
+
 # ------------------------------------------------------------------------------ downsample
 @pytest.mark.parametrize("n,window,seed,wh", [
     (200_000, 8192, 1, (346, 260)),
@@ -142,7 +163,7 @@ def test_kmeans_assign_ties_and_threshold(ecc, orc, gpu):
     gpu.sync()
     g = d_lab.numpy()
     assert (g == o).all()
-    assert list(g[:7]) == [0, 0, 255, 1, 3, 255, 1]
+    assert list(g[:7]) == [0, 0, 1, 1, 3, 255, 1]
 
 
 # ------------------------------------------------------------------------------ SAE + arc corners

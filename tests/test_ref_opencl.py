@@ -1,0 +1,71 @@
+"""Pinning the oracle against the REFERENCE ITSELF: the reference's own OpenCL kernels
+(coordinate_processor.cl, assign_to_centers.cl), compiled unmodified from /root/reference into
+oracle/_ref/ by oracle/ref/Makefile, executed on the GPU box's OpenCL device by
+oracle/ref/ref_harness.c.  Compares the reference kernel's outputs with the oracle (and so,
+transitively, with the HIP path that test_gpu_parity.py checks against the oracle)."""
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+REF = Path(__file__).resolve().parent.parent / "oracle" / "_ref"
+HARNESS = REF / "ref_harness"
+
+
+def _need_ref():
+    if not HARNESS.exists():
+        pytest.skip("oracle/_ref not built (reference tree absent where the repo was built)")
+
+
+def _run(args, tmp_path):
+    r = subprocess.run([str(HARNESS)] + [str(a) for a in args], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.parametrize("seed,n,wh", [(1, 8192, (346, 260)), (2, 8192, (1280, 720)), (3, 5000, (1400, 800)), (4, 1, (346, 260))])
+def test_reference_process_coordinates_pins_oracle(ecc, orc, tmp_path, seed, n, wh):
+    """Unique/repeated counts are deterministic in the reference kernel; the representative
+    chosen per bucket is a race (Q2), so the reference's set of occupied buckets is compared and
+    each of its representatives is checked to be an event of that bucket."""
+    _need_ref()
+    xy, _, _ = ecc.gen_events(n, seed=seed, width=wh[0], height=wh[1])
+    x, y = ecc.unpack_xy(xy)
+    pairs = np.stack([x, y], 1).astype(np.int32)
+    (tmp_path / "in.i32").write_bytes(pairs.tobytes())
+    _run(["downsample", REF / "coordinate_processor.gfx950.co", tmp_path / "in.i32", tmp_path / "out.i32"], tmp_path)
+    out = np.frombuffer((tmp_path / "out.i32").read_bytes(), np.int32)
+    ref_unique, ref_repeated = int(out[0]), int(out[1])
+    ref_reps = out[2:2 + 2 * ref_unique].reshape(-1, 2)
+    o_xy, o_idx, o_u, o_r = orc.downsample_hash(xy)
+    assert ref_unique == o_u[0] and ref_repeated == o_r[0]
+    bucket = lambda xx, yy: (np.asarray(xx, np.int64) * 1619 + np.asarray(yy, np.int64) * 31) % 8192
+    ref_b = bucket(ref_reps[:, 0], ref_reps[:, 1])
+    ox, oy = ecc.unpack_xy(o_xy[:o_u[0]])
+    assert sorted(ref_b.tolist()) == sorted(bucket(ox, oy).tolist())
+    valid = set(zip(x.tolist(), y.tolist()))
+    assert all((int(a), int(b)) in valid for a, b in ref_reps)
+
+
+def test_reference_assign_to_centers_pins_oracle(ecc, orc, tmp_path):
+    """assign_to_centers is deterministic: the reference kernel's label (2c or 255) must equal
+    the oracle's (c or 255) for every point — pins the distance/threshold/tie semantics,
+    including the device's OpenCL length() against IEEE sqrtf(dx*dx + dy*dy)."""
+    _need_ref()
+    rng = np.random.default_rng(7)
+    cen = np.array([1, 1, 10, 10, 20, 20, 30, 30, 50, 50, 60, 60, 70, 70, 80, 80], np.float32)  # assign_to_centers2.c:131
+    n = 256 * 400
+    pts = np.concatenate([
+        (np.arange(4096) % 100).astype(np.float32).reshape(-1, 2),        # the reference demo data (:123-129)
+        rng.uniform(-30, 130, (n - 2048 - 4096, 2)).astype(np.float32),
+        rng.integers(-20, 120, (4096, 2)).astype(np.float32),              # integer pixels: exact ties
+    ])
+    (tmp_path / "in.f32").write_bytes(pts.astype(np.float32).tobytes())
+    (tmp_path / "c.f32").write_bytes(cen.tobytes())
+    _run(["assign", REF / "assign_to_centers.gfx950.co", tmp_path / "in.f32", tmp_path / "c.f32", tmp_path / "out.i32"], tmp_path)
+    ref = np.frombuffer((tmp_path / "out.i32").read_bytes(), np.int32)
+    ref_lab = np.where(ref == 255, 255, ref // 2)
+    o = orc.kmeans_assign_f32(pts.ravel(), cen).astype(np.int32)
+    mism = np.nonzero(ref_lab != o)[0]
+    assert len(mism) == 0, (len(mism), pts[mism[:5]], ref_lab[mism[:5]], o[mism[:5]])
