@@ -4,13 +4,14 @@
  * oracle/ref/Makefile into the oracle/_ref code objects) on the GPU box's OpenCL device, the way the
  * reference hosts launch them, and writes the raw outputs for tests/test_ref_opencl.py:
  *
- *   ref_harness downsample <co> <in.i32> <out.i32>
+ *   ref_harness downsample <co> <in.i32> <out.i32> [lanes]
  *       process_coordinates (coordinate_processor.cl:16-89) as in SMP/…opencl_store.cpp:
  *       297-326: ONE work-group, total_coords = number of (x,y) pairs, width 1280, height 720.
  *       in: int32 pairs x,y.  out: [unique_count, repeated_count, unique_coords[2*unique]].
- *       (The device reports a 256-lane work-group limit for clang-built kernels, so the single
- *       work-group has 256 lanes instead of the reference's 1024; the kernel strides over
- *       all pairs either way.)
+ *       The single work-group has `lanes` lanes (default 64 = one wave).  The reference
+ *       launches 1024, but its lane 0 adds the LDS counters to the globals with no barrier
+ *       (:80-81 commented out), so with more than one wave the counts race (quirk Q21);
+ *       with one wave they are final.  The unique_coords buffer is pre-filled with -1.
  *   ref_harness assign <co> <in.f32> <centers.f32> <out.i32>
  *       assign_to_centers (assign_to_centers.cl:1-34): in = float x,y pairs (padded by the
  *       caller to a multiple of 256 points), centers = 8 (x,y); out = assignments (2c or 255).
@@ -75,7 +76,9 @@ int main(int argc, char **argv) {
         int zero = 0;
         cl_mem bin_ = clCreateBuffer(ctx, CL_MEM_READ_ONLY | CL_MEM_COPY_HOST_PTR, ilen ? ilen : 8, in, &err);
         cl_mem brep = clCreateBuffer(ctx, CL_MEM_READ_WRITE, 16384 * sizeof(int), NULL, &err);
-        cl_mem buni = clCreateBuffer(ctx, CL_MEM_READ_WRITE, 2 * 8192 * sizeof(int), NULL, &err);
+        int *init = malloc(2 * 8192 * sizeof(int));
+        for (int i = 0; i < 2 * 8192; ++i) init[i] = -1;
+        cl_mem buni = clCreateBuffer(ctx, CL_MEM_READ_WRITE | CL_MEM_COPY_HOST_PTR, 2 * 8192 * sizeof(int), init, &err);
         cl_mem brc = clCreateBuffer(ctx, CL_MEM_READ_WRITE | CL_MEM_COPY_HOST_PTR, sizeof(int), &zero, &err);
         cl_mem buc = clCreateBuffer(ctx, CL_MEM_READ_WRITE | CL_MEM_COPY_HOST_PTR, sizeof(int), &zero, &err);
         if (err) die("clCreateBuffer", err);
@@ -88,18 +91,18 @@ int main(int argc, char **argv) {
         clSetKernelArg(k, 5, sizeof(int), &pairs);
         clSetKernelArg(k, 6, sizeof(int), &w);
         clSetKernelArg(k, 7, sizeof(int), &h);
-        size_t g = 256, l = 256;
+        size_t g = argc > 5 ? (size_t)atoi(argv[5]) : 64, l = g;
         if ((err = clEnqueueNDRangeKernel(q, k, 1, NULL, &g, &l, 0, NULL, NULL)) != CL_SUCCESS) die("clEnqueueNDRangeKernel", err);
         clFinish(q);
         int counts[2];
         clEnqueueReadBuffer(q, buc, CL_TRUE, 0, sizeof(int), &counts[0], 0, NULL, NULL);
         clEnqueueReadBuffer(q, brc, CL_TRUE, 0, sizeof(int), &counts[1], 0, NULL, NULL);
-        int nu = counts[0] > 8192 ? 8192 : counts[0];
-        int *out = malloc((2 + 2 * (size_t)nu) * sizeof(int));
+        /* the whole coordinate buffer: entries past the final local counter stay -1 */
+        int *out = malloc((2 + 2 * 8192) * sizeof(int));
         out[0] = counts[0];
         out[1] = counts[1];
-        if (nu) clEnqueueReadBuffer(q, buni, CL_TRUE, 0, 2 * (size_t)nu * sizeof(int), out + 2, 0, NULL, NULL);
-        spit(argv[4], out, (2 + 2 * (size_t)nu) * sizeof(int));
+        clEnqueueReadBuffer(q, buni, CL_TRUE, 0, 2 * 8192 * sizeof(int), out + 2, 0, NULL, NULL);
+        spit(argv[4], out, (2 + 2 * 8192) * sizeof(int));
     } else if (!strcmp(argv[1], "assign")) {
         if (argc < 6) return 2;
         size_t ilen, clen;
