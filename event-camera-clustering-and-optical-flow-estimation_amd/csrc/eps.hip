@@ -6,7 +6,7 @@
 // and optics::compute_core_dist (OPT/include/optics/optics.hpp:286-299: nth_element of the
 // squared distances at min_pts-1, self included).
 //
-// MI355X design: one workgroup per segment (<= 8192 points, e.g. one downsample window).  The
+// MI355X design: one workgroup per segment (<= 16384 points, e.g. one downsample window).  The
 // segment is binned in LDS into a uniform grid of cell size >= eps (counting sort with LDS
 // atomics; each cell's index list is then sorted so lists come out ascending), and every lane
 // answers one query from the 3x3 surrounding cells: exact integer d^2 compared against eps^2
@@ -21,7 +21,7 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kMaxPts = 8192;
+constexpr int kMaxPts = 16384;
 constexpr int kMaxCells = 8192;
 
 struct SegView {
@@ -324,7 +324,7 @@ int check_segs(const ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t s
                double eps) {
     if (!ctx || n_segs < 0 || stride < 1 || !(eps >= 0.0) || eps > 32767.0) return ECC_ERR_INVALID;
     if (n_segs > 0 && !xy) return ECC_ERR_INVALID;
-    if (stride > kMaxPts) return ECC_ERR_INVALID;  // segments hold <= 8192 points
+    if (stride > kMaxPts) return ECC_ERR_INVALID;  // segments hold <= 16384 points
     return ECC_OK;
 }
 

@@ -1,0 +1,456 @@
+// C++ host layer (include/ecc.hpp) over the C ABI: mirrors the reference's class interfaces.
+// All compute goes through libecc's HIP kernels; the host only does what the reference does
+// sequentially by nature (OPTICS seed-set ordering, DBSCAN cluster expansion) on GPU-computed
+// neighbourhoods, plus argument marshalling.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <set>
+#include <sstream>
+
+#include "../../include/ecc.hpp"
+
+namespace ecc {
+
+static void check(int rc, const char *what) {
+    if (rc != ECC_OK) throw Error(rc, what);
+}
+
+// ------------------------------------------------------------------------------ runtime
+Context::Context(int device) {
+    check(ecc_set_device(device), "ecc_set_device");
+    check(ecc_ctx_create(&ctx_, device), "ecc_ctx_create");
+    check(ecc_stream_create(&stream_), "ecc_stream_create");
+}
+
+Context::~Context() {
+    if (ctx_) ecc_ctx_destroy(ctx_);
+    if (stream_) ecc_stream_destroy(stream_);
+}
+
+void Context::sync() const { check(ecc_stream_sync(stream_), "ecc_stream_sync"); }
+
+Context &Context::default_context() {
+    static Context ctx(0);
+    return ctx;
+}
+
+DeviceBuffer::DeviceBuffer(size_t bytes) { reserve(bytes); }
+
+DeviceBuffer::~DeviceBuffer() {
+    if (p_) ecc_dev_free(p_);
+}
+
+DeviceBuffer &DeviceBuffer::operator=(DeviceBuffer &&o) noexcept {
+    if (this != &o) {
+        if (p_) ecc_dev_free(p_);
+        p_ = o.p_;
+        n_ = o.n_;
+        o.p_ = nullptr;
+        o.n_ = 0;
+    }
+    return *this;
+}
+
+void DeviceBuffer::reserve(size_t bytes) {
+    if (bytes <= n_ && p_) return;
+    if (p_) ecc_dev_free(p_);
+    p_ = nullptr;
+    n_ = 0;
+    check(ecc_dev_alloc(&p_, bytes ? bytes : 16), "ecc_dev_alloc");
+    n_ = bytes;
+}
+
+void DeviceBuffer::upload(const void *src, size_t bytes, ecc_stream_t s) {
+    reserve(bytes);
+    if (bytes) check(ecc_memcpy_h2d(p_, src, bytes, s), "ecc_memcpy_h2d");
+}
+
+void DeviceBuffer::download(void *dst, size_t bytes, ecc_stream_t s) const {
+    if (bytes) check(ecc_memcpy_d2h(dst, p_, bytes, s), "ecc_memcpy_d2h");
+}
+
+// ------------------------------------------------------------------------------ corners
+std::vector<Corner> CornerFilter::filterCorners(const std::vector<Corner> &corners, int w, int h,
+                                                int box, float threshold) {
+    return filterCorners(Context::default_context(), corners, w, h, box, threshold);
+}
+
+std::vector<Corner> CornerFilter::filterCorners(Context &ctx, const std::vector<Corner> &corners,
+                                                int w, int h, int box, float /*threshold: unused
+                                                in the reference too, :107-108*/) {
+    if (corners.empty()) return {};  // :88-89
+    const int64_t n = (int64_t)corners.size();
+    if (n > 16384) throw Error(ECC_ERR_INVALID, "filterCorners: more than 16384 corners in one call");
+    std::vector<uint32_t> xy(n);
+    std::vector<uint8_t> flags(n, 1);
+    for (int64_t i = 0; i < n; ++i) xy[i] = pack_xy(corners[i].x, corners[i].y);
+    DeviceBuffer d_xy, d_f, d_out(sizeof(ecc_corner) * n), d_cnt(sizeof(int32_t));
+    d_xy.upload(xy.data(), xy.size() * 4, ctx.stream());
+    d_f.upload(flags.data(), flags.size(), ctx.stream());
+    check(ecc_corner_nms(ctx.get(), d_xy.as<uint32_t>(), d_f.as<uint8_t>(), n, (int32_t)n, w, h,
+                         box, (int32_t)n, d_out.as<ecc_corner>(), d_cnt.as<int32_t>(), ctx.stream()),
+          "ecc_corner_nms");
+    int32_t k = 0;
+    d_cnt.download(&k, 4, ctx.stream());
+    std::vector<ecc_corner> out(k);
+    d_out.download(out.data(), sizeof(ecc_corner) * k, ctx.stream());
+    std::vector<Corner> res(k);
+    for (int i = 0; i < k; ++i) res[i] = Corner{out[i].x, out[i].y, out[i].label};
+    return res;
+}
+
+CornerTracker::CornerTracker(float max_matching_distance, int max_frames, int history_size,
+                             int frames_to_skip, float damping, float smoothing, float group_rad)
+    : ctx_(&Context::default_context()), max_tracks_(16384), max_det_(4096) {
+    ecc_tracker_cfg c{max_matching_distance, max_frames, history_size, frames_to_skip, damping,
+                      smoothing, group_rad};
+    check(ecc_tracker_create(ctx_->get(), &c, max_tracks_, max_det_, &tr_), "ecc_tracker_create");
+}
+
+CornerTracker::CornerTracker(Context &ctx, const ecc_tracker_cfg &cfg, int max_tracks,
+                             int max_detections)
+    : ctx_(&ctx), max_tracks_(max_tracks), max_det_(max_detections) {
+    check(ecc_tracker_create(ctx.get(), &cfg, max_tracks, max_detections, &tr_), "ecc_tracker_create");
+}
+
+CornerTracker::~CornerTracker() {
+    if (tr_) ecc_tracker_destroy(tr_);
+}
+
+void CornerTracker::updateDevice(const ecc_corner *d_corners, const int32_t *d_counts, int n_slices,
+                                 int cap) {
+    check(ecc_tracker_update(tr_, d_corners, d_counts, n_slices, cap, ctx_->stream()), "ecc_tracker_update");
+}
+
+std::vector<TrackedCorner> CornerTracker::tracks() {
+    check(ecc_tracker_status(tr_, ctx_->stream()), "tracker device status");
+    std::vector<ecc_track> raw(max_tracks_);
+    int32_t n = 0;
+    check(ecc_tracker_get_tracks(tr_, raw.data(), max_tracks_, &n, ctx_->stream()), "ecc_tracker_get_tracks");
+    std::vector<TrackedCorner> out(n);
+    for (int i = 0; i < n; ++i) {
+        const ecc_track &t = raw[i];
+        TrackedCorner &o = out[i];
+        o.x = t.x; o.y = t.y; o.label = t.label; o.frame_count = t.frame_count;
+        o.is_matched = t.is_matched != 0;
+        o.frames_since_last_detection = t.frames_since_last_detection;
+        for (int k = 0; k < t.hist_len; ++k) o.position_history.push_back(Point{t.hist_x[k], t.hist_y[k]});
+        o.velocity = Point2f{t.vx, t.vy};
+        o.direction = DirectionVector{Point2f{t.dir_cur_x, t.dir_cur_y}, Point2f{t.dir_tgt_x, t.dir_tgt_y}, 0.f, 0.f};
+        o.group_id = t.group_id;
+    }
+    return out;
+}
+
+void CornerTracker::refreshGroups() {
+    std::vector<ecc_group> g(max_tracks_);
+    std::vector<int32_t> labels(max_tracks_);
+    int32_t n = 0;
+    check(ecc_tracker_get_groups(tr_, g.data(), max_tracks_, &n, labels.data(), max_tracks_, ctx_->stream()),
+          "ecc_tracker_get_groups");
+    groups_.clear();
+    for (int i = 0; i < n; ++i) {
+        CornerGroup cg;
+        cg.corner_labels.assign(labels.begin() + g[i].first_label_offset,
+                                labels.begin() + g[i].first_label_offset + g[i].n_labels);
+        cg.average_velocity = Point2f{g[i].avg_vx, g[i].avg_vy};
+        cg.centroid = Point2f{g[i].cx, g[i].cy};
+        cg.radius = g[i].radius;
+        groups_[g[i].id] = cg;
+    }
+}
+
+std::vector<TrackedCorner> CornerTracker::updateTrackedCorners(const std::vector<Corner> &cs) {
+    const int n = (int)std::min<size_t>(cs.size(), (size_t)max_det_);
+    std::vector<ecc_corner> raw(std::max(n, 1));
+    for (int i = 0; i < n; ++i) raw[i] = ecc_corner{cs[i].x, cs[i].y, cs[i].label};
+    d_corners_.upload(raw.data(), sizeof(ecc_corner) * raw.size(), ctx_->stream());
+    const int32_t cnt = n;
+    d_count_.upload(&cnt, 4, ctx_->stream());
+    updateDevice(d_corners_.as<ecc_corner>(), d_count_.as<int32_t>(), 1, (int)raw.size());
+    refreshGroups();
+    return tracks();
+}
+
+TimeSurfaceCornerDetector::TimeSurfaceCornerDetector(Context &ctx, int width, int height,
+                                                     int slice_events, int border_mode)
+    : ctx_(ctx) {
+    ecc_corner_cfg_default(&cfg_);
+    cfg_.width = width;
+    cfg_.height = height;
+    cfg_.slice_events = slice_events;
+    cfg_.border_mode = border_mode;
+    sae_.reserve((size_t)width * height * 8);
+    check(ecc_memset_async(sae_.data(), 0, (size_t)width * height * 8, ctx.stream()), "memset(sae)");
+}
+
+void TimeSurfaceCornerDetector::detect(const uint32_t *d_xy, const int64_t *d_t, int64_t n,
+                                       uint8_t *d_flags) {
+    cfg_.first_detect_slice = first_ ? 1 : 0;
+    check(ecc_fast_detect(ctx_.get(), d_xy, d_t, n, &cfg_, sae_.as<int64_t>(), d_flags, ctx_.stream()),
+          "ecc_fast_detect");
+    check(ecc_fast_detect_status(ctx_.get(), ctx_.stream()), "ecc_fast_detect");
+    first_ = false;
+}
+
+// ------------------------------------------------------------------------------ downsample / k-means
+HashDownsampler::HashDownsampler(Context &ctx, const ecc_hash_cfg *cfg) : ctx_(ctx) {
+    if (cfg) cfg_ = *cfg;
+    else ecc_hash_cfg_default(&cfg_);
+}
+
+void HashDownsampler::run(const uint32_t *d_xy, int64_t n, uint32_t *d_rep_xy, uint32_t *d_rep_idx,
+                          int32_t *d_unique, int32_t *d_repeated) {
+    check(ecc_downsample_hash(ctx_.get(), d_xy, n, &cfg_, d_rep_xy, d_rep_idx, d_unique, d_repeated,
+                              ctx_.stream()), "ecc_downsample_hash");
+}
+
+DownsampleResult HashDownsampler::process(const std::vector<std::pair<int, int>> &coords) {
+    const int64_t n = (int64_t)coords.size();
+    const int64_t nw = (n + cfg_.window - 1) / cfg_.window;
+    DownsampleResult r;
+    r.unique_count.assign(nw, 0);
+    r.repeated_count.assign(nw, 0);
+    r.unique_coords.assign(nw, {});
+    if (n == 0) return r;
+    std::vector<uint32_t> xy(n);
+    for (int64_t i = 0; i < n; ++i) {
+        const int x = coords[i].first, y = coords[i].second;
+        // negative / >u16 coordinates are outside 0<=x<=1280 anyway (:56); map them out of range
+        xy[i] = (x < 0 || y < 0 || x > 65535 || y > 65535) ? 0xffffffffu : pack_xy(x, y);
+    }
+    DeviceBuffer d_xy, d_rep((size_t)nw * cfg_.window * 4), d_u((size_t)nw * 4), d_r((size_t)nw * 4);
+    d_xy.upload(xy.data(), n * 4, ctx_.stream());
+    run(d_xy.as<uint32_t>(), n, d_rep.as<uint32_t>(), nullptr, d_u.as<int32_t>(), d_r.as<int32_t>());
+    std::vector<uint32_t> rep((size_t)nw * cfg_.window);
+    d_u.download(r.unique_count.data(), nw * 4, ctx_.stream());
+    d_r.download(r.repeated_count.data(), nw * 4, ctx_.stream());
+    d_rep.download(rep.data(), rep.size() * 4, ctx_.stream());
+    for (int64_t w = 0; w < nw; ++w)
+        for (int k = 0; k < r.unique_count[w]; ++k) {
+            const uint32_t v = rep[w * cfg_.window + k];
+            r.unique_coords[w].push_back({(int)(v & 0xffff), (int)(v >> 16)});
+        }
+    return r;
+}
+
+KMeans::KMeans(Context &ctx, int k, int max_iters, float threshold, float tol) : ctx_(ctx) {
+    cfg_ = ecc_kmeans_cfg{k, max_iters, threshold, tol};
+}
+
+std::vector<uint8_t> KMeans::fit(const std::vector<std::array<float, 2>> &points,
+                                 std::vector<std::array<float, 2>> &centroids, int *iters) {
+    if ((int)centroids.size() != cfg_.k) throw Error(ECC_ERR_INVALID, "KMeans::fit: centroids.size() != k");
+    const int64_t n = (int64_t)points.size();
+    DeviceBuffer d_p, d_c, d_l(std::max<int64_t>(n, 1)), d_it(4);
+    d_p.upload(points.data(), n * 8, ctx_.stream());
+    d_c.upload(centroids.data(), cfg_.k * 8, ctx_.stream());
+    check(ecc_kmeans_run_f32(ctx_.get(), d_p.as<float>(), n, &cfg_, d_c.as<float>(), d_l.as<uint8_t>(),
+                             d_it.as<int32_t>(), ctx_.stream()), "ecc_kmeans_run_f32");
+    std::vector<uint8_t> labels(n);
+    d_l.download(labels.data(), n, ctx_.stream());
+    d_c.download(centroids.data(), cfg_.k * 8, ctx_.stream());
+    if (iters) d_it.download(iters, 4, ctx_.stream());
+    return labels;
+}
+
+// ------------------------------------------------------------------------------ eps lists
+void eps_neighbour_lists(Context &ctx, const std::vector<std::array<int, 2>> &points, double eps,
+                         std::vector<int64_t> &offsets, std::vector<int32_t> &nbr, int min_pts,
+                         std::vector<double> *core_dist) {
+    const int64_t n = (int64_t)points.size();
+    offsets.assign(n + 1, 0);
+    nbr.clear();
+    if (n == 0) return;
+    if (n > 16384) throw Error(ECC_ERR_INVALID, "eps_neighbour_lists: more than 16384 points");
+    int mnx = points[0][0], mny = points[0][1], mxx = mnx, mxy = mny;
+    for (const auto &p : points) {
+        mnx = std::min(mnx, p[0]); mny = std::min(mny, p[1]);
+        mxx = std::max(mxx, p[0]); mxy = std::max(mxy, p[1]);
+    }
+    if ((int64_t)mxx - mnx > 65535 || (int64_t)mxy - mny > 65535)
+        throw Error(ECC_ERR_INVALID, "eps_neighbour_lists: coordinate span exceeds 65535");
+    std::vector<uint32_t> xy(n);  // translation keeps every distance
+    for (int64_t i = 0; i < n; ++i) xy[i] = pack_xy(points[i][0] - mnx, points[i][1] - mny);
+    DeviceBuffer d_xy, d_cnt(n * 4), d_core(core_dist ? n * 8 : 8), d_off((n + 1) * 8);
+    d_xy.upload(xy.data(), n * 4, ctx.stream());
+    check(ecc_eps_counts(ctx.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps, std::max(1, min_pts),
+                         d_cnt.as<int32_t>(), core_dist ? d_core.as<double>() : nullptr, ctx.stream()),
+          "ecc_eps_counts");
+    // list size from the counts (one small readback, as the reference reads sizes back)
+    std::vector<int32_t> cnt(n);
+    d_cnt.download(cnt.data(), n * 4, ctx.stream());
+    int64_t total = 0;
+    for (int32_t c : cnt) total += c;
+    DeviceBuffer d_nbr(std::max<int64_t>(total, 1) * 4);
+    check(ecc_eps_lists(ctx.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps, d_cnt.as<int32_t>(),
+                        d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, ctx.stream()),
+          "ecc_eps_lists");
+    int64_t tot2 = 0;
+    check(ecc_eps_total(ctx.get(), d_off.as<int64_t>(), n, &tot2, ctx.stream()), "ecc_eps_lists capacity");
+    offsets.resize(n + 1);
+    nbr.resize(total);
+    d_off.download(offsets.data(), (n + 1) * 8, ctx.stream());
+    d_nbr.download(nbr.data(), total * 4, ctx.stream());
+    if (core_dist) {
+        core_dist->resize(n);
+        d_core.download(core_dist->data(), n * 8, ctx.stream());
+    }
+}
+
+// ------------------------------------------------------------------------------ OPTICS
+namespace optics {
+
+std::string reachability_dist::to_string() const {
+    return "{" + std::to_string(point_index) + "," + std::to_string(reach_dist) + "}";
+}
+
+bool operator<(const reachability_dist &l, const reachability_dist &r) {
+    return (l.reach_dist <= r.reach_dist && l.reach_dist >= r.reach_dist) ? (l.point_index < r.point_index)
+                                                                          : (l.reach_dist < r.reach_dist);
+}
+
+bool operator==(const reachability_dist &l, const reachability_dist &r) {
+    return (l.reach_dist <= r.reach_dist && l.reach_dist >= r.reach_dist) && (l.point_index == r.point_index);
+}
+
+std::vector<reachability_dist> compute_reachability_dists(Context &ctx,
+                                                          const std::vector<std::array<int, 2>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    if (points.empty()) return {};
+    if (min_pts < 1 || min_pts > 64) throw Error(ECC_ERR_INVALID, "compute_reachability_dists: min_pts must be 1..64");
+    if (epsilon <= 0.0) epsilon = epsilon_estimation(points, min_pts);  // optics.hpp:428-430
+    std::vector<int64_t> off;
+    std::vector<int32_t> nbr;
+    std::vector<double> core;
+    eps_neighbour_lists(ctx, points, epsilon, off, nbr, (int)min_pts, &core);  // GPU (:496-503, :286-299)
+    const size_t n = points.size();
+    auto dist = [&](size_t a, size_t b) {
+        const double dx = (double)points[a][0] - points[b][0], dy = (double)points[a][1] - points[b][1];
+        return std::sqrt(dx * dx + dy * dy);
+    };
+    std::vector<bool> processed(n, false);
+    std::vector<double> reach(n, -1.0);
+    std::vector<size_t> ordered;
+    ordered.reserve(n);
+    auto update = [&](size_t p, double cd, std::set<reachability_dist> &seeds) {  // :315-337
+        for (int64_t k = off[p]; k < off[p + 1]; ++k) {
+            const size_t o = (size_t)nbr[k];
+            if (processed[o]) continue;
+            const double nr = std::max(cd, dist(p, o));
+            if (reach[o] < 0.0) {
+                reach[o] = nr;
+                seeds.insert(reachability_dist(o, nr));
+            } else if (nr < reach[o]) {
+                seeds.erase(reachability_dist(o, reach[o]));
+                reach[o] = nr;
+                seeds.insert(reachability_dist(o, nr));
+            }
+        }
+    };
+    for (size_t p = 0; p < n; ++p) {  // :525-555
+        if (processed[p]) continue;
+        processed[p] = true;
+        ordered.push_back(p);
+        std::set<reachability_dist> seeds;
+        if (core[p] < 0.0) continue;
+        update(p, core[p], seeds);
+        while (!seeds.empty()) {
+            const reachability_dist s = *seeds.begin();
+            seeds.erase(seeds.begin());
+            processed[s.point_index] = true;
+            ordered.push_back(s.point_index);
+            if (core[s.point_index] < 0.0) continue;
+            update(s.point_index, core[s.point_index], seeds);
+        }
+    }
+    std::vector<reachability_dist> result;
+    result.reserve(n);
+    for (size_t idx : ordered) result.emplace_back(idx, reach[idx]);
+    return result;
+}
+
+std::vector<reachability_dist> compute_reachability_dists(const std::vector<std::array<int, 2>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return compute_reachability_dists(Context::default_context(), points, min_pts, epsilon);
+}
+
+std::vector<reachability_dist> compute_reachability_dists(const std::vector<std::array<double, 2>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    std::vector<std::array<int, 2>> ip(points.size());
+    for (size_t i = 0; i < points.size(); ++i)
+        for (int d = 0; d < 2; ++d) {
+            const double v = points[i][d];
+            if (v != std::floor(v) || std::fabs(v) > 1e9)
+                throw Error(ECC_ERR_INVALID, "compute_reachability_dists: GPU path needs integer-valued coordinates");
+            ip[i][d] = (int)v;
+        }
+    if (epsilon <= 0.0) epsilon = epsilon_estimation(points, min_pts);
+    return compute_reachability_dists(Context::default_context(), ip, min_pts, epsilon);
+}
+
+std::vector<std::vector<std::size_t>> get_cluster_indices(const std::vector<reachability_dist> &rd,
+                                                          double thr) {  // optics.hpp:674-690
+    std::vector<std::vector<std::size_t>> result;
+    for (const auto &r : rd) {
+        if (r.reach_dist < 0.0 || r.reach_dist >= thr || result.empty()) result.push_back({r.point_index});
+        else result.back().push_back(r.point_index);
+    }
+    return result;
+}
+
+}  // namespace optics
+
+// ------------------------------------------------------------------------------ DBSCAN
+void DBSCANSimpleCluster::extract(std::vector<PointIndices> &cluster_indices) {  // DBSCAN_simple.h:27-90
+    enum { UN_PROCESSED = 0, PROCESSING = 1, PROCESSED = 2 };
+    cluster_indices.clear();
+    const size_t n = cloud_.size();
+    if (n == 0) return;
+    std::vector<std::array<int, 2>> pts(n);
+    for (size_t i = 0; i < n; ++i) {
+        const PointXYZ &p = cloud_[i];
+        if (p.x != std::floor(p.x) || p.y != std::floor(p.y) || p.z != cloud_[0].z)
+            throw Error(ECC_ERR_INVALID, "DBSCAN: GPU path needs integer-valued 2-D points (constant z)");
+        pts[i] = {(int)p.x, (int)p.y};
+    }
+    std::vector<int64_t> off;
+    std::vector<int32_t> nbr;
+    eps_neighbour_lists(ctx_, pts, eps_, off, nbr);  // radiusSearch for every point, on the GPU
+    auto nn_size = [&](size_t i) { return (int)(off[i + 1] - off[i]); };
+    std::vector<bool> is_noise(n, false);
+    std::vector<int> types(n, UN_PROCESSED);
+    std::vector<std::vector<int>> clusters;
+    for (size_t i = 0; i < n; i++) {
+        if (types[i] == PROCESSED) continue;
+        if (nn_size(i) < minPts_) { is_noise[i] = true; continue; }
+        std::vector<int> seed_queue{(int)i};
+        types[i] = PROCESSED;
+        for (int64_t k = off[i]; k < off[i + 1]; ++k)
+            if (nbr[k] != (int)i) { seed_queue.push_back(nbr[k]); types[nbr[k]] = PROCESSING; }
+        size_t sq = 1;
+        while (sq < seed_queue.size()) {
+            const int ci = seed_queue[sq];
+            if (is_noise[ci] || types[ci] == PROCESSED) { types[ci] = PROCESSED; sq++; continue; }
+            if (nn_size(ci) >= minPts_)
+                for (int64_t k = off[ci]; k < off[ci + 1]; ++k)
+                    if (types[nbr[k]] == UN_PROCESSED) { seed_queue.push_back(nbr[k]); types[nbr[k]] = PROCESSING; }
+            types[ci] = PROCESSED;
+            sq++;
+        }
+        if ((int)seed_queue.size() >= min_pts_per_cluster_ && (int)seed_queue.size() <= max_pts_per_cluster_) {
+            std::sort(seed_queue.begin(), seed_queue.end());
+            seed_queue.erase(std::unique(seed_queue.begin(), seed_queue.end()), seed_queue.end());
+            clusters.push_back(seed_queue);
+        }
+    }
+    std::stable_sort(clusters.begin(), clusters.end(), [](const std::vector<int> &a, const std::vector<int> &b) {
+        if (a.size() != b.size()) return a.size() > b.size();
+        return a.front() < b.front();
+    });
+    for (auto &c : clusters) cluster_indices.push_back(PointIndices{c});
+}
+
+}  // namespace ecc

@@ -264,7 +264,7 @@ int ecc_tracker_status(ecc_tracker *tr, ecc_stream_t stream);
  *            self included); kdt::KDTree::radius_search OPT/include/optics/kdTree.hpp:307-422;
  *            optics::compute_core_dist OPT/include/optics/optics.hpp:286-299.
  * Points are packed u16 xy, segmented like ecc_kmeans_run_xy16 (one independent
- * neighbourhood problem per segment, <= 8192 points each, e.g. one downsample window);
+ * neighbourhood problem per segment, <= 16384 points each, e.g. one downsample window);
  * duplicates allowed.  Arrays are indexed by the flattened point index p = s*seg_stride + j
  * (entries with j >= seg_counts[s] are left untouched, except offsets which stay monotone).
  *   counts[p]    = |{j in seg : (xi-xj)^2 + (yi-yj)^2 <= eps^2}| (self included);

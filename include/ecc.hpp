@@ -1,0 +1,321 @@
+// ecc.hpp — C++ host layer of the MI355X event pipeline, mirroring the reference's own
+// operator interfaces (same names, argument meaning and error behaviour) on top of the C ABI in
+// ecc.h, so a reference host program switches by changing its includes:
+//
+//   reference                                                    here
+//   CornerFilter::filterCorners      FCT/…group_track.cpp:81-152   ecc::CornerFilter::filterCorners
+//   CornerTracker(...)::updateTrackedCorners / getCornerGroups
+//                                    FCT/…group_track.cpp:401-536  ecc::CornerTracker
+//   struct Corner / TrackedCorner / CornerGroup / DirectionVector
+//                                    FCT/…group_track.cpp:61-199   ecc::Corner ... (cv::Point2f ->
+//                                                                  ecc::Point2f, cv::Point -> ecc::Point)
+//   optics::compute_reachability_dists<N>(pts, min_pts, eps)
+//                                    OPT/include/optics/optics.hpp:413-565  ecc::optics::compute_reachability_dists
+//                                                                  (runtime N instead of the template N)
+//   optics::get_cluster_indices / epsilon_estimation
+//                                    optics.hpp:674-690, 369-387   ecc::optics::...
+//   DBSCANSimpleCluster / DBSCANPrecompCluster::{setInputCloud, setClusterTolerance,
+//     setCorePointMinPts, setMin/MaxClusterSize, extract}
+//                                    PCC/DBSCAN_simple.h:14-143, DBSCAN_precomp.h  ecc::DBSCANSimpleCluster ...
+//   process_coordinates + host slice path  SMP/…opencl_store.cpp:250-417  ecc::HashDownsampler
+//   assign_to_centers + k-means host loop  KM/assign_to_centers2.c:184-548 ecc::KMeans
+//   aggregate lambda (batch SAE + arc test) FCT/…group_track.cpp:884-1070  ecc::TimeSurfaceCornerDetector
+//
+// Errors: the C ABI returns negative ecc_status codes; this layer throws ecc::Error (the
+// reference hosts perror()+exit(1); its host programs in apps/ do the same on an ecc::Error).
+// Compute always runs on the GPU through libecc; there is no CPU fallback.
+#pragma once
+
+#include <array>
+#include <cstddef>
+#include <cstdint>
+#include <cmath>
+#include <deque>
+#include <limits>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "ecc.h"
+
+#pragma GCC visibility push(default)
+namespace ecc {
+
+class Error : public std::runtime_error {
+  public:
+    Error(int status, const std::string &what)
+        : std::runtime_error(what + ": " + ecc_status_string(status)), status_(status) {}
+    int status() const { return status_; }
+
+  private:
+    int status_;
+};
+
+// One GPU context + stream (replaces create_device/clCreateContext/clCreateCommandQueue).
+class Context {
+  public:
+    explicit Context(int device = 0);
+    ~Context();
+    Context(const Context &) = delete;
+    Context &operator=(const Context &) = delete;
+    ecc_ctx *get() const { return ctx_; }
+    ecc_stream_t stream() const { return stream_; }
+    void sync() const;
+    // process-wide default context on device 0 (the reference's single global OpenCL device)
+    static Context &default_context();
+
+  private:
+    ecc_ctx *ctx_ = nullptr;
+    ecc_stream_t stream_ = nullptr;
+};
+
+// Owning device buffer.
+class DeviceBuffer {
+  public:
+    DeviceBuffer() = default;
+    explicit DeviceBuffer(size_t bytes);
+    ~DeviceBuffer();
+    DeviceBuffer(DeviceBuffer &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+    DeviceBuffer &operator=(DeviceBuffer &&o) noexcept;
+    DeviceBuffer(const DeviceBuffer &) = delete;
+    DeviceBuffer &operator=(const DeviceBuffer &) = delete;
+    void *data() const { return p_; }
+    size_t size() const { return n_; }
+    void reserve(size_t bytes);  // grows (content not kept)
+    template <typename T> T *as() const { return static_cast<T *>(p_); }
+    void upload(const void *src, size_t bytes, ecc_stream_t s);
+    void download(void *dst, size_t bytes, ecc_stream_t s) const;
+
+  private:
+    void *p_ = nullptr;
+    size_t n_ = 0;
+};
+
+inline uint32_t pack_xy(int x, int y) { return (uint32_t)(x & 0xffff) | ((uint32_t)(y & 0xffff) << 16); }
+
+// ------------------------------------------------------------------------------ corners
+struct Corner {  // FCT/…group_track.cpp:61-67
+    int x;
+    int y;
+    int label;
+};
+
+struct Point {  // cv::Point
+    int x, y;
+};
+
+struct Point2f {  // cv::Point2f
+    float x, y;
+};
+
+struct DirectionVector {  // :163-175
+    Point2f current;
+    Point2f target;
+    float damping;
+    float smoothing;
+};
+
+struct TrackedCorner {  // :177-190
+    int x;
+    int y;
+    int label;
+    int frame_count;
+    bool is_matched;
+    int frames_since_last_detection;
+    std::deque<Point> position_history;
+    Point2f velocity;
+    DirectionVector direction;
+    int group_id;
+};
+
+struct CornerGroup {  // :193-199
+    std::vector<int> corner_labels;
+    Point2f average_velocity;
+    Point2f centroid;
+    float radius;
+};
+
+class CornerFilter {  // :69-153
+  public:
+    static std::vector<Corner> filterCorners(const std::vector<Corner> &corners, int image_width,
+                                             int image_height, int box_size, float threshold);
+    static std::vector<Corner> filterCorners(Context &ctx, const std::vector<Corner> &corners,
+                                             int image_width, int image_height, int box_size,
+                                             float threshold);
+};
+
+class CornerTracker {  // :201-537, device-resident state
+  public:
+    CornerTracker(float max_matching_distance = 30.0f, int max_frames = 30, int history_size = 10,
+                  int frames_to_skip = 5, float damping = 0.8f, float smoothing = 0.3f,
+                  float group_rad = 50.0f);
+    CornerTracker(Context &ctx, const ecc_tracker_cfg &cfg, int max_tracks = 16384,
+                  int max_detections = 4096);
+    ~CornerTracker();
+    CornerTracker(const CornerTracker &) = delete;
+    CornerTracker &operator=(const CornerTracker &) = delete;
+
+    std::vector<TrackedCorner> updateTrackedCorners(const std::vector<Corner> &current_corners);
+    const std::map<int, CornerGroup> &getCornerGroups() const { return groups_; }
+    // Batched form: n_slices NMS outputs already on the device (one launch for all slices).
+    void updateDevice(const ecc_corner *d_corners, const int32_t *d_counts, int n_slices, int cap);
+    std::vector<TrackedCorner> tracks();  // current state (host copy)
+    void refreshGroups();
+
+  private:
+    Context *ctx_;
+    ecc_tracker *tr_ = nullptr;
+    int max_tracks_, max_det_;
+    DeviceBuffer d_corners_, d_count_;
+    std::map<int, CornerGroup> groups_;
+};
+
+// Batch SAE + arc-test corner detector (the aggregate lambda, :884-1070), stream-continuable.
+class TimeSurfaceCornerDetector {
+  public:
+    TimeSurfaceCornerDetector(Context &ctx, int width, int height, int slice_events = 16384,
+                              int border_mode = 0);
+    // xy/t on the device; flags (device, n bytes) receive 1 for corner events.  The SAE carries
+    // over between calls; the first call skips the first slice (time_surface_flag, :926).
+    void detect(const uint32_t *d_xy, const int64_t *d_t, int64_t n, uint8_t *d_flags);
+    int64_t *sae() const { return sae_.as<int64_t>(); }
+    const ecc_corner_cfg &config() const { return cfg_; }
+
+  private:
+    Context &ctx_;
+    ecc_corner_cfg cfg_;
+    DeviceBuffer sae_;
+    bool first_ = true;
+};
+
+// ------------------------------------------------------------------------------ downsample / k-means
+struct DownsampleResult {
+    std::vector<int32_t> unique_count, repeated_count;  // per window
+    std::vector<std::vector<std::pair<int, int>>> unique_coords;  // per window (ascending index)
+};
+
+class HashDownsampler {  // process_coordinates + slice path (SMP/…opencl_store.cpp:341-417)
+  public:
+    explicit HashDownsampler(Context &ctx, const ecc_hash_cfg *cfg = nullptr);
+    // device-level: all windows of a batch in one launch
+    void run(const uint32_t *d_xy, int64_t n, uint32_t *d_rep_xy, uint32_t *d_rep_idx,
+             int32_t *d_unique, int32_t *d_repeated);
+    // host convenience: (x,y) pairs in, per-window unique coordinates out
+    DownsampleResult process(const std::vector<std::pair<int, int>> &coords);
+    const ecc_hash_cfg &config() const { return cfg_; }
+
+  private:
+    Context &ctx_;
+    ecc_hash_cfg cfg_;
+};
+
+class KMeans {  // assign_to_centers + host loop, "fixed" mode (Appendix A Q7-Q10)
+  public:
+    KMeans(Context &ctx, int k, int max_iters = 20, float threshold = 50.f, float tol = 1e-3f);
+    // host convenience: points (x,y floats), centroids in/out; returns labels (255 = none)
+    std::vector<uint8_t> fit(const std::vector<std::array<float, 2>> &points,
+                             std::vector<std::array<float, 2>> &centroids, int *iters = nullptr);
+    const ecc_kmeans_cfg &config() const { return cfg_; }
+
+  private:
+    Context &ctx_;
+    ecc_kmeans_cfg cfg_;
+};
+
+// ------------------------------------------------------------------------------ OPTICS
+namespace optics {
+
+struct reachability_dist {  // optics.hpp:57-65
+    reachability_dist(std::size_t point_index_, double reach_dist_)
+        : point_index(point_index_), reach_dist(reach_dist_) {}
+    std::string to_string() const;
+    std::size_t point_index;
+    double reach_dist;
+};
+bool operator<(const reachability_dist &lhs, const reachability_dist &rhs);   // :67-69
+bool operator==(const reachability_dist &lhs, const reachability_dist &rhs);  // :70-72
+
+// eps-neighbourhoods and core distances on the GPU (integer-valued 2-D points, <= 16384 per
+// call), ordered seed-set expansion on the host (sequential by nature, :525-555).
+// epsilon <= 0: estimated with epsilon_estimation (:428-430).  Throws ecc::Error
+// (ECC_ERR_INVALID) for non-integer coordinates or spans beyond 65535.
+std::vector<reachability_dist> compute_reachability_dists(
+    const std::vector<std::array<int, 2>> &points, std::size_t min_pts, double epsilon = -1.0);
+std::vector<reachability_dist> compute_reachability_dists(
+    const std::vector<std::array<double, 2>> &points, std::size_t min_pts, double epsilon = -1.0);
+std::vector<reachability_dist> compute_reachability_dists(
+    Context &ctx, const std::vector<std::array<int, 2>> &points, std::size_t min_pts,
+    double epsilon = -1.0);
+
+template <typename T, std::size_t dimension>
+double epsilon_estimation(const std::vector<std::array<T, dimension>> &points, std::size_t min_pts);
+
+std::vector<std::vector<std::size_t>> get_cluster_indices(
+    const std::vector<reachability_dist> &reach_dists, double reachability_threshold);
+
+}  // namespace optics
+
+// ------------------------------------------------------------------------------ DBSCAN
+struct PointXYZ {  // pcl::PointXYZ
+    float x, y, z;
+};
+struct PointIndices {  // pcl::PointIndices
+    std::vector<int> indices;
+};
+
+class DBSCANSimpleCluster {  // PCC/DBSCAN_simple.h:14-143 (GPU eps-lists, host extraction)
+  public:
+    explicit DBSCANSimpleCluster(Context &ctx = Context::default_context()) : ctx_(ctx) {}
+    virtual ~DBSCANSimpleCluster() = default;
+    virtual void setInputCloud(const std::vector<PointXYZ> &cloud) { cloud_ = cloud; }
+    void setClusterTolerance(double tolerance) { eps_ = tolerance; }
+    void setMinClusterSize(int min_cluster_size) { min_pts_per_cluster_ = min_cluster_size; }
+    void setMaxClusterSize(int max_cluster_size) { max_pts_per_cluster_ = max_cluster_size; }
+    void setCorePointMinPts(int core_point_min_pts) { minPts_ = core_point_min_pts; }
+    // clusters sorted by size, descending (ties: smallest member index first)
+    void extract(std::vector<PointIndices> &cluster_indices);
+
+  protected:
+    Context &ctx_;
+    std::vector<PointXYZ> cloud_;
+    double eps_{0.0};
+    int minPts_{1};
+    int min_pts_per_cluster_{1};
+    int max_pts_per_cluster_{std::numeric_limits<int>::max()};
+};
+
+// DBSCAN_precomp.h: same neighbourhoods, precomputed — on the GPU both are one eps-list pass.
+using DBSCANPrecompCluster = DBSCANSimpleCluster;
+
+// Neighbour lists of 2-D integer points (x,y of the cloud) on the GPU: CSR, ascending indices.
+void eps_neighbour_lists(Context &ctx, const std::vector<std::array<int, 2>> &points, double eps,
+                         std::vector<int64_t> &offsets, std::vector<int32_t> &nbr,
+                         int min_pts = 1, std::vector<double> *core_dist = nullptr);
+
+// ---- template definitions
+namespace optics {
+// optics.hpp:340-387 — bounding box (max initialised from points[1], Q20), uniform-density
+// eps for min_pts points per unit ball.
+template <typename T, std::size_t dimension>
+double epsilon_estimation(const std::vector<std::array<T, dimension>> &points, std::size_t min_pts) {
+    if (points.size() <= 1) return 0;
+    const double d = static_cast<double>(dimension);
+    std::array<T, dimension> mn(points[0]), mx(points[1]);
+    for (const auto &p : points)
+        for (std::size_t i = 0; i < dimension; i++) {
+            if (p[i] < mn[i]) mn[i] = p[i];
+            if (p[i] > mx[i]) mx[i] = p[i];
+        }
+    double volume = 1;
+    for (std::size_t i = 0; i < dimension; i++) volume *= std::abs(static_cast<double>(mx[i] - mn[i]));
+    const double space_per_minpts = (volume / static_cast<double>(points.size())) * static_cast<double>(min_pts);
+    const double unit_ball = std::sqrt(std::pow(M_PI, d)) / std::tgamma(d / 2.0 + 1.0);
+    return std::pow(space_per_minpts / unit_ball, 1.0 / d);
+}
+}  // namespace optics
+
+}  // namespace ecc
+#pragma GCC visibility pop
