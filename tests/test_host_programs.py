@@ -98,7 +98,7 @@ def test_corner_track_program_matches_oracle(orc, ecc):
 
 def test_downsample_program_matches_oracle(orc, ecc):
     out = run("ecc_downsample_store", "--synthetic", 100000)
-    xy, _, _ = ecc.gen_events(100000)
+    xy, _, _ = ecc.gen_events(100000, width=1280, height=720)  # the program's sensor
     _, _, u, r = orc.downsample_hash(xy)
     got = [tuple(map(int, m)) for m in re.findall(r"unique_count: (\d+), repeated_count: (\d+)", out)]
     assert got == list(zip(u.tolist(), r.tolist()))
