@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--events", type=int, default=20_000_000, help="events per GPU per step")
+    ap.add_argument("--events", type=int, default=1221 * 16384,
+                    help="events per GPU per step (1221 slices of 16384 = 20.0 M, BASELINE C4)")
     ap.add_argument("--width", type=int, default=346)
     ap.add_argument("--height", type=int, default=260)
     ap.add_argument("--k", type=int, default=16)
@@ -49,6 +50,9 @@ def parse():
     ap.add_argument("--cpu-events", type=int, default=8_000_000, help="CPU-baseline sample size")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for rehearsal")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank on device 0 (with --dist-backend gloo)")
     return ap.parse_args()
 
 
@@ -57,17 +61,23 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:
+        local = 0
     dist = None
+    torch = None
     if world > 1:
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group(args.dist_backend)
         dist = tdist
     import eccpy as ecc
 
     W, H, n, K, I = args.width, args.height, args.events, args.k, args.iters
-    ctx = ecc.Context(local)
+    if n % 16384:
+        raise SystemExit("--events must be a multiple of the 16384-event slice (global slice alignment)")
+    # one stream for libecc and the collectives (torch's current stream) when sharded
+    ctx = ecc.Context(local, stream=torch.cuda.current_stream().cuda_stream) if dist else ecc.Context(local)
     xy_h, t_h, _ = ecc.gen_events(n, first=rank * n, seed=1, width=W, height=H)
     d_xy, d_t = ecc.DeviceArray.from_numpy(xy_h, ctx.stream), ecc.DeviceArray.from_numpy(t_h, ctx.stream)
     hcfg = ecc.hash_cfg(window=8192)  # reference bounds 0<=x<=1280, 0<=y<=720
@@ -87,8 +97,38 @@ def main():
     nms_out = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE)
     nms_cnt = ecc.DeviceArray(ns, np.int32)
     lib = ecc.lib
+    if dist:
+        # exchange buffers are torch tensors (RCCL operates on them); libecc gets their pointers
+        t_acc = torch.zeros(3 * K, dtype=torch.int64, device=f"cuda:{local}")
+        t_state = torch.zeros(2, dtype=torch.int32, device=f"cuda:{local}")
+        t_local = torch.zeros(W * H, dtype=torch.int64, device=f"cuda:{local}")
+        t_all = torch.zeros(world * W * H, dtype=torch.int64, device=f"cuda:{local}")
+
+    def step_sharded():
+        """Shard-local downsample/detection/NMS + global k-means + exact SAE hand-off."""
+        S = ctx.stream
+        ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
+                                          uniq.ptr, rep.ptr, S), "downsample")
+        ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, S))
+        t_acc.zero_()
+        t_state.zero_()
+        for _ in range(I):  # exact integer partial sums, all-reduced every iteration
+            ecc.check(lib.ecc_kmeans_accumulate_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, d_c.ptr, K,
+                                                     kcfg.threshold, t_acc.data_ptr(), t_state.data_ptr(), S))
+            dist.all_reduce(t_acc)
+            ecc.check(lib.ecc_kmeans_update(ctx.ctx, t_acc.data_ptr(), d_c.ptr, K, kcfg.tol, t_state.data_ptr(), S))
+        ecc.check(lib.ecc_kmeans_labels_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, d_c.ptr, K,
+                                             kcfg.threshold, labels.ptr, S))
+        t_local.zero_()
+        ecc.check(lib.ecc_sae_scatter(ctx.ctx, d_xy.ptr, d_t.ptr, n, W, H, t_local.data_ptr(), S))
+        dist.all_gather(list(t_all.view(world, -1).unbind(0)), t_local)
+        ecc.check(lib.ecc_sae_max_combine(ctx.ctx, t_all.data_ptr(), rank, W * H, sae.ptr, S))
+        ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
+        ctx.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, nms_out, nms_cnt)
 
     def step():
+        if dist:
+            return step_sharded()
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
                                           uniq.ptr, rep.ptr, ctx.stream), "downsample")
         ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, ctx.stream))
@@ -121,7 +161,6 @@ def main():
     ecc.check(lib.ecc_ctx_timing_report(ctx.ctx, buf, len(buf)))
     stats = json.loads(buf.value.decode())
     if dist:
-        import torch
         tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())

@@ -231,6 +231,17 @@ sae_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ 
     }
 }
 
+__global__ void __launch_bounds__(kThreads)
+sae_max_combine_kernel(const int64_t *__restrict__ images, int n_images, int64_t hw,
+                       int64_t *__restrict__ out) {
+    for (int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x; q < hw;
+         q += (int64_t)gridDim.x * kThreads) {
+        int64_t m = images[q];
+        for (int i = 1; i < n_images; ++i) m = max(m, images[(int64_t)i * hw + q]);
+        out[q] = m;
+    }
+}
+
 // Dedicated, always-clean group buffers: [2][mask HW u32] + [2][G][HW] int64 (+ first_border).
 struct CornerState {
     int W = 0, H = 0;
@@ -391,5 +402,25 @@ ECC_API int ecc_sae_scatter(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
                            ecc::as_stream(stream), xy, t, n, width, height, sae);
     }
     ECC_CHECK_LAUNCH(ctx, "sae_scatter");
+    return ECC_OK;
+}
+
+ECC_API int ecc_sae_max_combine(ecc_ctx *ctx, const int64_t *images, int32_t n_images, int64_t hw,
+                                int64_t *out, ecc_stream_t stream) {
+    if (!ctx || !out || hw < 0 || n_images < 0 || (n_images > 0 && !images)) return ECC_ERR_INVALID;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    if (n_images == 0) {
+        ECC_CHECK_HIP(ctx, hipMemsetAsync(out, 0, hw * 8, s), "memset(sae)");
+        return ECC_OK;
+    }
+    if (hw == 0) return ECC_OK;
+    const int64_t blocks = std::min<int64_t>((hw + kThreads - 1) / kThreads, 4096);
+    {
+        ECC_TIMED(ctx, s, "sae_max_combine_kernel");
+        hipLaunchKernelGGL(sae_max_combine_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, images,
+                           n_images, hw, out);
+    }
+    ECC_CHECK_LAUNCH(ctx, "sae_max_combine");
     return ECC_OK;
 }

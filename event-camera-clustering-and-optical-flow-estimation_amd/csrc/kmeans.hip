@@ -329,3 +329,74 @@ ECC_API int ecc_kmeans_assign_f32(ecc_ctx *ctx, const float *xy, int64_t n_point
     ECC_CHECK_LAUNCH(ctx, "kmeans assign");
     return ECC_OK;
 }
+
+// ---- split form (multi-GPU: accumulate -> all-reduce(acc) -> update) ---------------------
+static Segs make_segs(int64_t n_segs, int64_t seg_stride, const int32_t *seg_counts) {
+    Segs segs{seg_counts, n_segs, seg_stride, n_segs * seg_stride};
+    if (!seg_counts) {
+        const int64_t n = n_segs * seg_stride;
+        segs.stride = 16384;
+        segs.n_segs = (n + segs.stride - 1) / segs.stride;
+        segs.n_dense = n;
+    }
+    return segs;
+}
+
+ECC_API int ecc_kmeans_accumulate_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs,
+                                       int64_t seg_stride, const int32_t *seg_counts,
+                                       const float *centroids, int32_t k, float threshold,
+                                       uint64_t *acc, const int32_t *state, ecc_stream_t stream) {
+    if (!ctx || !centroids || !acc || !state || k < 1 || k > kMaxK || n_segs < 0 || seg_stride < 1)
+        return ECC_ERR_INVALID;
+    const Segs segs = make_segs(n_segs, seg_stride, seg_counts);
+    if (segs.n_segs == 0) return ECC_OK;
+    if (!xy) return ECC_ERR_INVALID;
+    const int grid = grid_for(segs.n_segs);
+    if (segs.n_segs * segs.stride / grid >= (1ll << 24)) return ECC_ERR_INVALID;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    {
+        ECC_TIMED(ctx, s, "kmeans_xy16_kernel");
+        hipLaunchKernelGGL(kmeans_xy16_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
+                           centroids, k, threshold, reinterpret_cast<unsigned long long *>(acc),
+                           reinterpret_cast<const KmState *>(state), (uint8_t *)nullptr);
+    }
+    ECC_CHECK_LAUNCH(ctx, "kmeans accumulate");
+    return ECC_OK;
+}
+
+ECC_API int ecc_kmeans_update(ecc_ctx *ctx, uint64_t *acc, float *centroids, int32_t k, float tol,
+                              int32_t *state, ecc_stream_t stream) {
+    if (!ctx || !acc || !centroids || !state || k < 1 || k > kMaxK) return ECC_ERR_INVALID;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    {
+        ECC_TIMED(ctx, s, "kmeans_update_kernel");
+        hipLaunchKernelGGL(kmeans_update_kernel<unsigned long long>, dim3(1), dim3(64), 0, s,
+                           reinterpret_cast<unsigned long long *>(acc), centroids, k, tol,
+                           reinterpret_cast<KmState *>(state));
+    }
+    ECC_CHECK_LAUNCH(ctx, "kmeans update");
+    return ECC_OK;
+}
+
+ECC_API int ecc_kmeans_labels_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs,
+                                   int64_t seg_stride, const int32_t *seg_counts,
+                                   const float *centroids, int32_t k, float threshold,
+                                   uint8_t *labels, ecc_stream_t stream) {
+    if (!ctx || !centroids || !labels || k < 1 || k > kMaxK || n_segs < 0 || seg_stride < 1)
+        return ECC_ERR_INVALID;
+    const Segs segs = make_segs(n_segs, seg_stride, seg_counts);
+    if (segs.n_segs == 0) return ECC_OK;
+    if (!xy) return ECC_ERR_INVALID;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    {
+        ECC_TIMED(ctx, s, "kmeans_xy16_labels");
+        hipLaunchKernelGGL(kmeans_xy16_kernel<false>, dim3(grid_for(segs.n_segs)), dim3(kThreads), 0,
+                           s, xy, segs, centroids, k, threshold, (unsigned long long *)nullptr,
+                           (const KmState *)nullptr, labels);
+    }
+    ECC_CHECK_LAUNCH(ctx, "kmeans labels");
+    return ECC_OK;
+}

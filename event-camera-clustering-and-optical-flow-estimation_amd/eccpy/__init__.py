@@ -123,6 +123,10 @@ _sigs = {
     "ecc_kmeans_run_xy16": (C.c_int, [P, P, i64, i64, P, C.POINTER(KmeansCfg), P, P, P, P]),
     "ecc_kmeans_run_f32": (C.c_int, [P, P, i64, C.POINTER(KmeansCfg), P, P, P, P]),
     "ecc_kmeans_assign_f32": (C.c_int, [P, P, i64, P, i32, C.c_float, P, P]),
+    "ecc_kmeans_accumulate_xy16": (C.c_int, [P, P, i64, i64, P, P, i32, C.c_float, P, P, P]),
+    "ecc_kmeans_update": (C.c_int, [P, P, P, i32, C.c_float, P, P]),
+    "ecc_kmeans_labels_xy16": (C.c_int, [P, P, i64, i64, P, P, i32, C.c_float, P, P]),
+    "ecc_sae_max_combine": (C.c_int, [P, P, i32, i64, P, P]),
     "ecc_corner_cfg_default": (None, [C.POINTER(CornerCfg)]),
     "ecc_fast_detect": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, P]),
     "ecc_fast_detect_status": (C.c_int, [P, P]),
@@ -218,17 +222,21 @@ class DeviceArray:
 class Context:
     """ecc_ctx + a private stream."""
 
-    def __init__(self, device: int = 0, own_stream: bool = True):
+    def __init__(self, device: int = 0, own_stream: bool = True, stream: int | None = None):
         check(lib.ecc_set_device(device), "ecc_set_device")
         p = P()
         check(lib.ecc_ctx_create(C.byref(p), device), "ecc_ctx_create")
         self.ctx = p.value
         self.device = device
         self.stream = None
-        if own_stream:
+        self._own_stream = False
+        if stream is not None:  # an external hipStream_t (e.g. torch's current stream)
+            self.stream = stream
+        elif own_stream:
             s = P()
             check(lib.ecc_stream_create(C.byref(s)), "ecc_stream_create")
             self.stream = s.value
+            self._own_stream = True
 
     def sync(self):
         check(lib.ecc_stream_sync(self.stream), "sync")
@@ -240,9 +248,9 @@ class Context:
         if self.ctx:
             lib.ecc_ctx_destroy(self.ctx)
             self.ctx = None
-        if self.stream:
+        if self.stream and self._own_stream:
             lib.ecc_stream_destroy(self.stream)
-            self.stream = None
+        self.stream = None
 
     def __del__(self):
         try:

@@ -1,0 +1,68 @@
+"""Multi-GPU time-window sharding of the event stream.
+
+One process per GPU.  Rank r owns events [r*n, (r+1)*n) of the stream.  The exchanges:
+  * k-means: every iteration, the shards' exact integer partial sums (count, sum x, sum y per
+    centre) are all-reduced (SUM) and every rank applies the same update -> identical
+    centroids on all ranks, bit-identical to the single-GPU run;
+  * SAE hand-off: the shards' local final time surfaces are all-gathered and rank r starts from
+    the element-wise max over ranks < r (time is non-decreasing across shards, so max == last
+    writer) -> corner flags identical to the single-GPU run; only rank 0 skips the first slice.
+Downsample, detection and NMS are shard-local.  The tracker is sequential (replicas only).
+
+The functions here are transport- and compute-agnostic: `comm` wraps torch.distributed (RCCL on
+GPUs, gloo in the CPU tests) and the compute callables are libecc on the GPU (bench.py) or the
+oracle in tests/test_dist.py.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+
+def shard_bounds(n_total: int, world: int, rank: int, align: int = 16384) -> tuple[int, int]:
+    """Contiguous time windows; every boundary is a multiple of `align` (the corner slice, which
+    is also a multiple of the 8192-event downsample window), so shard-local slices are global
+    slices; the last rank takes the remainder."""
+    per = (n_total // world) // align * align
+    lo = rank * per
+    hi = n_total if rank == world - 1 else lo + per
+    return lo, hi
+
+
+class TorchComm:
+    """torch.distributed transport (backend chosen at init_process_group)."""
+
+    def __init__(self, dist):
+        self.dist = dist
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+
+    def allreduce_sum(self, tensor):
+        self.dist.all_reduce(tensor, op=self.dist.ReduceOp.SUM)
+
+    def allgather_cat(self, out_tensor, in_tensor):
+        """out_tensor: [world * numel] contiguous; rank i's in_tensor lands at slot i."""
+        self.dist.all_gather_into_tensor(out_tensor, in_tensor)
+
+    def barrier(self):
+        self.dist.barrier()
+
+
+def global_kmeans(accumulate: Callable[[], object], allreduce: Callable[[object], None],
+                  update: Callable[[object], bool], max_iters: int) -> int:
+    """Lloyd iterations over sharded points.  accumulate() returns this rank's partial sums
+    (zeroed accumulator filled for the current centroids), allreduce sums them over ranks,
+    update applies the step and returns True when converged (may also always return False
+    when the convergence flag lives on the device).  Returns the iterations run."""
+    it = 0
+    for it in range(1, max_iters + 1):
+        acc = accumulate()
+        allreduce(acc)
+        if update(acc):
+            break
+    return it
+
+
+def sae_base_for_rank(local_images_all, rank: int, combine: Callable[[object, int], object]):
+    """Initial SAE of `rank` = element-wise max of the local final SAEs of ranks < rank
+    (zeros for rank 0).  local_images_all: the all-gathered [world, H*W] images."""
+    return combine(local_images_all, rank)

@@ -147,6 +147,21 @@ int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_
                         uint8_t *labels, int32_t *iters_out, ecc_stream_t stream);
 int ecc_kmeans_run_f32(ecc_ctx *ctx, const float *xy, int64_t n_points, const ecc_kmeans_cfg *cfg,
                        float *centroids, uint8_t *labels, int32_t *iters_out, ecc_stream_t stream);
+/* Split form of one Lloyd iteration, for multi-GPU: each rank accumulates its shard's exact
+ * integer partial sums into acc (DEVICE uint64[3k]: count, sum x, sum y per centre; added to,
+ * so zero it first), the ranks all-reduce acc (SUM), then every rank applies the identical
+ * update (which also zeroes acc).  state: DEVICE int32[2] = {done, iterations}, zeroed by the
+ * caller before the first iteration; once done, further accumulate/update calls are no-ops. */
+int ecc_kmeans_accumulate_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                               const int32_t *seg_counts, const float *centroids, int32_t k,
+                               float threshold, uint64_t *acc, const int32_t *state,
+                               ecc_stream_t stream);
+int ecc_kmeans_update(ecc_ctx *ctx, uint64_t *acc, float *centroids, int32_t k, float tol,
+                      int32_t *state, ecc_stream_t stream);
+/* Final labels against given centroids (packed u16 points, segmented). */
+int ecc_kmeans_labels_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                           const int32_t *seg_counts, const float *centroids, int32_t k,
+                           float threshold, uint8_t *labels, ecc_stream_t stream);
 /* One assignment pass only (assign_to_centers): labels[i] in [0,k) or 255. */
 int ecc_kmeans_assign_f32(ecc_ctx *ctx, const float *xy, int64_t n_points, const float *centroids,
                           int32_t k, float threshold, uint8_t *labels, ecc_stream_t stream);
@@ -184,6 +199,11 @@ int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t 
 /* Synchronises `stream` and reports ECC_ERR_UNSORTED_TIME if the last ecc_fast_detect on
  * this context saw decreasing timestamps, else ECC_OK. */
 int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream);
+/* Multi-GPU SAE hand-off: out[q] = max over images[i*hw + q], i < n_images (the shards'
+ * local final SAEs of all LOWER ranks give a rank its exact initial SAE; max == last writer
+ * because time is non-decreasing across shards). */
+int ecc_sae_max_combine(ecc_ctx *ctx, const int64_t *images, int32_t n_images, int64_t hw,
+                        int64_t *out, ecc_stream_t stream);
 /* Final-SAE-only pass (used for the multi-GPU hand-off: per-shard local SAE). */
 int ecc_sae_scatter(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n, int32_t width,
                     int32_t height, int64_t *sae, ecc_stream_t stream);

@@ -798,3 +798,18 @@ ORC_API int orc_radius_search(const double *pts, int n, int D, const double *q, 
     }
     return k;
 }
+
+// Partial sums of one Lloyd iteration over a shard (for the multi-process tests): acc[3k] +=
+// (count, sum x, sum y) of the points assigned to each centre (assign_to_centers semantics).
+ORC_API int orc_kmeans_partial_xy16(const uint32_t *xy, int64_t n, const float *c, int k, float thr,
+                                    int64_t *acc) {
+    for (int64_t i = 0; i < n; ++i) {
+        const float px = (float)(xy[i] & 0xffffu), py = (float)(xy[i] >> 16);
+        const uint8_t a = assign_one(px, py, c, k, thr);
+        if (a == 255) continue;
+        acc[3 * a] += 1;
+        acc[3 * a + 1] += (int64_t)(xy[i] & 0xffffu);
+        acc[3 * a + 2] += (int64_t)(xy[i] >> 16);
+    }
+    return 0;
+}

@@ -47,6 +47,7 @@ _sigs = {
     "orc_optics": (C.c_int, [P, i32, i32, i32, f64, P, P]),
     "orc_get_cluster_indices": (C.c_int, [P, i32, f64, P]),
     "orc_radius_search": (C.c_int, [P, i32, i32, P, f64, P, i32]),
+    "orc_kmeans_partial_xy16": (C.c_int, [P, i64, P, i32, f32, P]),
 }
 for _n, (_r, _a) in _sigs.items():
     f = getattr(lib, _n)
@@ -220,3 +221,11 @@ def radius_search(pts, q, r):
     out = np.zeros(n, np.int64)
     k = lib.orc_radius_search(_p(pts), n, d, _p(q), r, _p(out), n)
     return list(out[:k])
+
+
+def kmeans_partial_xy16(xy, centroids, thr=50.0):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    c = np.ascontiguousarray(centroids, np.float32)
+    acc = np.zeros(3 * (c.size // 2), np.int64)
+    lib.orc_kmeans_partial_xy16(_p(xy), len(xy), _p(c), c.size // 2, thr, _p(acc))
+    return acc
