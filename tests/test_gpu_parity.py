@@ -401,3 +401,54 @@ def test_eps_duplicates_and_kdtree_kat(ecc, gpu):
                 q = np.array([q[0] + shift, 0.0])
             i = int(np.where((pts == q).all(1))[0][0])
             assert list(nbr[off[i]:off[i + 1]]) == expected, (name, q)
+
+
+# ------------------------------------------------------------------------------ multi-GPU building blocks
+def test_split_kmeans_equals_fused(ecc, orc, gpu):
+    """accumulate -> (all-reduce) -> update, with two 'shards' summed on one device, equals the
+    fused single-device loop bit for bit (integer partial sums)."""
+    xy, rep_xy, u = _reps(ecc, orc, n=300_000, seed=13)
+    nw = len(u)
+    half = nw // 2
+    k, iters = 16, 7
+    c0 = _init_centroids(k, 9)
+    o_c, o_lab, _ = orc.kmeans_run_xy16(np.concatenate([rep_xy[w * 8192: w * 8192 + u[w]] for w in range(nw)]), c0, iters)
+    d_rep, d_u = dev(ecc, rep_xy), dev(ecc, u)
+    d_c = dev(ecc, c0)
+    acc = ecc.DeviceArray.zeros(3 * k, np.uint64)
+    st = ecc.DeviceArray.zeros(2, np.int32)
+    L = ecc.lib
+    for _ in range(iters):
+        # shard A = windows [0, half), shard B = windows [half, nw): same accumulator == all-reduce SUM
+        ecc.check(L.ecc_kmeans_accumulate_xy16(gpu.ctx, d_rep.ptr, half, 8192, d_u.ptr, d_c.ptr, k, 50.0, acc.ptr, st.ptr, gpu.stream))
+        ecc.check(L.ecc_kmeans_accumulate_xy16(gpu.ctx, d_rep.ptr + half * 8192 * 4, nw - half, 8192, d_u.ptr + half * 4,
+                                               d_c.ptr, k, 50.0, acc.ptr, st.ptr, gpu.stream))
+        ecc.check(L.ecc_kmeans_update(gpu.ctx, acc.ptr, d_c.ptr, k, -1.0, st.ptr, gpu.stream))
+    lab = ecc.DeviceArray(nw * 8192, np.uint8)
+    ecc.check(L.ecc_kmeans_labels_xy16(gpu.ctx, d_rep.ptr, nw, 8192, d_u.ptr, d_c.ptr, k, 50.0, lab.ptr, gpu.stream))
+    gpu.sync()
+    assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
+    g = lab.numpy()
+    assert (np.concatenate([g[w * 8192: w * 8192 + u[w]] for w in range(nw)]) == o_lab).all()
+    assert st.numpy()[1] == iters
+
+
+def test_sae_handoff_equals_single_stream(ecc, orc, gpu):
+    """Shard the stream in 3 time windows: local SAEs -> max over lower shards -> detection per
+    shard == detection over the whole stream."""
+    W, H = W_SMALL, H_SMALL
+    n = 16384 * 9
+    xy, t, _ = ecc.gen_events(n, seed=17)
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H)
+    shards = [(0, 16384 * 3), (16384 * 3, 16384 * 6), (16384 * 6, n)]
+    imgs = ecc.DeviceArray.zeros(len(shards) * W * H, np.int64)
+    for i, (lo, hi) in enumerate(shards):
+        ecc.check(ecc.lib.ecc_sae_scatter(gpu.ctx, dev(ecc, xy[lo:hi]).ptr, dev(ecc, t[lo:hi]).ptr, hi - lo, W, H,
+                                          imgs.ptr + i * W * H * 8, gpu.stream))
+    flags = []
+    for i, (lo, hi) in enumerate(shards):
+        base = ecc.DeviceArray(W * H, np.int64)
+        ecc.check(ecc.lib.ecc_sae_max_combine(gpu.ctx, imgs.ptr, i, W * H, base.ptr, gpu.stream))
+        f, _ = _fast_gpu(ecc, gpu, xy[lo:hi], t[lo:hi], W, H, first_detect=1 if i == 0 else 0, sae0=base.numpy())
+        flags.append(f)
+    assert (np.concatenate(flags) == o_flags).all()
