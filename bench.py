@@ -175,18 +175,23 @@ def main():
         "downsample_hash_kernel": 4.0 * n + 4.0 * n_reps + 8.0 * n_win,
         "kmeans_xy16_kernel": 4.0 * n_reps,
         "kmeans_xy16_labels": 5.0 * n_reps,
-        "sae_build_kernel": 12.0 * n / per_step_launches,
-        "arc_test_kernel": 5.0 * n / per_step_launches,
+        "bin_hist_kernel": 12.0 * n,
+        "bin_scatter_kernel": 28.0 * n,
+        "tile_build_kernel": 16.0 * n / per_step_launches,
+        "arc_test_kernel": 9.0 * n / per_step_launches,
         "nms_kernel": 1.0 * n,
         "kmeans_update_kernel": 0.0,
     }.get(dominant, 0.0)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    # HBM bytes per launch of the same kernel from the newest committed PMC summary
+    # (scripts/gpu_profile.sh + scripts/traffic.py; PMC passes cannot run inside this process)
     traffic = None
-    tfile = ROOT / "profiles" / "traffic_r01.json"
-    if tfile.exists():
+    tfiles = sorted((ROOT / "profiles").glob("*_traffic.json"))
+    if tfiles:
         try:
-            traffic = json.loads(tfile.read_text()).get(dominant)
-        except Exception:
+            rec = json.loads(tfiles[-1].read_text()).get(dominant)
+            traffic = round(rec["bytes_per_launch"]) if rec else None
+        except (ValueError, KeyError, TypeError):
             traffic = None
 
     # tracker (sequential over slices): reported separately, µs per slice

@@ -9,16 +9,24 @@
 // Exact batch semantics for a whole batch in few launches.  The arc test of an event in slice
 // s must see V(q,s) = t of the last event at pixel q with index < end(s).  Slices are
 // processed in GROUPS of G = 32.  For the group being tested we keep
-//   mask[q]    : u32 bitmask of the group's slices that touched q   (atomicOr)
-//   M[j][q]    : max t at q within slice j of the group              (atomicMax, int64)
+//   mask[q]    : u32 bitmask of the group's slices that touched q
+//   M[j][q]    : max t at q within slice j of the group (valid only where mask bit j is set)
 //   B[q]       : SAE before the group (the caller's `sae` buffer, updated in place)
 // so V(q,s) = M[j*][q] with j* = highest set bit of mask[q] & ((2 << j) - 1), else B[q]
 // (timestamps are non-decreasing, so max == last writer; a device check enforces it).
-// Two ping-pong buffer sets let one launch build group g while folding group g-1 into B, and
-// the next launch test group g while resetting group g-1's entries (sparse, per event), so
-// the buffers are clean between calls without full-image memsets:
-//   K_build(g):  build(g) + fold(g-1)          K_test(g): arc(g) + clean(g-1)
-// => 2 launches per 32 slices (524288 events) instead of 2 per slice.
+//
+// Locality.  The batch is counting-sorted by (group, 16x16-pixel TILE) into 4-byte keys
+// (event index within the group << 8 | pixel within the tile) + timestamps:
+// per-slice LDS histograms -> scan -> per-slice scatter.  Then per group:
+//   tile_build(g): one 1024-lane workgroup per tile OWNS that tile's 256 pixels: it folds group
+//                  g-1 into B, accumulates mask/M of its bin with LDS atomics and writes them
+//                  back with plain stores — no global atomics and no reset pass (M is only ever
+//                  read where the same group's mask bit is set);
+//   arc_test(g):   one workgroup per WORK ITEM (<= 4096 events of one tile): it stages the
+//                  tile's 24x24 neighbourhood — mask, B and the set M entries compacted per
+//                  pixel as u32 offsets from the group's first timestamp — in LDS, then tests
+//                  one event per lane against LDS only.  Hot tiles split into several items.
+// Two ping-pong buffer sets: tile_build(g) reads set (g-1)&1 and writes set g&1.
 //
 // Arc test: the reference loop "exists i,s: T[c(i)]>=T[c(i-1)], T[c(i+s-1)]>=T[c(i+s)], and
 // every T outside the streak < min(streak)" reduces to "the s largest values are strictly
@@ -29,20 +37,49 @@
 // Algorithmic bytes: 12 B/event in (xy + t) + 1 B/event out (corner flag).
 #include "ecc_internal.hpp"
 
+#include <map>
+#include <mutex>
+
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kGroup = 32;  // slices per group (mask bits)
+constexpr int kBuildThreads = 1024;
+constexpr int kBuildUnroll = 4;
+constexpr int kArcThreads = 512;
+constexpr int kItemEvents = 2048;  // events per arc work item
+constexpr int kGroup = 32;         // slices per group (mask bits)
+constexpr int kTile = 16;          // tile edge (pixels)
+constexpr int kTilePix = kTile * kTile;
+constexpr int kHalo = 4;           // circle radius
+constexpr int kWin = kTile + 2 * kHalo;  // 24
+constexpr int kWinPix = kWin * kWin;     // 576
+constexpr int kStageBatch = 12;          // staging loads in flight per lane
+constexpr int kMaxTiles = 8191;          // bins per group = n_tiles + 1 (8192 fit an LDS histogram)
+constexpr int kMaxSlice = 1 << 19;       // group-local event index must fit 24 bits
 constexpr int64_t kEmptyT = INT64_MIN;
 
 struct CornerGeom {
     int W, H, S, margin, border_mode, first_detect;
+    int tiles_x, n_tiles;  // bin n_tiles of each group holds the events outside the sensor
+    float inv_S;
     int64_t n, n_slices;
 };
 
 struct GroupBufs {
     uint32_t *mask;  // [H*W]
     int64_t *M;      // [kGroup][H*W]
+};
+
+// Batch sorted by (group, tile): bin b of group g is [bin_off[g*nb+b], bin_off[g*nb+b+1]).
+struct Sorted {
+    uint32_t *key;       // (event index - first event of the group) << 8 | y%16*16 + x%16
+    int64_t *t;
+    int32_t *bin_count;  // [n_bins]
+    int32_t *cursor;     // [n_bins]
+    int64_t *bin_off;    // [n_bins + 1]
+    int32_t *n_items;    // [n_bins] work items per bin
+    int64_t *item_off;   // [n_bins + 1]
+    uint32_t *items;     // bin-in-group | chunk << 13
 };
 
 __constant__ int8_t c3dy[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -54,59 +91,178 @@ __device__ __forceinline__ bool is_border(int x, int y, const CornerGeom &g) {
     return x < g.margin || x >= g.W - g.margin || y < g.margin || y >= g.H - g.margin;
 }
 
-// Build group `grp` (events of its slices) into buffer set `cur`; fold group grp-1 (buffer
-// set `prv`) into B.  One thread per event slot of a group.
+__device__ __forceinline__ int tile_of(uint32_t v, const CornerGeom &g) {
+    const int x = ecc::xy_x(v), y = ecc::xy_y(v);
+    if (x >= g.W || y >= g.H) return g.n_tiles;
+    return (y / kTile) * g.tiles_x + x / kTile;
+}
+
+__device__ __forceinline__ uint32_t tile_key(uint32_t v, uint32_t e_local) {
+    return (e_local << 8) | (uint32_t)((ecc::xy_y(v) % kTile) * kTile + ecc::xy_x(v) % kTile);
+}
+
+// floor(el / S) for el < 2^24 (float estimate, then exact correction).
+__device__ __forceinline__ int slice_in_group(uint32_t el, const CornerGeom &g) {
+    uint32_t q = (uint32_t)((float)el * g.inv_S);
+    const uint32_t S = (uint32_t)g.S;
+    q = (q * S > el) ? q - 1 : q;
+    q = ((q + 1) * S <= el) ? q + 1 : q;
+    return (int)q;
+}
+
+// 1. Per-slice tile histogram (+ time-order check, first border index per slice for Q11).
 __global__ void __launch_bounds__(kThreads)
-sae_build_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g,
-                 int64_t grp, GroupBufs cur, GroupBufs prv, int64_t *__restrict__ B,
-                 int32_t *__restrict__ first_border, int32_t *__restrict__ err) {
-    const int64_t slot = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    const int64_t grp_events = (int64_t)kGroup * g.S;
+bin_hist_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g,
+                Sorted so, int32_t *__restrict__ first_border, int32_t *__restrict__ err) {
+    extern __shared__ int32_t hist[];  // [nb]
+    const int64_t s = blockIdx.x;
+    const int64_t lo = s * g.S, hi = (lo + g.S < g.n) ? lo + g.S : g.n;
+    const int64_t grp = s / kGroup;
+    const int nb = g.n_tiles + 1;
+    for (int b = threadIdx.x; b < nb; b += kThreads) hist[b] = 0;
+    __syncthreads();
+    bool bad = false;
+    int fb = 0x7fffffff;
+    for (int64_t e = lo + threadIdx.x; e < hi; e += kThreads) {
+        const uint32_t v = xy[e];
+        atomicAdd(&hist[tile_of(v, g)], 1);
+        if (e > 0 && t[e - 1] > t[e]) bad = true;
+        if (is_border(ecc::xy_x(v), ecc::xy_y(v), g)) fb = min(fb, (int)(e - lo));
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) *err = 1;
+    if (g.border_mode == 1) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) fb = min(fb, __shfl_xor(fb, o));
+        if ((threadIdx.x & 63) == 0 && fb != 0x7fffffff) atomicMin(&first_border[s], fb);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += kThreads)
+        if (hist[b]) atomicAdd(&so.bin_count[grp * nb + b], hist[b]);
+}
+
+// 2. Scatter keys + timestamps into (group, tile) order; order inside a bin is irrelevant.
+__global__ void __launch_bounds__(kThreads)
+bin_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g,
+                   Sorted so) {
+    extern __shared__ int64_t lds64[];
+    const int nb = g.n_tiles + 1;
+    int64_t *base = lds64;                                   // [nb]
+    int32_t *cnt = reinterpret_cast<int32_t *>(lds64 + nb);  // [nb]
+    const int64_t s = blockIdx.x;
+    const int64_t lo = s * g.S, hi = (lo + g.S < g.n) ? lo + g.S : g.n;
+    const int64_t grp = s / kGroup;
+    const int64_t grp_first = grp * kGroup * (int64_t)g.S;
+    for (int b = threadIdx.x; b < nb; b += kThreads) cnt[b] = 0;
+    __syncthreads();
+    for (int64_t e = lo + threadIdx.x; e < hi; e += kThreads) atomicAdd(&cnt[tile_of(xy[e], g)], 1);
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += kThreads) {
+        const int c = cnt[b];
+        if (c) base[b] = so.bin_off[grp * nb + b] + atomicAdd(&so.cursor[grp * nb + b], c);
+        cnt[b] = 0;
+    }
+    __syncthreads();
+    for (int64_t e = lo + threadIdx.x; e < hi; e += kThreads) {
+        const uint32_t v = xy[e];
+        const int b = tile_of(v, g);
+        const int64_t pos = base[b] + atomicAdd(&cnt[b], 1);
+        so.key[pos] = tile_key(v, (uint32_t)(e - grp_first));
+        so.t[pos] = t[e];
+    }
+}
+
+// 3a. Work items of the arc test: ceil(count / kItemEvents) per in-sensor bin.
+__global__ void __launch_bounds__(kThreads)
+item_count_kernel(CornerGeom g, Sorted so, int64_t n_bins) {
+    const int64_t gb = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (gb >= n_bins) return;
+    const int b = (int)(gb % (g.n_tiles + 1));
+    so.n_items[gb] = (b == g.n_tiles) ? 0 : (so.bin_count[gb] + kItemEvents - 1) / kItemEvents;
+}
+
+__global__ void __launch_bounds__(kThreads)
+item_fill_kernel(CornerGeom g, Sorted so, int64_t n_bins) {
+    const int64_t gb = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (gb >= n_bins) return;
+    const uint32_t b = (uint32_t)(gb % (g.n_tiles + 1));
+    const int m = so.n_items[gb];
+    const int64_t o = so.item_off[gb];
+    for (int c = 0; c < m; ++c) so.items[o + c] = b | ((uint32_t)c << 13);
+}
+
+__device__ __forceinline__ void tile_origin(const CornerGeom &g, int tile, int &x0, int &y0) {
+    x0 = (tile % g.tiles_x) * kTile;
+    y0 = (tile / g.tiles_x) * kTile;
+}
+
+// 3. Build group `grp` for one tile (and fold group grp-1 into B for the same pixels).
+__global__ void __launch_bounds__(kBuildThreads)
+tile_build_kernel(CornerGeom g, int64_t grp, Sorted so, GroupBufs cur, GroupBufs prv,
+                  int64_t *__restrict__ B) {
+    __shared__ int64_t mloc[kGroup][kTilePix];  // 64 KiB
+    __shared__ uint32_t mask_l[kTilePix];
+    const int tile = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int p = tid % kTilePix, quarter = tid / kTilePix;  // 4 lanes per pixel
+    int x0, y0;
+    tile_origin(g, tile, x0, y0);
+    const int px = x0 + p % kTile, py = y0 + p / kTile;
+    const bool own = px < g.W && py < g.H;
     const int64_t HW = (int64_t)g.H * g.W;
-    // build(grp)
-    {
-        const int64_t e = grp * grp_events + slot;
-        if (e < g.n) {
-            const uint32_t v = xy[e];
-            const int64_t te = t[e];
-            if (e > 0 && t[e - 1] > te) *err = 1;
-            const int x = ecc::xy_x(v), y = ecc::xy_y(v);
-            const int64_t s = e / g.S;
-            const int j = (int)(s - grp * kGroup);
-            if (x < g.W && y < g.H) {
-                const int64_t q = (int64_t)y * g.W + x;
-                atomicOr(&cur.mask[q], 1u << j);
-                atomicMax(reinterpret_cast<long long *>(&cur.M[(int64_t)j * HW + q]), (long long)te);
-            }
-            if (g.border_mode == 1 && is_border(x, y, g))
-                atomicMin(&first_border[s], (int32_t)(e - s * g.S));
+    const int64_t q = (int64_t)py * g.W + px;
+    if (quarter == 0) {
+        if (own && grp > 0) {
+            const uint32_t mk = prv.mask[q];
+            if (mk) B[q] = prv.M[(int64_t)(31 - __clz(mk)) * HW + q];
+        }
+        mask_l[p] = 0u;
+    }
+#pragma unroll
+    for (int jj = 0; jj < kGroup / 4; ++jj) mloc[quarter * (kGroup / 4) + jj][p] = kEmptyT;
+    __syncthreads();
+    const int nb = g.n_tiles + 1;
+    const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
+    for (int64_t i0 = b0; i0 < b1; i0 += kBuildUnroll * kBuildThreads) {
+        uint32_t k[kBuildUnroll];
+        int64_t tv[kBuildUnroll];
+#pragma unroll
+        for (int u = 0; u < kBuildUnroll; ++u) {
+            const int64_t i = i0 + u * kBuildThreads + tid;
+            k[u] = (i < b1) ? so.key[i] : 0xffffffffu;
+            tv[u] = (i < b1) ? so.t[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kBuildUnroll; ++u) {
+            if (k[u] == 0xffffffffu) continue;
+            const int lp = (int)(k[u] & 255u);
+            const int j = slice_in_group(k[u] >> 8, g);
+            atomicOr(&mask_l[lp], 1u << j);
+            atomicMax(reinterpret_cast<long long *>(&mloc[j][lp]), (long long)tv[u]);
         }
     }
-    // fold(grp - 1): the last writer of each pixel of the previous group updates B
-    if (grp > 0) {
-        const int64_t e = (grp - 1) * grp_events + slot;
-        if (e < g.n) {
-            const uint32_t v = xy[e];
-            const int x = ecc::xy_x(v), y = ecc::xy_y(v);
-            if (x < g.W && y < g.H) {
-                const int64_t q = (int64_t)y * g.W + x;
-                const int j = (int)(e / g.S - (grp - 1) * kGroup);
-                const uint32_t mk = prv.mask[q];
-                if (31 - __clz(mk) == j) {
-                    const int64_t te = t[e];
-                    if (prv.M[(int64_t)j * HW + q] == te) B[q] = te;
-                }
-            }
+    __syncthreads();
+    if (own) {
+        const uint32_t mk_all = mask_l[p];
+        if (quarter == 0) cur.mask[q] = mk_all;
+        uint32_t mk = (mk_all >> (quarter * 8)) & 0xffu;
+        while (mk) {
+            const int j = quarter * 8 + __ffs(mk) - 1;
+            mk &= mk - 1;
+            cur.M[(int64_t)j * HW + q] = mloc[j][p];
         }
     }
 }
 
-// V(q, j): SAE value at pixel q as seen by slice j of the current group.
-__device__ __forceinline__ int64_t sae_at(int64_t q, uint32_t below, const GroupBufs &cur,
-                                          const int64_t *__restrict__ B, int64_t HW) {
-    const uint32_t mk = cur.mask[q] & below;
-    if (mk) return cur.M[(int64_t)(31 - __clz(mk)) * HW + q];
-    return B[q];
+// Fold of the last group into B.
+__global__ void __launch_bounds__(kThreads)
+tile_fold_kernel(CornerGeom g, GroupBufs buf, int64_t *__restrict__ B) {
+    int x0, y0;
+    tile_origin(g, blockIdx.x, x0, y0);
+    const int px = x0 + threadIdx.x % kTile, py = y0 + threadIdx.x / kTile;
+    if (px >= g.W || py >= g.H) return;
+    const int64_t q = (int64_t)py * g.W + px;
+    const uint32_t mk = buf.mask[q];
+    if (mk) B[q] = buf.M[(int64_t)(31 - __clz(mk)) * (int64_t)g.H * g.W + q];
 }
 
 template <int N, int SMIN, int SMAX>
@@ -136,86 +292,273 @@ __device__ __forceinline__ bool arc_streak(const int64_t (&v)[N]) {
     return ok;
 }
 
-// Arc test for group `grp` (buffer set cur) + sparse reset of group grp-1 (buffer set prv).
-__global__ void __launch_bounds__(kThreads)
-arc_test_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g,
-                int64_t grp, GroupBufs cur, GroupBufs prv, const int64_t *__restrict__ B,
-                const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags) {
-    const int64_t slot = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    const int64_t grp_events = (int64_t)kGroup * g.S;
-    const int64_t HW = (int64_t)g.H * g.W;
-    {
-        const int64_t e = grp * grp_events + slot;
-        if (e < g.n) {
-            const uint32_t v = xy[e];
-            const int x = ecc::xy_x(v), y = ecc::xy_y(v);
-            const int64_t s = e / g.S;
-            const int j = (int)(s - grp * kGroup);
-            bool test = s >= g.first_detect && !is_border(x, y, g);
-            if (test && g.border_mode == 1) test = (e - s * g.S) < first_border[s];
-            uint8_t corner = 0;
-            if (test) {
-                const uint32_t below = (j == 31) ? 0xffffffffu : ((2u << j) - 1u);
-                const int64_t q0 = (int64_t)y * g.W + x;
-                int64_t v3[16];
+// ---- fast arc test on 32-bit keys ------------------------------------------------------------
+// Values are mapped to v' = clamp(v - L, 0, 2^27 - 1) with L = t_last(group) - (2^27 - 1) and
+// keyed as (v' << IB) | position.  Clamping merges the values <= L into ties at 0.  This cannot
+// change the outcome when at least SMAX+1 values are unclamped: a witness k (the largest value
+// outside the arc) has <= SMAX values above it, so it and its arc are unclamped and compare as
+// before, while a clamped k' has every unclamped value (> SMAX of them) above it in both
+// forms.  Otherwise (or when some value exceeds t_last) the exact int64 test runs.
+constexpr int kVBits = 27;
+constexpr uint32_t kVMax = (1u << kVBits) - 1u;
+
+// Batcher odd-even merge sort, descending; with compile-time padding and only the top outputs
+// used, dead compare-exchanges fold away.
+template <int N>
+__device__ __forceinline__ void sort_desc(uint32_t (&k)[N]) {
 #pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    v3[k] = sae_at(q0 + (int64_t)c3dy[k] * g.W + c3dx[k], below, cur, B, HW);
-                if (arc_streak<16, 3, 6>(v3)) {
-                    int64_t v4[20];
+    for (int p = 1; p < N; p += p) {
 #pragma unroll
-                    for (int k = 0; k < 20; ++k)
-                        v4[k] = sae_at(q0 + (int64_t)c4dy[k] * g.W + c4dx[k], below, cur, B, HW);
-                    corner = arc_streak<20, 4, 8>(v4) ? 1 : 0;
+        for (int kk = p; kk > 0; kk /= 2) {
+#pragma unroll
+            for (int j = kk % p; j + kk < N; j += kk + kk) {
+#pragma unroll
+                for (int i = 0; i < kk; ++i) {
+                    if (i + j + kk < N && (i + j) / (p + p) == (i + j + kk) / (p + p)) {
+                        const uint32_t a = k[i + j], b = k[i + j + kk];
+                        k[i + j] = a > b ? a : b;
+                        k[i + j + kk] = a > b ? b : a;
+                    }
                 }
             }
-            flags[e] = corner;
         }
     }
-    if (grp > 0) {
-        const int64_t e = (grp - 1) * grp_events + slot;
-        if (e < g.n) {
-            const uint32_t v = xy[e];
-            const int x = ecc::xy_x(v), y = ecc::xy_y(v);
-            if (x < g.W && y < g.H) {
-                const int64_t q = (int64_t)y * g.W + x;
-                const int j = (int)(e / g.S - (grp - 1) * kGroup);
-                prv.mask[q] = 0u;
-                prv.M[(int64_t)j * HW + q] = kEmptyT;
+}
+
+// 1 = arc found, 0 = none, -1 = undecidable on clamped keys (fewer than SMAX+1 unclamped and
+// the clamped values not all equal).
+template <int N, int NP, int IB, int SMIN, int SMAX>
+__device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
+    sort_desc<NP>(k);
+    if (!ties_exact && (k[SMAX] >> IB) == 0u) return -1;
+    constexpr uint32_t full = (1u << N) - 1u;
+    uint32_t m = 0;
+    bool ok = false;
+#pragma unroll
+    for (int s = 1; s <= SMAX; ++s) {
+        m |= 1u << (k[s - 1] & ((1u << IB) - 1u));
+        if (s >= SMIN) {
+            const bool sep = (k[s - 1] >> IB) > (k[s] >> IB);
+            const uint32_t rot = ((m << 1) | (m >> (N - 1))) & full;
+            ok |= sep && (__popc(m & ~rot) == 1);
+        }
+    }
+    return ok ? 1 : 0;
+}
+
+// Staged neighbourhood of one work item: per window pixel its group mask and the offset of its
+// entries in vals: vals[off] = B', vals[off + 1 + r] = M' of the r-th set slice bit.
+struct WinPix {
+    uint32_t mask;
+    uint32_t off;
+};
+
+constexpr int kValsCap = 18700;  // 576 + 32*576 = 19008 worst case; beyond -> exact path
+
+struct ArcLds {
+    WinPix pix[kWinPix];
+    uint32_t vals[kValsCap];
+    int32_t wave_tot[kArcThreads / 64];
+    int64_t wave_min[kArcThreads / 64];
+    int32_t exact_only;  // a value above t_last: clamped keys unusable
+    int32_t mixed;       // clamped values not all equal to the window minimum of B
+};
+
+__device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, int32_t *exact_flag,
+                                              int32_t *mixed_flag) {
+    if (v <= L) {
+        if (v != vz) *mixed_flag = 1;
+        return 0u;
+    }
+    const int64_t d = v - L;
+    if (d > (int64_t)kVMax) { *exact_flag = 1; return kVMax; }
+    return (uint32_t)d;
+}
+
+__device__ __forceinline__ uint32_t win_key(const ArcLds &L, int wp, uint32_t below) {
+    const WinPix pm = L.pix[wp];
+    return L.vals[pm.off + __popc(pm.mask & below)];
+}
+
+// exact int64 V from the global images (fallback)
+__device__ __forceinline__ int64_t glob_at(const ArcLds &L, int wp, int64_t q, uint32_t below,
+                                           const GroupBufs &cur, const int64_t *__restrict__ B,
+                                           int64_t HW) {
+    const uint32_t mk = L.pix[wp].mask & below;
+    if (!mk) return B[q];
+    return cur.M[(int64_t)(31 - __clz(mk)) * HW + q];
+}
+
+// 4. Arc test of one work item (<= kItemEvents tile-sorted events of group `grp`).
+__global__ void __launch_bounds__(kArcThreads)
+arc_test_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, Sorted so, GroupBufs cur,
+                const int64_t *__restrict__ B, const int32_t *__restrict__ first_border,
+                uint8_t *__restrict__ flags) {
+    __shared__ ArcLds L;
+    const int nb = g.n_tiles + 1;
+    const int64_t it0 = so.item_off[grp * nb], it1 = so.item_off[(grp + 1) * nb];
+    if (it0 + blockIdx.x >= it1) return;
+    const uint32_t item = so.items[it0 + blockIdx.x];
+    const int tile = (int)(item & 8191u), chunk = (int)(item >> 13);
+    const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
+    const int64_t i0 = b0 + (int64_t)chunk * kItemEvents;
+    const int64_t i1 = (i0 + kItemEvents < b1) ? i0 + kItemEvents : b1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t HW = (int64_t)g.H * g.W;
+    int x0, y0;
+    tile_origin(g, tile, x0, y0);
+    const int wx0 = x0 - kHalo, wy0 = y0 - kHalo;
+    const int64_t grp_first = grp * kGroup * (int64_t)g.S;
+    const int64_t grp_end = (grp + 1) * kGroup * (int64_t)g.S;
+    const int64_t Lt = t[(grp_end < g.n ? grp_end : g.n) - 1] - (int64_t)kVMax;
+    if (tid == 0) {
+        L.exact_only = 0;
+        L.mixed = 0;
+    }
+
+    // keys of the item (preloaded; the loads overlap the staging)
+    constexpr int kPerLane = kItemEvents / kArcThreads;
+    uint32_t keys[kPerLane];
+#pragma unroll
+    for (int u = 0; u < kPerLane; ++u) {
+        const int64_t i = i0 + tid + (int64_t)u * kArcThreads;
+        keys[u] = (i < i1) ? so.key[i] : 0xffffffffu;
+    }
+    // (a) window masks + B; entry counts 1 + popc(mask)
+    uint32_t mk_r[2] = {0u, 0u};
+    int64_t b_r[2] = {INT64_MAX, INT64_MAX};  // INT64_MAX: outside the sensor (never read)
+    int c_own = 0;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int wp = tid + r * kArcThreads;
+        if (wp < kWinPix) {
+            const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
+            const bool in = wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
+            const int64_t qq = (int64_t)wy * g.W + wx;
+            mk_r[r] = in ? cur.mask[qq] : 0u;
+            b_r[r] = in ? B[qq] : INT64_MAX;
+            c_own += 1 + __popc(mk_r[r]);
+        }
+    }
+    // (b) block exclusive scan of the per-thread entry counts
+    int incl = c_own;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    int64_t bmin = b_r[0] < b_r[1] ? b_r[0] : b_r[1];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t v = __shfl_xor(bmin, o);
+        bmin = v < bmin ? v : bmin;
+    }
+    if (lane == 63) L.wave_tot[wave] = incl;
+    if (lane == 0) L.wave_min[wave] = bmin;
+    __syncthreads();
+    int before = 0, total = 0;
+    int64_t vz = INT64_MAX;
+#pragma unroll
+    for (int w = 0; w < kArcThreads / 64; ++w) {
+        const int v = L.wave_tot[w];
+        before += (w < wave) ? v : 0;
+        total += v;
+        vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
+    }
+    const bool fits = total <= kValsCap;
+    int off = before + incl - c_own;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int wp = tid + r * kArcThreads;
+        if (wp < kWinPix) {
+            L.pix[wp].mask = mk_r[r];
+            L.pix[wp].off = (uint32_t)off;
+            if (fits) L.vals[off] = (b_r[r] == INT64_MAX) ? 0u : clamp_rel(b_r[r], Lt, vz, &L.exact_only, &L.mixed);
+            off += 1 + __popc(mk_r[r]);
+        }
+    }
+    __syncthreads();
+    // (c) stage M entries: pair (j, wp) per lane, j-major so a wave reads rows of one plane;
+    //     kStageBatch loads in flight per lane before their LDS stores
+    if (fits) {
+        constexpr int kPairs = kGroup * kWinPix;
+        constexpr int kIters = (kPairs + kArcThreads - 1) / kArcThreads;  // 36
+#pragma unroll
+        for (int r0 = 0; r0 < kIters; r0 += kStageBatch) {
+            int dst[kStageBatch];
+            int64_t val[kStageBatch];
+#pragma unroll
+            for (int u = 0; u < kStageBatch; ++u) {
+                const int pr = tid + (r0 + u) * kArcThreads;
+                dst[u] = -1;
+                val[u] = 0;
+                if (r0 + u < kIters && pr < kPairs) {
+                    const int j = pr / kWinPix, wp = pr - j * kWinPix;
+                    const WinPix pm = L.pix[wp];
+                    if ((pm.mask >> j) & 1u) {
+                        const int64_t qq = (int64_t)(wy0 + wp / kWin) * g.W + (wx0 + wp % kWin);
+                        dst[u] = (int)(pm.off + 1 + __popc(pm.mask & ((1u << j) - 1u)));
+                        val[u] = cur.M[(int64_t)j * HW + qq];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kStageBatch; ++u)
+                if (dst[u] >= 0) L.vals[dst[u]] = clamp_rel(val[u], Lt, vz, &L.exact_only, &L.mixed);
+        }
+    }
+    __syncthreads();
+    const bool fast = fits && !L.exact_only;
+    const bool ties_exact = !L.mixed;
+    // (d) one event per lane
+#pragma unroll 1
+    for (int u = 0; u < kPerLane; ++u) {
+        const uint32_t key = keys[u];
+        if (key == 0xffffffffu) break;
+        const int lp = (int)(key & 255u);
+        const uint32_t el = key >> 8;
+        const int x = x0 + lp % kTile, y = y0 + lp / kTile;
+        const int j = slice_in_group(el, g);
+        const int64_t s = grp * kGroup + j;
+        bool test = s >= g.first_detect && !is_border(x, y, g);
+        if (test && g.border_mode == 1) test = (int64_t)el - (int64_t)j * g.S < first_border[s];
+        if (!test) continue;
+        const uint32_t below = (j == 31) ? 0xffffffffu : ((2u << j) - 1u);
+        const int wp0 = (y - wy0) * kWin + (x - wx0);
+        int res = -1;
+        if (fast) {
+            uint32_t k3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) k3[k] = (win_key(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
+            res = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+            if (res == 1) {
+                uint32_t k4[32];
+#pragma unroll
+                for (int k = 0; k < 20; ++k) k4[k] = (win_key(L, wp0 + c4dy[k] * kWin + c4dx[k], below) << 5) | k;
+#pragma unroll
+                for (int k = 20; k < 32; ++k) k4[k] = 0u;
+                res = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
             }
         }
-    }
-}
-
-// Final fold / final reset of the last group (separate launches: fold reads what reset writes).
-__global__ void __launch_bounds__(kThreads)
-sae_tail_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g,
-                int64_t grp, GroupBufs buf, int64_t *__restrict__ B, int reset) {
-    const int64_t slot = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    const int64_t e = grp * (int64_t)kGroup * g.S + slot;
-    if (e >= g.n) return;
-    const int64_t HW = (int64_t)g.H * g.W;
-    const uint32_t v = xy[e];
-    const int x = ecc::xy_x(v), y = ecc::xy_y(v);
-    if (x >= g.W || y >= g.H) return;
-    const int64_t q = (int64_t)y * g.W + x;
-    const int j = (int)(e / g.S - grp * kGroup);
-    if (!reset) {
-        const uint32_t mk = buf.mask[q];
-        if (31 - __clz(mk) == j) {
-            const int64_t te = t[e];
-            if (buf.M[(int64_t)j * HW + q] == te) B[q] = te;
+        if (res < 0) {  // exact int64 test from the global images
+            const int64_t q0 = (int64_t)y * g.W + x;
+            int64_t v3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                v3[k] = glob_at(L, wp0 + c3dy[k] * kWin + c3dx[k], q0 + (int64_t)c3dy[k] * g.W + c3dx[k], below,
+                                cur, B, HW);
+            res = 0;
+            if (arc_streak<16, 3, 6>(v3)) {
+                int64_t v4[20];
+#pragma unroll
+                for (int k = 0; k < 20; ++k)
+                    v4[k] = glob_at(L, wp0 + c4dy[k] * kWin + c4dx[k], q0 + (int64_t)c4dy[k] * g.W + c4dx[k],
+                                    below, cur, B, HW);
+                res = arc_streak<20, 4, 8>(v4) ? 1 : 0;
+            }
         }
-    } else {
-        buf.mask[q] = 0u;
-        buf.M[(int64_t)j * HW + q] = kEmptyT;
+        if (res == 1) flags[grp_first + el] = 1;
     }
-}
-
-__global__ void fill_i64_kernel(int64_t *__restrict__ p, int64_t n, int64_t v) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x)
-        p[i] = v;
 }
 
 // Plain final-SAE scatter (no detection): sae[q] = max t.
@@ -242,28 +585,20 @@ sae_max_combine_kernel(const int64_t *__restrict__ images, int n_images, int64_t
     }
 }
 
-// Dedicated, always-clean group buffers: [2][mask HW u32] + [2][G][HW] int64 (+ first_border).
+// Per-context corner workspace: group images (sized by the sensor) and the sorted batch with
+// its bin tables (sized by the batch; grown, never shrunk).
 struct CornerState {
     int W = 0, H = 0;
-    void *mem = nullptr;
-    size_t bytes = 0;
-    GroupBufs set[2];
-    int32_t *first_border = nullptr;
-    int64_t fb_cap = 0;
+    void *img = nullptr;
+    GroupBufs set[2]{};
+    void *evt = nullptr;
+    size_t evt_bytes = 0;
 };
 
-CornerState *state_of(ecc_ctx *ctx);
+std::mutex g_state_mu;
+std::map<const ecc_ctx *, CornerState *> g_states;
 
-}  // namespace
-
-// one CornerState per context (kept outside ecc_ctx to keep the header light)
-#include <map>
-#include <mutex>
-static std::mutex g_state_mu;
-static std::map<const ecc_ctx *, CornerState *> g_states;
-
-namespace {
-CornerState *state_of(ecc_ctx *ctx) {
+CornerState *state_of(const ecc_ctx *ctx) {
     std::lock_guard<std::mutex> lk(g_state_mu);
     auto it = g_states.find(ctx);
     if (it != g_states.end()) return it->second;
@@ -272,48 +607,95 @@ CornerState *state_of(ecc_ctx *ctx) {
     return s;
 }
 
-int corner_state_reserve(ecc_ctx *ctx, CornerState *st, int W, int H, int64_t n_slices,
-                         hipStream_t s) {
-    if (st->W != W || st->H != H || !st->mem) {
-        if (st->mem) {
-            ECC_CHECK_HIP(ctx, hipDeviceSynchronize(), "sync(corner state)");
-            hipFree(st->mem);
-            st->mem = nullptr;
+// Sequential carve of one allocation; with base == nullptr it only measures.
+struct Carve {
+    char *base;
+    size_t used = 0;
+    template <class T> T *take(size_t count) {
+        T *r = base ? reinterpret_cast<T *>(base + used) : nullptr;
+        used += ecc::align_up(count * sizeof(T), 256);
+        return r;
+    }
+};
+
+Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_bins, int32_t **first_border,
+                    int64_t **scan_scratch) {
+    Sorted so{};
+    so.key = cv.take<uint32_t>((size_t)g.n);
+    so.t = cv.take<int64_t>((size_t)g.n);
+    so.bin_count = cv.take<int32_t>((size_t)n_bins);
+    so.cursor = cv.take<int32_t>((size_t)n_bins);
+    so.bin_off = cv.take<int64_t>((size_t)n_bins + 1);
+    so.n_items = cv.take<int32_t>((size_t)n_bins);
+    so.item_off = cv.take<int64_t>((size_t)n_bins + 1);
+    so.items = cv.take<uint32_t>((size_t)(g.n / kItemEvents + n_bins + 1));
+    *first_border = cv.take<int32_t>((size_t)g.n_slices);
+    *scan_scratch = cv.take<int64_t>((ecc::scan_scratch_bytes(n_bins) + 7) / 8);
+    return so;
+}
+
+int corner_state_reserve(ecc_ctx *ctx, CornerState *st, const CornerGeom &g, size_t evt_need) {
+    if (st->W != g.W || st->H != g.H || !st->img) {
+        if (st->img) {
+            ECC_CHECK_HIP(ctx, hipDeviceSynchronize(), "sync(corner images)");
+            (void)hipFree(st->img);
+            st->img = nullptr;
         }
-        const size_t HW = (size_t)W * H;
+        const size_t HW = (size_t)g.W * g.H;
         const size_t mask_b = ecc::align_up(HW * 4, 256);
         const size_t m_b = ecc::align_up(HW * 8 * kGroup, 256);
-        const size_t bytes = 2 * mask_b + 2 * m_b;
-        hipError_t e = hipMalloc(&st->mem, bytes);
-        if (e != hipSuccess) { st->mem = nullptr; ecc::hip_fail(ctx, e, "hipMalloc(corner state)"); return ECC_ERR_NOMEM; }
-        char *p = static_cast<char *>(st->mem);
+        hipError_t e = hipMalloc(&st->img, 2 * mask_b + 2 * m_b);
+        if (e != hipSuccess) {
+            st->img = nullptr;
+            ecc::hip_fail(ctx, e, "hipMalloc(corner images)");
+            return ECC_ERR_NOMEM;
+        }
+        char *p = static_cast<char *>(st->img);
         for (int b = 0; b < 2; ++b) {
             st->set[b].mask = reinterpret_cast<uint32_t *>(p + b * mask_b);
             st->set[b].M = reinterpret_cast<int64_t *>(p + 2 * mask_b + b * m_b);
         }
-        ECC_CHECK_HIP(ctx, hipMemsetAsync(p, 0, 2 * mask_b, s), "memset(masks)");
-        {
-            ECC_TIMED(ctx, s, "fill_i64_kernel");
-            hipLaunchKernelGGL(fill_i64_kernel, dim3(2048), dim3(256), 0, s,
-                               reinterpret_cast<int64_t *>(p + 2 * mask_b), (int64_t)(2 * m_b / 8), kEmptyT);
-        }
-        ECC_CHECK_LAUNCH(ctx, "fill(M)");
-        st->W = W;
-        st->H = H;
-        st->bytes = bytes;
+        st->W = g.W;
+        st->H = g.H;
     }
-    if (n_slices > st->fb_cap) {
-        if (st->first_border) {
-            ECC_CHECK_HIP(ctx, hipDeviceSynchronize(), "sync(first_border)");
-            hipFree(st->first_border);
+    if (evt_need > st->evt_bytes) {
+        if (st->evt) {
+            ECC_CHECK_HIP(ctx, hipDeviceSynchronize(), "sync(corner batch)");
+            (void)hipFree(st->evt);
+            st->evt = nullptr;
+            st->evt_bytes = 0;
         }
-        st->fb_cap = ecc::align_up((size_t)n_slices, 4096);
-        hipError_t e = hipMalloc(&st->first_border, st->fb_cap * 4);
-        if (e != hipSuccess) { st->first_border = nullptr; st->fb_cap = 0; return ECC_ERR_NOMEM; }
+        const size_t want = ecc::align_up(evt_need + evt_need / 8, 1 << 20);
+        hipError_t e = hipMalloc(&st->evt, want);
+        if (e != hipSuccess) {
+            st->evt = nullptr;
+            ecc::hip_fail(ctx, e, "hipMalloc(corner batch)");
+            return ECC_ERR_NOMEM;
+        }
+        st->evt_bytes = want;
     }
     return ECC_OK;
 }
+
+unsigned blocks_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
+
 }  // namespace
+
+namespace ecc {
+void corner_state_release(const ecc_ctx *ctx) {
+    CornerState *st = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_state_mu);
+        auto it = g_states.find(ctx);
+        if (it == g_states.end()) return;
+        st = it->second;
+        g_states.erase(it);
+    }
+    if (st->img) (void)hipFree(st->img);
+    if (st->evt) (void)hipFree(st->evt);
+    delete st;
+}
+}  // namespace ecc
 
 ECC_API void ecc_corner_cfg_default(ecc_corner_cfg *cfg) {
     if (!cfg) return;
@@ -334,47 +716,90 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
         return ECC_ERR_INVALID;
     if (cfg->margin < 4 || 2 * cfg->margin >= cfg->width || 2 * cfg->margin >= cfg->height)
         return ECC_ERR_INVALID;  // the circles reach 4 px from the event
-    if (cfg->slice_events < 1 || (cfg->border_mode != 0 && cfg->border_mode != 1))
+    if (cfg->slice_events < 1 || cfg->slice_events > kMaxSlice ||
+        (cfg->border_mode != 0 && cfg->border_mode != 1))
         return ECC_ERR_INVALID;
+    CornerGeom g{};
+    g.W = cfg->width;
+    g.H = cfg->height;
+    g.S = cfg->slice_events;
+    g.inv_S = 1.0f / (float)g.S;
+    g.margin = cfg->margin;
+    g.border_mode = cfg->border_mode;
+    g.first_detect = cfg->first_detect_slice;
+    g.tiles_x = (g.W + kTile - 1) / kTile;
+    g.n_tiles = g.tiles_x * ((g.H + kTile - 1) / kTile);
+    if (g.n_tiles > kMaxTiles) return ECC_ERR_INVALID;  // > 8191 16x16 tiles (~2.1 Mpixel)
+    g.n = n;
+    g.n_slices = (n + g.S - 1) / g.S;
+    if (g.n_slices > INT32_MAX) return ECC_ERR_INVALID;
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags, 0, 4, s), "memset(err flag)");
     if (n == 0) return ECC_OK;
-    CornerGeom g{cfg->width, cfg->height, cfg->slice_events, cfg->margin, cfg->border_mode,
-                 cfg->first_detect_slice, n, (n + cfg->slice_events - 1) / cfg->slice_events};
+    const int nb = g.n_tiles + 1;
+    const int64_t n_groups = (g.n_slices + kGroup - 1) / kGroup;
+    const int64_t n_bins = n_groups * nb;
     CornerState *st = state_of(ctx);
-    int rc = corner_state_reserve(ctx, st, g.W, g.H, g.n_slices, s);
+    int32_t *first_border = nullptr;
+    int64_t *scan_scratch = nullptr;
+    Carve measure{nullptr};
+    carve_sorted(measure, g, n_bins, &first_border, &scan_scratch);
+    int rc = corner_state_reserve(ctx, st, g, measure.used);
     if (rc) return rc;
+    Carve cv{static_cast<char *>(st->evt)};
+    const Sorted so = carve_sorted(cv, g, n_bins, &first_border, &scan_scratch);
+
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(corner_flags, 0, (size_t)n, s), "memset(flags)");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(so.bin_count, 0, (size_t)n_bins * 4, s), "memset(bins)");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(so.cursor, 0, (size_t)n_bins * 4, s), "memset(cursor)");
     if (g.border_mode == 1)
-        ECC_CHECK_HIP(ctx, hipMemsetAsync(st->first_border, 0x7f, g.n_slices * 4, s), "memset(fb)");
-    const int64_t grp_events = (int64_t)kGroup * g.S;
-    const int64_t n_groups = (n + grp_events - 1) / grp_events;
-    const int64_t blocks64 = (std::min<int64_t>(grp_events, n) + kThreads - 1) / kThreads;
-    if (blocks64 > INT32_MAX) return ECC_ERR_INVALID;
-    const dim3 grid((unsigned)blocks64);
+        ECC_CHECK_HIP(ctx, hipMemsetAsync(first_border, 0x7f, (size_t)g.n_slices * 4, s), "memset(fb)");
+    {
+        ECC_TIMED(ctx, s, "bin_hist_kernel");
+        hipLaunchKernelGGL(bin_hist_kernel, dim3((unsigned)g.n_slices), dim3(kThreads), nb * 4, s, xy, t,
+                           g, so, first_border, ctx->flags);
+    }
+    rc = ecc::exclusive_scan_i32_i64(ctx, so.bin_count, n_bins, so.bin_off, scan_scratch, s);
+    if (rc) return rc;
+    {
+        ECC_TIMED(ctx, s, "bin_scatter_kernel");
+        hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)g.n_slices), dim3(kThreads), nb * 12, s, xy,
+                           t, g, so);
+    }
+    {
+        ECC_TIMED(ctx, s, "item_count_kernel");
+        hipLaunchKernelGGL(item_count_kernel, dim3(blocks_for(n_bins, kThreads)), dim3(kThreads), 0, s, g,
+                           so, n_bins);
+    }
+    rc = ecc::exclusive_scan_i32_i64(ctx, so.n_items, n_bins, so.item_off, scan_scratch, s);
+    if (rc) return rc;
+    {
+        ECC_TIMED(ctx, s, "item_fill_kernel");
+        hipLaunchKernelGGL(item_fill_kernel, dim3(blocks_for(n_bins, kThreads)), dim3(kThreads), 0, s, g,
+                           so, n_bins);
+    }
+    // upper bound of the work items of one group: one partial item per tile + full items
+    const int64_t grp_events = std::min<int64_t>((int64_t)kGroup * g.S, n);
+    const int64_t arc_blocks = g.n_tiles + grp_events / kItemEvents;
+    if (arc_blocks > INT32_MAX) return ECC_ERR_INVALID;
     for (int64_t gi = 0; gi < n_groups; ++gi) {
         const GroupBufs cur = st->set[gi & 1], prv = st->set[(gi + 1) & 1];
         {
-            ECC_TIMED(ctx, s, "sae_build_kernel");
-            hipLaunchKernelGGL(sae_build_kernel, grid, dim3(kThreads), 0, s, xy, t, g, gi, cur, prv,
-                               sae, st->first_border, ctx->flags);
+            ECC_TIMED(ctx, s, "tile_build_kernel");
+            hipLaunchKernelGGL(tile_build_kernel, dim3(g.n_tiles), dim3(kBuildThreads), 0, s, g, gi, so, cur,
+                               prv, sae);
         }
         {
             ECC_TIMED(ctx, s, "arc_test_kernel");
-            hipLaunchKernelGGL(arc_test_kernel, grid, dim3(kThreads), 0, s, xy, t, g, gi, cur, prv,
-                               (const int64_t *)sae, (const int32_t *)st->first_border, corner_flags);
+            hipLaunchKernelGGL(arc_test_kernel, dim3((unsigned)arc_blocks), dim3(kArcThreads), 0, s, t, g, gi,
+                               so, cur, (const int64_t *)sae, (const int32_t *)first_border, corner_flags);
         }
     }
-    const int64_t last = n_groups - 1;
     {
-        ECC_TIMED(ctx, s, "sae_tail_kernel");
-        hipLaunchKernelGGL(sae_tail_kernel, grid, dim3(kThreads), 0, s, xy, t, g, last,
-                           st->set[last & 1], sae, 0);
-    }
-    {
-        ECC_TIMED(ctx, s, "sae_tail_kernel");
-        hipLaunchKernelGGL(sae_tail_kernel, grid, dim3(kThreads), 0, s, xy, t, g, last,
-                           st->set[last & 1], sae, 1);
+        ECC_TIMED(ctx, s, "tile_fold_kernel");
+        hipLaunchKernelGGL(tile_fold_kernel, dim3(g.n_tiles), dim3(kThreads), 0, s, g,
+                           st->set[(n_groups - 1) & 1], sae);
     }
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
     return ECC_OK;

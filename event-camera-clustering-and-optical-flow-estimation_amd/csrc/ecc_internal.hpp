@@ -61,6 +61,14 @@ struct TimedLaunch {
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// out[0..n] = exclusive scan of in[0..n) with out[n] = total (scratch: scan_scratch_bytes(n)).
+size_t scan_scratch_bytes(int64_t n);
+int exclusive_scan_i32_i64(ecc_ctx *ctx, const int32_t *in, int64_t n, int64_t *out, int64_t *scratch,
+                           hipStream_t s);
+
+// Frees the per-context corner-stage workspace (corners.hip); called by ecc_ctx_destroy.
+void corner_state_release(const ecc_ctx *ctx);
+
 // Launch-error check: kernel launches are asynchronous; this surfaces configuration errors.
 #define ECC_CHECK_LAUNCH(ctx, what)                                  \
     do {                                                             \

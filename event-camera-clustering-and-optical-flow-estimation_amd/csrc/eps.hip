@@ -243,83 +243,6 @@ eps_lists_kernel(const uint32_t *__restrict__ xy, SegView sv, double eps,
     }
 }
 
-// ---- exclusive scan int32 -> int64 (3 kernels: block sums, scan of sums, finish) ----------
-constexpr int kScanBlock = 1024;  // elements per block (4 per thread)
-
-__global__ void __launch_bounds__(kThreads)
-scan_block_sums(const int32_t *__restrict__ in, int64_t n, int64_t *__restrict__ bsum) {
-    __shared__ int64_t red[kThreads / 64];
-    const int64_t b0 = (int64_t)blockIdx.x * kScanBlock;
-    int64_t s = 0;
-    for (int k = 0; k < 4; ++k) {
-        const int64_t i = b0 + threadIdx.x * 4 + k;
-        if (i < n) s += in[i];
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-}
-
-__global__ void __launch_bounds__(kThreads)
-scan_sums(int64_t *__restrict__ bsum, int64_t nb) {
-    // single workgroup: exclusive scan in place, chunks of kThreads
-    __shared__ int64_t wtot[kThreads / 64];
-    int64_t carry = 0;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int64_t c0 = 0; c0 < nb; c0 += kThreads) {
-        const int64_t i = c0 + threadIdx.x;
-        const int64_t v = i < nb ? bsum[i] : 0;
-        int64_t inc = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int64_t y = __shfl_up(inc, o);
-            if (lane >= o) inc += y;
-        }
-        if (lane == 63) wtot[wave] = inc;
-        __syncthreads();
-        int64_t off = carry + inc - v, tot = 0;
-        for (int w = 0; w < kThreads / 64; ++w) {
-            if (w < wave) off += wtot[w];
-            tot += wtot[w];
-        }
-        if (i < nb) bsum[i] = off;
-        carry += tot;
-        __syncthreads();
-    }
-}
-
-__global__ void __launch_bounds__(kThreads)
-scan_finish(const int32_t *__restrict__ in, int64_t n, const int64_t *__restrict__ bsum,
-            int64_t *__restrict__ out) {
-    __shared__ int64_t wtot[kThreads / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t b0 = (int64_t)blockIdx.x * kScanBlock;
-    int64_t v[4], s = 0;
-    for (int k = 0; k < 4; ++k) {
-        const int64_t i = b0 + threadIdx.x * 4 + k;
-        v[k] = i < n ? in[i] : 0;
-        s += v[k];
-    }
-    int64_t inc = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int64_t y = __shfl_up(inc, o);
-        if (lane >= o) inc += y;
-    }
-    if (lane == 63) wtot[wave] = inc;
-    __syncthreads();
-    int64_t off = bsum[blockIdx.x] + inc - s;
-    for (int w = 0; w < wave; ++w) off += wtot[w];
-    for (int k = 0; k < 4; ++k) {
-        const int64_t i = b0 + threadIdx.x * 4 + k;
-        if (i < n) out[i] = off;
-        off += v[k];
-        if (i == n - 1) out[n] = off;  // total
-    }
-}
-
 int check_segs(const ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t stride,
                double eps) {
     if (!ctx || n_segs < 0 || stride < 1 || !(eps >= 0.0) || eps > 32767.0) return ECC_ERR_INVALID;
@@ -358,24 +281,12 @@ ECC_API int ecc_eps_lists(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int6
     if (!counts || !offsets || (nbr_cap > 0 && !nbr) || nbr_cap < 0) return ECC_ERR_INVALID;
     if (n_segs == 0) return ECC_OK;
     const int64_t n = n_segs * seg_stride;
-    const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
-    rc = ecc::ws_reserve(ctx, (size_t)nb * 8 + 256);
+    rc = ecc::ws_reserve(ctx, ecc::scan_scratch_bytes(n));
     if (rc) return rc;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t s = ecc::as_stream(stream);
-    auto *bsum = reinterpret_cast<int64_t *>(ctx->ws);
-    {
-        ECC_TIMED(ctx, s, "scan_block_sums");
-        hipLaunchKernelGGL(scan_block_sums, dim3((unsigned)nb), dim3(kThreads), 0, s, counts, n, bsum);
-    }
-    {
-        ECC_TIMED(ctx, s, "scan_sums");
-        hipLaunchKernelGGL(scan_sums, dim3(1), dim3(kThreads), 0, s, bsum, nb);
-    }
-    {
-        ECC_TIMED(ctx, s, "scan_finish");
-        hipLaunchKernelGGL(scan_finish, dim3((unsigned)nb), dim3(kThreads), 0, s, counts, n, bsum, offsets);
-    }
+    rc = ecc::exclusive_scan_i32_i64(ctx, counts, n, offsets, reinterpret_cast<int64_t *>(ctx->ws), s);
+    if (rc) return rc;
     ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + 2, 0, 4, s), "memset(eps err)");
     SegView sv{seg_counts, n_segs, seg_stride};
     const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 4096);

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Corner-stage probe: per-kernel times of ecc_fast_detect on the bench workload, plus the
+tile/bin statistics of the synthetic stream.  Usage: corner_probe.py [events] [W] [H]"""
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "event-camera-clustering-and-optical-flow-estimation_amd"))
+import eccpy as ecc  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1221 * 16384
+W = int(sys.argv[2]) if len(sys.argv) > 2 else 346
+H = int(sys.argv[3]) if len(sys.argv) > 3 else 260
+ctx = ecc.Context(0)
+xy, t, _ = ecc.gen_events(n, seed=1, width=W, height=H)
+x, y = xy & 0xffff, xy >> 16
+g = np.arange(n) // (32 * 16384)
+tile = (y // 16) * ((W + 15) // 16) + x // 16
+cnt = np.bincount(g * 10000 + tile)
+cnt = cnt[cnt > 0]
+print(f"bins/group stats: n_bins={len(cnt)} mean={cnt.mean():.0f} p50={np.median(cnt):.0f} "
+      f"p99={np.percentile(cnt, 99):.0f} max={cnt.max()}  items={int(np.ceil(cnt / 4096).sum())}")
+d_xy, d_t = ecc.DeviceArray.from_numpy(xy, ctx.stream), ecc.DeviceArray.from_numpy(t, ctx.stream)
+cfg = ecc.corner_cfg(width=W, height=H)
+sae = ecc.DeviceArray(W * H, np.int64)
+flags = ecc.DeviceArray(n, np.uint8)
+lib = ecc.lib
+for rep in range(2):
+    ecc.check(lib.ecc_ctx_set_timing(ctx.ctx, 1 if rep else 0))
+    ecc.check(lib.ecc_ctx_timing_reset(ctx.ctx))
+    ctx.fast_detect(d_xy, d_t, n, cfg, sae, flags)
+    ctx.sync()
+buf = ecc.C.create_string_buffer(1 << 16)
+ecc.check(lib.ecc_ctx_timing_report(ctx.ctx, buf, len(buf)))
+st = json.loads(buf.value.decode())
+tot = sum(v["total_ms"] for v in st.values())
+print(f"total {tot:.3f} ms; " + "; ".join(f"{k} {v['total_ms']:.3f} ms/{v['launches']} = {1e3*v['total_ms']/v['launches']:.1f} us"
+                                         for k, v in sorted(st.items(), key=lambda kv: -kv[1]['total_ms'])))
+print("corners:", int(flags.numpy().sum()))

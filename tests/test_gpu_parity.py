@@ -443,8 +443,10 @@ def test_sae_handoff_equals_single_stream(ecc, orc, gpu):
     shards = [(0, 16384 * 3), (16384 * 3, 16384 * 6), (16384 * 6, n)]
     imgs = ecc.DeviceArray.zeros(len(shards) * W * H, np.int64)
     for i, (lo, hi) in enumerate(shards):
-        ecc.check(ecc.lib.ecc_sae_scatter(gpu.ctx, dev(ecc, xy[lo:hi]).ptr, dev(ecc, t[lo:hi]).ptr, hi - lo, W, H,
+        d_xy, d_t = dev(ecc, xy[lo:hi]), dev(ecc, t[lo:hi])  # keep alive until the launch completes
+        ecc.check(ecc.lib.ecc_sae_scatter(gpu.ctx, d_xy.ptr, d_t.ptr, hi - lo, W, H,
                                           imgs.ptr + i * W * H * 8, gpu.stream))
+        gpu.sync()
     flags = []
     for i, (lo, hi) in enumerate(shards):
         base = ecc.DeviceArray(W * H, np.int64)
