@@ -28,6 +28,8 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxK = 64;
 constexpr int kMaxGrid = 2048;
+constexpr int kFastMaxK = 32;
+constexpr int kFlushBatches = 2;  // packed u64 slot fields stay exact for < 512 points
 
 struct KmState {
     int32_t done;
@@ -137,6 +139,145 @@ kmeans_xy16_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__re
     }
 }
 
+// ---- fast path for k <= 32: compile-time K, centroids in scalar registers -----------------
+// Exact argmin without a square root per centre: sqrt_rn is monotone, so the reference's
+// choice (first centre with the smallest sqrt_rn(d2), if below thr) is the first index of the
+// smallest d2 — unless an EARLIER centre has a larger d2 that rounds to the same square root.
+// That needs d2_i / d2_min <= ((1 + 2^-24) / (1 - 2^-24))^2 < 1 + 2^-22; the single pass
+// keeps m_prev = min d2 over the indices before the winner and takes the exact
+// sqrt-per-centre loop (assign_point's rule) only when m_prev <= m * (1 + 2^-20).
+template <int K>
+__device__ __forceinline__ uint32_t assign_fast(float px, float py, const float (&cx)[K],
+                                                const float (&cy)[K], float thr) {
+    float m = __builtin_inff(), m_prev = __builtin_inff();
+    int ia = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const float dx = __fsub_rn(cx[i], px), dy = __fsub_rn(cy[i], py);
+        const float d2 = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+        const bool lt = d2 < m;
+        m_prev = lt ? m : m_prev;
+        ia = lt ? i : ia;
+        m = lt ? d2 : m;
+    }
+    if (__builtin_expect(m_prev <= __fmul_rn(m, 1.0f + 0x1p-20f), 0)) {
+        uint32_t best = 255u;
+        float best_s = thr;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const float dx = __fsub_rn(cx[i], px), dy = __fsub_rn(cy[i], py);
+            const float s = ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
+            if (s < best_s) { best_s = s; best = (uint32_t)i; }
+        }
+        return best;
+    }
+    return ecc::sqrt_rn(m) < thr ? (uint32_t)ia : 255u;
+}
+
+__device__ __forceinline__ float uniform_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// Replicated accumulators: the per-WG flush goes to replica blockIdx % n_copies, which spreads
+// the same-address global atomics; the update kernel sums the replicas.
+constexpr int kAccStride = 3 * kMaxK;
+constexpr int kAccCopies = 8;
+
+// One Lloyd pass (kAccumulate) or the final labelling.  Accumulation: every point adds
+// (1 << 52) | (x << 26) | y to its cluster's u64 slot of its WAVE in LDS with one no-return
+// ds_add_u64 (64 lanes spread over <= K addresses).  The packed fields are exact while a slot
+// receives < 512 points of < 2^16 per coordinate, so each wave unpacks its slots into u64 lane
+// totals (lane c = cluster c) every kFlushBatches = 2 batches of 256 points.  One global u64
+// atomic per (WG, cluster, field) at the end, spread over n_copies accumulator replicas.
+// (Fusing the update into the last-arriving workgroup was measured slower: the device-scope
+// release every workgroup needs before arriving costs more than the separate 1-wave launch.)
+template <int K, bool kAccumulate>
+__global__ void __launch_bounds__(kThreads)
+kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__restrict__ cent, int k, float thr,
+                   unsigned long long *acc, int n_copies, const KmState *st, uint8_t *__restrict__ labels) {
+    if (kAccumulate && st->done) return;
+    __shared__ unsigned long long slot[kWaves][K];
+    __shared__ unsigned long long w_acc[3][K];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    float cx[K], cy[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
+        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+    }
+    if (kAccumulate) {
+        for (int i = tid; i < 3 * K; i += kThreads) (&w_acc[0][0])[i] = 0ull;
+        if (lane < K) slot[wave][lane] = 0ull;
+        __syncthreads();
+    }
+    unsigned long long tn = 0, tx = 0, ty = 0;  // lane c: wave totals of cluster c
+    int batches = 0;
+    auto flush = [&]() {  // the wave's own slots: LDS ops of one wave complete in order
+        if (lane < K) {
+            const unsigned long long w = slot[wave][lane];
+            slot[wave][lane] = 0ull;
+            tn += w >> 52;
+            tx += (w >> 26) & ((1ull << 26) - 1);
+            ty += w & ((1ull << 26) - 1);
+        }
+    };
+    const bool vec_ok = (segs.stride & 3) == 0;
+    for (int64_t s = blockIdx.x; s < segs.n_segs; s += gridDim.x) {
+        const int64_t cnt = segs.count(s);
+        const int64_t base = s * segs.stride;
+        for (int64_t j0 = 0; j0 < cnt; j0 += 4 * kThreads) {  // uniform trip count per WG
+            const int64_t j = j0 + 4 * tid;
+            uint32_t v[4];
+            if (vec_ok && j + 3 < cnt) {
+                const uint4 q = *reinterpret_cast<const uint4 *>(xy + base + j);
+                v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (j + e < cnt) ? xy[base + j + e] : 0u;
+            }
+            uint32_t lab[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                lab[e] = (j + e < cnt) ? assign_fast<K>((float)ecc::xy_x(v[e]), (float)ecc::xy_y(v[e]), cx, cy, thr)
+                                       : 255u;
+            if (kAccumulate) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (lab[e] < (uint32_t)K)
+                        atomicAdd(&slot[wave][lab[e]], (1ull << 52) | ((unsigned long long)ecc::xy_x(v[e]) << 26) |
+                                                          (unsigned long long)ecc::xy_y(v[e]));
+                if (++batches == kFlushBatches) {
+                    flush();
+                    batches = 0;
+                }
+            }
+            if (labels) {
+                if (j + 3 < cnt && ((base + j) & 3) == 0) {
+                    const uint32_t pk = lab[0] | (lab[1] << 8) | (lab[2] << 16) | (lab[3] << 24);
+                    *reinterpret_cast<uint32_t *>(labels + base + j) = pk;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (j + e < cnt) labels[base + j + e] = (uint8_t)lab[e];
+                }
+            }
+        }
+    }
+    if (!kAccumulate) return;
+    flush();
+    if (lane < K && tn) {
+        atomicAdd(&w_acc[0][lane], tn);
+        atomicAdd(&w_acc[1][lane], tx);
+        atomicAdd(&w_acc[2][lane], ty);
+    }
+    __syncthreads();
+    if (tid < 3 * k) {
+        const int f = tid / k, c = tid - f * k;
+        const unsigned long long sum = w_acc[f][c];
+        if (sum) atomicAdd(&acc[(int)(blockIdx.x % n_copies) * kAccStride + 3 * c + f], sum);
+    }
+}
+
 // float-input variant (reference data layout: interleaved float x,y): fp64 LDS + global
 // atomics (order-dependent only at the 1e-16 relative level).
 template <bool kAccumulate>
@@ -169,25 +310,31 @@ kmeans_f32_kernel(const float *__restrict__ xy, int64_t n, const float *__restri
 }
 
 // Centroid update, one wave: c = (float)(sum / n) (fp64), shift = max |new - old|.
+// Sums n_copies replicas of acc (stride kAccStride) and zeroes them.
 template <typename AccT>
 __global__ void __launch_bounds__(64)
-kmeans_update_kernel(AccT *__restrict__ acc, float *__restrict__ cent, int k, float tol,
+kmeans_update_kernel(AccT *__restrict__ acc, int n_copies, float *__restrict__ cent, int k, float tol,
                      KmState *__restrict__ st) {
     if (st->done) return;
     const int lane = threadIdx.x;
     float shift = 0.f;
     if (lane < k) {
-        const double n_pts = (double)acc[3 * lane + 0];
+        AccT a[3] = {0, 0, 0};
+        for (int r = 0; r < n_copies; ++r) {
+#pragma unroll
+            for (int f = 0; f < 3; ++f) {
+                a[f] += acc[r * kAccStride + 3 * lane + f];
+                acc[r * kAccStride + 3 * lane + f] = 0;
+            }
+        }
+        const double n_pts = (double)a[0];
         if (n_pts > 0.0) {
-            const float nx = (float)((double)acc[3 * lane + 1] / n_pts);
-            const float ny = (float)((double)acc[3 * lane + 2] / n_pts);
+            const float nx = (float)((double)a[1] / n_pts);
+            const float ny = (float)((double)a[2] / n_pts);
             shift = fmaxf(fabsf(nx - cent[2 * lane]), fabsf(ny - cent[2 * lane + 1]));
             cent[2 * lane] = nx;
             cent[2 * lane + 1] = ny;
         }
-        acc[3 * lane + 0] = 0;
-        acc[3 * lane + 1] = 0;
-        acc[3 * lane + 2] = 0;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) shift = fmaxf(shift, __shfl_xor(shift, o));
@@ -195,6 +342,21 @@ kmeans_update_kernel(AccT *__restrict__ acc, float *__restrict__ cent, int k, fl
         st->iters += 1;
         if (tol >= 0.f && shift <= tol) st->done = 1;
     }
+}
+
+// Launch helpers for the fast path (k <= kFastMaxK); false when k needs the generic kernel.
+template <bool kAccumulate>
+bool launch_fast(int k, dim3 grid, hipStream_t s, const uint32_t *xy, const Segs &segs, const float *cent,
+                 float thr, unsigned long long *acc, int n_copies, const KmState *st, uint8_t *labels) {
+    if (k <= 16)
+        hipLaunchKernelGGL((kmeans_fast_kernel<16, kAccumulate>), grid, dim3(kThreads), 0, s, xy, segs, cent, k,
+                           thr, acc, n_copies, st, labels);
+    else if (k <= kFastMaxK)
+        hipLaunchKernelGGL((kmeans_fast_kernel<32, kAccumulate>), grid, dim3(kThreads), 0, s, xy, segs, cent, k,
+                           thr, acc, n_copies, st, labels);
+    else
+        return false;
+    return true;
 }
 
 int grid_for(int64_t units) {
@@ -237,31 +399,38 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
     // per-WG packed counts must stay < 2^24 points (sum_x < 2^40)
     const int grid = grid_for(segs.n_segs);
     if (segs.n_segs * segs.stride / grid >= (1ll << 24)) return ECC_ERR_INVALID;
-    rc = ecc::ws_reserve(ctx, 4096);
+    // workspace: kAccCopies accumulator replicas (copy 0 alone on the generic path), then the state
+    constexpr size_t kAccBytes = (size_t)kAccCopies * kAccStride * 8;
+    rc = ecc::ws_reserve(ctx, kAccBytes + 64);
     if (rc) return rc;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t s = ecc::as_stream(stream);
     auto *acc = reinterpret_cast<unsigned long long *>(ctx->ws);
-    auto *st = reinterpret_cast<KmState *>(reinterpret_cast<char *>(ctx->ws) + 3 * kMaxK * 8);
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, 3 * kMaxK * 8 + 64, s), "memset(kmeans acc)");
-    for (int it = 0; it < cfg->max_iters; ++it) {
+    auto *st = reinterpret_cast<KmState *>(reinterpret_cast<char *>(ctx->ws) + kAccBytes);
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, kAccBytes + 64, s), "memset(kmeans acc)");
+    const bool fast = cfg->k <= kFastMaxK;
+    for (int it = 0; it < cfg->max_iters && segs.n_segs > 0; ++it) {
         {
             ECC_TIMED(ctx, s, "kmeans_xy16_kernel");
-            hipLaunchKernelGGL(kmeans_xy16_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
-                               centroids, cfg->k, cfg->threshold, acc, st, (uint8_t *)nullptr);
+            if (!launch_fast<true>(cfg->k, dim3(grid), s, xy, segs, centroids, cfg->threshold, acc,
+                                   fast ? kAccCopies : 1, st, nullptr))
+                hipLaunchKernelGGL(kmeans_xy16_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
+                                   centroids, cfg->k, cfg->threshold, acc, st, (uint8_t *)nullptr);
         }
         {
             ECC_TIMED(ctx, s, "kmeans_update_kernel");
             hipLaunchKernelGGL(kmeans_update_kernel<unsigned long long>, dim3(1), dim3(64), 0, s, acc,
-                               centroids, cfg->k, cfg->tol, st);
+                               fast ? kAccCopies : 1, centroids, cfg->k, cfg->tol, st);
         }
     }
     ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 iteration");
     if (labels && segs.n_segs > 0) {
         {
             ECC_TIMED(ctx, s, "kmeans_xy16_labels");
-            hipLaunchKernelGGL(kmeans_xy16_kernel<false>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
-                               centroids, cfg->k, cfg->threshold, acc, st, labels);
+            if (!launch_fast<false>(cfg->k, dim3(grid), s, xy, segs, centroids, cfg->threshold, acc, 1, st,
+                                    labels))
+                hipLaunchKernelGGL(kmeans_xy16_kernel<false>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
+                                   centroids, cfg->k, cfg->threshold, acc, st, labels);
         }
         ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 labels");
     }
@@ -293,7 +462,7 @@ ECC_API int ecc_kmeans_run_f32(ecc_ctx *ctx, const float *xy, int64_t n_points,
         }
         {
             ECC_TIMED(ctx, s, "kmeans_update_kernel");
-            hipLaunchKernelGGL(kmeans_update_kernel<double>, dim3(1), dim3(64), 0, s, acc, centroids,
+            hipLaunchKernelGGL(kmeans_update_kernel<double>, dim3(1), dim3(64), 0, s, acc, 1, centroids,
                                cfg->k, cfg->tol, st);
         }
     }
@@ -357,9 +526,11 @@ ECC_API int ecc_kmeans_accumulate_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t
     hipStream_t s = ecc::as_stream(stream);
     {
         ECC_TIMED(ctx, s, "kmeans_xy16_kernel");
-        hipLaunchKernelGGL(kmeans_xy16_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
-                           centroids, k, threshold, reinterpret_cast<unsigned long long *>(acc),
-                           reinterpret_cast<const KmState *>(state), (uint8_t *)nullptr);
+        auto *acc64 = reinterpret_cast<unsigned long long *>(acc);
+        auto *km = reinterpret_cast<const KmState *>(state);
+        if (!launch_fast<true>(k, dim3(grid), s, xy, segs, centroids, threshold, acc64, 1, km, nullptr))
+            hipLaunchKernelGGL(kmeans_xy16_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
+                               centroids, k, threshold, acc64, km, (uint8_t *)nullptr);
     }
     ECC_CHECK_LAUNCH(ctx, "kmeans accumulate");
     return ECC_OK;
@@ -373,7 +544,7 @@ ECC_API int ecc_kmeans_update(ecc_ctx *ctx, uint64_t *acc, float *centroids, int
     {
         ECC_TIMED(ctx, s, "kmeans_update_kernel");
         hipLaunchKernelGGL(kmeans_update_kernel<unsigned long long>, dim3(1), dim3(64), 0, s,
-                           reinterpret_cast<unsigned long long *>(acc), centroids, k, tol,
+                           reinterpret_cast<unsigned long long *>(acc), 1, centroids, k, tol,
                            reinterpret_cast<KmState *>(state));
     }
     ECC_CHECK_LAUNCH(ctx, "kmeans update");
@@ -393,9 +564,10 @@ ECC_API int ecc_kmeans_labels_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_s
     hipStream_t s = ecc::as_stream(stream);
     {
         ECC_TIMED(ctx, s, "kmeans_xy16_labels");
-        hipLaunchKernelGGL(kmeans_xy16_kernel<false>, dim3(grid_for(segs.n_segs)), dim3(kThreads), 0,
-                           s, xy, segs, centroids, k, threshold, (unsigned long long *)nullptr,
-                           (const KmState *)nullptr, labels);
+        const dim3 grid(grid_for(segs.n_segs));
+        if (!launch_fast<false>(k, grid, s, xy, segs, centroids, threshold, nullptr, 1, nullptr, labels))
+            hipLaunchKernelGGL(kmeans_xy16_kernel<false>, grid, dim3(kThreads), 0, s, xy, segs, centroids, k,
+                               threshold, (unsigned long long *)nullptr, (const KmState *)nullptr, labels);
     }
     ECC_CHECK_LAUNCH(ctx, "kmeans labels");
     return ECC_OK;
