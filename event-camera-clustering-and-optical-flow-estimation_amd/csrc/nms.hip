@@ -12,6 +12,15 @@
 // Candidates are processed 64 at a time: each lane tests its candidate against the kept list
 // (LDS broadcast reads), then the within-chunk order dependency is resolved on a 64x64
 // overlap bitmask with scalar bit logic.  Output label = rank in the kept list (:140).
+//
+// Grid form (nms_grid_kernel, used whenever the grid fits LDS): two boxes [c±h] overlap iff
+// their centres are within Chebyshev distance 2h (clipping to the image never separates two
+// boxes whose centres lie inside it), so kept boxes are pairwise disjoint and a grid of
+// (2h+1)-pixel cells holds at most ONE kept centre per cell.  "Overlaps an earlier kept box"
+// is then 9 LDS probes.  One wave per slice streams the flags 1024 events at a time; within a
+// chunk of 64 candidates the kept ones are found by a scalar loop over the surviving lanes
+// (each kept lane's centre is broadcast and kills the later lanes it overlaps).  ~6 KiB of LDS
+// per slice, so many slices run per CU.
 #include "ecc_internal.hpp"
 
 namespace {
@@ -135,7 +144,110 @@ nms_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ flags, i
     overflow = __any(overflow);
     if (lane == 0) {
         out_count[s] = n_kept < cap ? n_kept : cap;
-        if (overflow) *err = 1;
+        if (overflow) atomicOr(err, 1);
+    }
+}
+
+
+constexpr int kGridThreads = 64;
+constexpr int kGridMaxCells = 16384;  // 64 KiB of LDS
+constexpr int kChunkEvents = kGridThreads * 16;
+constexpr uint32_t kNoCentre = 0xffffffffu;
+
+__device__ __forceinline__ bool near_centre(uint32_t a, uint32_t b, int reach) {
+    return abs(ecc::xy_x(a) - ecc::xy_x(b)) <= reach && abs(ecc::xy_y(a) - ecc::xy_y(b)) <= reach;
+}
+
+__global__ void __launch_bounds__(kGridThreads)
+nms_grid_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ flags, int64_t n, int S, int W,
+                int H, int half, int gw, int gh, int cap, ecc_corner *__restrict__ out,
+                int32_t *__restrict__ out_count, int32_t *__restrict__ err) {
+    extern __shared__ uint32_t grid[];  // [gh][gw] kept centre per cell
+    __shared__ uint32_t cbuf[kChunkEvents];
+    const int lane = threadIdx.x;
+    const int64_t s = blockIdx.x;
+    const int64_t lo = s * (int64_t)S;
+    const int64_t len = ((lo + S < n) ? lo + S : n) - lo;
+    const int cs = 2 * half + 1, reach = 2 * half;
+    for (int i = lane; i < gw * gh; i += kGridThreads) grid[i] = kNoCentre;
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int n_kept = 0;
+    bool overflow = false, bad_input = false;
+    __syncthreads();
+    for (int64_t c0 = 0; c0 < len; c0 += kChunkEvents) {
+        // (a) compact the chunk's flagged events in event order
+        const int64_t my0 = c0 + (int64_t)lane * 16;
+        uint32_t bits = 0;
+        if (my0 + 15 < len && ((lo + my0) & 15) == 0) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(flags + lo + my0);
+            const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) bits |= (((w4[k >> 2] >> (8 * (k & 3))) & 0xffu) ? 1u : 0u) << k;
+        } else {
+            for (int k = 0; k < 16; ++k)
+                if (my0 + k < len && flags[lo + my0 + k]) bits |= 1u << k;
+        }
+        const int cnt = __popc(bits);
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const int total = __shfl(incl, 63);
+        int off = incl - cnt;
+        while (bits) {
+            const int k = __ffs(bits) - 1;
+            bits &= bits - 1;
+            cbuf[off++] = xy[lo + my0 + k];
+        }
+        __syncthreads();
+        // (b) greedy over the chunk's candidates, 64 at a time
+        for (int p0 = 0; p0 < total; p0 += kGridThreads) {
+            uint32_t v = (p0 + lane < total) ? cbuf[p0 + lane] : 0u;
+            int x = ecc::xy_x(v), y = ecc::xy_y(v);
+            const bool outside = p0 + lane < total && (x >= W || y >= H);
+            if (outside) bad_input = true;  // skipped and reported (ecc_corner_nms_status)
+            const bool valid = p0 + lane < total && !outside;
+            if (!valid) { v = 0u; x = 0; y = 0; }
+            const int cx = x / cs, cy = y / cs;
+            bool alive = valid;
+#pragma unroll
+            for (int dy = -1; dy <= 1; ++dy) {
+#pragma unroll
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const int gx = cx + dx, gy = cy + dy;
+                    if (gx >= 0 && gy >= 0 && gx < gw && gy < gh) {
+                        const uint32_t k = grid[gy * gw + gx];
+                        if (k != kNoCentre && near_centre(k, v, reach)) alive = false;
+                    }
+                }
+            }
+            uint64_t am = __ballot(alive), keepm = 0;
+            while (am) {  // wave-uniform: each step keeps the first surviving lane
+                const int i0 = __ffsll((unsigned long long)am) - 1;
+                keepm |= 1ull << i0;
+                am &= am - 1;
+                const uint32_t vi = (uint32_t)__builtin_amdgcn_readlane((int)v, i0);
+                am &= ~__ballot(lane > i0 && near_centre(vi, v, reach));
+            }
+            if ((keepm >> lane) & 1ull) {
+                const int rank = n_kept + __popcll(keepm & lt_mask);
+                grid[cy * gw + cx] = v;
+                if (rank < cap) out[s * (int64_t)cap + rank] = ecc_corner{x, y, rank};
+                else overflow = true;
+            }
+            n_kept += __popcll(keepm);
+            __syncthreads();
+        }
+        __syncthreads();
+    }
+    overflow = __any(overflow);
+    bad_input = __any(bad_input);
+    if (lane == 0) {
+        out_count[s] = n_kept < cap ? n_kept : cap;
+        if (overflow) atomicOr(err, 1);
+        if (bad_input) atomicOr(err, 2);
     }
 }
 
@@ -155,7 +267,14 @@ ECC_API int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corn
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + 1, 0, 4, s), "memset(nms err)");
-    {
+    const int half = box_size / 2, cs = 2 * half + 1;
+    const int gw = (width + cs - 1) / cs, gh = (height + cs - 1) / cs;
+    if ((int64_t)gw * gh <= kGridMaxCells) {
+        ECC_TIMED(ctx, s, "nms_kernel");
+        hipLaunchKernelGGL(nms_grid_kernel, dim3((unsigned)n_slices), dim3(kGridThreads), (size_t)gw * gh * 4, s,
+                           xy, corner_flags, n, slice_events, width, height, half, gw, gh, cap, out, out_count,
+                           ctx->flags + 1);
+    } else {
         ECC_TIMED(ctx, s, "nms_kernel");
         hipLaunchKernelGGL(nms_kernel, dim3((unsigned)n_slices), dim3(kThreads), 0, s, xy,
                            corner_flags, n, slice_events, width, height, box_size / 2, cap, out,
@@ -163,4 +282,14 @@ ECC_API int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corn
     }
     ECC_CHECK_LAUNCH(ctx, "nms_kernel");
     return ECC_OK;
+}
+
+ECC_API int ecc_corner_nms_status(ecc_ctx *ctx, ecc_stream_t stream) {
+    if (!ctx) return ECC_ERR_INVALID;
+    int32_t f = 0;
+    ECC_CHECK_HIP(ctx, hipMemcpyAsync(&f, ctx->flags + 1, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
+                  "read nms flag");
+    ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
+    if (f & 2) return ECC_ERR_INVALID;
+    return (f & 1) ? ECC_ERR_CAPACITY : ECC_OK;
 }

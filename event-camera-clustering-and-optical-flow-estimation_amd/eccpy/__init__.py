@@ -132,6 +132,7 @@ _sigs = {
     "ecc_fast_detect_status": (C.c_int, [P, P]),
     "ecc_sae_scatter": (C.c_int, [P, P, P, i64, i32, i32, P, P]),
     "ecc_corner_nms": (C.c_int, [P, P, P, i64, i32, i32, i32, i32, i32, P, P, P]),
+    "ecc_corner_nms_status": (C.c_int, [P, P]),
     "ecc_tracker_cfg_default": (None, [C.POINTER(TrackerCfg)]),
     "ecc_tracker_create": (C.c_int, [P, C.POINTER(TrackerCfg), i32, i32, C.POINTER(P)]),
     "ecc_tracker_destroy": (C.c_int, [P]),
@@ -309,6 +310,9 @@ class Context:
                    h: int, box: int, cap: int, out: DeviceArray, counts: DeviceArray):
         check(lib.ecc_corner_nms(self.ctx, xy.ptr, flags.ptr, n, slice_events, w, h, box, cap,
                                  out.ptr, counts.ptr, self.stream), "ecc_corner_nms")
+
+    def corner_nms_status(self) -> int:
+        return lib.ecc_corner_nms_status(self.ctx, self.stream)
 
     # ---- 6. eps-neighbourhoods
     def eps_counts(self, xy: DeviceArray, n_segs: int, stride: int, counts_in, eps: float,

@@ -215,14 +215,17 @@ int ecc_sae_scatter(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t 
  * Corners of slice s are the events with corner_flags==1 in event order; a corner is kept
  * iff its clipped box [x±box/2]×[y±box/2] touches no box of an earlier kept corner; kept
  * corner label = its rank in the kept list (":140").  out: DEVICE ecc_corner[n_slices*cap],
- * slice s at s*cap; out_count: DEVICE int32[n_slices] (ECC_ERR_CAPACITY if a slice
- * overflows: counts are clamped to cap).
+ * slice s at s*cap; out_count: DEVICE int32[n_slices] (counts are clamped to cap).
+ * Corners must lie inside the image (ecc_fast_detect never flags border events).
  * ------------------------------------------------------------------------------------- */
 typedef struct ecc_corner { int32_t x, y, label; } ecc_corner; /* reference struct Corner */
 
 int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corner_flags, int64_t n,
                    int32_t slice_events, int32_t width, int32_t height, int32_t box_size,
                    int32_t cap, ecc_corner *out, int32_t *out_count, ecc_stream_t stream);
+/* Synchronises `stream`; ECC_ERR_CAPACITY if a slice kept more than `cap` corners in the last
+ * ecc_corner_nms, ECC_ERR_INVALID if a flagged event lay outside the image (it was skipped). */
+int ecc_corner_nms_status(ecc_ctx *ctx, ecc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * 5. Corner tracker (damped predictor-corrector + grouping)

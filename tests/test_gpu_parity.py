@@ -137,6 +137,36 @@ def test_kmeans_xy16_dense_matches_oracle(ecc, orc, gpu):
     assert (d_lab.numpy() == o_lab).all()
 
 
+@pytest.mark.parametrize("k", [16, 24, 40])
+def test_kmeans_xy16_ties_take_exact_path(ecc, orc, gpu, k):
+    """Each centre has an EARLIER twin one ulp to its right: for points roughly above/below the
+    pair, the twin's d2 is a few ulps larger (the fast kernel's near-tie branch, ~25% of points)
+    and in ~4% the two square roots round equal, so the reference picks the earlier twin despite
+    its larger d2.  k=24 uses the K=32 instance, k=40 the generic kernel."""
+    rng = np.random.default_rng(k)
+    n = 200_003
+    half = k // 2
+    cx = rng.integers(20, 320, half).astype(np.float32) + np.float32(0.25)
+    cy = rng.integers(20, 240, half).astype(np.float32)
+    c0 = np.empty((k, 2), np.float32)
+    c0[:half, 0], c0[:half, 1] = np.nextafter(cx, np.float32(np.inf)), cy
+    c0[half:2 * half, 0], c0[half:2 * half, 1] = cx, cy
+    if k % 2:
+        c0[-1] = c0[0]
+    c0 = c0.ravel()
+    ci = rng.integers(0, half, n)
+    x = np.clip(np.round(cx[ci] + rng.normal(0, 2, n)), 0, 345).astype(np.int64)
+    y = np.clip(np.round(cy[ci] + rng.normal(0, 25, n)), 0, 259).astype(np.int64)
+    xy = ecc.pack_xy(x, y)
+    o_c, o_lab, o_it = orc.kmeans_run_xy16(xy, c0, 2, 50.0, -1.0)
+    d_c = dev(ecc, c0)
+    d_lab = ecc.DeviceArray(n, np.uint8)
+    gpu.kmeans_xy16(dev(ecc, xy), 1, n, None, d_c, ecc.kmeans_cfg(k=k, max_iters=2, tol=-1.0), d_lab)
+    gpu.sync()
+    assert (d_lab.numpy() == o_lab).all()
+    assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
+
+
 def test_kmeans_f32_matches_oracle(ecc, orc, gpu):
     rng = np.random.default_rng(5)
     pts = np.concatenate([rng.normal(m, 6.0, (20000, 2)) for m in ([40, 40], [120, 60], [200, 180], [300, 90])])
@@ -303,6 +333,53 @@ def test_nms_dense_candidates(ecc, orc, gpu):
     k = o_cnt[0]
     assert d_cnt.numpy()[0] == k
     assert (d_out.numpy()[:k] == o_out[:k]).all()
+    assert gpu.corner_nms_status() == 0
+
+
+@pytest.mark.parametrize("box,wh,density", [
+    (15, (346, 260), 0.05),   # grid kernel, reference box
+    (8, (346, 260), 0.3),     # even box size (half = 4)
+    (31, (640, 480), 0.5),    # large boxes
+    (1, (346, 260), 0.2),     # 1-pixel cells: grid too large for LDS -> kept-list kernel
+    (15, (1280, 720), 0.02),  # reference sensor
+])
+def test_nms_box_sizes(ecc, orc, gpu, box, wh, density):
+    W, H = wh
+    rng = np.random.default_rng(box * 7 + W)
+    n = 16384 * 5 + 333  # ragged last slice
+    xy = ecc.pack_xy(rng.integers(0, W, n), rng.integers(0, H, n))
+    flags = (rng.random(n) < density).astype(np.uint8)
+    cap = 8192
+    o_out, o_cnt, rc = orc.corner_nms(xy, flags, W, H, box=box, cap=cap)
+    assert rc == 0
+    ns = len(o_cnt)
+    d_out = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE)
+    d_cnt = ecc.DeviceArray(ns, np.int32)
+    gpu.corner_nms(dev(ecc, xy), dev(ecc, flags), n, 16384, W, H, box, cap, d_out, d_cnt)
+    assert gpu.corner_nms_status() == 0
+    assert (d_cnt.numpy() == o_cnt).all()
+    g_out = d_out.numpy()
+    for s in range(ns):
+        k = o_cnt[s]
+        assert (g_out[s * cap: s * cap + k] == o_out[s * cap: s * cap + k]).all(), s
+
+
+def test_nms_status_capacity_and_outside(ecc, gpu):
+    W, H = 346, 260
+    rng = np.random.default_rng(9)
+    n = 16384
+    xy = ecc.pack_xy(rng.integers(0, W, n), rng.integers(0, H, n))
+    flags = np.ones(n, np.uint8)
+    d_out = ecc.DeviceArray(8, ecc.CORNER_DTYPE)
+    d_cnt = ecc.DeviceArray(1, np.int32)
+    gpu.corner_nms(dev(ecc, xy), dev(ecc, flags), n, n, W, H, 15, 8, d_out, d_cnt)
+    assert gpu.corner_nms_status() == ecc.ERR_CAPACITY
+    assert d_cnt.numpy()[0] == 8
+    xy2 = xy.copy()
+    xy2[5] = ecc.pack_xy(np.array([W + 3]), np.array([10]))[0]  # flagged event outside the image
+    d_out = ecc.DeviceArray(4096, ecc.CORNER_DTYPE)
+    gpu.corner_nms(dev(ecc, xy2), dev(ecc, flags), n, n, W, H, 15, 4096, d_out, d_cnt)
+    assert gpu.corner_nms_status() == ecc.ERR_INVALID
 
 
 # ------------------------------------------------------------------------------ tracker
