@@ -43,8 +43,7 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kBuildThreads = 1024;
-constexpr int kBuildUnroll = 4;
+constexpr int kBuildUnroll = 8;
 constexpr int kArcThreads = 512;
 constexpr int kItemEvents = 2048;  // events per arc work item
 constexpr int kGroup = 32;         // slices per group (mask bits)
@@ -53,7 +52,6 @@ constexpr int kTilePix = kTile * kTile;
 constexpr int kHalo = 4;           // circle radius
 constexpr int kWin = kTile + 2 * kHalo;  // 24
 constexpr int kWinPix = kWin * kWin;     // 576
-constexpr int kStageBatch = 12;          // staging loads in flight per lane
 constexpr int kMaxTiles = 8191;          // bins per group = n_tiles + 1 (8192 fit an LDS histogram)
 constexpr int kMaxSlice = 1 << 19;       // group-local event index must fit 24 bits
 constexpr int64_t kEmptyT = INT64_MIN;
@@ -195,39 +193,46 @@ __device__ __forceinline__ void tile_origin(const CornerGeom &g, int tile, int &
     y0 = (tile / g.tiles_x) * kTile;
 }
 
-// 3. Build group `grp` for one tile (and fold group grp-1 into B for the same pixels).
-__global__ void __launch_bounds__(kBuildThreads)
-tile_build_kernel(CornerGeom g, int64_t grp, Sorted so, GroupBufs cur, GroupBufs prv,
-                  int64_t *__restrict__ B) {
-    __shared__ int64_t mloc[kGroup][kTilePix];  // 64 KiB
-    __shared__ uint32_t mask_l[kTilePix];
-    const int tile = blockIdx.x;
+// 3. Build group `grp` for one tile: fold group grp-1 (set `prv`) into B_out = fold(B_in) for
+// the tile's pixels (dense; grp > 0), then accumulate mask/M of the tile's bin in LDS and store
+// them into set `cur`.  Runs as the first n_tiles workgroups of group_kernel(grp - 1).
+struct BuildLds {
+    int64_t mloc[kGroup][kTilePix];  // 64 KiB
+    uint32_t mask_l[kTilePix];
+};
+
+__device__ __forceinline__ void build_tile(const CornerGeom &g, int64_t grp, int tile, const Sorted &so,
+                                           const GroupBufs &cur, const GroupBufs &prv,
+                                           const int64_t *__restrict__ B_in, int64_t *__restrict__ B_out,
+                                           BuildLds &L) {
+    constexpr int kHalves = kArcThreads / kTilePix;  // 2 lanes per pixel
+    constexpr int kPlanes = kGroup / kHalves;
     const int tid = threadIdx.x;
-    const int p = tid % kTilePix, quarter = tid / kTilePix;  // 4 lanes per pixel
+    const int p = tid % kTilePix, part = tid / kTilePix;
     int x0, y0;
     tile_origin(g, tile, x0, y0);
     const int px = x0 + p % kTile, py = y0 + p / kTile;
     const bool own = px < g.W && py < g.H;
     const int64_t HW = (int64_t)g.H * g.W;
     const int64_t q = (int64_t)py * g.W + px;
-    if (quarter == 0) {
+    if (part == 0) {
         if (own && grp > 0) {
             const uint32_t mk = prv.mask[q];
-            if (mk) B[q] = prv.M[(int64_t)(31 - __clz(mk)) * HW + q];
+            B_out[q] = mk ? prv.M[(int64_t)(31 - __clz(mk)) * HW + q] : B_in[q];
         }
-        mask_l[p] = 0u;
+        L.mask_l[p] = 0u;
     }
 #pragma unroll
-    for (int jj = 0; jj < kGroup / 4; ++jj) mloc[quarter * (kGroup / 4) + jj][p] = kEmptyT;
+    for (int jj = 0; jj < kPlanes; ++jj) L.mloc[part * kPlanes + jj][p] = kEmptyT;
     __syncthreads();
     const int nb = g.n_tiles + 1;
     const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
-    for (int64_t i0 = b0; i0 < b1; i0 += kBuildUnroll * kBuildThreads) {
+    for (int64_t i0 = b0; i0 < b1; i0 += kBuildUnroll * kArcThreads) {
         uint32_t k[kBuildUnroll];
         int64_t tv[kBuildUnroll];
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u) {
-            const int64_t i = i0 + u * kBuildThreads + tid;
+            const int64_t i = i0 + u * kArcThreads + tid;
             k[u] = (i < b1) ? so.key[i] : 0xffffffffu;
             tv[u] = (i < b1) ? so.t[i] : 0;
         }
@@ -236,33 +241,33 @@ tile_build_kernel(CornerGeom g, int64_t grp, Sorted so, GroupBufs cur, GroupBufs
             if (k[u] == 0xffffffffu) continue;
             const int lp = (int)(k[u] & 255u);
             const int j = slice_in_group(k[u] >> 8, g);
-            atomicOr(&mask_l[lp], 1u << j);
-            atomicMax(reinterpret_cast<long long *>(&mloc[j][lp]), (long long)tv[u]);
+            atomicOr(&L.mask_l[lp], 1u << j);
+            atomicMax(reinterpret_cast<long long *>(&L.mloc[j][lp]), (long long)tv[u]);
         }
     }
     __syncthreads();
     if (own) {
-        const uint32_t mk_all = mask_l[p];
-        if (quarter == 0) cur.mask[q] = mk_all;
-        uint32_t mk = (mk_all >> (quarter * 8)) & 0xffu;
+        const uint32_t mk_all = L.mask_l[p];
+        if (part == 0) cur.mask[q] = mk_all;
+        uint32_t mk = (mk_all >> (part * kPlanes)) & ((1u << kPlanes) - 1u);
         while (mk) {
-            const int j = quarter * 8 + __ffs(mk) - 1;
+            const int j = part * kPlanes + __ffs(mk) - 1;
             mk &= mk - 1;
-            cur.M[(int64_t)j * HW + q] = mloc[j][p];
+            cur.M[(int64_t)j * HW + q] = L.mloc[j][p];
         }
     }
 }
 
-// Fold of the last group into B.
+// Final fold of the last group: B_out = fold(B_in) (dense; may be in place).
 __global__ void __launch_bounds__(kThreads)
-tile_fold_kernel(CornerGeom g, GroupBufs buf, int64_t *__restrict__ B) {
+tile_fold_kernel(CornerGeom g, GroupBufs buf, const int64_t *B_in, int64_t *B_out) {
     int x0, y0;
     tile_origin(g, blockIdx.x, x0, y0);
     const int px = x0 + threadIdx.x % kTile, py = y0 + threadIdx.x / kTile;
     if (px >= g.W || py >= g.H) return;
     const int64_t q = (int64_t)py * g.W + px;
     const uint32_t mk = buf.mask[q];
-    if (mk) B[q] = buf.M[(int64_t)(31 - __clz(mk)) * (int64_t)g.H * g.W + q];
+    B_out[q] = mk ? buf.M[(int64_t)(31 - __clz(mk)) * (int64_t)g.H * g.W + q] : B_in[q];
 }
 
 template <int N, int SMIN, int SMAX>
@@ -346,22 +351,17 @@ __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
     return ok ? 1 : 0;
 }
 
-// Staged neighbourhood of one work item: per window pixel its group mask and the offset of its
-// entries in vals: vals[off] = B', vals[off + 1 + r] = M' of the r-th set slice bit.
-struct WinPix {
-    uint32_t mask;
-    uint32_t off;
-};
-
-constexpr int kValsCap = 18700;  // 576 + 32*576 = 19008 worst case; beyond -> exact path
-
+// Staged neighbourhood of one work item: T[j][wp] = V'(window pixel wp, slice j of the group) —
+// the clamped value the arc test of an event in slice j sees — so every circle lookup is one
+// independent LDS read.  mask[] (the group mask per window pixel) serves the exact fallback.
 struct ArcLds {
-    WinPix pix[kWinPix];
-    uint32_t vals[kValsCap];
-    int32_t wave_tot[kArcThreads / 64];
+    uint32_t T[kGroup][kWinPix];  // 72 KiB
+    uint32_t mask[kWinPix];
+    uint16_t q4[kItemEvents];     // events that passed circle 3 (item-local index)
     int64_t wave_min[kArcThreads / 64];
     int32_t exact_only;  // a value above t_last: clamped keys unusable
     int32_t mixed;       // clamped values not all equal to the window minimum of B
+    int32_t q4n;
 };
 
 __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, int32_t *exact_flag,
@@ -375,30 +375,24 @@ __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, 
     return (uint32_t)d;
 }
 
-__device__ __forceinline__ uint32_t win_key(const ArcLds &L, int wp, uint32_t below) {
-    const WinPix pm = L.pix[wp];
-    return L.vals[pm.off + __popc(pm.mask & below)];
-}
-
 // exact int64 V from the global images (fallback)
 __device__ __forceinline__ int64_t glob_at(const ArcLds &L, int wp, int64_t q, uint32_t below,
                                            const GroupBufs &cur, const int64_t *__restrict__ B,
                                            int64_t HW) {
-    const uint32_t mk = L.pix[wp].mask & below;
+    const uint32_t mk = L.mask[wp] & below;
     if (!mk) return B[q];
     return cur.M[(int64_t)(31 - __clz(mk)) * HW + q];
 }
 
 // 4. Arc test of one work item (<= kItemEvents tile-sorted events of group `grp`).
-__global__ void __launch_bounds__(kArcThreads)
-arc_test_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, Sorted so, GroupBufs cur,
-                const int64_t *__restrict__ B, const int32_t *__restrict__ first_border,
-                uint8_t *__restrict__ flags) {
-    __shared__ ArcLds L;
+__device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const CornerGeom &g, int64_t grp,
+                                         int item_idx, const Sorted &so, const GroupBufs &cur,
+                                         const int64_t *__restrict__ B, const int32_t *__restrict__ first_border,
+                                         uint8_t *__restrict__ flags, ArcLds &L) {
     const int nb = g.n_tiles + 1;
     const int64_t it0 = so.item_off[grp * nb], it1 = so.item_off[(grp + 1) * nb];
-    if (it0 + blockIdx.x >= it1) return;
-    const uint32_t item = so.items[it0 + blockIdx.x];
+    if (it0 + item_idx >= it1) return;
+    const uint32_t item = so.items[it0 + item_idx];
     const int tile = (int)(item & 8191u), chunk = (int)(item >> 13);
     const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
     const int64_t i0 = b0 + (int64_t)chunk * kItemEvents;
@@ -424,10 +418,9 @@ arc_test_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, Sorted
         const int64_t i = i0 + tid + (int64_t)u * kArcThreads;
         keys[u] = (i < i1) ? so.key[i] : 0xffffffffu;
     }
-    // (a) window masks + B; entry counts 1 + popc(mask)
+    // (a) window masks + B (lanes own window pixels tid and tid + kArcThreads)
     uint32_t mk_r[2] = {0u, 0u};
     int64_t b_r[2] = {INT64_MAX, INT64_MAX};  // INT64_MAX: outside the sensor (never read)
-    int c_own = 0;
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
         const int wp = tid + r * kArcThreads;
@@ -437,15 +430,8 @@ arc_test_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, Sorted
             const int64_t qq = (int64_t)wy * g.W + wx;
             mk_r[r] = in ? cur.mask[qq] : 0u;
             b_r[r] = in ? B[qq] : INT64_MAX;
-            c_own += 1 + __popc(mk_r[r]);
+            L.mask[wp] = mk_r[r];
         }
-    }
-    // (b) block exclusive scan of the per-thread entry counts
-    int incl = c_own;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
     }
     int64_t bmin = b_r[0] < b_r[1] ? b_r[0] : b_r[1];
 #pragma unroll
@@ -453,112 +439,141 @@ arc_test_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, Sorted
         const int64_t v = __shfl_xor(bmin, o);
         bmin = v < bmin ? v : bmin;
     }
-    if (lane == 63) L.wave_tot[wave] = incl;
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
-    int before = 0, total = 0;
     int64_t vz = INT64_MAX;
 #pragma unroll
-    for (int w = 0; w < kArcThreads / 64; ++w) {
-        const int v = L.wave_tot[w];
-        before += (w < wave) ? v : 0;
-        total += v;
-        vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
-    }
-    const bool fits = total <= kValsCap;
-    int off = before + incl - c_own;
+    for (int w = 0; w < kArcThreads / 64; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
+    // (b) one lane per window pixel: gather the pixel's set M planes (all loads in flight), then
+    //     forward-fill along j in registers: T[j] = bit j set ? M'_j : T[j-1], T[-1] = B'.
+    //     When the group spans < 2^27 ticks every M lies in (Lt, t_last], so M' = M - Lt is
+    //     exact from the low 32 bits alone (half the bytes, one subtract).
+    const int64_t t_first = t[grp_first];
+    const bool narrow = (Lt + (int64_t)kVMax) - t_first < (int64_t)kVMax;  // uniform
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
         const int wp = tid + r * kArcThreads;
         if (wp < kWinPix) {
-            L.pix[wp].mask = mk_r[r];
-            L.pix[wp].off = (uint32_t)off;
-            if (fits) L.vals[off] = (b_r[r] == INT64_MAX) ? 0u : clamp_rel(b_r[r], Lt, vz, &L.exact_only, &L.mixed);
-            off += 1 + __popc(mk_r[r]);
-        }
-    }
-    __syncthreads();
-    // (c) stage M entries: pair (j, wp) per lane, j-major so a wave reads rows of one plane;
-    //     kStageBatch loads in flight per lane before their LDS stores
-    if (fits) {
-        constexpr int kPairs = kGroup * kWinPix;
-        constexpr int kIters = (kPairs + kArcThreads - 1) / kArcThreads;  // 36
+            const uint32_t mk = mk_r[r];
+            const int64_t qq = (int64_t)(wy0 + wp / kWin) * g.W + (wx0 + wp % kWin);
+            uint32_t cur_v = (b_r[r] == INT64_MAX) ? 0u : clamp_rel(b_r[r], Lt, vz, &L.exact_only, &L.mixed);
+            if (narrow) {
+                const uint32_t *M32 = reinterpret_cast<const uint32_t *>(cur.M + qq);  // low words
+                uint32_t v[kGroup];
 #pragma unroll
-        for (int r0 = 0; r0 < kIters; r0 += kStageBatch) {
-            int dst[kStageBatch];
-            int64_t val[kStageBatch];
+                for (int j = 0; j < kGroup; ++j) v[j] = ((mk >> j) & 1u) ? M32[(int64_t)j * HW * 2] : 0u;
+                const uint32_t lt32 = (uint32_t)Lt;
 #pragma unroll
-            for (int u = 0; u < kStageBatch; ++u) {
-                const int pr = tid + (r0 + u) * kArcThreads;
-                dst[u] = -1;
-                val[u] = 0;
-                if (r0 + u < kIters && pr < kPairs) {
-                    const int j = pr / kWinPix, wp = pr - j * kWinPix;
-                    const WinPix pm = L.pix[wp];
-                    if ((pm.mask >> j) & 1u) {
-                        const int64_t qq = (int64_t)(wy0 + wp / kWin) * g.W + (wx0 + wp % kWin);
-                        dst[u] = (int)(pm.off + 1 + __popc(pm.mask & ((1u << j) - 1u)));
-                        val[u] = cur.M[(int64_t)j * HW + qq];
-                    }
+                for (int j = 0; j < kGroup; ++j) {
+                    cur_v = ((mk >> j) & 1u) ? v[j] - lt32 : cur_v;
+                    L.T[j][wp] = cur_v;
+                }
+            } else {
+#pragma unroll 4
+                for (int j = 0; j < kGroup; ++j) {
+                    if ((mk >> j) & 1u) cur_v = clamp_rel(cur.M[(int64_t)j * HW + qq], Lt, vz, &L.exact_only, &L.mixed);
+                    L.T[j][wp] = cur_v;
                 }
             }
-#pragma unroll
-            for (int u = 0; u < kStageBatch; ++u)
-                if (dst[u] >= 0) L.vals[dst[u]] = clamp_rel(val[u], Lt, vz, &L.exact_only, &L.mixed);
         }
     }
     __syncthreads();
-    const bool fast = fits && !L.exact_only;
+    const bool fast = !L.exact_only;
     const bool ties_exact = !L.mixed;
-    // (d) one event per lane
+    // (d) circle 3 for one event per lane; survivors go to an LDS queue so that circle 4 runs
+    //     densely over them (a whole wave would otherwise execute it for any single survivor)
+    struct Ev {
+        int x, y, j, wp0;
+        uint32_t el;
+        bool test;
+    };
+    auto decode = [&](uint32_t key) {
+        Ev e;
+        const int lp = (int)(key & 255u);
+        e.el = key >> 8;
+        e.x = x0 + lp % kTile;
+        e.y = y0 + lp / kTile;
+        e.j = slice_in_group(e.el, g);
+        const int64_t s = grp * kGroup + e.j;
+        e.test = s >= g.first_detect && !is_border(e.x, e.y, g);
+        if (e.test && g.border_mode == 1) e.test = (int64_t)e.el - (int64_t)e.j * g.S < first_border[s];
+        e.wp0 = (e.y - wy0) * kWin + (e.x - wx0);
+        return e;
+    };
+    auto exact_circle = [&](const Ev &e, bool c3) {  // exact int64 test from the global images
+        const uint32_t below = (e.j == 31) ? 0xffffffffu : ((2u << e.j) - 1u);
+        const int64_t q0 = (int64_t)e.y * g.W + e.x;
+        if (c3) {
+            int64_t v3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                v3[k] = glob_at(L, e.wp0 + c3dy[k] * kWin + c3dx[k], q0 + (int64_t)c3dy[k] * g.W + c3dx[k], below,
+                                cur, B, HW);
+            return arc_streak<16, 3, 6>(v3);
+        }
+        int64_t v4[20];
+#pragma unroll
+        for (int k = 0; k < 20; ++k)
+            v4[k] = glob_at(L, e.wp0 + c4dy[k] * kWin + c4dx[k], q0 + (int64_t)c4dy[k] * g.W + c4dx[k], below,
+                            cur, B, HW);
+        return arc_streak<20, 4, 8>(v4);
+    };
+    if (tid == 0) L.q4n = 0;
+    __syncthreads();
 #pragma unroll 1
     for (int u = 0; u < kPerLane; ++u) {
         const uint32_t key = keys[u];
         if (key == 0xffffffffu) break;
-        const int lp = (int)(key & 255u);
-        const uint32_t el = key >> 8;
-        const int x = x0 + lp % kTile, y = y0 + lp / kTile;
-        const int j = slice_in_group(el, g);
-        const int64_t s = grp * kGroup + j;
-        bool test = s >= g.first_detect && !is_border(x, y, g);
-        if (test && g.border_mode == 1) test = (int64_t)el - (int64_t)j * g.S < first_border[s];
-        if (!test) continue;
-        const uint32_t below = (j == 31) ? 0xffffffffu : ((2u << j) - 1u);
-        const int wp0 = (y - wy0) * kWin + (x - wx0);
+        const Ev e = decode(key);
+        if (!e.test) continue;
         int res = -1;
         if (fast) {
+            const uint32_t *Tj = L.T[e.j];
             uint32_t k3[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) k3[k] = (win_key(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
+            for (int k = 0; k < 16; ++k) k3[k] = (Tj[e.wp0 + c3dy[k] * kWin + c3dx[k]] << 4) | k;
             res = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
-            if (res == 1) {
-                uint32_t k4[32];
-#pragma unroll
-                for (int k = 0; k < 20; ++k) k4[k] = (win_key(L, wp0 + c4dy[k] * kWin + c4dx[k], below) << 5) | k;
-#pragma unroll
-                for (int k = 20; k < 32; ++k) k4[k] = 0u;
-                res = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
-            }
         }
-        if (res < 0) {  // exact int64 test from the global images
-            const int64_t q0 = (int64_t)y * g.W + x;
-            int64_t v3[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                v3[k] = glob_at(L, wp0 + c3dy[k] * kWin + c3dx[k], q0 + (int64_t)c3dy[k] * g.W + c3dx[k], below,
-                                cur, B, HW);
-            res = 0;
-            if (arc_streak<16, 3, 6>(v3)) {
-                int64_t v4[20];
-#pragma unroll
-                for (int k = 0; k < 20; ++k)
-                    v4[k] = glob_at(L, wp0 + c4dy[k] * kWin + c4dx[k], q0 + (int64_t)c4dy[k] * g.W + c4dx[k],
-                                    below, cur, B, HW);
-                res = arc_streak<20, 4, 8>(v4) ? 1 : 0;
-            }
-        }
-        if (res == 1) flags[grp_first + el] = 1;
+        if (res < 0) res = exact_circle(e, true) ? 1 : 0;
+        if (res == 1) L.q4[atomicAdd(&L.q4n, 1)] = (uint16_t)(tid + u * kArcThreads);
     }
+    __syncthreads();
+    const int n4 = L.q4n;
+    for (int qi = tid; qi < n4; qi += kArcThreads) {
+        const Ev e = decode(so.key[i0 + L.q4[qi]]);
+        int res = -1;
+        if (fast) {
+            const uint32_t *Tj = L.T[e.j];
+            uint32_t k4[32];
+#pragma unroll
+            for (int k = 0; k < 20; ++k) k4[k] = (Tj[e.wp0 + c4dy[k] * kWin + c4dx[k]] << 5) | k;
+#pragma unroll
+            for (int k = 20; k < 32; ++k) k4[k] = 0u;
+            res = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
+        }
+        if (res < 0) res = exact_circle(e, false) ? 1 : 0;
+        if (res == 1) flags[grp_first + e.el] = 1;
+    }
+}
+
+// One launch per group g: workgroups [0, n_build) build group g+1 (tile = blockIdx) while the
+// rest test the work items of group g.  Both read set g&1; the build writes set (g+1)&1 and
+// B_{g+1} = fold(B_g) into the other B buffer, so nothing the arc test reads changes under it.
+union GroupLds {
+    ArcLds arc;
+    BuildLds build;
+};
+
+__global__ void __launch_bounds__(kArcThreads)
+group_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, int n_build, int do_arc, Sorted so,
+             GroupBufs cur, GroupBufs nxt, const int64_t *B_in, int64_t *B_out,
+             const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags) {
+    __shared__ GroupLds L;
+    if ((int)blockIdx.x < n_build) {
+        build_tile(g, grp + 1, (int)blockIdx.x, so, nxt, cur, B_in, B_out, L.build);
+        return;
+    }
+    if (do_arc) arc_item(t, g, grp, (int)blockIdx.x - n_build, so, cur, B_in, first_border, flags, L.arc);
 }
 
 // Plain final-SAE scatter (no detection): sae[q] = max t.
@@ -591,6 +606,7 @@ struct CornerState {
     int W = 0, H = 0;
     void *img = nullptr;
     GroupBufs set[2]{};
+    int64_t *b_alt = nullptr;  // second SAE buffer (B ping-pong with the caller's `sae`)
     void *evt = nullptr;
     size_t evt_bytes = 0;
 };
@@ -644,7 +660,8 @@ int corner_state_reserve(ecc_ctx *ctx, CornerState *st, const CornerGeom &g, siz
         const size_t HW = (size_t)g.W * g.H;
         const size_t mask_b = ecc::align_up(HW * 4, 256);
         const size_t m_b = ecc::align_up(HW * 8 * kGroup, 256);
-        hipError_t e = hipMalloc(&st->img, 2 * mask_b + 2 * m_b);
+        const size_t b_b = ecc::align_up(HW * 8, 256);
+        hipError_t e = hipMalloc(&st->img, 2 * mask_b + 2 * m_b + b_b);
         if (e != hipSuccess) {
             st->img = nullptr;
             ecc::hip_fail(ctx, e, "hipMalloc(corner images)");
@@ -655,6 +672,7 @@ int corner_state_reserve(ecc_ctx *ctx, CornerState *st, const CornerGeom &g, siz
             st->set[b].mask = reinterpret_cast<uint32_t *>(p + b * mask_b);
             st->set[b].M = reinterpret_cast<int64_t *>(p + 2 * mask_b + b * m_b);
         }
+        st->b_alt = reinterpret_cast<int64_t *>(p + 2 * mask_b + 2 * m_b);
         st->W = g.W;
         st->H = g.H;
     }
@@ -783,23 +801,25 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     const int64_t grp_events = std::min<int64_t>((int64_t)kGroup * g.S, n);
     const int64_t arc_blocks = g.n_tiles + grp_events / kItemEvents;
     if (arc_blocks > INT32_MAX) return ECC_ERR_INVALID;
+    // B_g lives in bufB[g & 1]: B_0 = the caller's sae, B_1 = b_alt, ...
+    int64_t *bufB[2] = {sae, st->b_alt};
+    {
+        ECC_TIMED(ctx, s, "group_kernel");  // build(0) only
+        hipLaunchKernelGGL(group_kernel, dim3(g.n_tiles), dim3(kArcThreads), 0, s, t, g, (int64_t)-1, g.n_tiles, 0,
+                           so, st->set[1], st->set[0], (const int64_t *)bufB[0], bufB[1], (const int32_t *)first_border,
+                           corner_flags);
+    }
     for (int64_t gi = 0; gi < n_groups; ++gi) {
-        const GroupBufs cur = st->set[gi & 1], prv = st->set[(gi + 1) & 1];
-        {
-            ECC_TIMED(ctx, s, "tile_build_kernel");
-            hipLaunchKernelGGL(tile_build_kernel, dim3(g.n_tiles), dim3(kBuildThreads), 0, s, g, gi, so, cur,
-                               prv, sae);
-        }
-        {
-            ECC_TIMED(ctx, s, "arc_test_kernel");
-            hipLaunchKernelGGL(arc_test_kernel, dim3((unsigned)arc_blocks), dim3(kArcThreads), 0, s, t, g, gi,
-                               so, cur, (const int64_t *)sae, (const int32_t *)first_border, corner_flags);
-        }
+        const int n_build = (gi + 1 < n_groups) ? g.n_tiles : 0;
+        ECC_TIMED(ctx, s, "group_kernel");
+        hipLaunchKernelGGL(group_kernel, dim3((unsigned)(n_build + arc_blocks)), dim3(kArcThreads), 0, s, t, g, gi,
+                           n_build, 1, so, st->set[gi & 1], st->set[(gi + 1) & 1], (const int64_t *)bufB[gi & 1],
+                           bufB[(gi + 1) & 1], (const int32_t *)first_border, corner_flags);
     }
     {
-        ECC_TIMED(ctx, s, "tile_fold_kernel");
-        hipLaunchKernelGGL(tile_fold_kernel, dim3(g.n_tiles), dim3(kThreads), 0, s, g,
-                           st->set[(n_groups - 1) & 1], sae);
+        ECC_TIMED(ctx, s, "tile_fold_kernel");  // B_G into the caller's buffer
+        hipLaunchKernelGGL(tile_fold_kernel, dim3(g.n_tiles), dim3(kThreads), 0, s, g, st->set[(n_groups - 1) & 1],
+                           (const int64_t *)bufB[(n_groups - 1) & 1], sae);
     }
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
     return ECC_OK;
