@@ -52,6 +52,7 @@ constexpr int kTilePix = kTile * kTile;
 constexpr int kHalo = 4;           // circle radius
 constexpr int kWin = kTile + 2 * kHalo;  // 24
 constexpr int kWinPix = kWin * kWin;     // 576
+constexpr int kStageMinEvents = 128;     // smaller work items skip the window staging
 constexpr int kMaxTiles = 8191;          // bins per group = n_tiles + 1 (8192 fit an LDS histogram)
 constexpr int kMaxSlice = 1 << 19;       // group-local event index must fit 24 bits
 constexpr int64_t kEmptyT = INT64_MIN;
@@ -138,34 +139,100 @@ bin_hist_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, 
         if (hist[b]) atomicAdd(&so.bin_count[grp * nb + b], hist[b]);
 }
 
-// 2. Scatter keys + timestamps into (group, tile) order; order inside a bin is irrelevant.
+// Block-wide exclusive scan of in[0, n) into out (256 threads, each owning a contiguous run).
+__device__ __forceinline__ void block_excl_scan(const int32_t *in, int32_t *out, int n, int32_t *wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int per = (n + kThreads - 1) / kThreads;
+    const int b0 = min(n, tid * per), b1 = min(n, b0 + per);
+    int sum = 0;
+    for (int i = b0; i < b1; ++i) sum += in[i];
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int run = incl - sum;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+    for (int i = b0; i < b1; ++i) {
+        const int c = in[i];
+        out[i] = run;
+        run += c;
+    }
+}
+
+// 2. Scatter keys + timestamps into (group, tile) order (order inside a bin is irrelevant).
+// The slice reserves its range of every bin once; then each chunk of C events is counting-
+// sorted by bin in LDS and written out in bin order, so consecutive lanes store to
+// consecutive addresses (a direct scatter stores every lane to a different line).
+template <int C>
 __global__ void __launch_bounds__(kThreads)
 bin_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g,
                    Sorted so) {
     extern __shared__ int64_t lds64[];
+    __shared__ int32_t wsum[kThreads / 64];
     const int nb = g.n_tiles + 1;
-    int64_t *base = lds64;                                   // [nb]
-    int32_t *cnt = reinterpret_cast<int32_t *>(lds64 + nb);  // [nb]
+    int64_t *base = lds64;                                    // [nb] next free slot per bin
+    int32_t *cnt = reinterpret_cast<int32_t *>(base + nb);    // [nb]
+    int32_t *loff = cnt + nb;                                 // [nb]
+    int64_t *st_t = reinterpret_cast<int64_t *>(loff + nb);   // [C]  (nb*16 bytes: 8-aligned)
+    uint32_t *st_key = reinterpret_cast<uint32_t *>(st_t + C);  // [C]
+    uint16_t *st_bin = reinterpret_cast<uint16_t *>(st_key + C);  // [C]
+    const int tid = threadIdx.x;
     const int64_t s = blockIdx.x;
     const int64_t lo = s * g.S, hi = (lo + g.S < g.n) ? lo + g.S : g.n;
     const int64_t grp = s / kGroup;
     const int64_t grp_first = grp * kGroup * (int64_t)g.S;
-    for (int b = threadIdx.x; b < nb; b += kThreads) cnt[b] = 0;
+    for (int b = tid; b < nb; b += kThreads) cnt[b] = 0;
     __syncthreads();
-    for (int64_t e = lo + threadIdx.x; e < hi; e += kThreads) atomicAdd(&cnt[tile_of(xy[e], g)], 1);
+    for (int64_t e = lo + tid; e < hi; e += kThreads) atomicAdd(&cnt[tile_of(xy[e], g)], 1);
     __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += kThreads) {
+    for (int b = tid; b < nb; b += kThreads) {
         const int c = cnt[b];
         if (c) base[b] = so.bin_off[grp * nb + b] + atomicAdd(&so.cursor[grp * nb + b], c);
         cnt[b] = 0;
     }
     __syncthreads();
-    for (int64_t e = lo + threadIdx.x; e < hi; e += kThreads) {
-        const uint32_t v = xy[e];
-        const int b = tile_of(v, g);
-        const int64_t pos = base[b] + atomicAdd(&cnt[b], 1);
-        so.key[pos] = tile_key(v, (uint32_t)(e - grp_first));
-        so.t[pos] = t[e];
+    constexpr int kPer = C / kThreads;
+    for (int64_t c0 = lo; c0 < hi; c0 += C) {
+        const int cn = (int)((hi - c0) < C ? (hi - c0) : C);
+        uint32_t v[kPer];
+        int bb[kPer], rr[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int i = u * kThreads + tid;
+            v[u] = (i < cn) ? xy[c0 + i] : 0u;
+            bb[u] = (i < cn) ? tile_of(v[u], g) : -1;
+            rr[u] = (i < cn) ? atomicAdd(&cnt[bb[u]], 1) : 0;
+        }
+        __syncthreads();
+        block_excl_scan(cnt, loff, nb, wsum);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int i = u * kThreads + tid;
+            if (i < cn) {
+                const int pos = loff[bb[u]] + rr[u];
+                st_key[pos] = tile_key(v[u], (uint32_t)(c0 + i - grp_first));
+                st_t[pos] = t[c0 + i];
+                st_bin[pos] = (uint16_t)bb[u];
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < cn; i += kThreads) {
+            const int b = st_bin[i];
+            const int64_t gpos = base[b] + (i - loff[b]);
+            so.key[gpos] = st_key[i];
+            so.t[gpos] = st_t[i];
+        }
+        __syncthreads();
+        for (int b = tid; b < nb; b += kThreads) {
+            base[b] += cnt[b];
+            cnt[b] = 0;
+        }
+        __syncthreads();
     }
 }
 
@@ -375,7 +442,15 @@ __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, 
     return (uint32_t)d;
 }
 
-// exact int64 V from the global images (fallback)
+// exact int64 V(q, j) from the global images
+__device__ __forceinline__ int64_t sae_at(int64_t q, uint32_t below, const GroupBufs &cur,
+                                          const int64_t *__restrict__ B, int64_t HW) {
+    const uint32_t mk = cur.mask[q] & below;
+    if (mk) return cur.M[(int64_t)(31 - __clz(mk)) * HW + q];
+    return B[q];
+}
+
+// exact int64 V from the global images (fallback; mask from the staged window)
 __device__ __forceinline__ int64_t glob_at(const ArcLds &L, int wp, int64_t q, uint32_t below,
                                            const GroupBufs &cur, const int64_t *__restrict__ B,
                                            int64_t HW) {
@@ -405,6 +480,32 @@ __device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const Co
     const int64_t grp_first = grp * kGroup * (int64_t)g.S;
     const int64_t grp_end = (grp + 1) * kGroup * (int64_t)g.S;
     const int64_t Lt = t[(grp_end < g.n ? grp_end : g.n) - 1] - (int64_t)kVMax;
+    if (i1 - i0 < kStageMinEvents) {
+        // small item (sparse tile): staging 576 pixels would cost more than the events — exact
+        // int64 test straight from the global images, one event per lane
+        for (int64_t i = i0 + tid; i < i1; i += kArcThreads) {
+            const uint32_t key = so.key[i];
+            const int lp = (int)(key & 255u);
+            const uint32_t el = key >> 8;
+            const int x = x0 + lp % kTile, y = y0 + lp / kTile;
+            const int j = slice_in_group(el, g);
+            const int64_t s = grp * kGroup + j;
+            bool test = s >= g.first_detect && !is_border(x, y, g);
+            if (test && g.border_mode == 1) test = (int64_t)el - (int64_t)j * g.S < first_border[s];
+            if (!test) continue;
+            const uint32_t below = (j == 31) ? 0xffffffffu : ((2u << j) - 1u);
+            const int64_t q0 = (int64_t)y * g.W + x;
+            int64_t v3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v3[k] = sae_at(q0 + (int64_t)c3dy[k] * g.W + c3dx[k], below, cur, B, HW);
+            if (!arc_streak<16, 3, 6>(v3)) continue;
+            int64_t v4[20];
+#pragma unroll
+            for (int k = 0; k < 20; ++k) v4[k] = sae_at(q0 + (int64_t)c4dy[k] * g.W + c4dx[k], below, cur, B, HW);
+            if (arc_streak<20, 4, 8>(v4)) flags[grp_first + el] = 1;
+        }
+        return;
+    }
     if (tid == 0) {
         L.exact_only = 0;
         L.mixed = 0;
@@ -782,8 +883,13 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     if (rc) return rc;
     {
         ECC_TIMED(ctx, s, "bin_scatter_kernel");
-        hipLaunchKernelGGL(bin_scatter_kernel, dim3((unsigned)g.n_slices), dim3(kThreads), nb * 12, s, xy,
-                           t, g, so);
+        const size_t lds_big = (size_t)nb * 16 + 4096 * 14, lds_small = (size_t)nb * 16 + 1024 * 14;
+        if (lds_big <= 96 * 1024)
+            hipLaunchKernelGGL(bin_scatter_kernel<4096>, dim3((unsigned)g.n_slices), dim3(kThreads), lds_big, s, xy,
+                               t, g, so);
+        else
+            hipLaunchKernelGGL(bin_scatter_kernel<1024>, dim3((unsigned)g.n_slices), dim3(kThreads), lds_small, s,
+                               xy, t, g, so);
     }
     {
         ECC_TIMED(ctx, s, "item_count_kernel");
