@@ -74,7 +74,7 @@ struct Sorted {
     uint32_t *key;       // (event index - first event of the group) << 8 | y%16*16 + x%16
     int64_t *t;
     int32_t *bin_count;  // [n_bins]
-    int32_t *cursor;     // [n_bins]
+    int32_t *rel;        // [n_slices * nb] slice's offset inside each bin it touches
     int64_t *bin_off;    // [n_bins + 1]
     int32_t *n_items;    // [n_bins] work items per bin
     int64_t *item_off;   // [n_bins + 1]
@@ -109,7 +109,10 @@ __device__ __forceinline__ int slice_in_group(uint32_t el, const CornerGeom &g) 
     return (int)q;
 }
 
-// 1. Per-slice tile histogram (+ time-order check, first border index per slice for Q11).
+// 1. Per-slice tile histogram (+ time-order check, first border index per slice for Q11).  The
+// value returned by the bin-total atomic is the slice's offset inside the bin (kept in rel[]).
+constexpr int kHistUnroll = 8;
+
 __global__ void __launch_bounds__(kThreads)
 bin_hist_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g,
                 Sorted so, int32_t *__restrict__ first_border, int32_t *__restrict__ err) {
@@ -122,11 +125,25 @@ bin_hist_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, 
     __syncthreads();
     bool bad = false;
     int fb = 0x7fffffff;
-    for (int64_t e = lo + threadIdx.x; e < hi; e += kThreads) {
-        const uint32_t v = xy[e];
-        atomicAdd(&hist[tile_of(v, g)], 1);
-        if (e > 0 && t[e - 1] > t[e]) bad = true;
-        if (is_border(ecc::xy_x(v), ecc::xy_y(v), g)) fb = min(fb, (int)(e - lo));
+    for (int64_t e0 = lo; e0 < hi; e0 += kHistUnroll * kThreads) {
+        uint32_t v[kHistUnroll];
+        int64_t tc[kHistUnroll], tp[kHistUnroll];
+#pragma unroll
+        for (int u = 0; u < kHistUnroll; ++u) {
+            const int64_t e = e0 + u * kThreads + threadIdx.x;
+            v[u] = (e < hi) ? xy[e] : 0u;
+            tc[u] = (e < hi) ? t[e] : 0;
+            tp[u] = (e < hi && e > 0) ? t[e - 1] : INT64_MIN;
+        }
+#pragma unroll
+        for (int u = 0; u < kHistUnroll; ++u) {
+            const int64_t e = e0 + u * kThreads + threadIdx.x;
+            if (e < hi) {
+                atomicAdd(&hist[tile_of(v[u], g)], 1);
+                bad |= tp[u] > tc[u];
+                if (is_border(ecc::xy_x(v[u]), ecc::xy_y(v[u]), g)) fb = min(fb, (int)(e - lo));
+            }
+        }
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) *err = 1;
     if (g.border_mode == 1) {
@@ -136,7 +153,7 @@ bin_hist_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, 
     }
     __syncthreads();
     for (int b = threadIdx.x; b < nb; b += kThreads)
-        if (hist[b]) atomicAdd(&so.bin_count[grp * nb + b], hist[b]);
+        if (hist[b]) so.rel[s * nb + b] = atomicAdd(&so.bin_count[grp * nb + b], hist[b]);
 }
 
 // Block-wide exclusive scan of in[0, n) into out (256 threads, each owning a contiguous run).
@@ -164,7 +181,7 @@ __device__ __forceinline__ void block_excl_scan(const int32_t *in, int32_t *out,
 }
 
 // 2. Scatter keys + timestamps into (group, tile) order (order inside a bin is irrelevant).
-// The slice reserves its range of every bin once; then each chunk of C events is counting-
+// The slice's range of every bin comes from bin_hist (rel[]); each chunk of C events is counting-
 // sorted by bin in LDS and written out in bin order, so consecutive lanes store to
 // consecutive addresses (a direct scatter stores every lane to a different line).
 template <int C>
@@ -185,13 +202,8 @@ bin_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ 
     const int64_t lo = s * g.S, hi = (lo + g.S < g.n) ? lo + g.S : g.n;
     const int64_t grp = s / kGroup;
     const int64_t grp_first = grp * kGroup * (int64_t)g.S;
-    for (int b = tid; b < nb; b += kThreads) cnt[b] = 0;
-    __syncthreads();
-    for (int64_t e = lo + tid; e < hi; e += kThreads) atomicAdd(&cnt[tile_of(xy[e], g)], 1);
-    __syncthreads();
-    for (int b = tid; b < nb; b += kThreads) {
-        const int c = cnt[b];
-        if (c) base[b] = so.bin_off[grp * nb + b] + atomicAdd(&so.cursor[grp * nb + b], c);
+    for (int b = tid; b < nb; b += kThreads) {  // rel[] is only defined for bins the slice touches
+        base[b] = so.bin_off[grp * nb + b] + so.rel[s * nb + b];
         cnt[b] = 0;
     }
     __syncthreads();
@@ -741,7 +753,7 @@ Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_bins, int32_t **fi
     so.key = cv.take<uint32_t>((size_t)g.n);
     so.t = cv.take<int64_t>((size_t)g.n);
     so.bin_count = cv.take<int32_t>((size_t)n_bins);
-    so.cursor = cv.take<int32_t>((size_t)n_bins);
+    so.rel = cv.take<int32_t>((size_t)g.n_slices * (g.n_tiles + 1));
     so.bin_off = cv.take<int64_t>((size_t)n_bins + 1);
     so.n_items = cv.take<int32_t>((size_t)n_bins);
     so.item_off = cv.take<int64_t>((size_t)n_bins + 1);
@@ -871,7 +883,6 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
 
     ECC_CHECK_HIP(ctx, hipMemsetAsync(corner_flags, 0, (size_t)n, s), "memset(flags)");
     ECC_CHECK_HIP(ctx, hipMemsetAsync(so.bin_count, 0, (size_t)n_bins * 4, s), "memset(bins)");
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(so.cursor, 0, (size_t)n_bins * 4, s), "memset(cursor)");
     if (g.border_mode == 1)
         ECC_CHECK_HIP(ctx, hipMemsetAsync(first_border, 0x7f, (size_t)g.n_slices * 4, s), "memset(fb)");
     {
@@ -883,9 +894,9 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     if (rc) return rc;
     {
         ECC_TIMED(ctx, s, "bin_scatter_kernel");
-        const size_t lds_big = (size_t)nb * 16 + 4096 * 14, lds_small = (size_t)nb * 16 + 1024 * 14;
-        if (lds_big <= 96 * 1024)
-            hipLaunchKernelGGL(bin_scatter_kernel<4096>, dim3((unsigned)g.n_slices), dim3(kThreads), lds_big, s, xy,
+        const size_t lds_big = (size_t)nb * 16 + 2048 * 14, lds_small = (size_t)nb * 16 + 1024 * 14;
+        if (lds_big <= 48 * 1024)  // 4 workgroups per CU
+            hipLaunchKernelGGL(bin_scatter_kernel<2048>, dim3((unsigned)g.n_slices), dim3(kThreads), lds_big, s, xy,
                                t, g, so);
         else
             hipLaunchKernelGGL(bin_scatter_kernel<1024>, dim3((unsigned)g.n_slices), dim3(kThreads), lds_small, s,
