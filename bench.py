@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--height", type=int, default=260)
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--cpu-events", type=int, default=8_000_000, help="CPU-baseline sample size")
+    ap.add_argument("--cpu-events", type=int, default=40_000_000,
+                    help="CPU-baseline sample size (~16 s of single-thread oracle work)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for rehearsal")
@@ -171,15 +172,16 @@ def main():
     launches = stats[dominant]["launches"]
     avg_ms = kern_ms[dominant] / launches
     per_step_launches = launches / args.steps
+    # algorithmic bytes per launch (DESIGN.md "Measurement"): what the kernel must move at minimum
     bytes_per_launch = {
-        "downsample_hash_kernel": 4.0 * n + 4.0 * n_reps + 8.0 * n_win,
-        "kmeans_xy16_kernel": 4.0 * n_reps,
-        "kmeans_xy16_labels": 5.0 * n_reps,
-        "bin_hist_kernel": 12.0 * n,
-        "bin_scatter_kernel": 28.0 * n,
-        "tile_build_kernel": 16.0 * n / per_step_launches,
-        "arc_test_kernel": 9.0 * n / per_step_launches,
-        "nms_kernel": 1.0 * n,
+        "downsample_hash_kernel": 4.0 * n + 4.0 * n_reps + 8.0 * n_win,   # xy in, reps + counts out
+        "kmeans_xy16_kernel": 4.0 * n_reps,                               # packed u16 xy per point
+        "kmeans_xy16_labels": 5.0 * n_reps,                               # + u8 label out
+        "bin_hist_kernel": 12.0 * n,                                      # xy + t
+        "bin_scatter_kernel": 24.0 * n,                                   # xy + t in, key + t out
+        # group_kernel: key + t of group g+1 (build) and key of group g (arc); n_groups + 1 launches
+        "group_kernel": 16.0 * n / per_step_launches,
+        "nms_kernel": 1.0 * n,                                            # corner flags
         "kmeans_update_kernel": 0.0,
     }.get(dominant, 0.0)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9

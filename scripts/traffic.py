@@ -17,8 +17,11 @@ from pathlib import Path
 def short(name: str) -> str:
     m = re.search(r"::([A-Za-z_0-9]+)(<[^>]*>)?\(", name)
     base = m.group(1) if m else name.split("(")[0]
-    if base == "kmeans_xy16_kernel" and "<false>" in name:
-        return "kmeans_xy16_labels"
+    # map to the names libecc's timing report (and bench.py) use
+    if base in ("kmeans_xy16_kernel", "kmeans_fast_kernel"):
+        return "kmeans_xy16_labels" if re.search(r"<(\d+, )?false>", name) else "kmeans_xy16_kernel"
+    if base == "nms_grid_kernel":
+        return "nms_kernel"
     return base
 
 
