@@ -37,21 +37,30 @@
 // Algorithmic bytes: 12 B/event in (xy + t) + 1 B/event out (corner flag).
 #include "ecc_internal.hpp"
 
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
+
+// Development instrumentation (make CORNER_PROFILE=1): per-workgroup s_memrealtime stamps of one
+// group launch (ECC_CORNER_TS=<group>, ECC_CORNER_TS_FILE) and phase cut-offs (ECC_CORNER_DBG),
+// read by scripts/ts_analyze.py / ts_phases.py.  Compiled out by default.
+#ifndef ECC_CORNER_PROFILE
+#define ECC_CORNER_PROFILE 0
+#endif
 
 namespace {
 
 constexpr int kThreads = 256;
 constexpr int kBuildUnroll = 8;
-constexpr int kArcThreads = 512;
+constexpr int kArcThreads = 512;  // 8 waves: one lane per window pixel (484) when staging
 constexpr int kItemEvents = 2048;  // events per arc work item
 constexpr int kGroup = 32;         // slices per group (mask bits)
-constexpr int kTile = 16;          // tile edge (pixels)
+constexpr int kTile = 14;          // tile edge (pixels): the 22x22 window fits one 8-wave workgroup
 constexpr int kTilePix = kTile * kTile;
 constexpr int kHalo = 4;           // circle radius
-constexpr int kWin = kTile + 2 * kHalo;  // 24
-constexpr int kWinPix = kWin * kWin;     // 576
+constexpr int kWin = kTile + 2 * kHalo;  // 22
+constexpr int kWinPix = kWin * kWin;     // 484
 constexpr int kStageMinEvents = 128;     // smaller work items skip the window staging
 constexpr int kMaxTiles = 8191;          // bins per group = n_tiles + 1 (8192 fit an LDS histogram)
 constexpr int kMaxSlice = 1 << 19;       // group-local event index must fit 24 bits
@@ -61,6 +70,9 @@ struct CornerGeom {
     int W, H, S, margin, border_mode, first_detect;
     int tiles_x, n_tiles;  // bin n_tiles of each group holds the events outside the sensor
     float inv_S;
+    int dbg;                 // ECC_CORNER_PROFILE only
+    unsigned long long *ts;  // ECC_CORNER_PROFILE only
+    int64_t ts_grp;
     int64_t n, n_slices;
 };
 
@@ -78,7 +90,9 @@ struct Sorted {
     int64_t *bin_off;    // [n_bins + 1]
     int32_t *n_items;    // [n_bins] work items per bin
     int64_t *item_off;   // [n_bins + 1]
-    uint32_t *items;     // bin-in-group | chunk << 13
+    uint4 *items;        // [n_groups][max_items] {tile, first event, end event, -}
+    int32_t *grp_items;  // [n_groups] work items per group
+    int max_items;       // per-group stride of items
 };
 
 __constant__ int8_t c3dy[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -257,14 +271,26 @@ item_count_kernel(CornerGeom g, Sorted so, int64_t n_bins) {
     so.n_items[gb] = (b == g.n_tiles) ? 0 : (so.bin_count[gb] + kItemEvents - 1) / kItemEvents;
 }
 
+__device__ __forceinline__ int64_t i1_of(int64_t i0, int64_t b1) {
+    return (i0 + kItemEvents < b1) ? i0 + kItemEvents : b1;
+}
+
 __global__ void __launch_bounds__(kThreads)
 item_fill_kernel(CornerGeom g, Sorted so, int64_t n_bins) {
     const int64_t gb = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gb >= n_bins) return;
-    const uint32_t b = (uint32_t)(gb % (g.n_tiles + 1));
+    const int nb = g.n_tiles + 1;
+    const int64_t grp = gb / nb;
+    const uint32_t b = (uint32_t)(gb % nb);
     const int m = so.n_items[gb];
-    const int64_t o = so.item_off[gb];
-    for (int c = 0; c < m; ++c) so.items[o + c] = b | ((uint32_t)c << 13);
+    const int64_t first = so.item_off[grp * nb];
+    const int64_t o = so.item_off[gb] - first;
+    const int64_t b0 = so.bin_off[gb], b1 = so.bin_off[gb + 1];
+    for (int c = 0; c < m; ++c) {
+        const int64_t i0 = b0 + (int64_t)c * kItemEvents;
+        so.items[grp * so.max_items + o + c] = make_uint4(b, (uint32_t)i0, (uint32_t)(i1_of(i0, b1)), 0u);
+    }
+    if (b == (uint32_t)(nb - 1)) so.grp_items[grp] = (int32_t)(so.item_off[gb + 1] - first);
 }
 
 __device__ __forceinline__ void tile_origin(const CornerGeom &g, int tile, int &x0, int &y0) {
@@ -276,7 +302,7 @@ __device__ __forceinline__ void tile_origin(const CornerGeom &g, int tile, int &
 // the tile's pixels (dense; grp > 0), then accumulate mask/M of the tile's bin in LDS and store
 // them into set `cur`.  Runs as the first n_tiles workgroups of group_kernel(grp - 1).
 struct BuildLds {
-    int64_t mloc[kGroup][kTilePix];  // 64 KiB
+    int64_t mloc[kGroup][kTilePix];  // 49 KiB
     uint32_t mask_l[kTilePix];
 };
 
@@ -284,14 +310,16 @@ __device__ __forceinline__ void build_tile(const CornerGeom &g, int64_t grp, int
                                            const GroupBufs &cur, const GroupBufs &prv,
                                            const int64_t *__restrict__ B_in, int64_t *__restrict__ B_out,
                                            BuildLds &L) {
-    constexpr int kHalves = kArcThreads / kTilePix;  // 2 lanes per pixel
+    constexpr int kHalves = 2;  // 2 lanes per pixel (lanes >= 2 * kTilePix only load events)
+    static_assert(kArcThreads >= kHalves * kTilePix, "build lanes");
     constexpr int kPlanes = kGroup / kHalves;
     const int tid = threadIdx.x;
     const int p = tid % kTilePix, part = tid / kTilePix;
+    const bool pix_lane = part < kHalves;  // lanes beyond 2 x 256 only help with the events
     int x0, y0;
     tile_origin(g, tile, x0, y0);
     const int px = x0 + p % kTile, py = y0 + p / kTile;
-    const bool own = px < g.W && py < g.H;
+    const bool own = pix_lane && px < g.W && py < g.H;
     const int64_t HW = (int64_t)g.H * g.W;
     const int64_t q = (int64_t)py * g.W + px;
     if (part == 0) {
@@ -301,8 +329,10 @@ __device__ __forceinline__ void build_tile(const CornerGeom &g, int64_t grp, int
         }
         L.mask_l[p] = 0u;
     }
+    if (pix_lane) {
 #pragma unroll
-    for (int jj = 0; jj < kPlanes; ++jj) L.mloc[part * kPlanes + jj][p] = kEmptyT;
+        for (int jj = 0; jj < kPlanes; ++jj) L.mloc[part * kPlanes + jj][p] = kEmptyT;
+    }
     __syncthreads();
     const int nb = g.n_tiles + 1;
     const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
@@ -342,6 +372,7 @@ __global__ void __launch_bounds__(kThreads)
 tile_fold_kernel(CornerGeom g, GroupBufs buf, const int64_t *B_in, int64_t *B_out) {
     int x0, y0;
     tile_origin(g, blockIdx.x, x0, y0);
+    if (threadIdx.x >= kTilePix) return;
     const int px = x0 + threadIdx.x % kTile, py = y0 + threadIdx.x / kTile;
     if (px >= g.W || py >= g.H) return;
     const int64_t q = (int64_t)py * g.W + px;
@@ -434,13 +465,22 @@ __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
 // the clamped value the arc test of an event in slice j sees — so every circle lookup is one
 // independent LDS read.  mask[] (the group mask per window pixel) serves the exact fallback.
 struct ArcLds {
-    uint32_t T[kGroup][kWinPix];  // 72 KiB
-    uint32_t mask[kWinPix];
-    uint16_t q4[kItemEvents];     // events that passed circle 3 (item-local index)
+    uint32_t T[kGroup][kWinPix];  // 60.5 KiB
+    union {
+        uint32_t mask[kWinPix];  // staging: group mask per window pixel
+        struct {                 // tests: bit j*256 + pixel-in-tile
+            uint32_t pairs[kGroup * kTilePix / 32];  // (slice, pixel) pairs with an eligible event
+            uint32_t res[kGroup * kTilePix / 32];    // ... that are corners
+        } bits;
+    } u;
+    uint16_t word_off[kGroup * kTilePix / 32];  // exclusive prefix of popc(pairs)
+    uint16_t q4[kItemEvents];                    // pairs that passed circle 3
     int64_t wave_min[kArcThreads / 64];
+    int32_t wave_tot[kArcThreads / 64];
     int32_t exact_only;  // a value above t_last: clamped keys unusable
     int32_t mixed;       // clamped values not all equal to the window minimum of B
     int32_t q4n;
+    int32_t n_tasks;
 };
 
 __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, int32_t *exact_flag,
@@ -454,36 +494,53 @@ __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, 
     return (uint32_t)d;
 }
 
-// exact int64 V(q, j) from the global images
-__device__ __forceinline__ int64_t sae_at(int64_t q, uint32_t below, const GroupBufs &cur,
-                                          const int64_t *__restrict__ B, int64_t HW) {
-    const uint32_t mk = cur.mask[q] & below;
-    if (mk) return cur.M[(int64_t)(31 - __clz(mk)) * HW + q];
-    return B[q];
+// Exact int64 V(q_k, j) of N circle pixels from the global images in two dependent levels:
+// all masks, then one selected address per pixel (no branch between a mask and its load).
+template <int N>
+__device__ __forceinline__ void sae_gather(int64_t q0, const int8_t *dy, const int8_t *dx, int W, uint32_t below,
+                                           const GroupBufs &cur, const int64_t *__restrict__ B, int64_t HW,
+                                           int64_t (&v)[N]) {
+    uint32_t mk[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) mk[k] = cur.mask[q0 + (int64_t)dy[k] * W + dx[k]] & below;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int64_t q = q0 + (int64_t)dy[k] * W + dx[k];
+        const int64_t *p = mk[k] ? cur.M + (int64_t)(31 - __clz(mk[k])) * HW + q : B + q;
+        v[k] = *p;
+    }
 }
 
-// exact int64 V from the global images (fallback; mask from the staged window)
-__device__ __forceinline__ int64_t glob_at(const ArcLds &L, int wp, int64_t q, uint32_t below,
-                                           const GroupBufs &cur, const int64_t *__restrict__ B,
-                                           int64_t HW) {
-    const uint32_t mk = L.mask[wp] & below;
-    if (!mk) return B[q];
-    return cur.M[(int64_t)(31 - __clz(mk)) * HW + q];
+// Exact int64 arc test of one circle from the global images (rare fallback; out of line so its
+// registers do not raise the pressure of the main kernel body).
+__device__ __noinline__ bool exact_circle_test(int x, int y, int j, bool c3, int W, const GroupBufs cur,
+                                               const int64_t *__restrict__ B, int64_t HW) {
+    const uint32_t below = (j == 31) ? 0xffffffffu : ((2u << j) - 1u);
+    const int64_t q0 = (int64_t)y * W + x;
+    if (c3) {
+        int64_t v3[16];
+        sae_gather<16>(q0, c3dy, c3dx, W, below, cur, B, HW, v3);
+        return arc_streak<16, 3, 6>(v3);
+    }
+    int64_t v4[20];
+    sae_gather<20>(q0, c4dy, c4dx, W, below, cur, B, HW, v4);
+    return arc_streak<20, 4, 8>(v4);
 }
 
 // 4. Arc test of one work item (<= kItemEvents tile-sorted events of group `grp`).
+#define ARC_STAMP(k)                                                                              \
+    do {                                                                                          \
+        if (ECC_CORNER_PROFILE && g.ts && grp == g.ts_grp && threadIdx.x == 0)                    \
+            g.ts[(size_t)item_idx * 16 + 4 + (k)] = __builtin_amdgcn_s_memrealtime();             \
+    } while (0)
 __device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const CornerGeom &g, int64_t grp,
                                          int item_idx, const Sorted &so, const GroupBufs &cur,
                                          const int64_t *__restrict__ B, const int32_t *__restrict__ first_border,
                                          uint8_t *__restrict__ flags, ArcLds &L) {
-    const int nb = g.n_tiles + 1;
-    const int64_t it0 = so.item_off[grp * nb], it1 = so.item_off[(grp + 1) * nb];
-    if (it0 + item_idx >= it1) return;
-    const uint32_t item = so.items[it0 + item_idx];
-    const int tile = (int)(item & 8191u), chunk = (int)(item >> 13);
-    const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
-    const int64_t i0 = b0 + (int64_t)chunk * kItemEvents;
-    const int64_t i1 = (i0 + kItemEvents < b1) ? i0 + kItemEvents : b1;
+    const uint4 rec = so.items[grp * so.max_items + item_idx];  // one load resolves the item
+    if (item_idx >= so.grp_items[grp]) return;
+    const int tile = (int)rec.x;
+    const int64_t i0 = rec.y, i1 = rec.z;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t HW = (int64_t)g.H * g.W;
     int x0, y0;
@@ -492,6 +549,7 @@ __device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const Co
     const int64_t grp_first = grp * kGroup * (int64_t)g.S;
     const int64_t grp_end = (grp + 1) * kGroup * (int64_t)g.S;
     const int64_t Lt = t[(grp_end < g.n ? grp_end : g.n) - 1] - (int64_t)kVMax;
+    if (ECC_CORNER_PROFILE && (g.dbg & 4)) return;
     if (i1 - i0 < kStageMinEvents) {
         // small item (sparse tile): staging 576 pixels would cost more than the events — exact
         // int64 test straight from the global images, one event per lane
@@ -505,16 +563,8 @@ __device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const Co
             bool test = s >= g.first_detect && !is_border(x, y, g);
             if (test && g.border_mode == 1) test = (int64_t)el - (int64_t)j * g.S < first_border[s];
             if (!test) continue;
-            const uint32_t below = (j == 31) ? 0xffffffffu : ((2u << j) - 1u);
-            const int64_t q0 = (int64_t)y * g.W + x;
-            int64_t v3[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) v3[k] = sae_at(q0 + (int64_t)c3dy[k] * g.W + c3dx[k], below, cur, B, HW);
-            if (!arc_streak<16, 3, 6>(v3)) continue;
-            int64_t v4[20];
-#pragma unroll
-            for (int k = 0; k < 20; ++k) v4[k] = sae_at(q0 + (int64_t)c4dy[k] * g.W + c4dx[k], below, cur, B, HW);
-            if (arc_streak<20, 4, 8>(v4)) flags[grp_first + el] = 1;
+            if (exact_circle_test(x, y, j, true, g.W, cur, B, HW) && exact_circle_test(x, y, j, false, g.W, cur, B, HW))
+                flags[grp_first + el] = 1;
         }
         return;
     }
@@ -524,169 +574,207 @@ __device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const Co
     }
 
     // keys of the item (preloaded; the loads overlap the staging)
-    constexpr int kPerLane = kItemEvents / kArcThreads;
+    constexpr int kPerLane = (kItemEvents + kArcThreads - 1) / kArcThreads;
     uint32_t keys[kPerLane];
 #pragma unroll
     for (int u = 0; u < kPerLane; ++u) {
         const int64_t i = i0 + tid + (int64_t)u * kArcThreads;
         keys[u] = (i < i1) ? so.key[i] : 0xffffffffu;
     }
-    // (a) window masks + B (lanes own window pixels tid and tid + kArcThreads)
-    uint32_t mk_r[2] = {0u, 0u};
-    int64_t b_r[2] = {INT64_MAX, INT64_MAX};  // INT64_MAX: outside the sensor (never read)
+    // (a) one lane per window pixel: its group mask and B, then the low 32 bits of its set M
+    //     planes, issued before the barrier.  When the group spans < 2^27 ticks every M lies in
+    //     (Lt, t_last], so M' = M - Lt is exact from the low words.  (Loading all 32 planes
+    //     without waiting for the mask was measured slower: ~73 KB of extra L2 traffic per item.)
+    static_assert(kArcThreads >= kWinPix, "one lane per window pixel");
+    const int wp = tid;
+    const bool win_lane = wp < kWinPix;
+    const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
+    const bool in = win_lane && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
+    const int64_t qq = (int64_t)wy * g.W + wx;
+    const uint32_t mk = in ? cur.mask[qq] : 0u;
+    const int64_t bq = in ? B[qq] : INT64_MAX;  // INT64_MAX: outside the sensor (never read)
+    uint32_t v[kGroup];
+    {  // only the planes whose mask bit is set (issued before the barrier below)
+        const uint32_t *M32 = reinterpret_cast<const uint32_t *>(cur.M + (in ? qq : 0));
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const int wp = tid + r * kArcThreads;
-        if (wp < kWinPix) {
-            const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
-            const bool in = wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
-            const int64_t qq = (int64_t)wy * g.W + wx;
-            mk_r[r] = in ? cur.mask[qq] : 0u;
-            b_r[r] = in ? B[qq] : INT64_MAX;
-            L.mask[wp] = mk_r[r];
-        }
+        for (int j = 0; j < kGroup; ++j) v[j] = ((mk >> j) & 1u) ? M32[(int64_t)j * HW * 2] : 0u;
     }
-    int64_t bmin = b_r[0] < b_r[1] ? b_r[0] : b_r[1];
+    if (win_lane) L.u.mask[wp] = mk;
+    int64_t bmin = bq;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const int64_t v = __shfl_xor(bmin, o);
-        bmin = v < bmin ? v : bmin;
+        const int64_t x = __shfl_xor(bmin, o);
+        bmin = x < bmin ? x : bmin;
     }
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
     int64_t vz = INT64_MAX;
 #pragma unroll
     for (int w = 0; w < kArcThreads / 64; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
-    // (b) one lane per window pixel: gather the pixel's set M planes (all loads in flight), then
-    //     forward-fill along j in registers: T[j] = bit j set ? M'_j : T[j-1], T[-1] = B'.
-    //     When the group spans < 2^27 ticks every M lies in (Lt, t_last], so M' = M - Lt is
-    //     exact from the low 32 bits alone (half the bytes, one subtract).
+    ARC_STAMP(0);
+    if (ECC_CORNER_PROFILE && (g.dbg & 2)) return;
+    // (b) forward fill along j in registers: T[j] = bit j set ? M'_j : T[j-1], T[-1] = B'
     const int64_t t_first = t[grp_first];
     const bool narrow = (Lt + (int64_t)kVMax) - t_first < (int64_t)kVMax;  // uniform
+    uint32_t cur_v = (bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
+    if (!win_lane) {
+    } else if (narrow) {
+        const uint32_t lt32 = (uint32_t)Lt;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const int wp = tid + r * kArcThreads;
-        if (wp < kWinPix) {
-            const uint32_t mk = mk_r[r];
-            const int64_t qq = (int64_t)(wy0 + wp / kWin) * g.W + (wx0 + wp % kWin);
-            uint32_t cur_v = (b_r[r] == INT64_MAX) ? 0u : clamp_rel(b_r[r], Lt, vz, &L.exact_only, &L.mixed);
-            if (narrow) {
-                const uint32_t *M32 = reinterpret_cast<const uint32_t *>(cur.M + qq);  // low words
-                uint32_t v[kGroup];
-#pragma unroll
-                for (int j = 0; j < kGroup; ++j) v[j] = ((mk >> j) & 1u) ? M32[(int64_t)j * HW * 2] : 0u;
-                const uint32_t lt32 = (uint32_t)Lt;
-#pragma unroll
-                for (int j = 0; j < kGroup; ++j) {
-                    cur_v = ((mk >> j) & 1u) ? v[j] - lt32 : cur_v;
-                    L.T[j][wp] = cur_v;
-                }
-            } else {
+        for (int j = 0; j < kGroup; ++j) {
+            cur_v = ((mk >> j) & 1u) ? v[j] - lt32 : cur_v;
+            L.T[j][wp] = cur_v;
+        }
+    } else {
 #pragma unroll 4
-                for (int j = 0; j < kGroup; ++j) {
-                    if ((mk >> j) & 1u) cur_v = clamp_rel(cur.M[(int64_t)j * HW + qq], Lt, vz, &L.exact_only, &L.mixed);
-                    L.T[j][wp] = cur_v;
-                }
-            }
+        for (int j = 0; j < kGroup; ++j) {
+            if ((mk >> j) & 1u) cur_v = clamp_rel(cur.M[(int64_t)j * HW + qq], Lt, vz, &L.exact_only, &L.mixed);
+            L.T[j][wp] = cur_v;
         }
     }
     __syncthreads();
     const bool fast = !L.exact_only;
+    ARC_STAMP(1);
+    if (ECC_CORNER_PROFILE && (g.dbg & 1)) return;
     const bool ties_exact = !L.mixed;
-    // (d) circle 3 for one event per lane; survivors go to an LDS queue so that circle 4 runs
-    //     densely over them (a whole wave would otherwise execute it for any single survivor)
-    struct Ev {
-        int x, y, j, wp0;
-        uint32_t el;
-        bool test;
-    };
-    auto decode = [&](uint32_t key) {
-        Ev e;
-        const int lp = (int)(key & 255u);
-        e.el = key >> 8;
-        e.x = x0 + lp % kTile;
-        e.y = y0 + lp / kTile;
-        e.j = slice_in_group(e.el, g);
-        const int64_t s = grp * kGroup + e.j;
-        e.test = s >= g.first_detect && !is_border(e.x, e.y, g);
-        if (e.test && g.border_mode == 1) e.test = (int64_t)e.el - (int64_t)e.j * g.S < first_border[s];
-        e.wp0 = (e.y - wy0) * kWin + (e.x - wx0);
-        return e;
-    };
-    auto exact_circle = [&](const Ev &e, bool c3) {  // exact int64 test from the global images
-        const uint32_t below = (e.j == 31) ? 0xffffffffu : ((2u << e.j) - 1u);
-        const int64_t q0 = (int64_t)e.y * g.W + e.x;
-        if (c3) {
-            int64_t v3[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                v3[k] = glob_at(L, e.wp0 + c3dy[k] * kWin + c3dx[k], q0 + (int64_t)c3dy[k] * g.W + c3dx[k], below,
-                                cur, B, HW);
-            return arc_streak<16, 3, 6>(v3);
-        }
-        int64_t v4[20];
-#pragma unroll
-        for (int k = 0; k < 20; ++k)
-            v4[k] = glob_at(L, e.wp0 + c4dy[k] * kWin + c4dx[k], q0 + (int64_t)c4dy[k] * g.W + c4dx[k], below,
-                            cur, B, HW);
-        return arc_streak<20, 4, 8>(v4);
-    };
+    // (d) the test depends only on (slice j, pixel): eligible events mark their pair in a bitmap,
+    //     each distinct pair is tested once (one per lane; ~2.5x fewer tests than events on
+    //     dense tiles), circle-3 survivors are queued so circle 4 runs densely, and every event
+    //     finally reads its pair's result.  Eligibility (first slice, border, the border-mode-1
+    //     cut at the slice's first border event) stays per event.
+    constexpr int kPairWords = kGroup * kTilePix / 32;  // 196
+    for (int w = tid; w < 2 * kPairWords; w += kArcThreads) (&L.u.bits.pairs[0])[w] = 0u;
     if (tid == 0) L.q4n = 0;
     __syncthreads();
-#pragma unroll 1
+    uint32_t pidx[kPerLane];
+#pragma unroll
     for (int u = 0; u < kPerLane; ++u) {
+        pidx[u] = 0xffffffffu;
         const uint32_t key = keys[u];
-        if (key == 0xffffffffu) break;
-        const Ev e = decode(key);
-        if (!e.test) continue;
+        if (key == 0xffffffffu) continue;
+        const int lp = (int)(key & 255u);
+        const uint32_t el = key >> 8;
+        const int j = slice_in_group(el, g);
+        const int64_t s = grp * kGroup + j;
+        bool test = s >= g.first_detect && !is_border(x0 + lp % kTile, y0 + lp / kTile, g);
+        if (test && g.border_mode == 1) test = (int64_t)el - (int64_t)j * g.S < first_border[s];
+        if (!test) continue;
+        pidx[u] = (uint32_t)(j * kTilePix + lp);
+        atomicOr(&L.u.bits.pairs[pidx[u] >> 5], 1u << (pidx[u] & 31u));
+    }
+    __syncthreads();
+    int wcnt = 0, wincl = 0;
+    if (tid < kPairWords) {  // exclusive prefix of the words' popcounts (waves 0-3)
+        wcnt = __popc(L.u.bits.pairs[tid]);
+        wincl = wcnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(wincl, o);
+            if (lane >= o) wincl += v;
+        }
+        if (lane == 63) L.wave_tot[wave] = wincl;
+    }
+    __syncthreads();
+    if (tid < kPairWords) {
+        int before = 0;
+        for (int w = 0; w < wave; ++w) before += L.wave_tot[w];
+        L.word_off[tid] = (uint16_t)(before + wincl - wcnt);
+        if (tid == kPairWords - 1) L.n_tasks = before + wincl;
+    }
+    __syncthreads();
+    const int n_tasks = L.n_tasks;
+    ARC_STAMP(2);
+    auto task_pair = [&](int ti) {  // ti-th set bit of the pair bitmap
+        int lo = 0, hi = kPairWords;
+#pragma unroll
+        for (int step = 0; step < 8; ++step) {  // 2^8 >= kPairWords
+            const int mid = (lo + hi) >> 1;
+            if ((int)L.word_off[mid] <= ti) lo = mid; else hi = mid;
+        }
+        uint32_t m = L.u.bits.pairs[lo];
+        for (int r = ti - (int)L.word_off[lo]; r > 0; --r) m &= m - 1;
+        return lo * 32 + (__ffs(m) - 1);
+    };
+    auto exact_circle = [&](int x, int y, int j, bool c3) {
+        return exact_circle_test(x, y, j, c3, g.W, cur, B, HW);
+    };
+    for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+        const int pi = task_pair(ti);
+        const int j = pi / kTilePix, lp = pi % kTilePix;
+        const int x = x0 + lp % kTile, y = y0 + lp / kTile;
+        const int wp0 = (y - wy0) * kWin + (x - wx0);
         int res = -1;
         if (fast) {
-            const uint32_t *Tj = L.T[e.j];
+            const uint32_t *Tj = L.T[j];
             uint32_t k3[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) k3[k] = (Tj[e.wp0 + c3dy[k] * kWin + c3dx[k]] << 4) | k;
+            for (int k = 0; k < 16; ++k) k3[k] = (Tj[wp0 + c3dy[k] * kWin + c3dx[k]] << 4) | k;
             res = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
         }
-        if (res < 0) res = exact_circle(e, true) ? 1 : 0;
-        if (res == 1) L.q4[atomicAdd(&L.q4n, 1)] = (uint16_t)(tid + u * kArcThreads);
+        if (res < 0) res = exact_circle(x, y, j, true) ? 1 : 0;
+        if (res == 1) L.q4[atomicAdd(&L.q4n, 1)] = (uint16_t)pi;
     }
     __syncthreads();
     const int n4 = L.q4n;
+    ARC_STAMP(3);
     for (int qi = tid; qi < n4; qi += kArcThreads) {
-        const Ev e = decode(so.key[i0 + L.q4[qi]]);
+        const int pi = L.q4[qi];
+        const int j = pi / kTilePix, lp = pi % kTilePix;
+        const int x = x0 + lp % kTile, y = y0 + lp / kTile;
+        const int wp0 = (y - wy0) * kWin + (x - wx0);
         int res = -1;
         if (fast) {
-            const uint32_t *Tj = L.T[e.j];
+            const uint32_t *Tj = L.T[j];
             uint32_t k4[32];
 #pragma unroll
-            for (int k = 0; k < 20; ++k) k4[k] = (Tj[e.wp0 + c4dy[k] * kWin + c4dx[k]] << 5) | k;
+            for (int k = 0; k < 20; ++k) k4[k] = (Tj[wp0 + c4dy[k] * kWin + c4dx[k]] << 5) | k;
 #pragma unroll
             for (int k = 20; k < 32; ++k) k4[k] = 0u;
             res = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
         }
-        if (res < 0) res = exact_circle(e, false) ? 1 : 0;
-        if (res == 1) flags[grp_first + e.el] = 1;
+        if (res < 0) res = exact_circle(x, y, j, false) ? 1 : 0;
+        if (res == 1) atomicOr(&L.u.bits.res[pi >> 5], 1u << (pi & 31));
     }
+    __syncthreads();
+    ARC_STAMP(4);
+#pragma unroll
+    for (int u = 0; u < kPerLane; ++u)
+        if (pidx[u] != 0xffffffffu && ((L.u.bits.res[pidx[u] >> 5] >> (pidx[u] & 31u)) & 1u))
+            flags[grp_first + (keys[u] >> 8)] = 1;
 }
 
-// One launch per group g: workgroups [0, n_build) build group g+1 (tile = blockIdx) while the
-// rest test the work items of group g.  Both read set g&1; the build writes set (g+1)&1 and
+// One launch per group g: workgroups [0, n_arc) test the work items of group g, the rest build
+// group g+1 (one tile each).  Both read set g&1; the build writes set (g+1)&1 and
 // B_{g+1} = fold(B_g) into the other B buffer, so nothing the arc test reads changes under it.
 union GroupLds {
     ArcLds arc;
     BuildLds build;
 };
 
-__global__ void __launch_bounds__(kArcThreads)
-group_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, int n_build, int do_arc, Sorted so,
+__global__ void __launch_bounds__(kArcThreads, 4)  // two 8-wave workgroups per CU
+group_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, int n_arc, Sorted so,
              GroupBufs cur, GroupBufs nxt, const int64_t *B_in, int64_t *B_out,
              const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags) {
     __shared__ GroupLds L;
-    if ((int)blockIdx.x < n_build) {
-        build_tile(g, grp + 1, (int)blockIdx.x, so, nxt, cur, B_in, B_out, L.build);
-        return;
+    const bool rec = ECC_CORNER_PROFILE && g.ts && grp == g.ts_grp && threadIdx.x == 0;
+    unsigned long long t_start = rec ? __builtin_amdgcn_s_memrealtime() : 0;
+    if ((int)blockIdx.x < n_arc) {  // long arc items first, short build workgroups fill in after
+        if (!(ECC_CORNER_PROFILE && (g.dbg & 8))) arc_item(t, g, grp, (int)blockIdx.x, so, cur, B_in, first_border, flags, L.arc);
+    } else {
+        build_tile(g, grp + 1, (int)blockIdx.x - n_arc, so, nxt, cur, B_in, B_out, L.build);
     }
-    if (do_arc) arc_item(t, g, grp, (int)blockIdx.x - n_build, so, cur, B_in, first_border, flags, L.arc);
+    if (rec) {
+        unsigned int hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned int xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g.ts[blockIdx.x * 16 + 0] = t_start;
+        g.ts[blockIdx.x * 16 + 1] = __builtin_amdgcn_s_memrealtime();
+        g.ts[blockIdx.x * 16 + 2] = ((int)blockIdx.x < n_arc && (int)blockIdx.x < so.grp_items[grp])
+                                       ? (so.items[grp * so.max_items + blockIdx.x].z - so.items[grp * so.max_items + blockIdx.x].y)
+                                       : 0xfffff;
+        g.ts[blockIdx.x * 16 + 3] = xcc;
+    }
 }
 
 // Plain final-SAE scatter (no detection): sae[q] = max t.
@@ -757,7 +845,10 @@ Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_bins, int32_t **fi
     so.bin_off = cv.take<int64_t>((size_t)n_bins + 1);
     so.n_items = cv.take<int32_t>((size_t)n_bins);
     so.item_off = cv.take<int64_t>((size_t)n_bins + 1);
-    so.items = cv.take<uint32_t>((size_t)(g.n / kItemEvents + n_bins + 1));
+    const int64_t n_groups = (g.n_slices + kGroup - 1) / kGroup;
+    so.max_items = (int)(g.n_tiles + std::min<int64_t>((int64_t)kGroup * g.S, g.n) / kItemEvents);
+    so.items = cv.take<uint4>((size_t)n_groups * so.max_items);
+    so.grp_items = cv.take<int32_t>((size_t)n_groups);
     *first_border = cv.take<int32_t>((size_t)g.n_slices);
     *scan_scratch = cv.take<int64_t>((ecc::scan_scratch_bytes(n_bins) + 7) / 8);
     return so;
@@ -855,6 +946,19 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     g.H = cfg->height;
     g.S = cfg->slice_events;
     g.inv_S = 1.0f / (float)g.S;
+    g.dbg = 0;
+    g.ts = nullptr;
+    g.ts_grp = -1;
+#if ECC_CORNER_PROFILE
+    g.dbg = getenv("ECC_CORNER_DBG") ? atoi(getenv("ECC_CORNER_DBG")) : 0;
+    static unsigned long long *ts_buf = nullptr;
+    g.ts_grp = getenv("ECC_CORNER_TS") ? atoi(getenv("ECC_CORNER_TS")) : -1;
+    if (g.ts_grp >= 0) {
+        if (!ts_buf) (void)hipMalloc(&ts_buf, 1 << 20);
+        (void)hipMemset(ts_buf, 0, 1 << 20);
+        g.ts = ts_buf;
+    }
+#endif
     g.margin = cfg->margin;
     g.border_mode = cfg->border_mode;
     g.first_detect = cfg->first_detect_slice;
@@ -922,15 +1026,14 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     int64_t *bufB[2] = {sae, st->b_alt};
     {
         ECC_TIMED(ctx, s, "group_kernel");  // build(0) only
-        hipLaunchKernelGGL(group_kernel, dim3(g.n_tiles), dim3(kArcThreads), 0, s, t, g, (int64_t)-1, g.n_tiles, 0,
-                           so, st->set[1], st->set[0], (const int64_t *)bufB[0], bufB[1], (const int32_t *)first_border,
+        hipLaunchKernelGGL(group_kernel, dim3(g.n_tiles), dim3(kArcThreads), 0, s, t, g, (int64_t)-1, 0, so, st->set[1], st->set[0], (const int64_t *)bufB[0], bufB[1], (const int32_t *)first_border,
                            corner_flags);
     }
     for (int64_t gi = 0; gi < n_groups; ++gi) {
         const int n_build = (gi + 1 < n_groups) ? g.n_tiles : 0;
         ECC_TIMED(ctx, s, "group_kernel");
         hipLaunchKernelGGL(group_kernel, dim3((unsigned)(n_build + arc_blocks)), dim3(kArcThreads), 0, s, t, g, gi,
-                           n_build, 1, so, st->set[gi & 1], st->set[(gi + 1) & 1], (const int64_t *)bufB[gi & 1],
+                           (int)arc_blocks, so, st->set[gi & 1], st->set[(gi + 1) & 1], (const int64_t *)bufB[gi & 1],
                            bufB[(gi + 1) & 1], (const int32_t *)first_border, corner_flags);
     }
     {
@@ -939,6 +1042,15 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
                            (const int64_t *)bufB[(n_groups - 1) & 1], sae);
     }
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
+#if ECC_CORNER_PROFILE
+    if (g.ts) {
+        (void)hipStreamSynchronize(s);
+        static unsigned long long hb[1 << 17];
+        (void)hipMemcpy(hb, g.ts, 1 << 20, hipMemcpyDeviceToHost);
+        FILE *f = fopen(getenv("ECC_CORNER_TS_FILE") ? getenv("ECC_CORNER_TS_FILE") : "/tmp/ts.bin", "wb");
+        if (f) { fwrite(hb, 1, 1 << 20, f); fclose(f); }
+    }
+#endif
     return ECC_OK;
 }
 
