@@ -64,7 +64,6 @@ constexpr int kWinPix = kWin * kWin;     // 484
 constexpr int kStageMinEvents = 128;     // smaller work items skip the window staging
 constexpr int kMaxTiles = 8191;          // bins per group = n_tiles + 1 (8192 fit an LDS histogram)
 constexpr int kMaxSlice = 1 << 19;       // group-local event index must fit 24 bits
-constexpr int64_t kEmptyT = INT64_MIN;
 
 struct CornerGeom {
     int W, H, S, margin, border_mode, first_detect;
@@ -83,8 +82,8 @@ struct GroupBufs {
 
 // Batch sorted by (group, tile): bin b of group g is [bin_off[g*nb+b], bin_off[g*nb+b+1]).
 struct Sorted {
-    uint32_t *key;       // (event index - first event of the group) << 8 | y%16*16 + x%16
-    int64_t *t;
+    uint32_t *key;       // (event index - first event of the group) << 8 | pixel in tile
+    uint32_t *t32;       // t - t(first event of the group), written for groups spanning < 2^32 - 1
     int32_t *bin_count;  // [n_bins]
     int32_t *rel;        // [n_slices * nb] slice's offset inside each bin it touches
     int64_t *bin_off;    // [n_bins + 1]
@@ -112,6 +111,15 @@ __device__ __forceinline__ int tile_of(uint32_t v, const CornerGeom &g) {
 
 __device__ __forceinline__ uint32_t tile_key(uint32_t v, uint32_t e_local) {
     return (e_local << 8) | (uint32_t)((ecc::xy_y(v) % kTile) * kTile + ecc::xy_x(v) % kTile);
+}
+
+// The group's events span < 2^32 - 1 ticks: t - t(first event) fits a u32 (+1 still fits).
+__device__ __forceinline__ bool group_narrow(const int64_t *__restrict__ t, const CornerGeom &g, int64_t grp,
+                                             int64_t *t_first) {
+    const int64_t first = grp * kGroup * (int64_t)g.S;
+    const int64_t end = (grp + 1) * kGroup * (int64_t)g.S;
+    *t_first = t[first];
+    return (uint64_t)(t[(end < g.n ? end : g.n) - 1] - *t_first) < 0xffffffffull;
 }
 
 // floor(el / S) for el < 2^24 (float estimate, then exact correction).
@@ -194,28 +202,30 @@ __device__ __forceinline__ void block_excl_scan(const int32_t *in, int32_t *out,
     }
 }
 
-// 2. Scatter keys + timestamps into (group, tile) order (order inside a bin is irrelevant).
+// 2. Scatter 4-byte keys (+ 4-byte group-relative timestamps when the group spans < 2^32 - 1
+// ticks) into (group, tile) order; order inside a bin is irrelevant.
 // The slice's range of every bin comes from bin_hist (rel[]); each chunk of C events is counting-
 // sorted by bin in LDS and written out in bin order, so consecutive lanes store to
 // consecutive addresses (a direct scatter stores every lane to a different line).
 template <int C>
 __global__ void __launch_bounds__(kThreads)
-bin_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g,
-                   Sorted so) {
+bin_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g, Sorted so) {
     extern __shared__ int64_t lds64[];
     __shared__ int32_t wsum[kThreads / 64];
     const int nb = g.n_tiles + 1;
     int64_t *base = lds64;                                    // [nb] next free slot per bin
     int32_t *cnt = reinterpret_cast<int32_t *>(base + nb);    // [nb]
     int32_t *loff = cnt + nb;                                 // [nb]
-    int64_t *st_t = reinterpret_cast<int64_t *>(loff + nb);   // [C]  (nb*16 bytes: 8-aligned)
-    uint32_t *st_key = reinterpret_cast<uint32_t *>(st_t + C);  // [C]
-    uint16_t *st_bin = reinterpret_cast<uint16_t *>(st_key + C);  // [C]
+    uint32_t *st_key = reinterpret_cast<uint32_t *>(loff + nb);  // [C]
+    uint32_t *st_t = st_key + C;                                  // [C]
+    uint16_t *st_bin = reinterpret_cast<uint16_t *>(st_t + C);    // [C]
     const int tid = threadIdx.x;
     const int64_t s = blockIdx.x;
     const int64_t lo = s * g.S, hi = (lo + g.S < g.n) ? lo + g.S : g.n;
     const int64_t grp = s / kGroup;
     const int64_t grp_first = grp * kGroup * (int64_t)g.S;
+    int64_t t_first;
+    const bool narrow = group_narrow(t, g, grp, &t_first);  // uniform
     for (int b = tid; b < nb; b += kThreads) {  // rel[] is only defined for bins the slice touches
         base[b] = so.bin_off[grp * nb + b] + so.rel[s * nb + b];
         cnt[b] = 0;
@@ -242,7 +252,7 @@ bin_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ 
             if (i < cn) {
                 const int pos = loff[bb[u]] + rr[u];
                 st_key[pos] = tile_key(v[u], (uint32_t)(c0 + i - grp_first));
-                st_t[pos] = t[c0 + i];
+                if (narrow) st_t[pos] = (uint32_t)(t[c0 + i] - t_first);
                 st_bin[pos] = (uint16_t)bb[u];
             }
         }
@@ -251,7 +261,7 @@ bin_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ 
             const int b = st_bin[i];
             const int64_t gpos = base[b] + (i - loff[b]);
             so.key[gpos] = st_key[i];
-            so.t[gpos] = st_t[i];
+            if (narrow) so.t32[gpos] = st_t[i];
         }
         __syncthreads();
         for (int b = tid; b < nb; b += kThreads) {
@@ -299,14 +309,17 @@ __device__ __forceinline__ void tile_origin(const CornerGeom &g, int tile, int &
 }
 
 // 3. Build group `grp` for one tile: fold group grp-1 (set `prv`) into B_out = fold(B_in) for
-// the tile's pixels (dense; grp > 0), then accumulate mask/M of the tile's bin in LDS and store
-// them into set `cur`.  Runs as the first n_tiles workgroups of group_kernel(grp - 1).
+// the tile's pixels (dense; grp > 0), then accumulate mask/M of the tile's bin and store them
+// into set `cur`.  The LDS keeps a u32 per (slice, pixel): the max group-relative timestamp + 1
+// (narrow groups, from the sorted t32), else the max event index + 1 — timestamps are
+// non-decreasing, so the last event carries the max t, gathered once per set pair at the end.
 struct BuildLds {
-    int64_t mloc[kGroup][kTilePix];  // 49 KiB
+    uint32_t mlast[kGroup][kTilePix];  // value + 1 (0 = none), 24.5 KiB
     uint32_t mask_l[kTilePix];
 };
 
-__device__ __forceinline__ void build_tile(const CornerGeom &g, int64_t grp, int tile, const Sorted &so,
+__device__ __forceinline__ void build_tile(const int64_t *__restrict__ t, const CornerGeom &g, int64_t grp,
+                                           int tile, const Sorted &so,
                                            const GroupBufs &cur, const GroupBufs &prv,
                                            const int64_t *__restrict__ B_in, int64_t *__restrict__ B_out,
                                            BuildLds &L) {
@@ -331,19 +344,20 @@ __device__ __forceinline__ void build_tile(const CornerGeom &g, int64_t grp, int
     }
     if (pix_lane) {
 #pragma unroll
-        for (int jj = 0; jj < kPlanes; ++jj) L.mloc[part * kPlanes + jj][p] = kEmptyT;
+        for (int jj = 0; jj < kPlanes; ++jj) L.mlast[part * kPlanes + jj][p] = 0u;
     }
     __syncthreads();
     const int nb = g.n_tiles + 1;
     const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
+    int64_t t_first;
+    const bool narrow = group_narrow(t, g, grp, &t_first);  // uniform
     for (int64_t i0 = b0; i0 < b1; i0 += kBuildUnroll * kArcThreads) {
-        uint32_t k[kBuildUnroll];
-        int64_t tv[kBuildUnroll];
+        uint32_t k[kBuildUnroll], tv32[kBuildUnroll];
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u) {
             const int64_t i = i0 + u * kArcThreads + tid;
             k[u] = (i < b1) ? so.key[i] : 0xffffffffu;
-            tv[u] = (i < b1) ? so.t[i] : 0;
+            tv32[u] = (i < b1 && narrow) ? so.t32[i] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u) {
@@ -351,18 +365,25 @@ __device__ __forceinline__ void build_tile(const CornerGeom &g, int64_t grp, int
             const int lp = (int)(k[u] & 255u);
             const int j = slice_in_group(k[u] >> 8, g);
             atomicOr(&L.mask_l[lp], 1u << j);
-            atomicMax(reinterpret_cast<long long *>(&L.mloc[j][lp]), (long long)tv[u]);
+            atomicMax(&L.mlast[j][lp], (narrow ? tv32[u] : (k[u] >> 8)) + 1u);
         }
     }
     __syncthreads();
     if (own) {
         const uint32_t mk_all = L.mask_l[p];
         if (part == 0) cur.mask[q] = mk_all;
-        uint32_t mk = (mk_all >> (part * kPlanes)) & ((1u << kPlanes) - 1u);
-        while (mk) {
-            const int j = part * kPlanes + __ffs(mk) - 1;
-            mk &= mk - 1;
-            cur.M[(int64_t)j * HW + q] = L.mloc[j][p];
+        const int64_t grp_first = grp * kGroup * (int64_t)g.S;
+        int64_t tv[kPlanes];  // all gathers in flight, then the stores
+#pragma unroll
+        for (int jj = 0; jj < kPlanes; ++jj) {
+            const int j = part * kPlanes + jj;
+            const uint32_t m = L.mlast[j][p] - 1u;
+            tv[jj] = !((mk_all >> j) & 1u) ? 0 : narrow ? t_first + (int64_t)m : t[grp_first + m];
+        }
+#pragma unroll
+        for (int jj = 0; jj < kPlanes; ++jj) {
+            const int j = part * kPlanes + jj;
+            if ((mk_all >> j) & 1u) cur.M[(int64_t)j * HW + q] = tv[jj];
         }
     }
 }
@@ -761,7 +782,7 @@ group_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, int n_arc
     if ((int)blockIdx.x < n_arc) {  // long arc items first, short build workgroups fill in after
         if (!(ECC_CORNER_PROFILE && (g.dbg & 8))) arc_item(t, g, grp, (int)blockIdx.x, so, cur, B_in, first_border, flags, L.arc);
     } else {
-        build_tile(g, grp + 1, (int)blockIdx.x - n_arc, so, nxt, cur, B_in, B_out, L.build);
+        build_tile(t, g, grp + 1, (int)blockIdx.x - n_arc, so, nxt, cur, B_in, B_out, L.build);
     }
     if (rec) {
         unsigned int hw;
@@ -839,7 +860,7 @@ Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_bins, int32_t **fi
                     int64_t **scan_scratch) {
     Sorted so{};
     so.key = cv.take<uint32_t>((size_t)g.n);
-    so.t = cv.take<int64_t>((size_t)g.n);
+    so.t32 = cv.take<uint32_t>((size_t)g.n);
     so.bin_count = cv.take<int32_t>((size_t)n_bins);
     so.rel = cv.take<int32_t>((size_t)g.n_slices * (g.n_tiles + 1));
     so.bin_off = cv.take<int64_t>((size_t)n_bins + 1);
@@ -998,8 +1019,8 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     if (rc) return rc;
     {
         ECC_TIMED(ctx, s, "bin_scatter_kernel");
-        const size_t lds_big = (size_t)nb * 16 + 2048 * 14, lds_small = (size_t)nb * 16 + 1024 * 14;
-        if (lds_big <= 48 * 1024)  // 4 workgroups per CU
+        const size_t lds_big = (size_t)nb * 16 + 2048 * 10, lds_small = (size_t)nb * 16 + 1024 * 10;
+        if (lds_big <= 40 * 1024)  // 4 workgroups per CU
             hipLaunchKernelGGL(bin_scatter_kernel<2048>, dim3((unsigned)g.n_slices), dim3(kThreads), lds_big, s, xy,
                                t, g, so);
         else

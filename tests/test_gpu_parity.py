@@ -207,6 +207,24 @@ def _fast_gpu(ecc, gpu, xy, t, W, H, border_mode=0, first_detect=1, sae0=None, s
     return flags.numpy(), sae.numpy()
 
 
+@pytest.mark.parametrize("scale,jump", [
+    (1000, 0),        # ns ticks: a group spans > 2^27 ticks (arc staging takes the int64 clamp path)
+    (1, 1 << 33),     # a 2^33-tick gap inside a group: t32 does not fit (build gathers t by index)
+    (997, 1 << 40),   # both, plus odd spacing
+])
+def test_fast_detect_wide_time_ranges(ecc, orc, gpu, scale, jump):
+    W, H = 346, 260
+    n = 16384 * 40 + 77  # two groups + a ragged tail
+    xy, t, _ = ecc.gen_events(n, seed=41, width=W, height=H)
+    t = t.astype(np.int64) * scale
+    t[n // 3:] += jump
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H)
+    g_flags, g_sae = _fast_gpu(ecc, gpu, xy, t, W, H)
+    assert o_flags.sum() > 0
+    assert (g_flags == o_flags).all(), f"{(g_flags != o_flags).sum()} corner labels differ"
+    assert (g_sae == o_sae).all()
+
+
 @pytest.mark.parametrize("n,wh,mode,seed,slice_events", [
     (600_000, (346, 260), 0, 1, 16384),
     (600_000, (346, 260), 1, 2, 16384),
