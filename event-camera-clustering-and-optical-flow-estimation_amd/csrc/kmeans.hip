@@ -28,7 +28,9 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxK = 64;
 constexpr int kMaxGrid = 2048;
+constexpr int kMaxGridPts = 4096;  // label-image point passes
 constexpr int kFastMaxK = 32;
+constexpr int kImgSide = 2048;  // label image side (see kmeans_label_image_kernel)
 constexpr int kFlushBatches = 2;  // packed u64 slot fields stay exact for < 512 points
 
 struct KmState {
@@ -174,9 +176,43 @@ __device__ __forceinline__ uint32_t assign_fast(float px, float py, const float 
     return ecc::sqrt_rn(m) < thr ? (uint32_t)ia : 255u;
 }
 
+// assign_fast's arithmetic, step for step, with the centres read from LDS inside a rolled loop
+// (the asm barrier keeps the compiler from hoisting them into registers).  Used by the
+// label-image passes for points outside the image only; tests/test_gpu_parity.py covers both
+// the outside points and the near-tie rule.
+template <int K>
+__device__ __forceinline__ uint32_t assign_lds(float px, float py, const float *s_cx, const float *s_cy, float thr) {
+    float m = __builtin_inff(), m_prev = __builtin_inff();
+    int ia = 0;
+#pragma unroll 1
+    for (int i = 0; i < K; ++i) {
+        asm volatile("" ::: "memory");
+        const float dx = __fsub_rn(s_cx[i], px), dy = __fsub_rn(s_cy[i], py);
+        const float d2 = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+        const bool lt = d2 < m;
+        m_prev = lt ? m : m_prev;
+        ia = lt ? i : ia;
+        m = lt ? d2 : m;
+    }
+    if (m_prev <= __fmul_rn(m, 1.0f + 0x1p-20f)) {
+        uint32_t best = 255u;
+        float best_s = thr;
+#pragma unroll 1
+        for (int i = 0; i < K; ++i) {
+            asm volatile("" ::: "memory");
+            const float dx = __fsub_rn(s_cx[i], px), dy = __fsub_rn(s_cy[i], py);
+            const float s = ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
+            if (s < best_s) { best_s = s; best = (uint32_t)i; }
+        }
+        return best;
+    }
+    return ecc::sqrt_rn(m) < thr ? (uint32_t)ia : 255u;
+}
+
 __device__ __forceinline__ float uniform_f32(float v) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
+
 
 // Replicated accumulators: the per-WG flush goes to replica blockIdx % n_copies, which spreads
 // the same-address global atomics; the update kernel sums the replicas.
@@ -191,19 +227,31 @@ constexpr int kAccCopies = 8;
 // atomic per (WG, cluster, field) at the end, spread over n_copies accumulator replicas.
 // (Fusing the update into the last-arriving workgroup was measured slower: the device-scope
 // release every workgroup needs before arriving costs more than the separate 1-wave launch.)
-template <int K, bool kAccumulate>
+template <int K, bool kAccumulate, bool kImg>
 __global__ void __launch_bounds__(kThreads)
 kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__restrict__ cent, int k, float thr,
-                   unsigned long long *acc, int n_copies, const KmState *st, uint8_t *__restrict__ labels) {
+                   unsigned long long *acc, int n_copies, const KmState *st, uint8_t *__restrict__ labels,
+                   const uint8_t *__restrict__ img) {
     if (kAccumulate && st->done) return;
     __shared__ unsigned long long slot[kWaves][K];
     __shared__ unsigned long long w_acc[3][K];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    float cx[K], cy[K];
+    // Label-image passes keep the centroids in LDS (only points outside the image read them), so
+    // the kernel holds no 2K centre registers; otherwise they live in scalar registers.
+    __shared__ float s_cx[kImg ? K : 1], s_cy[kImg ? K : 1];
+    float cx[kImg ? 1 : K], cy[kImg ? 1 : K];
+    if constexpr (kImg) {
+        if (tid < K) {
+            s_cx[tid] = tid < k ? cent[2 * tid] : 1e30f;
+            s_cy[tid] = tid < k ? cent[2 * tid + 1] : 1e30f;
+        }
+        if (!kAccumulate) __syncthreads();
+    } else {
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
-        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+        for (int i = 0; i < K; ++i) {
+            cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
+            cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+        }
     }
     if (kAccumulate) {
         for (int i = tid; i < 3 * K; i += kThreads) (&w_acc[0][0])[i] = 0ull;
@@ -225,40 +273,75 @@ kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__re
     for (int64_t s = blockIdx.x; s < segs.n_segs; s += gridDim.x) {
         const int64_t cnt = segs.count(s);
         const int64_t base = s * segs.stride;
-        for (int64_t j0 = 0; j0 < cnt; j0 += 4 * kThreads) {  // uniform trip count per WG
-            const int64_t j = j0 + 4 * tid;
-            uint32_t v[4];
-            if (vec_ok && j + 3 < cnt) {
-                const uint4 q = *reinterpret_cast<const uint4 *>(xy + base + j);
-                v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-            } else {
+        // Two 4-point batches per lane per trip: both loads and all eight label gathers are in
+        // flight before the first LDS add, halving the dependent load -> gather -> add rounds.
+        for (int64_t j0 = 0; j0 < cnt; j0 += 8 * kThreads) {  // uniform trip count per WG
+            uint32_t v[8], lab[8];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = (j + e < cnt) ? xy[base + j + e] : 0u;
+            for (int u = 0; u < 2; ++u) {
+                const int64_t j = j0 + u * 4 * kThreads + 4 * tid;
+                if (vec_ok && j + 3 < cnt) {
+                    const uint4 q = *reinterpret_cast<const uint4 *>(xy + base + j);
+                    v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[4 * u + e] = (j + e < cnt) ? xy[base + j + e] : 0u;
+                }
             }
-            uint32_t lab[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-                lab[e] = (j + e < cnt) ? assign_fast<K>((float)ecc::xy_x(v[e]), (float)ecc::xy_y(v[e]), cx, cy, thr)
-                                       : 255u;
+            for (int u = 0; u < 2; ++u) {
+                const int64_t j = j0 + u * 4 * kThreads + 4 * tid;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t w = v[4 * u + e];
+                    const uint32_t x = (uint32_t)ecc::xy_x(w), y = (uint32_t)ecc::xy_y(w);
+                    uint32_t l;
+                    if (j + e >= cnt) l = 255u;
+                    else if constexpr (kImg) {
+                        if (__builtin_expect(x < kImgSide && y < kImgSide, 1)) l = img[y * kImgSide + x];
+                        else l = assign_lds<K>((float)x, (float)y, s_cx, s_cy, thr);
+                    } else {
+                        l = assign_fast<K>((float)x, (float)y, cx, cy, thr);
+                    }
+                    lab[4 * u + e] = l;
+                }
+            }
             if (kAccumulate) {
+                // Runs of equal labels are summed in registers first: neighbouring events mostly share
+                // a cluster, and LDS atomics from many lanes to one slot serialise.
+                uint32_t cl = lab[0];
+                unsigned long long run = 0ull;
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (lab[e] < (uint32_t)K)
-                        atomicAdd(&slot[wave][lab[e]], (1ull << 52) | ((unsigned long long)ecc::xy_x(v[e]) << 26) |
-                                                          (unsigned long long)ecc::xy_y(v[e]));
-                if (++batches == kFlushBatches) {
+                for (int e = 0; e < 8; ++e) {
+                    const unsigned long long pk = (1ull << 52) | ((unsigned long long)ecc::xy_x(v[e]) << 26) |
+                                                  (unsigned long long)ecc::xy_y(v[e]);
+                    if (lab[e] != cl) {
+                        if (cl < (uint32_t)K) atomicAdd(&slot[wave][cl], run);
+                        cl = lab[e];
+                        run = 0ull;
+                    }
+                    run += pk;
+                }
+                if (cl < (uint32_t)K) atomicAdd(&slot[wave][cl], run);
+                batches += 2;
+                if (batches >= kFlushBatches) {
                     flush();
                     batches = 0;
                 }
             }
             if (labels) {
-                if (j + 3 < cnt && ((base + j) & 3) == 0) {
-                    const uint32_t pk = lab[0] | (lab[1] << 8) | (lab[2] << 16) | (lab[3] << 24);
-                    *reinterpret_cast<uint32_t *>(labels + base + j) = pk;
-                } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (j + e < cnt) labels[base + j + e] = (uint8_t)lab[e];
+                for (int u = 0; u < 2; ++u) {
+                    const int64_t j = j0 + u * 4 * kThreads + 4 * tid;
+                    if (j + 3 < cnt && ((base + j) & 3) == 0) {
+                        const uint32_t pk = lab[4 * u] | (lab[4 * u + 1] << 8) | (lab[4 * u + 2] << 16) |
+                                            (lab[4 * u + 3] << 24);
+                        *reinterpret_cast<uint32_t *>(labels + base + j) = pk;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (j + e < cnt) labels[base + j + e] = (uint8_t)lab[4 * u + e];
+                    }
                 }
             }
         }
@@ -344,18 +427,109 @@ kmeans_update_kernel(AccT *__restrict__ acc, int n_copies, float *__restrict__ c
     }
 }
 
+// ---- label image (k <= 32) -------------------------------------------------------------------
+// The assignment depends on a point's (x, y) only, and event representatives sit on a sensor
+// grid (the bench: 7.7 M points on 346x260 pixels, ~85 per pixel).  Each pass therefore first
+// labels every pixel of the points' bounding box once (assign_fast, the same function), and the
+// accumulation pass reads a point's label from that image instead of testing k centres.  Points
+// outside the kImgSide x kImgSide area are assigned directly.
+
+__global__ void __launch_bounds__(kThreads)
+kmeans_extent_kernel(const uint32_t *__restrict__ xy, Segs segs, uint32_t *__restrict__ ext) {
+    uint32_t mx = 0, my = 0;
+    bool any = false;
+    for (int64_t s = blockIdx.x; s < segs.n_segs; s += gridDim.x) {
+        const int64_t cnt = segs.count(s), base = s * segs.stride;
+        for (int64_t j = threadIdx.x; j < cnt; j += kThreads) {
+            const uint32_t v = xy[base + j], x = v & 0xffffu, y = v >> 16;
+            if (x < kImgSide && y < kImgSide) {
+                mx = max(mx, x);
+                my = max(my, y);
+                any = true;
+            }
+        }
+    }
+    // per-WG maxima into ext[2 * blockIdx] (no atomics: same-address device atomics serialise)
+    __shared__ uint32_t wmx[kThreads / 64], wmy[kThreads / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        my = max(my, (uint32_t)__shfl_xor((int)my, o));
+    }
+    const bool wany = __any(any);
+    if ((threadIdx.x & 63) == 0) {
+        wmx[threadIdx.x >> 6] = wany ? mx + 1 : 0u;
+        wmy[threadIdx.x >> 6] = wany ? my + 1 : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, b = 0;
+        for (int w = 0; w < kThreads / 64; ++w) { a = max(a, wmx[w]); b = max(b, wmy[w]); }
+        ext[2 * blockIdx.x] = a;
+        ext[2 * blockIdx.x + 1] = b;
+    }
+}
+
+template <int K>
+__global__ void __launch_bounds__(kThreads)
+kmeans_label_image_kernel(const float *__restrict__ cent, int k, float thr, const uint32_t *__restrict__ ext,
+                          int n_ext, uint8_t *__restrict__ img, const KmState *st) {
+    if (st && st->done) return;
+    __shared__ uint32_t s_wh[2][kThreads];
+    {  // bounding box = max over the extent kernel's per-WG maxima
+        uint32_t a = 0, b = 0;
+        for (int i = threadIdx.x; i < n_ext; i += kThreads) { a = max(a, ext[2 * i]); b = max(b, ext[2 * i + 1]); }
+        s_wh[0][threadIdx.x] = a;
+        s_wh[1][threadIdx.x] = b;
+        __syncthreads();
+        for (int o = kThreads / 2; o > 0; o >>= 1) {
+            if (threadIdx.x < o) {
+                s_wh[0][threadIdx.x] = max(s_wh[0][threadIdx.x], s_wh[0][threadIdx.x + o]);
+                s_wh[1][threadIdx.x] = max(s_wh[1][threadIdx.x], s_wh[1][threadIdx.x + o]);
+            }
+            __syncthreads();
+        }
+    }
+    float cx[K], cy[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
+        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+    }
+    const uint32_t w = s_wh[0][0], h = s_wh[1][0];
+    const int64_t cells = (int64_t)w * h;
+    for (int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x; c < cells; c += (int64_t)gridDim.x * kThreads) {
+        const uint32_t x = (uint32_t)(c % w), y = (uint32_t)(c / w);
+        img[(int64_t)y * kImgSide + x] = (uint8_t)assign_fast<K>((float)x, (float)y, cx, cy, thr);
+    }
+}
+
+template <int K>
+void launch_label_image(dim3 grid, hipStream_t s, const float *cent, int k, float thr, const uint32_t *ext,
+                        int n_ext, uint8_t *img, const KmState *st) {
+    hipLaunchKernelGGL(kmeans_label_image_kernel<K>, grid, dim3(kThreads), 0, s, cent, k, thr, ext, n_ext, img, st);
+}
+
 // Launch helpers for the fast path (k <= kFastMaxK); false when k needs the generic kernel.
 template <bool kAccumulate>
 bool launch_fast(int k, dim3 grid, hipStream_t s, const uint32_t *xy, const Segs &segs, const float *cent,
-                 float thr, unsigned long long *acc, int n_copies, const KmState *st, uint8_t *labels) {
-    if (k <= 16)
-        hipLaunchKernelGGL((kmeans_fast_kernel<16, kAccumulate>), grid, dim3(kThreads), 0, s, xy, segs, cent, k,
-                           thr, acc, n_copies, st, labels);
-    else if (k <= kFastMaxK)
-        hipLaunchKernelGGL((kmeans_fast_kernel<32, kAccumulate>), grid, dim3(kThreads), 0, s, xy, segs, cent, k,
-                           thr, acc, n_copies, st, labels);
-    else
-        return false;
+                 float thr, unsigned long long *acc, int n_copies, const KmState *st, uint8_t *labels,
+                 const uint8_t *img = nullptr) {
+    if (k > kFastMaxK) return false;
+    if (img) {
+        if (k <= 16)
+            hipLaunchKernelGGL((kmeans_fast_kernel<16, kAccumulate, true>), grid, dim3(kThreads), 0, s, xy, segs,
+                               cent, k, thr, acc, n_copies, st, labels, img);
+        else
+            hipLaunchKernelGGL((kmeans_fast_kernel<32, kAccumulate, true>), grid, dim3(kThreads), 0, s, xy, segs,
+                               cent, k, thr, acc, n_copies, st, labels, img);
+    } else if (k <= 16) {
+        hipLaunchKernelGGL((kmeans_fast_kernel<16, kAccumulate, false>), grid, dim3(kThreads), 0, s, xy, segs,
+                           cent, k, thr, acc, n_copies, st, labels, img);
+    } else {
+        hipLaunchKernelGGL((kmeans_fast_kernel<32, kAccumulate, false>), grid, dim3(kThreads), 0, s, xy, segs,
+                           cent, k, thr, acc, n_copies, st, labels, img);
+    }
     return true;
 }
 
@@ -401,19 +575,36 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
     if (segs.n_segs * segs.stride / grid >= (1ll << 24)) return ECC_ERR_INVALID;
     // workspace: kAccCopies accumulator replicas (copy 0 alone on the generic path), then the state
     constexpr size_t kAccBytes = (size_t)kAccCopies * kAccStride * 8;
-    rc = ecc::ws_reserve(ctx, kAccBytes + 64);
+    const size_t off_ext = ecc::align_up(kAccBytes + 64, 256);
+    const size_t off_img = ecc::align_up(off_ext + (size_t)grid * 8, 256);
+    rc = ecc::ws_reserve(ctx, off_img + (size_t)kImgSide * kImgSide);
     if (rc) return rc;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t s = ecc::as_stream(stream);
-    auto *acc = reinterpret_cast<unsigned long long *>(ctx->ws);
-    auto *st = reinterpret_cast<KmState *>(reinterpret_cast<char *>(ctx->ws) + kAccBytes);
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, kAccBytes + 64, s), "memset(kmeans acc)");
+    char *ws = static_cast<char *>(ctx->ws);
+    auto *acc = reinterpret_cast<unsigned long long *>(ws);
+    auto *st = reinterpret_cast<KmState *>(ws + kAccBytes);
+    auto *ext = reinterpret_cast<uint32_t *>(ws + off_ext);
+    auto *img = reinterpret_cast<uint8_t *>(ws + off_img);
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ws, 0, kAccBytes + 64, s), "memset(kmeans acc)");
     const bool fast = cfg->k <= kFastMaxK;
+    // label-image passes: one WG per segment (<= 32 waves/CU resident at 8 waves/SIMD)
+    const int grid_pts = fast ? (int)std::min<int64_t>(std::max<int64_t>(segs.n_segs, 1), kMaxGridPts) : grid;
+    auto label_image = [&](const KmState *stp) {
+        ECC_TIMED(ctx, s, "kmeans_label_image_kernel");
+        if (cfg->k <= 16) launch_label_image<16>(dim3(512), s, centroids, cfg->k, cfg->threshold, ext, grid, img, stp);
+        else launch_label_image<32>(dim3(512), s, centroids, cfg->k, cfg->threshold, ext, grid, img, stp);
+    };
+    if (fast && segs.n_segs > 0) {
+        ECC_TIMED(ctx, s, "kmeans_extent_kernel");
+        hipLaunchKernelGGL(kmeans_extent_kernel, dim3(grid), dim3(kThreads), 0, s, xy, segs, ext);
+    }
     for (int it = 0; it < cfg->max_iters && segs.n_segs > 0; ++it) {
+        if (fast) label_image(st);
         {
             ECC_TIMED(ctx, s, "kmeans_xy16_kernel");
-            if (!launch_fast<true>(cfg->k, dim3(grid), s, xy, segs, centroids, cfg->threshold, acc,
-                                   fast ? kAccCopies : 1, st, nullptr))
+            if (!launch_fast<true>(cfg->k, dim3(grid_pts), s, xy, segs, centroids, cfg->threshold, acc,
+                                   fast ? kAccCopies : 1, st, nullptr, img))
                 hipLaunchKernelGGL(kmeans_xy16_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
                                    centroids, cfg->k, cfg->threshold, acc, st, (uint8_t *)nullptr);
         }
@@ -425,10 +616,11 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
     }
     ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 iteration");
     if (labels && segs.n_segs > 0) {
+        if (fast) label_image(nullptr);  // final centroids
         {
             ECC_TIMED(ctx, s, "kmeans_xy16_labels");
-            if (!launch_fast<false>(cfg->k, dim3(grid), s, xy, segs, centroids, cfg->threshold, acc, 1, st,
-                                    labels))
+            if (!launch_fast<false>(cfg->k, dim3(grid_pts), s, xy, segs, centroids, cfg->threshold, acc, 1, st,
+                                    labels, img))
                 hipLaunchKernelGGL(kmeans_xy16_kernel<false>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
                                    centroids, cfg->k, cfg->threshold, acc, st, labels);
         }

@@ -167,6 +167,25 @@ def test_kmeans_xy16_ties_take_exact_path(ecc, orc, gpu, k):
     assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
 
 
+@pytest.mark.parametrize("k", [16, 32])
+def test_kmeans_xy16_points_outside_pixel_grid(ecc, orc, gpu, k):
+    """Coordinates up to 6000 x 3000: the pixel-histogram path sends the points beyond its
+    2048 x 2048 grid through the overflow list; results must not change."""
+    rng = np.random.default_rng(77 + k)
+    n = 300_007
+    x = np.concatenate([rng.integers(0, 6000, n // 2), rng.normal(700, 80, n - n // 2).clip(0, 65535)]).astype(np.int64)
+    y = np.concatenate([rng.integers(0, 3000, n // 2), rng.normal(400, 60, n - n // 2).clip(0, 65535)]).astype(np.int64)
+    xy = ecc.pack_xy(x, y)
+    c0 = np.stack([rng.uniform(0, 6000, k), rng.uniform(0, 3000, k)], 1).astype(np.float32).ravel()
+    o_c, o_lab, o_it = orc.kmeans_run_xy16(xy, c0, 5, 3000.0, -1.0)
+    d_c = dev(ecc, c0)
+    d_lab = ecc.DeviceArray(n, np.uint8)
+    gpu.kmeans_xy16(dev(ecc, xy), 1, n, None, d_c, ecc.kmeans_cfg(k=k, max_iters=5, tol=-1.0, threshold=3000.0), d_lab)
+    gpu.sync()
+    assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
+    assert (d_lab.numpy() == o_lab).all()
+
+
 def test_kmeans_f32_matches_oracle(ecc, orc, gpu):
     rng = np.random.default_rng(5)
     pts = np.concatenate([rng.normal(m, 6.0, (20000, 2)) for m in ([40, 40], [120, 60], [200, 180], [300, 90])])
