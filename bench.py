@@ -193,7 +193,7 @@ def main():
         # group_kernel: key + t of group g+1 (build) and key of group g (arc); n_groups + 1 launches
         "group_kernel": 16.0 * n / per_step_launches,
         "nms_kernel": 1.0 * n,                                            # corner flags
-        "kmeans_update_kernel": 0.0,
+        "kmeans_step_kernel": 0.0,
     }.get(dominant, 0.0)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     # HBM bytes per launch of the same kernel from the newest committed PMC summary

@@ -30,7 +30,7 @@ constexpr int kMaxK = 64;
 constexpr int kMaxGrid = 2048;
 constexpr int kMaxGridPts = 4096;  // label-image point passes
 constexpr int kFastMaxK = 32;
-constexpr int kImgSide = 2048;  // label image side (see kmeans_label_image_kernel)
+constexpr int kImgSide = 2048;  // label image side (see kmeans_step_kernel)
 constexpr int kFlushBatches = 2;  // packed u64 slot fields stay exact for < 512 points
 
 struct KmState {
@@ -470,44 +470,124 @@ kmeans_extent_kernel(const uint32_t *__restrict__ xy, Segs segs, uint32_t *__res
     }
 }
 
+// One kmeans_step_kernel per Lloyd pass replaces "update, then label image": every workgroup
+// re-derives the centroid update from the previous pass's accumulator replicas (a few hundred
+// L2 reads), so no second launch and no grid-wide hand-off is needed.  Buffers alternate by pass:
+// pass it accumulates into acc[it & 1] and labels with C_it, stored in cb[it & 1].  step(it)
+// reads acc[(it-1) & 1] and cb[(it-1) & 1], so WG 0 alone may write cb[it & 1], the caller's
+// centroids and the state, and zero acc[it & 1] (last read by step(it-1)).  The update
+// arithmetic is kmeans_update_kernel's, in the same order.
+struct StepArgs {
+    const unsigned long long *acc_in;  // pass it-1's replicas (nullptr: no update in this step)
+    unsigned long long *acc_zero;      // pass it's replicas, zeroed by WG 0
+    const float *c_prev;               // C_{it-1} (or C_0 when acc_in is null)
+    float *c_next;                     // cb[it & 1]
+    float *cent;                       // the caller's centroids (final result)
+    int n_copies, k;
+    float thr, tol;
+    bool final_pass;                   // after the last pass: update, then label image if wanted
+    bool want_image;
+};
+
 template <int K>
 __global__ void __launch_bounds__(kThreads)
-kmeans_label_image_kernel(const float *__restrict__ cent, int k, float thr, const uint32_t *__restrict__ ext,
-                          int n_ext, uint8_t *__restrict__ img, const KmState *st) {
-    if (st && st->done) return;
+kmeans_step_kernel(StepArgs a, const uint32_t *__restrict__ ext, int n_ext, uint8_t *__restrict__ img,
+                   KmState *st) {
+    const bool done_in = st->done != 0;
+    if (done_in && !a.final_pass) return;
+    const int tid = threadIdx.x;
     __shared__ uint32_t s_wh[2][kThreads];
+    __shared__ unsigned long long s_sum[3][K];
+    __shared__ float s_c[2][K];
+    __shared__ int s_done;
+    const bool update = a.acc_in && !done_in;
+    const float *c_src = done_in ? a.cent : a.c_prev;  // converged earlier: the caller's array is final
+    if (update) {
+        if (tid < 3 * a.k) {
+            const int c = tid / 3, f = tid - 3 * c;
+            unsigned long long v = 0;
+            for (int r = 0; r < a.n_copies; ++r) v += a.acc_in[r * kAccStride + 3 * c + f];
+            s_sum[f][c] = v;
+        }
+        if (blockIdx.x == 0)
+            for (int i = tid; i < a.n_copies * kAccStride; i += kThreads) a.acc_zero[i] = 0ull;
+        __syncthreads();
+        if (tid < 64) {
+            float shift = 0.f;
+            if (tid < a.k) {
+                const float ox = c_src[2 * tid], oy = c_src[2 * tid + 1];
+                float nx = ox, ny = oy;
+                const double n_pts = (double)s_sum[0][tid];
+                if (n_pts > 0.0) {
+                    nx = (float)((double)s_sum[1][tid] / n_pts);
+                    ny = (float)((double)s_sum[2][tid] / n_pts);
+                    shift = fmaxf(fabsf(nx - ox), fabsf(ny - oy));
+                }
+                s_c[0][tid] = nx;
+                s_c[1][tid] = ny;
+                if (blockIdx.x == 0) {
+                    a.c_next[2 * tid] = nx;
+                    a.c_next[2 * tid + 1] = ny;
+                    a.cent[2 * tid] = nx;
+                    a.cent[2 * tid + 1] = ny;
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) shift = fmaxf(shift, __shfl_xor(shift, o));
+            if (tid == 0) {
+                const int done = (a.tol >= 0.f && shift <= a.tol) ? 1 : 0;
+                s_done = done;
+                if (blockIdx.x == 0) {
+                    st->iters += 1;
+                    st->done = done;
+                }
+            }
+        }
+    } else {
+        if (tid < a.k) {
+            s_c[0][tid] = c_src[2 * tid];
+            s_c[1][tid] = c_src[2 * tid + 1];
+            if (blockIdx.x == 0 && !done_in) {
+                a.c_next[2 * tid] = s_c[0][tid];
+                a.c_next[2 * tid + 1] = s_c[1][tid];
+            }
+        }
+        if (tid == 0) s_done = done_in ? 1 : 0;
+    }
     {  // bounding box = max over the extent kernel's per-WG maxima
-        uint32_t a = 0, b = 0;
-        for (int i = threadIdx.x; i < n_ext; i += kThreads) { a = max(a, ext[2 * i]); b = max(b, ext[2 * i + 1]); }
-        s_wh[0][threadIdx.x] = a;
-        s_wh[1][threadIdx.x] = b;
+        uint32_t p = 0, q = 0;
+        for (int i = tid; i < n_ext; i += kThreads) { p = max(p, ext[2 * i]); q = max(q, ext[2 * i + 1]); }
+        s_wh[0][tid] = p;
+        s_wh[1][tid] = q;
         __syncthreads();
         for (int o = kThreads / 2; o > 0; o >>= 1) {
-            if (threadIdx.x < o) {
-                s_wh[0][threadIdx.x] = max(s_wh[0][threadIdx.x], s_wh[0][threadIdx.x + o]);
-                s_wh[1][threadIdx.x] = max(s_wh[1][threadIdx.x], s_wh[1][threadIdx.x + o]);
+            if (tid < o) {
+                s_wh[0][tid] = max(s_wh[0][tid], s_wh[0][tid + o]);
+                s_wh[1][tid] = max(s_wh[1][tid], s_wh[1][tid + o]);
             }
             __syncthreads();
         }
     }
+    // a pass that converged runs no further accumulation: its image is only needed for labels
+    if (a.final_pass ? !a.want_image : s_done != 0) return;
     float cx[K], cy[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
-        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+        cx[i] = uniform_f32(i < a.k ? s_c[0][i] : 1e30f);
+        cy[i] = uniform_f32(i < a.k ? s_c[1][i] : 1e30f);
     }
     const uint32_t w = s_wh[0][0], h = s_wh[1][0];
     const int64_t cells = (int64_t)w * h;
-    for (int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x; c < cells; c += (int64_t)gridDim.x * kThreads) {
+    for (int64_t c = (int64_t)blockIdx.x * kThreads + tid; c < cells; c += (int64_t)gridDim.x * kThreads) {
         const uint32_t x = (uint32_t)(c % w), y = (uint32_t)(c / w);
-        img[(int64_t)y * kImgSide + x] = (uint8_t)assign_fast<K>((float)x, (float)y, cx, cy, thr);
+        img[(int64_t)y * kImgSide + x] = (uint8_t)assign_fast<K>((float)x, (float)y, cx, cy, a.thr);
     }
 }
 
 template <int K>
-void launch_label_image(dim3 grid, hipStream_t s, const float *cent, int k, float thr, const uint32_t *ext,
-                        int n_ext, uint8_t *img, const KmState *st) {
-    hipLaunchKernelGGL(kmeans_label_image_kernel<K>, grid, dim3(kThreads), 0, s, cent, k, thr, ext, n_ext, img, st);
+void launch_step(dim3 grid, hipStream_t s, const StepArgs &a, const uint32_t *ext, int n_ext, uint8_t *img,
+                 KmState *st) {
+    hipLaunchKernelGGL(kmeans_step_kernel<K>, grid, dim3(kThreads), 0, s, a, ext, n_ext, img, st);
 }
 
 // Launch helpers for the fast path (k <= kFastMaxK); false when k needs the generic kernel.
@@ -573,58 +653,88 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
     // per-WG packed counts must stay < 2^24 points (sum_x < 2^40)
     const int grid = grid_for(segs.n_segs);
     if (segs.n_segs * segs.stride / grid >= (1ll << 24)) return ECC_ERR_INVALID;
-    // workspace: kAccCopies accumulator replicas (copy 0 alone on the generic path), then the state
+    // workspace: two sets of kAccCopies accumulator replicas (pass parity; the generic path uses
+    // copy 0 of set 0), the state, the centroid history cb[2], the per-WG extents, the label image
     constexpr size_t kAccBytes = (size_t)kAccCopies * kAccStride * 8;
-    const size_t off_ext = ecc::align_up(kAccBytes + 64, 256);
+    const size_t off_st = 2 * kAccBytes;
+    const size_t off_cb = off_st + 64;
+    const size_t off_ext = ecc::align_up(off_cb + 2 * 2 * kMaxK * sizeof(float), 256);
     const size_t off_img = ecc::align_up(off_ext + (size_t)grid * 8, 256);
     rc = ecc::ws_reserve(ctx, off_img + (size_t)kImgSide * kImgSide);
     if (rc) return rc;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t s = ecc::as_stream(stream);
     char *ws = static_cast<char *>(ctx->ws);
-    auto *acc = reinterpret_cast<unsigned long long *>(ws);
-    auto *st = reinterpret_cast<KmState *>(ws + kAccBytes);
+    unsigned long long *accb[2] = {reinterpret_cast<unsigned long long *>(ws),
+                                   reinterpret_cast<unsigned long long *>(ws + kAccBytes)};
+    auto *st = reinterpret_cast<KmState *>(ws + off_st);
+    float *cb[2] = {reinterpret_cast<float *>(ws + off_cb), reinterpret_cast<float *>(ws + off_cb) + 2 * kMaxK};
     auto *ext = reinterpret_cast<uint32_t *>(ws + off_ext);
     auto *img = reinterpret_cast<uint8_t *>(ws + off_img);
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(ws, 0, kAccBytes + 64, s), "memset(kmeans acc)");
-    const bool fast = cfg->k <= kFastMaxK;
-    // label-image passes: one WG per segment (<= 32 waves/CU resident at 8 waves/SIMD)
-    const int grid_pts = fast ? (int)std::min<int64_t>(std::max<int64_t>(segs.n_segs, 1), kMaxGridPts) : grid;
-    auto label_image = [&](const KmState *stp) {
-        ECC_TIMED(ctx, s, "kmeans_label_image_kernel");
-        if (cfg->k <= 16) launch_label_image<16>(dim3(512), s, centroids, cfg->k, cfg->threshold, ext, grid, img, stp);
-        else launch_label_image<32>(dim3(512), s, centroids, cfg->k, cfg->threshold, ext, grid, img, stp);
-    };
-    if (fast && segs.n_segs > 0) {
-        ECC_TIMED(ctx, s, "kmeans_extent_kernel");
-        hipLaunchKernelGGL(kmeans_extent_kernel, dim3(grid), dim3(kThreads), 0, s, xy, segs, ext);
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ws, 0, off_st + 64, s), "memset(kmeans acc)");
+    if (segs.n_segs == 0) {
+        if (iters_out)
+            ECC_CHECK_HIP(ctx, hipMemcpyAsync(iters_out, &st->iters, 4, hipMemcpyDeviceToDevice, s), "copy iters");
+        return ECC_OK;
     }
-    for (int it = 0; it < cfg->max_iters && segs.n_segs > 0; ++it) {
-        if (fast) label_image(st);
-        {
-            ECC_TIMED(ctx, s, "kmeans_xy16_kernel");
-            if (!launch_fast<true>(cfg->k, dim3(grid_pts), s, xy, segs, centroids, cfg->threshold, acc,
-                                   fast ? kAccCopies : 1, st, nullptr, img))
-                hipLaunchKernelGGL(kmeans_xy16_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
-                                   centroids, cfg->k, cfg->threshold, acc, st, (uint8_t *)nullptr);
+    if (cfg->k > kFastMaxK) {  // generic kernel: assign per point, separate update launch
+        for (int it = 0; it < cfg->max_iters; ++it) {
+            {
+                ECC_TIMED(ctx, s, "kmeans_xy16_kernel");
+                hipLaunchKernelGGL(kmeans_xy16_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, segs, centroids,
+                                   cfg->k, cfg->threshold, accb[0], st, (uint8_t *)nullptr);
+            }
+            {
+                ECC_TIMED(ctx, s, "kmeans_update_kernel");
+                hipLaunchKernelGGL(kmeans_update_kernel<unsigned long long>, dim3(1), dim3(64), 0, s, accb[0], 1,
+                                   centroids, cfg->k, cfg->tol, st);
+            }
         }
-        {
-            ECC_TIMED(ctx, s, "kmeans_update_kernel");
-            hipLaunchKernelGGL(kmeans_update_kernel<unsigned long long>, dim3(1), dim3(64), 0, s, acc,
-                               fast ? kAccCopies : 1, centroids, cfg->k, cfg->tol, st);
-        }
-    }
-    ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 iteration");
-    if (labels && segs.n_segs > 0) {
-        if (fast) label_image(nullptr);  // final centroids
-        {
+        ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 iteration");
+        if (labels) {
             ECC_TIMED(ctx, s, "kmeans_xy16_labels");
-            if (!launch_fast<false>(cfg->k, dim3(grid_pts), s, xy, segs, centroids, cfg->threshold, acc, 1, st,
-                                    labels, img))
-                hipLaunchKernelGGL(kmeans_xy16_kernel<false>, dim3(grid), dim3(kThreads), 0, s, xy, segs,
-                                   centroids, cfg->k, cfg->threshold, acc, st, labels);
+            hipLaunchKernelGGL(kmeans_xy16_kernel<false>, dim3(grid), dim3(kThreads), 0, s, xy, segs, centroids,
+                               cfg->k, cfg->threshold, accb[0], st, labels);
+            ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 labels");
         }
-        ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 labels");
+    } else {
+        // label-image passes: one WG per segment (<= 32 waves/CU resident at 8 waves/SIMD)
+        const int grid_pts = (int)std::min<int64_t>(segs.n_segs, kMaxGridPts);
+        {
+            ECC_TIMED(ctx, s, "kmeans_extent_kernel");
+            hipLaunchKernelGGL(kmeans_extent_kernel, dim3(grid), dim3(kThreads), 0, s, xy, segs, ext);
+        }
+        auto step = [&](int it, bool final_pass) {
+            StepArgs a{};
+            a.acc_in = it ? accb[(it - 1) & 1] : nullptr;
+            a.acc_zero = accb[it & 1];
+            a.c_prev = it ? cb[(it - 1) & 1] : centroids;
+            a.c_next = cb[it & 1];
+            a.cent = centroids;
+            a.n_copies = kAccCopies;
+            a.k = cfg->k;
+            a.thr = cfg->threshold;
+            a.tol = cfg->tol;
+            a.final_pass = final_pass;
+            a.want_image = labels != nullptr;
+            ECC_TIMED(ctx, s, "kmeans_step_kernel");
+            if (cfg->k <= 16) launch_step<16>(dim3(512), s, a, ext, grid, img, st);
+            else launch_step<32>(dim3(512), s, a, ext, grid, img, st);
+        };
+        for (int it = 0; it < cfg->max_iters; ++it) {
+            step(it, false);
+            ECC_TIMED(ctx, s, "kmeans_xy16_kernel");
+            launch_fast<true>(cfg->k, dim3(grid_pts), s, xy, segs, cb[it & 1], cfg->threshold, accb[it & 1],
+                              kAccCopies, st, nullptr, img);
+        }
+        if (cfg->max_iters > 0 || labels) step(cfg->max_iters, true);  // last update (+ image for labels)
+        ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 iteration");
+        if (labels) {
+            ECC_TIMED(ctx, s, "kmeans_xy16_labels");
+            launch_fast<false>(cfg->k, dim3(grid_pts), s, xy, segs, centroids, cfg->threshold, nullptr, 1, st,
+                               labels, img);
+            ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 labels");
+        }
     }
     if (iters_out)
         ECC_CHECK_HIP(ctx, hipMemcpyAsync(iters_out, &st->iters, 4, hipMemcpyDeviceToDevice, s),

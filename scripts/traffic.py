@@ -19,7 +19,7 @@ def short(name: str) -> str:
     base = m.group(1) if m else name.split("(")[0]
     # map to the names libecc's timing report (and bench.py) use
     if base in ("kmeans_xy16_kernel", "kmeans_fast_kernel"):
-        return "kmeans_xy16_labels" if re.search(r"<(\d+, )?false>", name) else "kmeans_xy16_kernel"
+        return "kmeans_xy16_labels" if re.search(r"<(\d+, )?false[,>]", name) else "kmeans_xy16_kernel"
     if base == "nms_grid_kernel":
         return "nms_kernel"
     return base
