@@ -1,5 +1,6 @@
-// Shared helpers of the host programs: event input (CSV "x,y,t,p" path as argv[1], the way the
-// reference mains take Camera::from_file(argv[1]); or --synthetic N for a seeded stream).
+// Shared helpers of the host programs: event input as argv[1], the way the reference mains take
+// Camera::from_file(argv[1]) — a Prophesee RAW recording (EVT 2.0 / 3.0, GPU-decoded), a CSV
+// "x,y,t,p" file, or --synthetic N for a seeded stream.
 #pragma once
 #include <cstdio>
 #include <cstdlib>
@@ -31,8 +32,19 @@ inline Events load_events(int argc, char **argv, int width, int height) {
         return ev;
     }
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s <events.csv> | --synthetic N\n", argv[0]);
+        std::fprintf(stderr, "usage: %s <events.raw|events.csv> | --synthetic N\n", argv[0]);
         std::exit(1);
+    }
+    const size_t len = std::strlen(argv[1]);
+    if (len > 4 && !std::strcmp(argv[1] + len - 4, ".raw")) {
+        try {
+            ecc::RawFileReader rd(ecc::Context::default_context(), argv[1]);
+            rd.read_all(ev.xy, ev.t, ev.p);
+        } catch (const ecc::Error &e) {
+            std::fprintf(stderr, "%s: %s\n", argv[1], e.what());
+            std::exit(1);
+        }
+        return ev;
     }
     const int64_t n = ecc_count_csv(argv[1]);
     if (n < 0) {

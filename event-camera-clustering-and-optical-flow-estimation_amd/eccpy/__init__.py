@@ -54,6 +54,11 @@ class CornerCfg(C.Structure):
                 ("first_detect_slice", C.c_int32)]
 
 
+class RawInfo(C.Structure):
+    _fields_ = [("format", C.c_int32), ("width", C.c_int32), ("height", C.c_int32),
+                ("word_bytes", C.c_int32), ("header_bytes", C.c_int64), ("n_words", C.c_int64)]
+
+
 class Corner(C.Structure):
     _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("label", C.c_int32)]
 
@@ -148,6 +153,11 @@ _sigs = {
     "ecc_fast_detect_status": (C.c_int, [P, P]),
     "ecc_read_csv": (i64, [C.c_char_p, P, P, P, i64]),
     "ecc_count_csv": (i64, [C.c_char_p]),
+    "ecc_raw_probe": (C.c_int, [C.c_char_p, C.POINTER(RawInfo)]),
+    "ecc_raw_read_words": (i64, [C.c_char_p, C.POINTER(RawInfo), i64, i64, P]),
+    "ecc_evt_decode": (C.c_int, [P, i32, P, i64, P, P, P, i64, P, P, P]),
+    "ecc_evt_status": (C.c_int, [P, P]),
+    "ecc_reslice_n_us": (C.c_int, [P, P, i64, i64, P, i64, P, P]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)  # every bound symbol must exist (fail loudly on a stale build)
@@ -327,6 +337,22 @@ class Context:
               "ecc_eps_lists")
 
 
+    # ---- 8. RAW ingest
+    def evt_decode(self, fmt: int, words: DeviceArray, n_words: int, xy: DeviceArray | None,
+                   t: DeviceArray | None, p: DeviceArray | None, cap: int, n_out: DeviceArray,
+                   state: DeviceArray | None = None):
+        check(lib.ecc_evt_decode(self.ctx, fmt, words.ptr, n_words, _ptr(xy), _ptr(t), _ptr(p), cap,
+                                 n_out.ptr, _ptr(state), self.stream), "ecc_evt_decode")
+
+    def evt_status(self) -> int:
+        return lib.ecc_evt_status(self.ctx, self.stream)
+
+    def reslice_n_us(self, t: DeviceArray, n: int, period_us: int, bounds: DeviceArray,
+                     max_slices: int, n_slices: DeviceArray):
+        check(lib.ecc_reslice_n_us(self.ctx, t.ptr, n, period_us, bounds.ptr, max_slices,
+                                   n_slices.ptr, self.stream), "ecc_reslice_n_us")
+
+
 class Tracker:
     """Device-resident CornerTracker (FCT/…group_track.cpp:201-537)."""
 
@@ -466,6 +492,25 @@ def read_csv(path: str):
     p = np.empty(n, np.uint8)
     got = lib.ecc_read_csv(str(path).encode(), xy.ctypes.data, t.ctypes.data, p.ctypes.data, n)
     return xy[:got], t[:got], p[:got]
+
+
+EVT2, EVT3 = 2, 3
+EVT_STATE_BYTES = 64
+
+
+def raw_probe(path) -> RawInfo:
+    info = RawInfo()
+    check(lib.ecc_raw_probe(str(path).encode(), C.byref(info)), f"raw_probe({path})")
+    return info
+
+
+def raw_read_words(path, info: RawInfo, first: int = 0, n: int | None = None) -> np.ndarray:
+    n = info.n_words - first if n is None else n
+    out = np.empty(max(n, 0), np.uint32 if info.format == EVT2 else np.uint16)
+    got = lib.ecc_raw_read_words(str(path).encode(), C.byref(info), first, n, out.ctypes.data)
+    if got < 0:
+        raise EccError(int(got), f"raw_read_words({path})")
+    return out[:got]
 
 
 def pack_xy(x, y) -> np.ndarray:

@@ -174,6 +174,85 @@ std::vector<TrackedCorner> CornerTracker::updateTrackedCorners(const std::vector
     return tracks();
 }
 
+// ------------------------------------------------------------------------------ ingest
+RawFileReader::RawFileReader(Context &ctx, const std::string &path, int64_t chunk_words)
+    : ctx_(ctx), path_(path), chunk_(chunk_words > 0 ? chunk_words : int64_t(1) << 24) {
+    check(ecc_raw_probe(path.c_str(), &info_), "ecc_raw_probe");
+    const int64_t max_events = chunk_ * (info_.format == ECC_RAW_EVT3 ? 12 : 1);  // <= 12 per VECT_12 word
+    host_.resize((size_t)(chunk_ * info_.word_bytes));
+    words_.reserve(host_.size());
+    xy_.reserve((size_t)max_events * 4);
+    t_.reserve((size_t)max_events * 8);
+    p_.reserve((size_t)max_events);
+    n_.reserve(8);
+    state_.reserve(ECC_EVT_STATE_BYTES);
+    check(ecc_memset_async(state_.data(), 0, ECC_EVT_STATE_BYTES, ctx_.stream()), "memset(state)");
+}
+
+int64_t RawFileReader::next(const uint32_t **d_xy, const int64_t **d_t, const uint8_t **d_p) {
+    const int64_t got = ecc_raw_read_words(path_.c_str(), &info_, pos_, chunk_, host_.data());
+    if (got < 0) throw Error((int)got, "ecc_raw_read_words");
+    if (got == 0) return 0;
+    pos_ += got;
+    words_.upload(host_.data(), (size_t)(got * info_.word_bytes), ctx_.stream());
+    const int64_t cap = (int64_t)p_.size();
+    check(ecc_evt_decode(ctx_.get(), info_.format, words_.data(), got, xy_.as<uint32_t>(), t_.as<int64_t>(),
+                         p_.as<uint8_t>(), cap, n_.as<int64_t>(), state_.data(), ctx_.stream()),
+          "ecc_evt_decode");
+    int64_t n = 0;
+    n_.download(&n, 8, ctx_.stream());
+    ctx_.sync();
+    if (d_xy) *d_xy = xy_.as<uint32_t>();
+    if (d_t) *d_t = t_.as<int64_t>();
+    if (d_p) *d_p = p_.as<uint8_t>();
+    return n;
+}
+
+void RawFileReader::read_all(std::vector<uint32_t> &xy, std::vector<int64_t> &t, std::vector<uint8_t> &p) {
+    xy.clear(); t.clear(); p.clear();
+    pos_ = 0;
+    check(ecc_memset_async(state_.data(), 0, ECC_EVT_STATE_BYTES, ctx_.stream()), "memset(state)");
+    const uint32_t *dx;
+    const int64_t *dt;
+    const uint8_t *dp;
+    for (int64_t n; (n = next(&dx, &dt, &dp)) > 0;) {
+        const size_t o = xy.size();
+        xy.resize(o + n); t.resize(o + n); p.resize(o + n);
+        check(ecc_memcpy_d2h(xy.data() + o, dx, (size_t)n * 4, ctx_.stream()), "d2h xy");
+        check(ecc_memcpy_d2h(t.data() + o, dt, (size_t)n * 8, ctx_.stream()), "d2h t");
+        check(ecc_memcpy_d2h(p.data() + o, dp, (size_t)n, ctx_.stream()), "d2h p");
+        ctx_.sync();
+    }
+}
+
+std::vector<int64_t> reslice_n_events(int64_t n, int64_t n_events) {
+    std::vector<int64_t> b;
+    if (n_events <= 0) throw Error(ECC_ERR_INVALID, "reslice_n_events");
+    for (int64_t k = 0; k < n; k += n_events) b.push_back(k);
+    b.push_back(n);
+    return b;
+}
+
+std::vector<int64_t> reslice_n_us(Context &ctx, const int64_t *d_t, int64_t n, int64_t period_us) {
+    if (n <= 0) return {0};
+    int64_t first = 0, last = 0;
+    check(ecc_memcpy_d2h(&first, d_t, 8, ctx.stream()), "d2h t[0]");
+    check(ecc_memcpy_d2h(&last, d_t + n - 1, 8, ctx.stream()), "d2h t[n-1]");
+    ctx.sync();
+    if (period_us <= 0 || last < first) throw Error(ECC_ERR_INVALID, "reslice_n_us");
+    const int64_t base = (first >= 0 ? first / period_us : -((-first + period_us - 1) / period_us)) * period_us;
+    const int64_t ns = (last - base) / period_us + 1;
+    DeviceBuffer bounds((size_t)(ns + 1) * 8), d_ns(8);
+    check(ecc_reslice_n_us(ctx.get(), d_t, n, period_us, bounds.as<int64_t>(), ns, d_ns.as<int64_t>(),
+                           ctx.stream()),
+          "ecc_reslice_n_us");
+    check(ecc_evt_status(ctx.get(), ctx.stream()), "ecc_reslice_n_us");
+    std::vector<int64_t> b((size_t)ns + 1);
+    bounds.download(b.data(), b.size() * 8, ctx.stream());
+    ctx.sync();
+    return b;
+}
+
 TimeSurfaceCornerDetector::TimeSurfaceCornerDetector(Context &ctx, int width, int height,
                                                      int slice_events, int border_mode)
     : ctx_(ctx) {

@@ -1,10 +1,11 @@
-// Host-side event sources: deterministic synthetic streams and CSV event files.
+// Host-side event sources: deterministic synthetic streams, CSV event files and the RAW
+// (EVT 2.0 / EVT 3.0) file header + payload reader.
 //
 // The reference ingests events through Metavision's Camera::from_file(argv[1]) / live camera
 // callbacks (FCT/…group_track.cpp:756-765, 1073-1074) and its OPTICS driver reads "x,y,t,p" CSV
-// files (OPT/test/cluster_event_data.cpp:21-55, fixture OPT/test/event_raw_data8.csv).  Metavision
-// .raw decoding is out of this round's scope; the CSV reader and a
-// seeded generator feed every host program, test and benchmark instead.
+// files (OPT/test/cluster_event_data.cpp:21-55, fixture OPT/test/event_raw_data8.csv).  RAW
+// payload words are decoded on the GPU (csrc/evt.hip, ecc_evt_decode); this file only parses
+// the '%' header and streams the little-endian words from disk.
 //
 // Generator: counter-based splitmix64 streams, so any slice [first, first+n) of
 // an event stream can be produced independently and in parallel; 70 % edge events of moving
@@ -189,4 +190,77 @@ ECC_HOST_API int64_t ecc_count_csv(const char *path) {
 ECC_HOST_API int64_t ecc_read_csv(const char *path, uint32_t *xy, int64_t *t, uint8_t *p, int64_t cap) {
     const int64_t n = csv_scan(path, xy, t, p, cap);
     return n < 0 ? n : std::min(n, cap);
+}
+
+// ---- RAW files (include/ecc.h §8) ----------------------------------------------------------
+// Header: lines starting with '%' up to "% end" (or the first line not starting with '%').
+// Recognised keys: "% evt 2.0|3.0", "% format EVT2|EVT3[;height=H;width=W]", "% geometry WxH".
+static int parse_format_name(const char *v) {
+    if (!std::strncmp(v, "EVT3", 4) || !std::strncmp(v, "evt3", 4) || !std::strncmp(v, "3.0", 3)) return ECC_RAW_EVT3;
+    if (!std::strncmp(v, "EVT2", 4) || !std::strncmp(v, "evt2", 4) || !std::strncmp(v, "2.0", 3)) return ECC_RAW_EVT2;
+    return ECC_RAW_UNKNOWN;
+}
+
+ECC_HOST_API int ecc_raw_probe(const char *path, ecc_raw_info *info) {
+    if (!path || !info) return ECC_ERR_INVALID;
+    std::memset(info, 0, sizeof(*info));
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return ECC_ERR_INVALID;
+    int64_t pos = 0;
+    char line[1024];
+    for (;;) {
+        const int c = std::fgetc(f);
+        if (c != '%') break;  // payload starts here
+        std::ungetc(c, f);
+        if (!std::fgets(line, sizeof(line), f)) break;
+        const size_t len = std::strlen(line);
+        pos += (int64_t)len;
+        if (len == sizeof(line) - 1 && line[len - 1] != '\n') {  // over-long header line: skip the rest
+            int d;
+            while ((d = std::fgetc(f)) != EOF && d != '\n') ++pos;
+            if (d == '\n') ++pos;
+        }
+        char *v = line + 1;
+        while (*v == ' ') ++v;
+        if (!std::strncmp(v, "end", 3) && (v[3] == '\n' || v[3] == '\r' || v[3] == 0)) break;
+        if (!std::strncmp(v, "evt ", 4)) {
+            info->format = parse_format_name(v + 4);
+        } else if (!std::strncmp(v, "format ", 7)) {
+            const int fmt = parse_format_name(v + 7);
+            if (fmt) info->format = fmt;
+            const char *h = std::strstr(v, "height="), *w = std::strstr(v, "width=");
+            if (h) info->height = std::atoi(h + 7);
+            if (w) info->width = std::atoi(w + 6);
+        } else if (!std::strncmp(v, "geometry ", 9)) {
+            int w = 0, h = 0;
+            if (std::sscanf(v + 9, "%dx%d", &w, &h) == 2) {
+                info->width = w;
+                info->height = h;
+            }
+        }
+    }
+    std::fseek(f, 0, SEEK_END);
+    const int64_t size = (int64_t)std::ftell(f);
+    std::fclose(f);
+    if (info->format == ECC_RAW_UNKNOWN) return ECC_ERR_INVALID;
+    info->word_bytes = info->format == ECC_RAW_EVT2 ? 4 : 2;
+    info->header_bytes = pos;
+    info->n_words = size > pos ? (size - pos) / info->word_bytes : 0;
+    return ECC_OK;
+}
+
+ECC_HOST_API int64_t ecc_raw_read_words(const char *path, const ecc_raw_info *info, int64_t first_word, int64_t n,
+                                        void *buf) {
+    if (!path || !info || !buf || first_word < 0 || n < 0 || info->word_bytes <= 0) return ECC_ERR_INVALID;
+    if (first_word >= info->n_words) return 0;
+    n = std::min(n, info->n_words - first_word);
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return ECC_ERR_INVALID;
+    if (std::fseek(f, (long)(info->header_bytes + first_word * info->word_bytes), SEEK_SET) != 0) {
+        std::fclose(f);
+        return ECC_ERR_INVALID;
+    }
+    const size_t got = std::fread(buf, (size_t)info->word_bytes, (size_t)n, f);
+    std::fclose(f);
+    return (int64_t)got;  // little-endian host (x86-64): words are used as read
 }

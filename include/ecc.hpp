@@ -191,6 +191,33 @@ class TimeSurfaceCornerDetector {
     bool first_ = true;
 };
 
+// ------------------------------------------------------------------------------ ingest
+// RAW recording reader (the role of Metavision::Camera::from_file(argv[1]), FCT/…group_track.cpp
+// :756-760): the host streams payload words from disk, the GPU decodes them (ecc_evt_decode)
+// with the carry state between chunks, so a recording of any length decodes piecewise.
+class RawFileReader {
+  public:
+    RawFileReader(Context &ctx, const std::string &path, int64_t chunk_words = int64_t(1) << 24);
+    const ecc_raw_info &info() const { return info_; }
+    // Decodes the next chunk; device arrays stay valid until the next call.  0 at end of file.
+    int64_t next(const uint32_t **d_xy, const int64_t **d_t, const uint8_t **d_p);
+    // Whole recording into host vectors.
+    void read_all(std::vector<uint32_t> &xy, std::vector<int64_t> &t, std::vector<uint8_t> &p);
+
+  private:
+    Context &ctx_;
+    std::string path_;
+    ecc_raw_info info_{};
+    int64_t chunk_, pos_ = 0;
+    std::vector<uint8_t> host_;
+    DeviceBuffer words_, xy_, t_, p_, n_, state_;
+};
+
+// n-events / n-µs slicing (EventBufferReslicerAlgorithm::Condition::make_n_events /
+// make_n_us): slice k = events [bounds[k], bounds[k+1]).  t on the device.
+std::vector<int64_t> reslice_n_events(int64_t n, int64_t n_events);
+std::vector<int64_t> reslice_n_us(Context &ctx, const int64_t *d_t, int64_t n, int64_t period_us);
+
 // ------------------------------------------------------------------------------ downsample / k-means
 struct DownsampleResult {
     std::vector<int32_t> unique_count, repeated_count;  // per window

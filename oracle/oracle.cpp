@@ -813,3 +813,179 @@ ORC_API int orc_kmeans_partial_xy16(const uint32_t *xy, int64_t n, const float *
     }
     return 0;
 }
+
+// ------------------------------------------------------------------------------------------
+// §8f rank 1: RAW event ingest.  The reference decodes through Metavision::Camera::from_file
+// (FCT/…group_track.cpp:756-760), which is not vendored; these are sequential restatements of
+// the published EVT 2.0 / EVT 3.0 word formats (include/ecc.h §8) — parity "unpinned" against
+// OpenEB itself — plus stream ENCODERS that build test recordings (vector words, trigger /
+// OTHERS / CONTINUED words, redundant TIME_HIGH words, 24-bit time loops).
+// ------------------------------------------------------------------------------------------
+namespace {
+struct Rng {
+    uint64_t s;
+    uint64_t next() {
+        uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    int pct(int p) { return (int)(next() % 100) < p; }
+};
+}  // namespace
+
+ORC_API int64_t orc_evt2_decode(const uint32_t *w, int64_t n, uint32_t *xy, int64_t *t, uint8_t *p, int64_t cap) {
+    uint32_t th = 0;
+    int64_t k = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t ty = w[i] >> 28;
+        if (ty == 0x0 || ty == 0x1) {  // CD_OFF / CD_ON
+            if (k < cap) {
+                xy[k] = (w[i] >> 11 & 0x7FFu) | ((w[i] & 0x7FFu) << 16);
+                t[k] = ((int64_t)th << 6) | (int64_t)(w[i] >> 22 & 0x3Fu);
+                p[k] = (uint8_t)ty;
+            }
+            ++k;
+        } else if (ty == 0x8) {  // EVT_TIME_HIGH
+            th = w[i] & 0x0FFFFFFFu;
+        }
+    }
+    return k;
+}
+
+ORC_API int64_t orc_evt3_decode(const uint16_t *w, int64_t n, uint32_t *xy, int64_t *t, uint8_t *p, int64_t cap) {
+    uint32_t y = 0, tl = 0, th = 0, base = 0, pol = 0;
+    int64_t loops = 0, k = 0;
+    bool has_th = false;
+    auto emit = [&](uint32_t x, uint32_t pp) {
+        if (k < cap) {
+            xy[k] = (x & 0xFFFFu) | (y << 16);
+            t[k] = (loops << 24) | (int64_t)(th << 12 | tl);
+            p[k] = (uint8_t)pp;
+        }
+        ++k;
+    };
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t v = w[i];
+        switch (v >> 12) {
+            case 0x0: y = v & 0x7FFu; break;                         // EVT_ADDR_Y
+            case 0x2: emit(v & 0x7FFu, v >> 11 & 1u); break;         // EVT_ADDR_X
+            case 0x3: base = v & 0x7FFu; pol = v >> 11 & 1u; break;  // VECT_BASE_X
+            case 0x4:                                                // VECT_12
+                for (int b = 0; b < 12; ++b)
+                    if (v >> b & 1u) emit(base + b, pol);
+                base += 12;
+                break;
+            case 0x5:  // VECT_8
+                for (int b = 0; b < 8; ++b)
+                    if (v >> b & 1u) emit(base + b, pol);
+                base += 8;
+                break;
+            case 0x6: tl = v & 0xFFFu; break;  // EVT_TIME_LOW
+            case 0x8: {                        // EVT_TIME_HIGH
+                const uint32_t nt = v & 0xFFFu;
+                if (has_th && nt < th) ++loops;
+                th = nt;
+                has_th = true;
+                break;
+            }
+            default: break;  // 0x7 CONTINUED_4, 0xA EXT_TRIGGER, 0xE OTHERS, 0xF CONTINUED_12
+        }
+    }
+    return k;
+}
+
+// Noise words that carry no CD event (EXT_TRIGGER / OTHERS / CONTINUED).
+static uint32_t evt2_noise(Rng &r) {
+    static const uint32_t ty[3] = {0xA, 0xE, 0xF};
+    return (ty[r.next() % 3] << 28) | (uint32_t)(r.next() & 0x0FFFFFFFu);
+}
+static uint16_t evt3_noise(Rng &r) {
+    static const uint32_t ty[4] = {0x7, 0xA, 0xE, 0xF};
+    return (uint16_t)((ty[r.next() % 4] << 12) | (uint32_t)(r.next() & 0xFFFu));
+}
+
+// EVT 2.0 encoder: TIME_HIGH whenever t >> 6 changes (plus redundant repeats), noise_pct %
+// extra noise words.  Events need x, y < 2048, non-decreasing t < 2^34.  Returns words.
+ORC_API int64_t orc_evt2_encode(const uint32_t *xy, const int64_t *t, const uint8_t *p, int64_t n, uint64_t seed,
+                                int noise_pct, uint32_t *out, int64_t cap) {
+    Rng r{seed};
+    int64_t k = 0;
+    auto put = [&](uint32_t v) { if (k < cap) out[k] = v; ++k; };
+    int64_t last_th = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t th = t[i] >> 6;
+        if (th != last_th || r.pct(noise_pct / 4)) put(0x80000000u | (uint32_t)(th & 0x0FFFFFFF));
+        last_th = th;
+        while (r.pct(noise_pct)) put(evt2_noise(r));
+        const uint32_t x = xy[i] & 0x7FFu, y = (xy[i] >> 16) & 0x7FFu;
+        put(((uint32_t)(p[i] & 1) << 28) | ((uint32_t)(t[i] & 63) << 22) | (x << 11) | y);
+    }
+    return k;
+}
+
+// EVT 3.0 encoder, order-preserving: runs of events with equal (t, y, p) and strictly
+// increasing x go out as VECT_BASE_X + VECT_12 / VECT_8 words (chosen at random, zero masks
+// allowed) when vect_pct allows; single events as EVT_ADDR_X.  TIME_HIGH on every change of
+// t >> 12, with (0xFFF, 0) pairs for every 2^24 loop crossed; TIME_LOW on every change of t.
+ORC_API int64_t orc_evt3_encode(const uint32_t *xy, const int64_t *t, const uint8_t *p, int64_t n, uint64_t seed,
+                                int noise_pct, int vect_pct, uint16_t *out, int64_t cap) {
+    Rng r{seed};
+    int64_t k = 0;
+    auto put = [&](uint32_t v) { if (k < cap) out[k] = (uint16_t)v; ++k; };
+    int64_t last_hi = -1, last_t = -1;  // t >> 12
+    int64_t last_y = -1;
+    int64_t i = 0;
+    while (i < n) {
+        const int64_t ti = t[i];
+        const int64_t hi = ti >> 12;
+        if (hi != last_hi || r.pct(noise_pct / 4)) {
+            if (last_hi >= 0)
+                for (int64_t L = (last_hi >> 12); L < (hi >> 12); ++L) { put(0x8000u | 0xFFFu); put(0x8000u); }
+            put(0x8000u | (uint32_t)(hi & 0xFFF));
+            last_hi = hi;
+            last_t = -1;
+        }
+        if (ti != last_t || r.pct(noise_pct / 4)) { put(0x6000u | (uint32_t)(ti & 0xFFF)); last_t = ti; }
+        const uint32_t y = (xy[i] >> 16) & 0x7FFu, x0 = xy[i] & 0x7FFu, pi = p[i] & 1u;
+        if ((int64_t)y != last_y || r.pct(noise_pct / 4)) { put(0x0000u | y); last_y = y; }
+        while (r.pct(noise_pct)) put(evt3_noise(r));
+        // run of equal (t, y, p) with strictly increasing x, within 64 px of x0
+        int64_t j = i + 1;
+        while (j < n && t[j] == ti && ((xy[j] >> 16) & 0x7FFu) == y && (p[j] & 1u) == pi &&
+               (xy[j] & 0x7FFu) > (xy[j - 1] & 0x7FFu) && (xy[j] & 0x7FFu) < x0 + 64)
+            ++j;
+        if (j - i >= 2 && r.pct(vect_pct)) {
+            put(0x3000u | (pi << 11) | x0);
+            uint32_t base = x0;
+            int64_t q = i;
+            while (q < j) {
+                const int nb = r.pct(50) ? 12 : 8;
+                uint32_t m = 0;
+                while (q < j && (xy[q] & 0x7FFu) < base + nb) { m |= 1u << ((xy[q] & 0x7FFu) - base); ++q; }
+                put((nb == 12 ? 0x4000u : 0x5000u) | m);
+                base += nb;
+            }
+            i = j;
+        } else {
+            put(0x2000u | (pi << 11) | x0);
+            ++i;
+        }
+    }
+    return k;
+}
+
+// n-µs reslicer (ecc_reslice_n_us semantics): bounds[k] = first event with t >= t_base + k*T.
+ORC_API int64_t orc_reslice_n_us(const int64_t *t, int64_t n, int64_t period, int64_t *bounds, int64_t max_slices) {
+    if (n == 0) { bounds[0] = 0; return 0; }
+    const int64_t t0 = t[0];
+    const int64_t base = (t0 >= 0 ? t0 / period : -((-t0 + period - 1) / period)) * period;
+    const int64_t ns = (t[n - 1] - base) / period + 1;
+    int64_t i = 0;
+    for (int64_t k = 0; k < ns && k < max_slices; ++k) {
+        while (i < n && t[i] < base + k * period) ++i;
+        bounds[k] = i;
+    }
+    bounds[ns < max_slices ? ns : max_slices] = n;
+    return ns;
+}

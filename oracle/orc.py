@@ -48,6 +48,11 @@ _sigs = {
     "orc_get_cluster_indices": (C.c_int, [P, i32, f64, P]),
     "orc_radius_search": (C.c_int, [P, i32, i32, P, f64, P, i32]),
     "orc_kmeans_partial_xy16": (C.c_int, [P, i64, P, i32, f32, P]),
+    "orc_evt2_decode": (i64, [P, i64, P, P, P, i64]),
+    "orc_evt3_decode": (i64, [P, i64, P, P, P, i64]),
+    "orc_evt2_encode": (i64, [P, P, P, i64, C.c_uint64, i32, P, i64]),
+    "orc_evt3_encode": (i64, [P, P, P, i64, C.c_uint64, i32, i32, P, i64]),
+    "orc_reslice_n_us": (i64, [P, i64, i64, P, i64]),
 }
 for _n, (_r, _a) in _sigs.items():
     f = getattr(lib, _n)
@@ -229,3 +234,43 @@ def kmeans_partial_xy16(xy, centroids, thr=50.0):
     acc = np.zeros(3 * (c.size // 2), np.int64)
     lib.orc_kmeans_partial_xy16(_p(xy), len(xy), _p(c), c.size // 2, thr, _p(acc))
     return acc
+
+
+# ---- RAW ingest (EVT 2.0 / 3.0) --------------------------------------------------------------
+def evt_encode(fmt, xy, t, p, seed=1, noise_pct=5, vect_pct=70):
+    """Encodes events into an EVT 2.0 (u32) or EVT 3.0 (u16) word stream."""
+    xy = np.ascontiguousarray(xy, np.uint32)
+    t = np.ascontiguousarray(t, np.int64)
+    p = np.ascontiguousarray(p, np.uint8)
+    n = len(xy)
+    if fmt == 2:
+        cap = 4 * n + 16
+        out = np.empty(cap, np.uint32)
+        k = lib.orc_evt2_encode(_p(xy), _p(t), _p(p), n, seed, noise_pct, _p(out), cap)
+    else:
+        cap = 8 * n + 64 + 2 * int((t[-1] >> 24) + 1 if n else 0)
+        out = np.empty(cap, np.uint16)
+        k = lib.orc_evt3_encode(_p(xy), _p(t), _p(p), n, seed, noise_pct, vect_pct, _p(out), cap)
+    assert k <= cap
+    return out[:k].copy()
+
+
+def evt_decode(fmt, words):
+    words = np.ascontiguousarray(words, np.uint32 if fmt == 2 else np.uint16)
+    n = len(words)
+    cap = n * (1 if fmt == 2 else 12)
+    xy = np.empty(cap, np.uint32)
+    t = np.empty(cap, np.int64)
+    p = np.empty(cap, np.uint8)
+    fn = lib.orc_evt2_decode if fmt == 2 else lib.orc_evt3_decode
+    k = fn(_p(words), n, _p(xy), _p(t), _p(p), cap)
+    return xy[:k].copy(), t[:k].copy(), p[:k].copy()
+
+
+def reslice_n_us(t, period, max_slices=None):
+    t = np.ascontiguousarray(t, np.int64)
+    if max_slices is None:
+        max_slices = 1 if len(t) == 0 else int((t[-1] - (t[0] // period) * period) // period + 1)
+    bounds = np.zeros(max_slices + 1, np.int64)
+    ns = lib.orc_reslice_n_us(_p(t), len(t), period, _p(bounds), max_slices)
+    return bounds, int(ns)

@@ -122,3 +122,18 @@ def test_dbscan_program_matches_oracle(orc, ecc, tmp_path):
     for i in range(len(x)):
         if olab[i] >= 0:
             assert got[(int(x[i]), int(y[i]))] == olab[i] % 8
+
+
+@pytest.mark.parametrize("fmt", [3, 2])
+def test_corner_track_program_reads_raw_recording(orc, ecc, tmp_path, fmt):
+    """argv[1] = a RAW recording (Camera::from_file, FCT/…group_track.cpp:756-760): the program's
+    output equals its output on the same events given as --synthetic."""
+    n, W, H = 16384 * 12, 346, 260
+    xy, t, p = ecc.gen_events(n, width=W, height=H)
+    words = orc.evt_encode(fmt, xy, t, p, seed=2)
+    path = tmp_path / "rec.raw"
+    hdr = f"% evt {fmt}.0\n% geometry {W}x{H}\n% end\n"
+    path.write_bytes(hdr.encode() + words.tobytes())
+    a = run("ecc_corner_track", path, "--width", W, "--height", H)
+    b = run("ecc_corner_track", "--synthetic", n, "--width", W, "--height", H)
+    assert a == b and "Corner size" in a
