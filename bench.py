@@ -51,6 +51,7 @@ def parse():
                     help="CPU-baseline sample size (~16 s of single-thread oracle work)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the RAW (EVT 3.0 / 2.0) decode measurement")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for rehearsal")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on device 0 (with --dist-backend gloo)")
@@ -79,7 +80,7 @@ def main():
         raise SystemExit("--events must be a multiple of the 16384-event slice (global slice alignment)")
     # one stream for libecc and the collectives (torch's current stream) when sharded
     ctx = ecc.Context(local, stream=torch.cuda.current_stream().cuda_stream) if dist else ecc.Context(local)
-    xy_h, t_h, _ = ecc.gen_events(n, first=rank * n, seed=1, width=W, height=H)
+    xy_h, t_h, p_h = ecc.gen_events(n, first=rank * n, seed=1, width=W, height=H)
     d_xy, d_t = ecc.DeviceArray.from_numpy(xy_h, ctx.stream), ecc.DeviceArray.from_numpy(t_h, ctx.stream)
     hcfg = ecc.hash_cfg(window=8192)  # reference bounds 0<=x<=1280, 0<=y<=720
     n_win = (n + 8191) // 8192
@@ -217,6 +218,46 @@ def main():
         tracker_us = tmr.stop() * 1e3 / ns
         tr.close()
 
+    # RAW ingest, reported beside the headline: the same events written
+    # as EVT 3.0 / EVT 2.0 words, decoded from device-resident words.
+    ingest = None
+    if not args.no_ingest and rank == 0:
+        ingest = {}
+        for fmt, name in ((ecc.EVT3, "EVT3"), (ecc.EVT2, "EVT2")):
+            words = ecc.evt_encode(fmt, xy_h, t_h, p_h)
+            d_words = ecc.DeviceArray.from_numpy(words, ctx.stream)
+            d_oxy, d_ot = ecc.DeviceArray(n, np.uint32), ecc.DeviceArray(n, np.int64)
+            d_op, d_on = ecc.DeviceArray(n, np.uint8), ecc.DeviceArray(1, np.int64)
+            run = lambda: ctx.evt_decode(fmt, d_words, len(words), d_oxy, d_ot, d_op, n, d_on)
+            run()
+            ctx.sync()
+            reps = max(args.steps, 5)
+            tmr = ecc.Timer(ctx.stream)
+            tmr.start()
+            for _ in range(reps):
+                run()
+            dec_ms = tmr.stop() / reps
+            assert int(d_on.numpy()[0]) == n and ctx.evt_status() == 0
+            ctx.set_timing(True)
+            ctx.timing_reset()
+            for _ in range(reps):
+                run()
+            st = ctx.timing_report()
+            ctx.set_timing(False)
+            kern = {k: v["total_ms"] / v["launches"] for k, v in st.items()}
+            wbytes = words.nbytes
+            dk = kern.get("evt_decode_kernel", float("nan"))
+            ach = (wbytes + 13.0 * n) / (dk * 1e-3) / 1e9  # words in + xy/t/p out
+            ingest[name] = {
+                "words": len(words), "word_bytes": words.itemsize, "events": n,
+                "mevents_s": round(n / (dec_ms * 1e-3) / 1e6, 1), "ms_per_decode": round(dec_ms, 4),
+                "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
+                "roofline": {"kernel": "evt_decode_kernel", "bound": "hbm", "achieved": round(ach, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                             "algorithmic_bytes": f"{words.itemsize} B/word in + 13 B/event out"},
+            }
+            del d_words, d_oxy, d_ot, d_op, d_on
+
     value = world * args.steps * n / elapsed / 1e6
     result = {
         "metric": "Mevents/s (downsample+cluster+corner)",
@@ -247,6 +288,7 @@ def main():
         },
         "stages_ms_per_step": {k: round(v / args.steps, 4) for k, v in sorted(kern_ms.items())},
         "tracker_us_per_slice": None if tracker_us is None else round(tracker_us, 2),
+        "ingest": ingest,
     }
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, W, H, K, I)

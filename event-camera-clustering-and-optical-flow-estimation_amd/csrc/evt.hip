@@ -11,12 +11,14 @@
 // TIME_HIGH; EVT 3.0: the last y, TIME_LOW, TIME_HIGH + loop count, vector base x and
 // polarity), and every state variable is a "last value set before this word" or a running
 // sum — an associative summary.  So decoding is a three-phase scan, all HBM-streaming:
-//   1. evt_summary_kernel: one workgroup per 4096-word chunk folds its words into the chunk's
-//      summary (16 consecutive words per lane, 16-B loads; LDS scan over the lanes);
-//   2. evt_carry_kernel: one workgroup scans the chunk summaries into per-chunk carry-in
-//      states and int64 event offsets (and advances the caller's streaming state);
+//   1. evt_summary_kernel: one workgroup per chunk folds its words into the chunk's
+//      summary (64 B of consecutive words per lane, 16-B loads; wave-shuffle scan over the lanes);
+//   2. evt_group_kernel + evt_carry_kernel: a two-level scan of the chunk summaries into
+//      per-chunk carry-in states and int64 event offsets (advancing the caller's streaming
+//      state);
 //   3. evt_decode_kernel: each chunk re-reads its words, rebuilds the per-lane carry-in with
-//      the same LDS scan, and walks its 16 words emitting events at their final positions.
+//      the same wave-shuffle scan, walks its words per lane into an LDS window of decoded
+//      events and writes the window out coalesced.
 // Algorithmic bytes: words read twice (2 x 2 B or 2 x 4 B per word) + 13 B per event out
 // (xy u32, t i64, p u8).
 #include "ecc_internal.hpp"
@@ -24,8 +26,8 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kPer = 16;                   // words per lane
-constexpr int kChunk = kThreads * kPer;    // words per workgroup
+// Each lane owns 64 B of words: 16 EVT 2.0 or 32 EVT 3.0 words (F::kPer); a workgroup owns a
+// chunk of kThreads * F::kPer words.
 constexpr int kFlagWord = 3;               // ctx->flags[3]: bit 1 capacity, bit 2 unsorted t
 
 // ---- EVT 3.0 -------------------------------------------------------------------------------
@@ -47,6 +49,8 @@ struct S3 {
 struct Evt3 {
     using Word = uint16_t;
     using S = S3;
+    static constexpr int kPer = 32;
+    static constexpr int kOut = 4096;  // decode window (events); the EVT 3.0 walk is costly to repeat
     __device__ static S identity() { return S{-1, -1, -1, -1, 0, -1, 0, 0}; }
     __device__ static S cat(const S &a, const S &b) {  // a, then b
         S r;
@@ -60,23 +64,22 @@ struct Evt3 {
         r.n = a.n + b.n;
         return r;
     }
-    __device__ static void fold(S &s, uint32_t w) {  // s = cat(s, word(w)), specialised
-        switch (w >> 12) {
-            case 0x0: s.y = (int32_t)(w & 0x7FFu); break;
-            case 0x2: s.n += 1; break;
-            case 0x3: s.base = (int32_t)((w & 0x7FFu) | ((w >> 11 & 1u) << 16)); s.inc = 0; break;
-            case 0x4: s.n += __popc(w & 0xFFFu); s.inc += 12; break;
-            case 0x5: s.n += __popc(w & 0xFFu); s.inc += 8; break;
-            case 0x6: s.tl = (int32_t)(w & 0xFFFu); break;
-            case 0x8: {
-                const int32_t th = (int32_t)(w & 0xFFFu);
-                if (s.th_last >= 0 && th < s.th_last) s.loops += 1;
-                if (s.th_first < 0) s.th_first = th;
-                s.th_last = th;
-                break;
-            }
-            default: break;
-        }
+    // s = cat(s, word(w)), branch-free: lanes hold words of different types, so a switch would
+    // run every case body per word.
+    __device__ static void fold(S &s, uint32_t w) {
+        const uint32_t ty = w >> 12;
+        const int32_t v11 = (int32_t)(w & 0x7FFu), v12 = (int32_t)(w & 0xFFFu);
+        s.y = ty == 0x0 ? v11 : s.y;
+        s.tl = ty == 0x6 ? v12 : s.tl;
+        const bool th_w = ty == 0x8;
+        s.loops += (th_w && s.th_last >= 0 && v12 < s.th_last) ? 1 : 0;
+        s.th_first = (th_w && s.th_first < 0) ? v12 : s.th_first;
+        s.th_last = th_w ? v12 : s.th_last;
+        const bool base_w = ty == 0x3;
+        s.base = base_w ? (v11 | (int32_t)((w >> 11 & 1u) << 16)) : s.base;
+        s.inc = base_w ? 0 : s.inc + (ty == 0x4 ? 12 : ty == 0x5 ? 8 : 0);
+        const uint32_t vm = ty == 0x4 ? (w & 0xFFFu) : ty == 0x5 ? (w & 0xFFu) : 0u;
+        s.n += (ty == 0x2 ? 1 : 0) + __popc(vm);
     }
     // Decoder registers rebuilt from a prefix summary (the state before the first word).
     struct Regs {
@@ -97,33 +100,24 @@ struct Evt3 {
     }
     template <class Emit>
     __device__ static void step(Regs &r, uint32_t w, Emit &emit) {
+        const uint32_t ty = w >> 12, v11 = w & 0x7FFu, v12 = w & 0xFFFu;
         const int64_t t = ((int64_t)r.loops << 24) | (int64_t)(r.th << 12 | r.tl);
-        switch (w >> 12) {
-            case 0x0: r.y = w & 0x7FFu; break;
-            case 0x2: emit((w & 0x7FFu) | (r.y << 16), t, (uint8_t)(w >> 11 & 1u)); break;
-            case 0x3: r.base = w & 0x7FFu; r.pol = w >> 11 & 1u; break;
-            case 0x4:
-            case 0x5: {
-                const int nb = (w >> 12) == 0x4 ? 12 : 8;
-                uint32_t m = w & ((1u << nb) - 1u);
-                while (m) {
-                    const uint32_t b = __builtin_ctz(m);
-                    m &= m - 1u;
-                    emit(((r.base + b) & 0xFFFFu) | (r.y << 16), t, (uint8_t)r.pol);
-                }
-                r.base += (uint32_t)nb;
-                break;
-            }
-            case 0x6: r.tl = w & 0xFFFu; break;
-            case 0x8: {
-                const uint32_t th = w & 0xFFFu;
-                if (r.has_th && th < r.th) r.loops += 1;
-                r.th = th;
-                r.has_th = true;
-                break;
-            }
-            default: break;
+        uint32_t vm = ty == 0x4 ? v12 : ty == 0x5 ? (w & 0xFFu) : 0u;
+        if (ty == 0x2) emit(v11 | (r.y << 16), t, (uint8_t)(w >> 11 & 1u));
+        while (vm) {
+            const uint32_t b = __builtin_ctz(vm);
+            vm &= vm - 1u;
+            emit(((r.base + b) & 0xFFFFu) | (r.y << 16), t, (uint8_t)r.pol);
         }
+        r.y = ty == 0x0 ? v11 : r.y;
+        r.tl = ty == 0x6 ? v12 : r.tl;
+        const bool th_w = ty == 0x8;
+        r.loops += (th_w && r.has_th && v12 < r.th) ? 1 : 0;
+        r.th = th_w ? v12 : r.th;
+        r.has_th = r.has_th || th_w;
+        const bool base_w = ty == 0x3;
+        r.pol = base_w ? (w >> 11 & 1u) : r.pol;
+        r.base = base_w ? v11 : r.base + (ty == 0x4 ? 12u : ty == 0x5 ? 8u : 0u);
     }
 };
 
@@ -141,6 +135,8 @@ struct S2 {
 struct Evt2 {
     using Word = uint32_t;
     using S = S2;
+    static constexpr int kPer = 16;
+    static constexpr int kOut = 1024;  // decode window (events): small LDS -> occupancy
     __device__ static S identity() { return S{-1, 0, {0, 0, 0, 0, 0, 0}}; }
     __device__ static S cat(const S &a, const S &b) {
         S r = identity();
@@ -174,7 +170,8 @@ static_assert(ECC_EVT_STATE_BYTES >= 32, "state holds one summary");
 // The chunk's words: lane l owns words [l*kPer, (l+1)*kPer), loaded with 16-B loads.
 template <class F>
 __device__ inline void load_words(const typename F::Word *__restrict__ words, int64_t n_words, int64_t c,
-                                  uint32_t (&w)[kPer], int &nw) {
+                                  uint32_t (&w)[F::kPer], int &nw) {
+    constexpr int kPer = F::kPer, kChunk = kThreads * kPer;
     using Word = typename F::Word;
     const int64_t first = c * kChunk + (int64_t)threadIdx.x * kPer;
     const int64_t left = n_words - first;
@@ -195,32 +192,54 @@ __device__ inline void load_words(const typename F::Word *__restrict__ words, in
     }
 }
 
-// Exclusive scan of per-lane summaries over the workgroup (Hillis-Steele in LDS); returns
-// the lane's exclusive prefix, and the inclusive total through *total.
-template <class F>
-__device__ typename F::S block_excl_scan(const typename F::S &mine, typename F::S *sh, typename F::S *total) {
+// Summary shuffles: the 32-B summaries move between lanes as eight 32-bit fields.
+template <class S>
+__device__ inline S shfl_up_s(const S &v, int d) {
+    static_assert(sizeof(S) == 32, "summary = 8 x int32");
+    S r;
+    const int *a = reinterpret_cast<const int *>(&v);
+    int *b = reinterpret_cast<int *>(&r);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) b[f] = __shfl_up(a[f], d);
+    return r;
+}
+
+// Exclusive scan of per-lane summaries over a workgroup of NT lanes: wave64 inclusive scans
+// with shuffles, then the wave totals through LDS.  Returns the lane's exclusive prefix and
+// the workgroup total through *total.
+template <class F, int NT>
+__device__ typename F::S block_excl_scan(const typename F::S &mine, typename F::S *wtot, typename F::S *total) {
     using S = typename F::S;
-    const int tid = threadIdx.x;
-    sh[tid] = mine;
-    __syncthreads();
-    for (int d = 1; d < kThreads; d <<= 1) {
-        S v = sh[tid];
-        if (tid >= d) v = F::cat(sh[tid - d], v);
-        __syncthreads();
-        sh[tid] = v;
-        __syncthreads();
+    constexpr int kW = NT / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    S inc = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const S o = shfl_up_s(inc, d);
+        if (lane >= d) inc = F::cat(o, inc);
     }
-    if (total) *total = sh[kThreads - 1];
-    const S ex = tid ? sh[tid - 1] : F::identity();
+    S ex = shfl_up_s(inc, 1);
+    if (lane == 0) ex = F::identity();
+    if (lane == 63) wtot[wave] = inc;
     __syncthreads();
-    return ex;
+    S pre = F::identity();
+    for (int w = 0; w < wave; ++w) pre = F::cat(pre, wtot[w]);
+    if (total) {
+        S t = F::identity();
+#pragma unroll
+        for (int w = 0; w < kW; ++w) t = F::cat(t, wtot[w]);
+        *total = t;
+    }
+    __syncthreads();
+    return F::cat(pre, ex);
 }
 
 template <class F>
 __global__ void __launch_bounds__(kThreads)
 evt_summary_kernel(const typename F::Word *__restrict__ words, int64_t n_words, typename F::S *__restrict__ sums) {
     using S = typename F::S;
-    __shared__ S sh[kThreads];
+    __shared__ S wtot[kThreads / 64];
+    constexpr int kPer = F::kPer;
     uint32_t w[kPer];
     int nw;
     load_words<F>(words, n_words, blockIdx.x, w, nw);
@@ -229,71 +248,106 @@ evt_summary_kernel(const typename F::Word *__restrict__ words, int64_t n_words, 
     for (int e = 0; e < kPer; ++e)
         if (e < nw) F::fold(s, w[e]);
     S tot;
-    block_excl_scan<F>(s, sh, &tot);
+    block_excl_scan<F, kThreads>(s, wtot, &tot);
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
-// One workgroup: carry[c] = state before chunk c (the caller's streaming state first),
-// off[c] = events before chunk c (int64), off[n_chunks] = total -> *n_out; state advanced.
+// Carry-in states and event offsets in two levels.  evt_group_kernel: one workgroup per group
+// of kGroup chunks scans their summaries (group-local exclusive prefixes + the group total).
+// evt_carry_kernel: one workgroup scans the group totals in rounds of kGroup (one round covers
+// 2^18 chunks), starting from the caller's streaming state, and writes the int64
+// event offset of every group, the total -> *n_out, and the advanced state.
+constexpr int kGroup = 512;
+
 template <class F>
-__global__ void __launch_bounds__(kThreads)
-evt_carry_kernel(const typename F::S *__restrict__ sums, int64_t n_chunks, typename F::S *__restrict__ carry,
-                 int64_t *__restrict__ off, typename F::S *state, int64_t *n_out, int64_t cap, int32_t *err) {
+__global__ void __launch_bounds__(kGroup)
+evt_group_kernel(const typename F::S *__restrict__ sums, int64_t n_chunks, typename F::S *__restrict__ carry_local,
+                 int32_t *__restrict__ off_local, typename F::S *__restrict__ gsum) {
     using S = typename F::S;
-    __shared__ S sh[kThreads];
-    __shared__ int64_t sn[kThreads];
-    const int tid = threadIdx.x;
-    const int64_t per = (n_chunks + kThreads - 1) / kThreads;
-    const int64_t lo = tid * per, hi = lo + per < n_chunks ? lo + per : n_chunks;
-    S s = F::identity();
-    int64_t n = 0;
-    for (int64_t c = lo; c < hi; ++c) {
-        const S v = sums[c];
-        s = F::cat(s, v);
-        n += v.n;
-    }
+    __shared__ S wtot[kGroup / 64];
+    const int64_t c = (int64_t)blockIdx.x * kGroup + threadIdx.x;
+    const S v = c < n_chunks ? sums[c] : F::identity();
     S tot;
-    S ex = block_excl_scan<F>(s, sh, &tot);
-    // int64 event counts: separate scan (summary n fields are per-chunk int32)
-    sn[tid] = n;
+    const S ex = block_excl_scan<F, kGroup>(v, wtot, &tot);
+    if (c < n_chunks) {
+        carry_local[c] = ex;
+        off_local[c] = ex.n;  // < 512 chunks * 8192 words * 12 events
+    }
+    if (threadIdx.x == 0) gsum[blockIdx.x] = tot;
+}
+
+template <class F>
+__global__ void __launch_bounds__(kGroup)
+evt_carry_kernel(const typename F::S *__restrict__ gsum, int64_t n_groups, typename F::S *__restrict__ gcarry,
+                 int64_t *__restrict__ goff, typename F::S *state, int64_t *n_out, int64_t cap, int32_t *err) {
+    using S = typename F::S;
+    __shared__ S wtot[kGroup / 64];
+    __shared__ int64_t wn[kGroup / 64];
+    __shared__ S run_s;
+    __shared__ int64_t run_n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) {
+        run_s = state ? *state : F::identity();
+        run_n = 0;
+    }
     __syncthreads();
-    for (int d = 1; d < kThreads; d <<= 1) {
-        const int64_t v = tid >= d ? sn[tid - d] + sn[tid] : sn[tid];
+    for (int64_t g0 = 0; g0 < n_groups; g0 += kGroup) {
+        const int64_t g = g0 + tid;
+        const S v = g < n_groups ? gsum[g] : F::identity();
+        S tot;
+        const S ex = block_excl_scan<F, kGroup>(v, wtot, &tot);
+        int64_t x = v.n;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t o = __shfl_up(x, d);
+            if (lane >= d) x += o;
+        }
+        if (lane == 63) wn[wave] = x;
         __syncthreads();
-        sn[tid] = v;
+        int64_t pre = 0, all = 0;
+        for (int w = 0; w < kGroup / 64; ++w) {
+            if (w < wave) pre += wn[w];
+            all += wn[w];
+        }
+        if (g < n_groups) {
+            gcarry[g] = F::cat(run_s, ex);
+            goff[g] = run_n + pre + x - v.n;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            run_s = F::cat(run_s, tot);
+            run_n += all;
+        }
         __syncthreads();
     }
-    int64_t nex = tid ? sn[tid - 1] : 0;
-    const S st0 = state ? *state : F::identity();
-    __syncthreads();
-    ex = F::cat(st0, ex);
-    for (int64_t c = lo; c < hi; ++c) {
-        carry[c] = ex;
-        off[c] = nex;
-        const S v = sums[c];
-        ex = F::cat(ex, v);
-        nex += v.n;
-    }
-    if (tid == kThreads - 1) {
-        const int64_t total = sn[kThreads - 1];
-        off[n_chunks] = total;
-        if (n_out) *n_out = total;
-        if (total > cap) atomicOr(err, 2);
+    if (tid == 0) {
+        if (n_out) *n_out = run_n;
+        if (run_n > cap) atomicOr(err, 2);
         if (state) {
-            S ns = F::cat(st0, tot);
+            S ns = run_s;
             ns.n = 0;
             *state = ns;
         }
     }
 }
 
+// Decoded events are staged in LDS windows of F::kOut events and written out coalesced (a
+// lane's own run of events would touch a different cache line per lane and store).  Lanes
+// whose events miss the current window skip the walk.
+
 template <class F>
 __global__ void __launch_bounds__(kThreads)
-evt_decode_kernel(const typename F::Word *__restrict__ words, int64_t n_words, const typename F::S *__restrict__ carry,
-                  const int64_t *__restrict__ off, uint32_t *__restrict__ xy, int64_t *__restrict__ t,
-                  uint8_t *__restrict__ p, int64_t cap) {
+evt_decode_kernel(const typename F::Word *__restrict__ words, int64_t n_words, const typename F::S *__restrict__ sums,
+                  const typename F::S *__restrict__ carry_local, const int32_t *__restrict__ off_local,
+                  const typename F::S *__restrict__ gcarry, const int64_t *__restrict__ goff,
+                  uint32_t *__restrict__ xy, int64_t *__restrict__ t, uint8_t *__restrict__ p, int64_t cap) {
     using S = typename F::S;
-    __shared__ S sh[kThreads];
+    constexpr int kOut = F::kOut;
+    __shared__ S wtot[kThreads / 64];
+    __shared__ int64_t o_t[kOut];
+    __shared__ uint32_t o_xy[kOut];
+    __shared__ uint8_t o_p[kOut];
+    constexpr int kPer = F::kPer;
     uint32_t w[kPer];
     int nw;
     load_words<F>(words, n_words, blockIdx.x, w, nw);
@@ -301,18 +355,38 @@ evt_decode_kernel(const typename F::Word *__restrict__ words, int64_t n_words, c
 #pragma unroll
     for (int e = 0; e < kPer; ++e)
         if (e < nw) F::fold(s, w[e]);
-    const S ex = F::cat(carry[blockIdx.x], block_excl_scan<F>(s, sh, nullptr));
-    int64_t pos = off[blockIdx.x] + (ex.n - carry[blockIdx.x].n);
-    typename F::Regs r = F::regs(ex);
-    auto emit = [&](uint32_t v, int64_t ts, uint8_t pol) {
-        if (pos < cap) {
-            if (xy) xy[pos] = v;
-            if (t) t[pos] = ts;
-            if (p) p[pos] = pol;
+    const int g = blockIdx.x / kGroup;
+    const S cin = F::cat(gcarry[g], carry_local[blockIdx.x]);
+    const S ex = F::cat(cin, block_excl_scan<F, kThreads>(s, wtot, nullptr));
+    const int64_t base = goff[g] + off_local[blockIdx.x];
+    const int64_t n_chunk = sums[blockIdx.x].n;
+    const int lane_first = ex.n - cin.n, lane_n = s.n;  // this lane's events within the chunk
+    for (int64_t w0 = 0; w0 < n_chunk; w0 += kOut) {
+        if (lane_first < w0 + kOut && lane_first + lane_n > w0) {
+            typename F::Regs r = F::regs(ex);
+            int64_t pos = lane_first - w0;
+            auto emit = [&](uint32_t v, int64_t ts, uint8_t pol) {
+                if (pos >= 0 && pos < kOut) {
+                    o_xy[pos] = v;
+                    o_t[pos] = ts;
+                    o_p[pos] = pol;
+                }
+                ++pos;
+            };
+            for (int e = 0; e < nw; ++e) F::step(r, w[e], emit);
         }
-        ++pos;
-    };
-    for (int e = 0; e < nw; ++e) F::step(r, w[e], emit);
+        __syncthreads();
+        const int m = (int)(n_chunk - w0 < kOut ? n_chunk - w0 : kOut);
+        for (int i = threadIdx.x; i < m; i += kThreads) {
+            const int64_t g = base + w0 + i;
+            if (g < cap) {
+                if (xy) xy[g] = o_xy[i];
+                if (t) t[g] = o_t[i];
+                if (p) p[g] = o_p[i];
+            }
+        }
+        __syncthreads();
+    }
 }
 
 template <class F>
@@ -320,16 +394,23 @@ int decode(ecc_ctx *ctx, const void *words_v, int64_t n_words, uint32_t *xy, int
            int64_t *n_out, void *state, hipStream_t s) {
     using S = typename F::S;
     const auto *words = static_cast<const typename F::Word *>(words_v);
+    constexpr int kChunk = kThreads * F::kPer;
     const int64_t n_chunks = (n_words + kChunk - 1) / kChunk;
     if (n_chunks > INT32_MAX) return ECC_ERR_INVALID;
-    const size_t off_carry = ecc::align_up((size_t)n_chunks * sizeof(S), 256);
-    const size_t off_off = off_carry + ecc::align_up((size_t)n_chunks * sizeof(S), 256);
-    int rc = ecc::ws_reserve(ctx, off_off + (size_t)(n_chunks + 1) * 8);
+    const int64_t n_groups = (n_chunks + kGroup - 1) / kGroup;
+    // workspace: sums | carry_local | off_local | gsum | gcarry | goff
+    size_t o = 0;
+    auto carve = [&](size_t bytes) { const size_t at = o; o = ecc::align_up(o + bytes, 256); return at; };
+    const size_t o_sums = carve((size_t)n_chunks * sizeof(S)), o_cl = carve((size_t)n_chunks * sizeof(S));
+    const size_t o_ol = carve((size_t)n_chunks * 4), o_gs = carve((size_t)n_groups * sizeof(S));
+    const size_t o_gc = carve((size_t)n_groups * sizeof(S)), o_go = carve((size_t)n_groups * 8);
+    int rc = ecc::ws_reserve(ctx, o);
     if (rc) return rc;
     char *ws = static_cast<char *>(ctx->ws);
-    S *sums = reinterpret_cast<S *>(ws);
-    S *carry = reinterpret_cast<S *>(ws + off_carry);
-    int64_t *off = reinterpret_cast<int64_t *>(ws + off_off);
+    S *sums = reinterpret_cast<S *>(ws + o_sums), *carry_local = reinterpret_cast<S *>(ws + o_cl);
+    int32_t *off_local = reinterpret_cast<int32_t *>(ws + o_ol);
+    S *gsum = reinterpret_cast<S *>(ws + o_gs), *gcarry = reinterpret_cast<S *>(ws + o_gc);
+    int64_t *goff = reinterpret_cast<int64_t *>(ws + o_go);
     int32_t *err = ctx->flags + kFlagWord;
     ECC_CHECK_HIP(ctx, hipMemsetAsync(err, 0, 4, s), "memset(evt err)");
     if (n_chunks == 0) {
@@ -341,14 +422,19 @@ int decode(ecc_ctx *ctx, const void *words_v, int64_t n_words, uint32_t *xy, int
         hipLaunchKernelGGL(evt_summary_kernel<F>, dim3((unsigned)n_chunks), dim3(kThreads), 0, s, words, n_words, sums);
     }
     {
+        ECC_TIMED(ctx, s, "evt_group_kernel");
+        hipLaunchKernelGGL(evt_group_kernel<F>, dim3((unsigned)n_groups), dim3(kGroup), 0, s, sums, n_chunks,
+                           carry_local, off_local, gsum);
+    }
+    {
         ECC_TIMED(ctx, s, "evt_carry_kernel");
-        hipLaunchKernelGGL(evt_carry_kernel<F>, dim3(1), dim3(kThreads), 0, s, sums, n_chunks, carry, off,
+        hipLaunchKernelGGL(evt_carry_kernel<F>, dim3(1), dim3(kGroup), 0, s, gsum, n_groups, gcarry, goff,
                            static_cast<S *>(state), n_out, cap, err);
     }
     {
         ECC_TIMED(ctx, s, "evt_decode_kernel");
-        hipLaunchKernelGGL(evt_decode_kernel<F>, dim3((unsigned)n_chunks), dim3(kThreads), 0, s, words, n_words, carry,
-                           off, xy, t, p, cap);
+        hipLaunchKernelGGL(evt_decode_kernel<F>, dim3((unsigned)n_chunks), dim3(kThreads), 0, s, words, n_words, sums,
+                           carry_local, off_local, gcarry, goff, xy, t, p, cap);
     }
     ECC_CHECK_LAUNCH(ctx, "evt decode");
     return ECC_OK;

@@ -7,6 +7,7 @@ every compute call goes through the C ABI (no CPU fallback exists here).
 from __future__ import annotations
 
 import ctypes as C
+import json
 import os
 from pathlib import Path
 
@@ -157,6 +158,7 @@ _sigs = {
     "ecc_raw_read_words": (i64, [C.c_char_p, C.POINTER(RawInfo), i64, i64, P]),
     "ecc_evt_decode": (C.c_int, [P, i32, P, i64, P, P, P, i64, P, P, P]),
     "ecc_evt_status": (C.c_int, [P, P]),
+    "ecc_evt_encode": (i64, [i32, P, P, P, i64, P, i64]),
     "ecc_reslice_n_us": (C.c_int, [P, P, i64, i64, P, i64, P, P]),
 }
 for _name, (_res, _args) in _sigs.items():
@@ -251,6 +253,18 @@ class Context:
 
     def sync(self):
         check(lib.ecc_stream_sync(self.stream), "sync")
+
+    # per-kernel timing (ecc_ctx_set_timing): HIP events around every launch of this context
+    def set_timing(self, on: bool):
+        check(lib.ecc_ctx_set_timing(self.ctx, 1 if on else 0), "ecc_ctx_set_timing")
+
+    def timing_reset(self):
+        check(lib.ecc_ctx_timing_reset(self.ctx), "ecc_ctx_timing_reset")
+
+    def timing_report(self) -> dict:
+        buf = C.create_string_buffer(1 << 16)
+        check(lib.ecc_ctx_timing_report(self.ctx, buf, len(buf)), "ecc_ctx_timing_report")
+        return json.loads(buf.value.decode())
 
     def last_error(self) -> str:
         return lib.ecc_ctx_last_error(self.ctx).decode()
@@ -511,6 +525,20 @@ def raw_read_words(path, info: RawInfo, first: int = 0, n: int | None = None) ->
     if got < 0:
         raise EccError(int(got), f"raw_read_words({path})")
     return out[:got]
+
+
+def evt_encode(fmt: int, xy, t, p) -> np.ndarray:
+    """RAW writer (ecc_evt_encode): events -> EVT 2.0 (u32) / EVT 3.0 (u16) words."""
+    xy = np.ascontiguousarray(xy, np.uint32)
+    t = np.ascontiguousarray(t, np.int64)
+    p = np.ascontiguousarray(p, np.uint8)
+    n = len(xy)
+    cap = 2 * n + 1 if fmt == EVT2 else 4 * n + 4 + (2 * int(t[-1] >> 24) if n else 0)
+    out = np.empty(max(cap, 1), np.uint32 if fmt == EVT2 else np.uint16)
+    k = lib.ecc_evt_encode(fmt, xy.ctypes.data, t.ctypes.data, p.ctypes.data, n, out.ctypes.data, cap)
+    if k < 0:
+        raise EccError(int(k), "evt_encode")
+    return out[:k].copy()
 
 
 def pack_xy(x, y) -> np.ndarray:

@@ -264,3 +264,74 @@ ECC_HOST_API int64_t ecc_raw_read_words(const char *path, const ecc_raw_info *in
     std::fclose(f);
     return (int64_t)got;  // little-endian host (x86-64): words are used as read
 }
+
+// RAW writer (include/ecc.h §8).  EVT 2.0: TIME_HIGH on every change of t >> 6.  EVT 3.0:
+// TIME_HIGH on every change of t >> 12 (with 0xFFF, 0 pairs per 2^24 loop crossed), TIME_LOW
+// on every change of t, ADDR_Y on every change of y, vector words for row runs.
+ECC_HOST_API int64_t ecc_evt_encode(int32_t format, const uint32_t *xy, const int64_t *t, const uint8_t *p,
+                                    int64_t n, void *out, int64_t cap) {
+    if (n < 0 || cap < 0 || (n > 0 && (!xy || !t || !p)) || (cap > 0 && !out)) return ECC_ERR_INVALID;
+    int64_t k = 0;
+    if (format == ECC_RAW_EVT2) {
+        auto *o = static_cast<uint32_t *>(out);
+        int64_t last = -1;
+        for (int64_t i = 0; i < n; ++i) {
+            if (i && t[i] < t[i - 1]) return ECC_ERR_UNSORTED_TIME;
+            const int64_t th = t[i] >> 6;
+            if (th != last) {
+                if (k < cap) o[k] = 0x80000000u | (uint32_t)(th & 0x0FFFFFFF);
+                ++k;
+                last = th;
+            }
+            const uint32_t x = xy[i] & 0x7FFu, y = (xy[i] >> 16) & 0x7FFu;
+            if (k < cap) o[k] = ((uint32_t)(p[i] & 1u) << 28) | ((uint32_t)(t[i] & 63) << 22) | (x << 11) | y;
+            ++k;
+        }
+        return k;
+    }
+    if (format != ECC_RAW_EVT3) return ECC_ERR_INVALID;
+    auto *o = static_cast<uint16_t *>(out);
+    auto put = [&](uint32_t v) {
+        if (k < cap) o[k] = (uint16_t)v;
+        ++k;
+    };
+    int64_t last_hi = -1, last_t = -1, last_y = -1;
+    for (int64_t i = 0; i < n;) {
+        if (i && t[i] < t[i - 1]) return ECC_ERR_UNSORTED_TIME;
+        const int64_t ti = t[i], hi = ti >> 12;
+        if (hi != last_hi) {
+            if (last_hi >= 0)
+                for (int64_t L = last_hi >> 12; L < (hi >> 12); ++L) {
+                    put(0x8FFFu);
+                    put(0x8000u);
+                }
+            put(0x8000u | (uint32_t)(hi & 0xFFF));
+            last_hi = hi;
+            last_t = -1;
+        }
+        if (ti != last_t) {
+            put(0x6000u | (uint32_t)(ti & 0xFFF));
+            last_t = ti;
+        }
+        const uint32_t y = (xy[i] >> 16) & 0x7FFu, x0 = xy[i] & 0x7FFu, pi = p[i] & 1u;
+        if ((int64_t)y != last_y) {
+            put(y);
+            last_y = y;
+        }
+        int64_t j = i + 1;
+        while (j < n && t[j] == ti && ((xy[j] >> 16) & 0x7FFu) == y && (p[j] & 1u) == pi &&
+               (xy[j] & 0x7FFu) > (xy[j - 1] & 0x7FFu) && (xy[j] & 0x7FFu) < x0 + 12)
+            ++j;
+        if (j - i >= 3) {
+            uint32_t m = 0;
+            for (int64_t q = i; q < j; ++q) m |= 1u << ((xy[q] & 0x7FFu) - x0);
+            put(0x3000u | (pi << 11) | x0);
+            put(0x4000u | m);
+            i = j;
+        } else {
+            put(0x2000u | (pi << 11) | x0);
+            ++i;
+        }
+    }
+    return k;
+}

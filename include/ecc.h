@@ -361,6 +361,13 @@ int ecc_raw_probe(const char *path, ecc_raw_info *info);
 int64_t ecc_raw_read_words(const char *path, const ecc_raw_info *info, int64_t first_word,
                            int64_t n, void *buf);
 
+/* Host: RAW writer — encodes events (x, y < 2048, non-decreasing t) into EVT 2.0 (u32) or
+ * EVT 3.0 (u16) words; EVT 3.0 runs of >= 3 events with equal (t, y, p) and increasing x
+ * within 12 px go out as VECT_BASE_X + VECT_12.  Returns the number of words (<= cap written)
+ * or a negative status.  Word bound: EVT 2.0 2n + 1, EVT 3.0 4n + 2 * (t_last >> 24) + 4. */
+int64_t ecc_evt_encode(int32_t format, const uint32_t *xy, const int64_t *t, const uint8_t *p, int64_t n,
+                       void *out, int64_t cap);
+
 /* Decoder carry state (device memory, ECC_EVT_STATE_BYTES, zeroed = stream start).  Passing
  * the same state to consecutive calls decodes a long recording in pieces exactly as if it
  * were one buffer; NULL = decode `words` as a complete stream. */

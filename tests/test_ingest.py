@@ -202,7 +202,7 @@ def test_gpu_evt_edges(ecc, orc, gpu, fmt):
     """Tiny and ragged buffers, chunk-boundary sizes, misaligned starts, arbitrary words."""
     ev = concat(events_random(30_000, 21), events_rows(3000, 22))
     words = orc.evt_encode(fmt, *ev, seed=5)
-    for n in (0, 1, 2, 15, 16, 17, 4095, 4096, 4097, 3 * 4096 + 5):
+    for n in (0, 1, 2, 15, 16, 17, 31, 32, 33, 4095, 4096, 4097, 8191, 8192, 8193, 3 * 8192 + 5):
         w = words[:n]
         got = _gpu_decode(ecc, gpu, fmt, w)
         _check_same(got, orc.evt_decode(fmt, w))
@@ -224,7 +224,7 @@ def test_gpu_evt_streaming_state(ecc, orc, gpu, fmt):
     words = orc.evt_encode(fmt, *ev, seed=9, noise_pct=10)
     rng = np.random.default_rng(4)
     cuts = np.sort(rng.choice(np.arange(1, len(words)), 40, replace=False))
-    cuts = np.unique(np.concatenate([cuts, [cuts[0] + 1, 4096, 4097]]))  # incl. 1-word pieces
+    cuts = np.unique(np.concatenate([cuts, [cuts[0] + 1, 4096, 4097, 8192, 8193]]))  # incl. 1-word pieces
     got = _gpu_decode(ecc, gpu, fmt, words, pieces=cuts)
     _check_same(got, orc.evt_decode(fmt, words))
 
@@ -285,3 +285,15 @@ def test_gpu_raw_file_to_corners(ecc, orc, gpu, tmp_path):
     w = ecc.raw_read_words(path, info)
     got = _gpu_decode(ecc, gpu, info.format, w)
     _check_same(got, (xy, t, p))
+
+
+@pytest.mark.parametrize("fmt", [2, 3])
+def test_raw_writer_roundtrip(ecc, orc, fmt):
+    """Product RAW writer (ecc_evt_encode) -> oracle decoder == the events (incl. loops, rows)."""
+    ev = concat(events_random(20_000, 51, t_span=1 << 27), events_rows(2000, 52))
+    words = ecc.evt_encode(fmt, *ev)
+    _check_same(orc.evt_decode(fmt, words), ev)
+    if fmt == 3:
+        assert ((words >> 12) == 4).sum() > 200
+    with pytest.raises(ecc.EccError):
+        ecc.evt_encode(fmt, ev[0][:3], np.array([5, 4, 6], np.int64), ev[2][:3])
