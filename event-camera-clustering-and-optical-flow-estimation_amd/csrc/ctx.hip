@@ -183,6 +183,9 @@ ECC_API int ecc_dev_free(void *ptr) { ECC_RT(hipFree(ptr)); }
 ECC_API int ecc_memset_async(void *dst, int value, size_t bytes, ecc_stream_t s) {
     ECC_RT(hipMemsetAsync(dst, value, bytes, ecc::as_stream(s)));
 }
+ECC_API int ecc_device_sync(void) {
+    ECC_RT(hipDeviceSynchronize());
+}
 ECC_API int ecc_memcpy_h2d(void *dst, const void *src, size_t bytes, ecc_stream_t s) {
     ECC_RT(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ecc::as_stream(s)));
 }

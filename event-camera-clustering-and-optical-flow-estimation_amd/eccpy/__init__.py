@@ -159,6 +159,9 @@ _sigs = {
     "ecc_evt_decode": (C.c_int, [P, i32, P, i64, P, P, P, i64, P, P, P]),
     "ecc_evt_status": (C.c_int, [P, P]),
     "ecc_evt_encode": (i64, [i32, P, P, P, i64, P, i64]),
+    "ecc_dbscan_extract": (C.c_int, [P, i64, i64, P, P, P, i64, i32, i32, i32, P, P, P, i64, P, P]),
+    "ecc_dbscan_status": (C.c_int, [P, P]),
+    "ecc_device_sync": (C.c_int, []),
     "ecc_reslice_n_us": (C.c_int, [P, P, i64, i64, P, i64, P, P]),
 }
 for _name, (_res, _args) in _sigs.items():
@@ -215,7 +218,11 @@ class DeviceArray:
         check(lib.ecc_memset_async(self.ptr, value, self.nbytes, stream), "memset")
 
     def numpy(self, stream=None) -> np.ndarray:
+        """Copies to the host.  stream=None waits for ALL device work first (library streams are
+        non-blocking, so the null stream alone does not order after them)."""
         out = np.empty(self.shape, self.dtype)
+        if stream is None:
+            check(lib.ecc_device_sync(), "ecc_device_sync")
         if self.nbytes:
             check(lib.ecc_memcpy_d2h(out.ctypes.data, self.ptr, self.nbytes, stream), "d2h")
         return out
@@ -350,6 +357,17 @@ class Context:
                                 counts.ptr, offsets.ptr, nbr.ptr, nbr_cap, self.stream),
               "ecc_eps_lists")
 
+
+    def dbscan_extract(self, n_segs: int, stride: int, counts_in, offsets: DeviceArray, nbr: DeviceArray,
+                       min_pts: int, min_size: int, max_size: int, labels: DeviceArray, n_clusters: DeviceArray,
+                       dups: DeviceArray | None, dup_cap: int, n_dups: DeviceArray):
+        check(lib.ecc_dbscan_extract(self.ctx, n_segs, stride, _ptr(counts_in), offsets.ptr, nbr.ptr,
+                                     nbr.nbytes // 4, min_pts,
+                                     min_size, max_size, labels.ptr, n_clusters.ptr, _ptr(dups), dup_cap,
+                                     n_dups.ptr, self.stream), "ecc_dbscan_extract")
+
+    def dbscan_status(self) -> int:
+        return lib.ecc_dbscan_status(self.ctx, self.stream)
 
     # ---- 8. RAW ingest
     def evt_decode(self, fmt: int, words: DeviceArray, n_words: int, xy: DeviceArray | None,

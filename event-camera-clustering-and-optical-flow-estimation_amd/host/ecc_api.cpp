@@ -484,52 +484,66 @@ std::vector<std::vector<std::size_t>> get_cluster_indices(const std::vector<reac
 
 // ------------------------------------------------------------------------------ DBSCAN
 void DBSCANSimpleCluster::extract(std::vector<PointIndices> &cluster_indices) {  // DBSCAN_simple.h:27-90
-    enum { UN_PROCESSED = 0, PROCESSING = 1, PROCESSED = 2 };
+    // radiusSearch for every point (ecc_eps_counts / ecc_eps_lists) and the seed-queue expansion
+    // (ecc_dbscan_extract: union-find closed form) both run on the GPU; the host only turns
+    // labels + duplicate memberships into PointIndices.
     cluster_indices.clear();
-    const size_t n = cloud_.size();
+    const int64_t n = (int64_t)cloud_.size();
     if (n == 0) return;
-    std::vector<std::array<int, 2>> pts(n);
-    for (size_t i = 0; i < n; ++i) {
+    if (n > 16384) throw Error(ECC_ERR_INVALID, "DBSCAN: more than 16384 points per cloud");
+    int mnx = 0, mny = 0, mxx = 0, mxy = 0;
+    for (int64_t i = 0; i < n; ++i) {
         const PointXYZ &p = cloud_[i];
         if (p.x != std::floor(p.x) || p.y != std::floor(p.y) || p.z != cloud_[0].z)
             throw Error(ECC_ERR_INVALID, "DBSCAN: GPU path needs integer-valued 2-D points (constant z)");
-        pts[i] = {(int)p.x, (int)p.y};
+        const int x = (int)p.x, y = (int)p.y;
+        if (i == 0 || x < mnx) mnx = x;
+        if (i == 0 || y < mny) mny = y;
+        if (i == 0 || x > mxx) mxx = x;
+        if (i == 0 || y > mxy) mxy = y;
     }
-    std::vector<int64_t> off;
-    std::vector<int32_t> nbr;
-    eps_neighbour_lists(ctx_, pts, eps_, off, nbr);  // radiusSearch for every point, on the GPU
-    auto nn_size = [&](size_t i) { return (int)(off[i + 1] - off[i]); };
-    std::vector<bool> is_noise(n, false);
-    std::vector<int> types(n, UN_PROCESSED);
-    std::vector<std::vector<int>> clusters;
-    for (size_t i = 0; i < n; i++) {
-        if (types[i] == PROCESSED) continue;
-        if (nn_size(i) < minPts_) { is_noise[i] = true; continue; }
-        std::vector<int> seed_queue{(int)i};
-        types[i] = PROCESSED;
-        for (int64_t k = off[i]; k < off[i + 1]; ++k)
-            if (nbr[k] != (int)i) { seed_queue.push_back(nbr[k]); types[nbr[k]] = PROCESSING; }
-        size_t sq = 1;
-        while (sq < seed_queue.size()) {
-            const int ci = seed_queue[sq];
-            if (is_noise[ci] || types[ci] == PROCESSED) { types[ci] = PROCESSED; sq++; continue; }
-            if (nn_size(ci) >= minPts_)
-                for (int64_t k = off[ci]; k < off[ci + 1]; ++k)
-                    if (types[nbr[k]] == UN_PROCESSED) { seed_queue.push_back(nbr[k]); types[nbr[k]] = PROCESSING; }
-            types[ci] = PROCESSED;
-            sq++;
-        }
-        if ((int)seed_queue.size() >= min_pts_per_cluster_ && (int)seed_queue.size() <= max_pts_per_cluster_) {
-            std::sort(seed_queue.begin(), seed_queue.end());
-            seed_queue.erase(std::unique(seed_queue.begin(), seed_queue.end()), seed_queue.end());
-            clusters.push_back(seed_queue);
-        }
+    if ((int64_t)mxx - mnx > 65535 || (int64_t)mxy - mny > 65535)
+        throw Error(ECC_ERR_INVALID, "DBSCAN: coordinate span exceeds 65535");
+    std::vector<uint32_t> xy(n);  // translation keeps every distance
+    for (int64_t i = 0; i < n; ++i) xy[i] = pack_xy((int)cloud_[i].x - mnx, (int)cloud_[i].y - mny);
+    ecc_stream_t s = ctx_.stream();
+    DeviceBuffer d_xy(n * 4), d_cnt(n * 4), d_off((n + 1) * 8), d_lab(n * 4), d_nc(4), d_nd(8);
+    d_xy.upload(xy.data(), n * 4, s);
+    check(ecc_eps_counts(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, 1, d_cnt.as<int32_t>(), nullptr, s),
+          "ecc_eps_counts");
+    std::vector<int32_t> cnt(n);
+    d_cnt.download(cnt.data(), n * 4, s);
+    ctx_.sync();
+    int64_t total = 0;
+    for (int32_t c : cnt) total += c;
+    DeviceBuffer d_nbr(std::max<int64_t>(total, 1) * 4);
+    check(ecc_eps_lists(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, d_cnt.as<int32_t>(),
+                        d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, s),
+          "ecc_eps_lists");
+    const int64_t dup_cap = std::max<int64_t>(n, 1024);
+    DeviceBuffer d_dups(dup_cap * 16);
+    check(ecc_dbscan_extract(ctx_.get(), 1, n, nullptr, d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, minPts_,
+                             min_pts_per_cluster_, max_pts_per_cluster_, d_lab.as<int32_t>(), d_nc.as<int32_t>(),
+                             d_dups.as<int64_t>(), dup_cap, d_nd.as<int64_t>(), s),
+          "ecc_dbscan_extract");
+    check(ecc_dbscan_status(ctx_.get(), s), "ecc_dbscan_extract");
+    int32_t nc = 0;
+    int64_t nd = 0;
+    std::vector<int32_t> lab(n);
+    d_nc.download(&nc, 4, s);
+    d_nd.download(&nd, 8, s);
+    d_lab.download(lab.data(), n * 4, s);
+    std::vector<int64_t> dups((size_t)nd * 2);
+    if (nd) d_dups.download(dups.data(), (size_t)nd * 16, s);
+    ctx_.sync();
+    std::vector<std::vector<int>> members((size_t)nc);
+    for (int64_t i = 0; i < n; ++i)
+        if (lab[i] >= 0) members[lab[i]].push_back((int)i);
+    for (int64_t k = 0; k < nd; ++k) members[dups[2 * k + 1]].push_back((int)dups[2 * k]);
+    for (auto &m : members) {
+        std::sort(m.begin(), m.end());
+        cluster_indices.push_back(PointIndices{m});
     }
-    std::stable_sort(clusters.begin(), clusters.end(), [](const std::vector<int> &a, const std::vector<int> &b) {
-        if (a.size() != b.size()) return a.size() > b.size();
-        return a.front() < b.front();
-    });
-    for (auto &c : clusters) cluster_indices.push_back(PointIndices{c});
 }
 
 }  // namespace ecc

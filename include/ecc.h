@@ -54,6 +54,8 @@ int ecc_version(void);
 const char *ecc_ctx_last_error(const ecc_ctx *ctx);
 /* Blocks until all work queued by this library on `stream` has finished. */
 int ecc_stream_sync(ecc_stream_t stream);
+/* Blocks until all work on the current device (every stream) has finished. */
+int ecc_device_sync(void);
 
 /* Runtime plumbing (the reference's clCreateBuffer / clEnqueueRead/WriteBuffer /
  * clGetEventProfilingInfo, SMP/…opencl_store.cpp:264-268, 406-422) so hosts and tests need
@@ -307,6 +309,33 @@ int ecc_eps_lists(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_
 /* Host helper: synchronises `stream`, returns offsets[n] (total list length) via *total. */
 int ecc_eps_total(ecc_ctx *ctx, const int64_t *offsets, int64_t n, int64_t *total,
                   ecc_stream_t stream);
+
+/* DBSCAN cluster extraction over the eps-lists.
+ * Reference: DBSCANSimpleCluster::extract PCC/DBSCAN_simple.h:27-90 (seed-queue expansion in
+ *   point order, clusters kept when min_cluster_size <= size <= max_cluster_size, each
+ *   cluster's indices sorted, clusters sorted by size descending :89; equal sizes: by first
+ *   index, then creation order — the reference's std::sort leaves ties unspecified).
+ * Consumes ecc_eps_lists' offsets / nbr for the same segments (core <=> count >= min_pts).
+ * The seed-queue result is computed without the queue: clusters are the core-connected
+ * components (union-find), created in order of their smallest core index (= the seed); a
+ * border point joins the first cluster with a core neighbour AND every later cluster whose
+ * seed is its neighbour (the seed's neighbours are queued unconditionally, :43-48).
+ * Outputs per point p (flattened s*seg_stride + j, j < seg_counts[s]):
+ *   labels[p] = index within segment s's output list of the cluster that claimed p first, or
+ *               -1 (noise, or that cluster was filtered out by size);
+ * n_clusters[s] = clusters kept for segment s;
+ * dups[2*i], dups[2*i+1] = (p, cluster index) for every further membership (unordered),
+ *   *n_dups (device int64) = their number; only dup_cap pairs are written.
+ * nbr_len = entries of nbr (a segment whose offsets run past it is rejected, not read).
+ * ecc_dbscan_status: ECC_ERR_CAPACITY if dups overflowed, a segment had more than 4096
+ * core-connected components, or its lists exceed nbr_len (that segment's labels are then
+ * all -1 and n_clusters 0). */
+int ecc_dbscan_extract(ecc_ctx *ctx, int64_t n_segs, int64_t seg_stride, const int32_t *seg_counts,
+                       const int64_t *offsets, const int32_t *nbr, int64_t nbr_len, int32_t min_pts,
+                       int32_t min_cluster_size, int32_t max_cluster_size, int32_t *labels,
+                       int32_t *n_clusters, int64_t *dups, int64_t dup_cap, int64_t *n_dups,
+                       ecc_stream_t stream);
+int ecc_dbscan_status(ecc_ctx *ctx, ecc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * 7. Host-side helpers (no GPU): synthetic event streams and event-file I/O.

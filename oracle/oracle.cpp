@@ -691,6 +691,57 @@ static double dist_d(const double *a, const double *b, int D) {
     return std::sqrt(s);
 }
 
+// §8f rank 3 checker: the same seed-queue restatement (DBSCAN_simple.h:27-90) over 2-D integer
+// points, returning the full cluster lists in output order (CSR: offs[c]..offs[c+1] indices
+// ascending); a point may appear in several clusters, as in the reference.  Returns clusters.
+ORC_API int orc_dbscan_lists(const int32_t *xy, int n, double eps, int min_pts, int min_size, int max_size,
+                             int64_t *offs, int32_t *members, int64_t cap) {
+    enum { UNP = 0, PROC = 1, DONE = 2 };
+    const double r2 = eps * eps;
+    // neighbour lists (self included, ascending) — radiusSearch :118-142
+    std::vector<std::vector<int>> nl(n);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            const double dx = (double)xy[2 * j] - xy[2 * i], dy = (double)xy[2 * j + 1] - xy[2 * i + 1];
+            if (dx * dx + dy * dy <= r2) nl[i].push_back(j);
+        }
+    std::vector<int> types(n, UNP);
+    std::vector<bool> noise(n, false);
+    std::vector<std::vector<int>> clusters;
+    for (int i = 0; i < n; i++) {
+        if (types[i] == DONE) continue;
+        if ((int)nl[i].size() < min_pts) { noise[i] = true; continue; }
+        std::vector<int> q{i};
+        types[i] = DONE;
+        for (int v : nl[i])
+            if (v != i) { q.push_back(v); types[v] = PROC; }
+        for (size_t qi = 1; qi < q.size(); ++qi) {
+            const int ci = q[qi];
+            if (noise[ci] || types[ci] == DONE) { types[ci] = DONE; continue; }
+            if ((int)nl[ci].size() >= min_pts)
+                for (int v : nl[ci])
+                    if (types[v] == UNP) { q.push_back(v); types[v] = PROC; }
+            types[ci] = DONE;
+        }
+        if ((int)q.size() >= min_size && (int)q.size() <= max_size) {
+            std::sort(q.begin(), q.end());
+            q.erase(std::unique(q.begin(), q.end()), q.end());
+            clusters.push_back(q);
+        }
+    }
+    std::stable_sort(clusters.begin(), clusters.end(), [](const std::vector<int> &a, const std::vector<int> &b) {
+        if (a.size() != b.size()) return a.size() > b.size();
+        return a.front() < b.front();
+    });
+    int64_t k = 0;
+    offs[0] = 0;
+    for (size_t c = 0; c < clusters.size(); ++c) {
+        for (int v : clusters[c]) { if (k < cap) members[k] = v; ++k; }
+        offs[c + 1] = k;
+    }
+    return (int)clusters.size();
+}
+
 ORC_API double orc_epsilon_estimation(const double *pts, int n, int D, int min_pts) {
     // optics.hpp:340-387 (bounding_box initialises max from points[1], Q20)
     if (n <= 1) return 0;

@@ -53,6 +53,7 @@ _sigs = {
     "orc_evt2_encode": (i64, [P, P, P, i64, C.c_uint64, i32, P, i64]),
     "orc_evt3_encode": (i64, [P, P, P, i64, C.c_uint64, i32, i32, P, i64]),
     "orc_reslice_n_us": (i64, [P, i64, i64, P, i64]),
+    "orc_dbscan_lists": (C.c_int, [P, i32, f64, i32, i32, i32, P, P, i64]),
 }
 for _n, (_r, _a) in _sigs.items():
     f = getattr(lib, _n)
@@ -274,3 +275,17 @@ def reslice_n_us(t, period, max_slices=None):
     bounds = np.zeros(max_slices + 1, np.int64)
     ns = lib.orc_reslice_n_us(_p(t), len(t), period, _p(bounds), max_slices)
     return bounds, int(ns)
+
+
+def dbscan_lists(pts_xy, eps, min_pts, min_size=1, max_size=1 << 30):
+    """Reference DBSCAN output (DBSCAN_simple.h:27-90) as a list of sorted index arrays."""
+    pts = np.ascontiguousarray(np.asarray(pts_xy, np.int32).reshape(-1, 2))
+    n = len(pts)
+    cap = max(1, 4 * n)
+    while True:
+        offs = np.zeros(n + 2, np.int64)
+        mem = np.empty(cap, np.int32)
+        nc = lib.orc_dbscan_lists(_p(pts), n, eps, min_pts, min_size, max_size, _p(offs), _p(mem), cap)
+        if offs[nc] <= cap:
+            return [mem[offs[c]:offs[c + 1]].copy() for c in range(nc)]
+        cap = int(offs[nc])

@@ -568,3 +568,95 @@ def test_sae_handoff_equals_single_stream(ecc, orc, gpu):
         f, _ = _fast_gpu(ecc, gpu, xy[lo:hi], t[lo:hi], W, H, first_detect=1 if i == 0 else 0, sae0=base.numpy())
         flags.append(f)
     assert (np.concatenate(flags) == o_flags).all()
+
+
+# ------------------------------------------------------------------------------ DBSCAN extraction (§8f rank 3)
+def _dbscan_gpu(ecc, gpu, xy, n_segs, stride, counts, eps, min_pts, min_size, max_size):
+    d_xy = dev(ecc, xy)
+    d_u = None if counts is None else dev(ecc, counts)
+    n = n_segs * stride
+    d_cnt = ecc.DeviceArray(n, np.int32)
+    gpu.eps_counts(d_xy, n_segs, stride, d_u, eps, 1, d_cnt, None)
+    d_off = ecc.DeviceArray(n + 1, np.int64)
+    gpu.sync()
+    cnt = d_cnt.numpy()
+    valid = np.zeros(n, bool)
+    for s in range(n_segs):
+        valid[s * stride: s * stride + (stride if counts is None else counts[s])] = True
+    cap = int(cnt[valid].sum()) + 16
+    d_nbr = ecc.DeviceArray(cap, np.int32)
+    gpu.eps_lists(d_xy, n_segs, stride, d_u, eps, d_cnt, d_off, d_nbr, cap)
+    total = C.c_int64(0)
+    ecc.check(ecc.lib.ecc_eps_total(gpu.ctx, d_off.ptr, n, C.byref(total), gpu.stream))
+    assert total.value <= cap
+    d_lab = ecc.DeviceArray(n, np.int32)
+    d_nc = ecc.DeviceArray(n_segs, np.int32)
+    dup_cap = 1 << 20
+    d_dups = ecc.DeviceArray(2 * dup_cap, np.int64)
+    d_nd = ecc.DeviceArray(1, np.int64)
+    gpu.dbscan_extract(n_segs, stride, d_u, d_off, d_nbr, min_pts, min_size, max_size, d_lab, d_nc, d_dups,
+                       dup_cap, d_nd)
+    st = gpu.dbscan_status()
+    assert st == 0, gpu.last_error()
+    lab, nc, nd = d_lab.numpy(), d_nc.numpy(), int(d_nd.numpy()[0])
+    dups = d_dups.numpy()[:2 * nd].reshape(-1, 2)
+    out = []
+    for s in range(n_segs):
+        m = stride if counts is None else counts[s]
+        members = [[] for _ in range(nc[s])]
+        for j in range(m):
+            if lab[s * stride + j] >= 0:
+                members[lab[s * stride + j]].append(j)
+        for p, c in dups[(dups[:, 0] >= s * stride) & (dups[:, 0] < s * stride + m)]:
+            members[c].append(int(p - s * stride))
+        out.append([np.array(sorted(c), np.int32) for c in members])
+    return out
+
+
+@pytest.mark.parametrize("eps,min_pts,min_size,max_size", [
+    (20.0, 20, 100, 25000),   # pcl_cluster.cpp:113-120 driver parameters
+    (3.0, 4, 1, 1 << 30),
+    (1.5, 3, 2, 50),
+])
+def test_dbscan_extract_matches_reference_semantics(ecc, orc, gpu, eps, min_pts, min_size, max_size):
+    xy, _, _ = ecc.gen_events(40_000, seed=61)
+    rep_xy, _, u, _ = orc.downsample_hash(xy)
+    nw = min(len(u), 4)
+    got = _dbscan_gpu(ecc, gpu, rep_xy[:nw * 8192], nw, 8192, u[:nw], eps, min_pts, min_size, max_size)
+    for w in range(nw):
+        pts = rep_xy[w * 8192: w * 8192 + u[w]]
+        ref = orc.dbscan_lists(np.stack([pts & 0xFFFF, pts >> 16], 1), eps, min_pts, min_size, max_size)
+        assert len(got[w]) == len(ref)
+        for a, b in zip(got[w], ref):
+            assert np.array_equal(a, b)
+
+
+def test_dbscan_extract_border_duplicates(ecc, orc, gpu):
+    """Many tiny random segments (dense in seeds, borders and duplicate memberships)."""
+    rng = np.random.default_rng(7)
+    n_segs, stride = 300, 64
+    counts = rng.integers(1, stride + 1, n_segs).astype(np.int32)
+    xy = ecc.pack_xy(rng.integers(0, 14, n_segs * stride), rng.integers(0, 14, n_segs * stride))
+    got = _dbscan_gpu(ecc, gpu, xy, n_segs, stride, counts, 2.0, 4, 1, 1 << 30)
+    n_dup = 0
+    for s in range(n_segs):
+        pts = xy[s * stride: s * stride + counts[s]]
+        ref = orc.dbscan_lists(np.stack([pts & 0xFFFF, pts >> 16], 1), 2.0, 4)
+        assert len(got[s]) == len(ref), s
+        for a, b in zip(got[s], ref):
+            assert np.array_equal(a, b), s
+        n_dup += sum(len(c) for c in ref) - len(set(np.concatenate(ref).tolist())) if ref else 0
+    assert n_dup > 0  # the case really exercises duplicate memberships
+
+
+def test_dbscan_extract_rejects_short_lists(ecc, gpu):
+    """offsets that run past nbr_len: the segment is rejected (status CAPACITY), never read."""
+    n = 64
+    d_off = dev(ecc, np.arange(n + 1, dtype=np.int64) * 10)    # claims 640 entries
+    d_nbr = dev(ecc, np.zeros(100, np.int32))                  # holds 100
+    d_lab = ecc.DeviceArray(n, np.int32)
+    d_nc = ecc.DeviceArray(1, np.int32)
+    d_nd = ecc.DeviceArray(1, np.int64)
+    gpu.dbscan_extract(1, n, None, d_off, d_nbr, 3, 1, 1 << 30, d_lab, d_nc, None, 0, d_nd)
+    assert gpu.dbscan_status() == ecc.ERR_CAPACITY
+    assert (d_lab.numpy() == -1).all() and int(d_nc.numpy()[0]) == 0
