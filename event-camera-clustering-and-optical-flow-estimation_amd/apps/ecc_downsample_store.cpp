@@ -1,7 +1,7 @@
 // Host program mirroring SMP|DSA/metavision_sdk_get_started5_opencl_store.cpp: the hash-map
 // downsampler (process_coordinates) over consecutive 8192-event windows, printing per window the
 // unique/repeated counts (the reference prints local_unique_count / unique_count, :87) and the
-// first representatives.  AEClustering of the representatives is out of scope.
+// first representatives (ecc_downsample_cluster adds the AEClustering consumer, §8f rank 2).
 #include "app_common.hpp"
 
 int main(int argc, char **argv) {

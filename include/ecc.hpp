@@ -252,6 +252,107 @@ class KMeans {  // assign_to_centers + host loop, "fixed" mode (Appendix A Q7-Q1
     ecc_kmeans_cfg cfg_;
 };
 
+// ------------------------------------------------------------------------------ AEClustering
+// Host restatement of the reference's downsample consumer:
+// DSA/MyCluster.{h,cpp} and DSA/AEClustering.{h,cpp} — a per-event incremental clusterer,
+// serial by construction, fed from the GPU downsampler.  Eigen::VectorXd(2) is a
+// std::array<double, 2>; arithmetic is the same double-precision expressions.
+using Vec2d = std::array<double, 2>;
+
+class MyCluster {  // MyCluster.h:9-77
+  public:
+    MyCluster();                       // :5-11
+    MyCluster(double alpha, int kappa);  // :13-20 (without the constructor print)
+    void reset(int kappa, double alpha, int minN);
+    // e = {t, x, y, pol}; t relative to t0 is stored; eventId is post-incremented (:26-49)
+    void add(const std::deque<double> &e, int &eventId, double t0);
+    void forget(double t);             // :51-63, guarded on an empty cluster (Appendix A Q18)
+    double manhattanDistance(const Vec2d &x) const;               // :65-68
+    double manhattanDistanceWithSampling(const Vec2d &x) const;   // :70-99 (std::rand, as the reference)
+    void setN(int n) { n_ = n; }
+    void setDatId(const std::deque<int> &v) { datId_ = v; }
+    void setDat(const std::deque<Vec2d> &v) { dat_ = v; }
+    void setDatT(const std::deque<double> &v) { datT_ = v; }
+    void setDatPol(const std::deque<bool> &v) { datPol_ = v; }
+    void setMu(const Vec2d &mu) { mu_ = mu; }
+    void setMuPrev(const Vec2d &mu) { muPrev_ = mu; }
+    void setClusterId(int id) { clusterId_ = id; }
+    int getN() const { return n_; }
+    const std::deque<int> &getDatId() const { return datId_; }
+    const std::deque<Vec2d> &getDat() const { return dat_; }
+    const std::deque<double> &getDatT() const { return datT_; }
+    const std::deque<bool> &getDatPol() const { return datPol_; }
+    Vec2d getClusterCentroid() const;  // :180-195 mean of the stored points
+    const Vec2d &getMu() const { return mu_; }
+    const Vec2d &getMuPrev() const { return muPrev_; }
+    int getClusterId() const { return clusterId_; }
+
+  private:
+    std::deque<int> datId_;
+    std::deque<Vec2d> dat_;
+    std::deque<double> datT_;
+    std::deque<bool> datPol_;
+    double alpha_ = 0.5;
+    Vec2d mu_{0.0, 0.0}, muPrev_{0.0, 0.0};
+    int n_ = 0, kappa_ = 0, clusterId_ = 0;
+};
+
+class AEClustering {  // AEClustering.h:6-44
+  public:
+    AEClustering();  // :7-18: minN 10, buffer 800, radius 40, alpha 0.5, kappa 0
+    void init(int szBuffer, double radius = 10, int kappa = 10, double alpha = 0.5, int minN = 5);
+    // e = {t, x, y, pol}; always returns false, as the reference (:51-125)
+    bool update(const std::deque<double> &e);
+    int getLastUpdatedClusterIdx() const { return lastUpdatedCluster_; }
+    int getMinN() const { return minN_; }
+    double t = 0.0;
+    std::deque<MyCluster> clusters;
+
+  private:
+    void updateBuffer_(double t);                        // :141-149
+    void merge_clusters_(const std::deque<int> &assigned);  // :151-211
+    int minN_, szBuffer_;
+    std::deque<double> tBuffer_;
+    double tMin_, radius_, alpha_;
+    int kappa_, eventId_;
+    double t0_;
+    int lastUpdatedCluster_, clusterID_;
+};
+
+// The downsample -> clusterer hand-off of DSA/…opencl_store.cpp:428-445 for one window's
+// representatives (ascending index): the reference walks the interleaved int array with
+// i += 4 while i < diff, i.e. representatives k = 0, 2, 4, ... with 2k < n_reps, each fed as
+// {cumulative_unique / 1000.0, x, y, 0} (the fake time axis, Appendix A Q6; per-window counts, Q4).
+void aeclustering_feed_window(AEClustering &ae, const std::vector<std::pair<int, int>> &reps,
+                              int64_t cumulative_unique);
+
+// Centroid-displacement "flow" (DSA/…opencl_store.cpp:470-518,
+// TWE/…opencl_store.cpp:396-448): per slice, every cluster with getN() >= minN gets
+// cen = getClusterCentroid(), prev = centroid_prev[id % 16384], diff = cen - prev, drawn as an
+// arrow from prev to prev + scale * diff (scale 1 DSA, 3 TWE) when prev.x > 0 && prev.y > 0;
+// then centroid_prev[id] = cen.
+struct ClusterFlow {
+    int cluster_id, n;
+    Vec2d centroid, prev, diff;
+    bool has_prev;
+};
+
+class CentroidFlow {
+  public:
+    std::vector<ClusterFlow> update(const AEClustering &ae);
+
+  private:
+    std::vector<Vec2d> prev_ = std::vector<Vec2d>(16384, Vec2d{0.0, 0.0});  // double centroid_prev[16384][2]
+};
+
+// Writers: the per-slice cluster frame the reference draws with OpenCV and saves with
+// cv::imwrite (DSA/…opencl_store.cpp:479-555) as a binary PPM (no OpenCV here): points in
+// the 10-colour palette by id % 10, centroid green, previous centroid red, flow arrow green.
+// CSV: one "x,y,t,cluster" line per clustered point (PCC/pcl_cluster.cpp:140 layout).
+bool write_cluster_ppm(const std::string &path, int width, int height, const AEClustering &ae,
+                       const std::vector<ClusterFlow> &flow, double arrow_scale = 1.0);
+bool write_cluster_csv(const std::string &path, const AEClustering &ae, int minN);
+
 // ------------------------------------------------------------------------------ OPTICS
 namespace optics {
 

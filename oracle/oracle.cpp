@@ -25,6 +25,7 @@
 // reference's gcc build does on x86-64 without FMA).
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -1039,4 +1040,160 @@ ORC_API int64_t orc_reslice_n_us(const int64_t *t, int64_t n, int64_t period, in
     }
     bounds[ns < max_slices ? ns : max_slices] = n;
     return ns;
+}
+
+// ------------------------------------------------------------------------------------------
+// §8f ranks 2 + 4: AEClustering (DSA/AEClustering.cpp:20-211, DSA/MyCluster.cpp:5-201) fed by
+// the downsample slice path (DSA/…opencl_store.cpp:428-445) and the centroid displacement
+// (:470-518).  Literal restatement: Eigen::VectorXd(2) -> double[2]; the unqualified abs() on
+// doubles binds to int abs(int) (truncation); merge returns before erasing emptied clusters.
+// ------------------------------------------------------------------------------------------
+namespace {
+struct OrcCluster {
+    std::deque<int> datId;
+    std::deque<std::array<double, 2>> dat;
+    std::deque<double> datT;
+    std::deque<bool> datPol;
+    double alpha = 0.5;
+    double mu[2] = {0, 0};
+    int n = 0, kappa = 0, id = 0;
+    void add(const double *e, int &eventId, double t0) {
+        const double t = e[0] - t0;
+        datId.push_back(eventId);
+        dat.push_back({e[1], e[2]});
+        datT.push_back(t);
+        datPol.push_back(e[3] != 0);
+        if (n == 0) { mu[0] = e[1]; mu[1] = e[2]; }
+        else { mu[0] = (1 - alpha) * mu[0] + alpha * e[1]; mu[1] = (1 - alpha) * mu[1] + alpha * e[2]; }
+        n++;
+        eventId++;
+    }
+    void forget(double t) {
+        while (n > 0 && datT[0] < t) { dat.pop_front(); datId.pop_front(); datT.pop_front(); if (!datPol.empty()) datPol.pop_front(); n--; }
+    }
+    static double tabs(double v) { return (double)std::abs((int)v); }
+    double manhattan(const double *x) const { return (double)((int)tabs(x[0] - mu[0]) + (int)tabs(x[1] - mu[1])); }
+    double sampled(const double *x) const {
+        double ma = std::numeric_limits<double>::max();
+        if (kappa > n) {
+            for (const auto &y : dat) { const double f = (double)((int)tabs(x[0] - y[0]) + (int)tabs(x[1] - y[1])); if (f < ma) ma = f; }
+        } else {
+            for (int ii = 0; ii < kappa; ++ii) {
+                const auto &y = dat[std::rand() % (int)dat.size()];
+                const double f = (double)((int)tabs(x[0] - y[0]) + (int)tabs(x[1] - y[1]));
+                if (f < ma) ma = f;
+            }
+        }
+        return ma;
+    }
+};
+
+struct OrcAEC {
+    int minN = 10, szBuffer = 800, kappa = 0, eventId = 0, lastUpdated = -1, nextId = 0;
+    double tMin = 0, radius = 40, alpha = 0.5, t0 = -1;
+    std::deque<double> tBuf;
+    std::deque<OrcCluster> clusters;
+    void merge(const std::deque<int> &as) {
+        const int m = (int)as.size();
+        std::vector<int> nn(m), cnt(m, 0);
+        int aux_n = 0;
+        for (int i = 0; i < m; ++i) { nn[i] = clusters[as[i]].n; aux_n += nn[i]; }
+        double amu[2] = {0, 0};
+        for (int i = 0; i < m; ++i) {
+            const double w = (double)clusters[as[i]].n / (double)aux_n;
+            amu[0] += w * clusters[as[i]].mu[0];
+            amu[1] += w * clusters[as[i]].mu[1];
+        }
+        std::vector<OrcCluster> src;
+        for (int i = 0; i < m; ++i) src.push_back(clusters[as[i]]);
+        OrcCluster &d = clusters[as[0]];
+        d.datId.clear(); d.dat.clear(); d.datT.clear(); d.datPol.clear();
+        for (int idx = 1; idx >= 0;) {
+            idx = -1;
+            double tt = std::numeric_limits<double>::max();
+            for (int j = 0; j < m; ++j)
+                if (cnt[j] < nn[j] && src[j].datT[cnt[j]] < tt) { idx = j; tt = src[j].datT[cnt[j]]; }
+            if (idx >= 0) {
+                d.datId.push_back(src[idx].datId[cnt[idx]]);
+                d.dat.push_back(src[idx].dat[cnt[idx]]);
+                d.datT.push_back(src[idx].datT[cnt[idx]]);
+                d.datPol.push_back(src[idx].datPol[cnt[idx]]);
+                cnt[idx]++;
+            }
+        }
+        d.n = (int)d.dat.size();
+        d.mu[0] = amu[0];
+        d.mu[1] = amu[1];
+        for (int i = m - 1; i > 0; --i) clusters.erase(clusters.begin() + as[i]);
+    }
+    void update(const double *e) {
+        if (t0 < 0) t0 = e[0];
+        const double t = e[0] - t0;
+        tBuf.push_back(t);
+        if ((int)tBuf.size() > szBuffer) tBuf.pop_front();
+        tMin = tBuf[0];
+        std::deque<int> as, rm;
+        const double pix[2] = {e[1], e[2]};
+        for (int i = 0; i < (int)clusters.size(); ++i) {
+            clusters[i].forget(tMin);
+            if (clusters[i].n == 0) rm.push_back(i);
+            else if (clusters[i].manhattan(pix) <= radius) as.push_back(i);
+            else if (clusters[i].n > minN && clusters[i].sampled(pix) <= radius) as.push_back(i);
+        }
+        if (as.empty()) {
+            OrcCluster c;
+            c.alpha = alpha;
+            c.kappa = kappa;
+            clusters.push_back(c);
+            clusters.back().add(e, eventId, t0);
+            clusters.back().id = nextId++;
+            lastUpdated = (int)clusters.size() - 1;
+        } else {
+            lastUpdated = as[0];
+            clusters[as[0]].add(e, eventId, t0);
+            if (as.size() >= 2) { merge(as); return; }
+        }
+        for (int i = (int)rm.size() - 1; i >= 0; --i) {
+            if (lastUpdated > rm[i]) lastUpdated--;
+            clusters.erase(clusters.begin() + rm[i]);
+        }
+    }
+};
+}  // namespace
+
+// rows (8 doubles each): window, cluster id, n, centroid x, y, has_prev, flow dx, dy — for the
+// clusters with n >= minN after each window, in cluster-deque order.  Returns the row count.
+ORC_API int64_t orc_aec_run(const uint32_t *rep_xy, const int32_t *win_unique, int64_t n_windows, int64_t stride,
+                            int szBuffer, double radius, int kappa, double alpha, int minN, double *rows,
+                            int64_t cap, int32_t *clusters_per_window) {
+    OrcAEC ae;
+    ae.szBuffer = szBuffer; ae.radius = radius; ae.kappa = kappa; ae.alpha = alpha; ae.minN = minN;
+    std::vector<std::array<double, 2>> prev(16384, {0.0, 0.0});  // double centroid_prev[16384][2]
+    int64_t k = 0, cumulative = 0;
+    for (int64_t w = 0; w < n_windows; ++w) {
+        const int diff = win_unique[w];
+        cumulative += diff;
+        for (int i = 0; i < diff; i += 4) {  // uniqueCoords[i], [i+1] of the interleaved ints
+            const uint32_t v = rep_xy[w * stride + i / 2];
+            const double e[4] = {(double)cumulative / 1000.0, (double)(v & 0xffff), (double)(v >> 16), 0.0};
+            ae.update(e);
+        }
+        clusters_per_window[w] = (int32_t)ae.clusters.size();
+        for (const auto &c : ae.clusters) {
+            if (c.n < ae.minN) continue;
+            double xa = 0, ya = 0;
+            for (const auto &p : c.dat) { xa = xa + p[0]; ya = ya + p[1]; }
+            xa = xa / (double)c.dat.size();
+            ya = ya / (double)c.dat.size();
+            int id = c.id;
+            if (id > 16384) id %= 16384;
+            auto &pv = prev[id % 16384];
+            const double row[8] = {(double)w, (double)c.id, (double)c.n, xa, ya,
+                                   (pv[0] > 0 && pv[1] > 0) ? 1.0 : 0.0, xa - pv[0], ya - pv[1]};
+            if (k < cap) std::memcpy(rows + 8 * k, row, sizeof(row));
+            ++k;
+            pv = {xa, ya};
+        }
+    }
+    return k;
 }

@@ -54,6 +54,7 @@ _sigs = {
     "orc_evt3_encode": (i64, [P, P, P, i64, C.c_uint64, i32, i32, P, i64]),
     "orc_reslice_n_us": (i64, [P, i64, i64, P, i64]),
     "orc_dbscan_lists": (C.c_int, [P, i32, f64, i32, i32, i32, P, P, i64]),
+    "orc_aec_run": (i64, [P, P, i64, i64, i32, f64, i32, f64, i32, P, i64, P]),
 }
 for _n, (_r, _a) in _sigs.items():
     f = getattr(lib, _n)
@@ -289,3 +290,20 @@ def dbscan_lists(pts_xy, eps, min_pts, min_size=1, max_size=1 << 30):
         if offs[nc] <= cap:
             return [mem[offs[c]:offs[c + 1]].copy() for c in range(nc)]
         cap = int(offs[nc])
+
+
+def aec_run(rep_xy, win_unique, stride=8192, sz_buffer=800, radius=40.0, kappa=0, alpha=0.5, min_n=10):
+    """AEClustering over the downsample windows (DSA slice path) -> (rows[k, 8], clusters per window);
+    row = window, cluster id, n, centroid x, y, has_prev, flow dx, dy."""
+    rep_xy = np.ascontiguousarray(rep_xy, np.uint32)
+    u = np.ascontiguousarray(win_unique, np.int32)
+    nw = len(u)
+    cap = 1 << 16
+    while True:
+        rows = np.zeros((cap, 8), np.float64)
+        cpw = np.zeros(max(nw, 1), np.int32)
+        k = lib.orc_aec_run(_p(rep_xy), _p(u), nw, stride, sz_buffer, radius, kappa, alpha, min_n, _p(rows), cap,
+                            _p(cpw))
+        if k <= cap:
+            return rows[:k].copy(), cpw[:nw].copy()
+        cap = int(k)

@@ -137,3 +137,45 @@ def test_corner_track_program_reads_raw_recording(orc, ecc, tmp_path, fmt):
     a = run("ecc_corner_track", path, "--width", W, "--height", H)
     b = run("ecc_corner_track", "--synthetic", n, "--width", W, "--height", H)
     assert a == b and "Corner size" in a
+
+
+def _parse_cluster_program(out):
+    windows, rows = [], []
+    w = -1
+    for line in out.splitlines():
+        m = re.match(r"window (\d+) reps (\d+) clusters (\d+)", line)
+        if m:
+            w = int(m.group(1))
+            windows.append(int(m.group(3)))
+            continue
+        m = re.match(r"\s+cluster (\d+) n (\d+) centroid (\S+) (\S+) flow (.*)", line)
+        if m:
+            fl = m.group(5).split()
+            rows.append([w, int(m.group(1)), int(m.group(2)), float(m.group(3)), float(m.group(4)),
+                         0.0 if fl == ["-"] else 1.0,
+                         *([float("nan")] * 2 if fl == ["-"] else [float(fl[0]), float(fl[1])])])
+    return windows, np.array(rows, np.float64).reshape(-1, 8)
+
+
+@pytest.mark.parametrize("args,kw", [
+    ((), {}),                                                  # the reference's defaults (AEClustering.cpp:7-18)
+    (("--kappa", 100000), {"kappa": 100000}),                  # sampled distance = full scan (kappa > n)
+    (("--radius", 10, "--min-n", 3), {"radius": 10.0, "min_n": 3}),
+])
+def test_downsample_cluster_program_matches_oracle(orc, ecc, tmp_path, args, kw):
+    """GPU downsample -> AEClustering -> centroid flow (DSA/…opencl_store.cpp:370-518) vs the oracle."""
+    n, W, H = 8192 * 40, 346, 260
+    out = run("ecc_downsample_cluster", "--synthetic", n, "--width", W, "--height", H, *args,
+              "--ppm-dir", tmp_path, "--csv", tmp_path / "c.csv")
+    xy, _, _ = ecc.gen_events(n, width=W, height=H)
+    rx, _, u, _ = orc.downsample_hash(xy)
+    o_rows, o_cpw = orc.aec_run(rx, u, **kw)
+    windows, rows = _parse_cluster_program(out)
+    assert windows == list(o_cpw)
+    assert rows.shape == o_rows.shape and rows.shape[0] > 0
+    assert np.array_equal(rows[:, :6], o_rows[:, :6])
+    has = o_rows[:, 5] == 1
+    assert np.array_equal(rows[has, 6:], o_rows[has, 6:])
+    ppm = (tmp_path / "cluster_frame_combined1.ppm").read_bytes()
+    assert ppm.startswith(f"P6\n{W} {H}\n255\n".encode()) and len(ppm) == len(f"P6\n{W} {H}\n255\n") + W * H * 3
+    assert (tmp_path / "c.csv").stat().st_size > 0

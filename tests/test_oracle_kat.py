@@ -189,3 +189,53 @@ def test_dbscan_kat(orc):
     assert (lab[-2:] == -1).all()
     for b in range(3):
         assert len(set(lab[b * 60:(b + 1) * 60])) == 1
+
+
+# ------------------------------------------------------------------------------ AEClustering (§8f rank 2)
+def test_unqualified_abs_on_double_truncates(tmp_path):
+    """The restatement's assumption for MyCluster.cpp:66/82/93: at global scope, with the standard
+    headers Eigen/Core pulls in, unqualified abs(double) binds to C's int abs(int) (this g++)."""
+    import subprocess
+    src = tmp_path / "p.cpp"
+    src.write_text("#include <cmath>\n#include <cstdlib>\n#include <complex>\n#include <functional>\n"
+                   "#include <limits>\n#include <algorithm>\n#include <deque>\n#include <iostream>\n"
+                   "double f(double a, double b) { return abs(a - b); }\n"
+                   "int main() { std::cout << f(0.75, 0.0) << ' ' << f(-2.5, 0.0) << std::endl; }\n")
+    exe = tmp_path / "p"
+    subprocess.run(["g++", "-O2", "-std=c++17", str(src), "-o", str(exe)], check=True, capture_output=True)
+    assert subprocess.run([str(exe)], capture_output=True, text=True).stdout.split() == ["0", "2"]
+
+
+def test_aeclustering_oracle_hand_case(orc):
+    """Hand-derived.  Window reps are fed at k = 0, 2, 4, ... with 2k < n (the i += 4 walk over
+    the interleaved ints).  radius 40: (12,10) joins the cluster at (10,10) (mu -> (11,10));
+    (100,100) and (56,56) open clusters 1 and 2; (45,45) joins cluster 2 (mu -> (50.5,50.5)).
+    Window 2's (71,71) is 20.5 + 20.5 = 41 from (50.5,50.5) exactly, but the truncating int
+    abs() makes it 20 + 20 = 40 <= 40: it joins cluster 2 instead of opening a fourth."""
+    reps = np.zeros(8192 * 2, np.uint32)
+    win0 = [(10, 10), (0, 0), (12, 10), (0, 0), (100, 100), (0, 0), (56, 56), (0, 0), (45, 45), (0, 0)]
+    for i, (x, y) in enumerate(win0 + [(0, 0)] * 10):  # n = 20 -> k = 0, 2, 4, 6, 8
+        reps[i] = x | (y << 16)
+    reps[8192] = 71 | (71 << 16)
+    rows, cpw = orc.aec_run(reps, np.array([20, 2], np.int32), min_n=1)
+    assert list(cpw) == [3, 3]
+    w0 = rows[rows[:, 0] == 0]
+    assert [(int(r[1]), int(r[2])) for r in w0] == [(0, 2), (1, 1), (2, 2)]
+    assert tuple(w0[0, 3:5]) == (11.0, 10.0) and tuple(w0[2, 3:5]) == (50.5, 50.5)
+    assert (w0[:, 5] == 0).all()  # no previous centroid on the first window
+    w1 = rows[rows[:, 0] == 1]
+    assert [(int(r[1]), int(r[2])) for r in w1] == [(0, 2), (1, 1), (2, 3)]
+    assert (w1[:, 5] == 1).all() and (w1[:2, 6:] == 0).all()
+    assert w1[2, 3] == (56 + 45 + 71) / 3 and w1[2, 6] == (56 + 45 + 71) / 3 - 50.5
+
+
+def test_aeclustering_oracle_merge(orc):
+    """An event within 40 of two cluster means is added to the first, then the two merge:
+    n = sum, mu = n-weighted mean, stored points merged by time."""
+    reps = np.zeros(8192, np.uint32)
+    for k, (x, y) in zip((0, 2, 4), [(10, 10), (90, 10), (50, 10)]):  # |50-10| = |50-90| = 40
+        reps[k] = x | (y << 16)
+    rows, cpw = orc.aec_run(reps, np.array([10, ], np.int32), min_n=1)  # k < 5: 0, 2, 4
+    assert list(cpw) == [1]
+    assert rows.shape[0] == 1 and rows[0, 2] == 3
+    assert tuple(rows[0, 3:5]) == (50.0, 10.0)  # centroid = mean of the three points
