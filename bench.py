@@ -190,9 +190,10 @@ def main():
         "kmeans_xy16_kernel": 4.0 * n_reps,                               # packed u16 xy per point
         "kmeans_xy16_labels": 5.0 * n_reps,                               # + u8 label out
         "bin_hist_kernel": 12.0 * n,                                      # xy + t
-        "bin_scatter_kernel": 24.0 * n,                                   # xy + t in, key + t out
-        # group_kernel: key + t of group g+1 (build) and key of group g (arc); n_groups + 1 launches
-        "group_kernel": 16.0 * n / per_step_launches,
+        "bin_scatter_kernel": 20.0 * n,                                   # xy + t in, key + relative t out
+        # group_kernel: key + relative t of group g+1 (build), key of group g (arc), corner flag
+        # out; n_groups + 1 launches
+        "group_kernel": 13.0 * n / per_step_launches,
         "nms_kernel": 1.0 * n,                                            # corner flags
         "kmeans_step_kernel": 0.0,
     }.get(dominant, 0.0)
