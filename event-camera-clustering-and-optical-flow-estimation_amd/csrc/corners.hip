@@ -6,27 +6,24 @@
 // (:948-1063; circle3 streaks of 3..6 of 16 then circle4 streaks of 4..8 of 20, circles
 // :44-45 as {dy,dx}), holding a mutex per event.
 //
-// Exact batch semantics for a whole batch in few launches.  The arc test of an event in slice
-// s must see V(q,s) = t of the last event at pixel q with index < end(s).  Slices are
-// processed in GROUPS of G = 32.  For the group being tested we keep
-//   mask[q]    : u32 bitmask of the group's slices that touched q
-//   M[j][q]    : max t at q within slice j of the group (valid only where mask bit j is set)
-//   B[q]       : SAE before the group (the caller's `sae` buffer, updated in place)
-// so V(q,s) = M[j*][q] with j* = highest set bit of mask[q] & ((2 << j) - 1), else B[q]
+// Exact batch semantics for a whole batch with no per-slice (or per-group) launches.  The arc
+// test of an event in slice s must see V(q,s) = t of the last event at pixel q with index
+// < end(s).  Slices are taken in GROUPS of G = 32; with B_g = the SAE before group g,
+// V(q,s) = the last t at q in slices j' <= j of the group (j = s mod 32), else B_g[q]
 // (timestamps are non-decreasing, so max == last writer; a device check enforces it).
 //
-// Locality.  The batch is counting-sorted by (group, 16x16-pixel TILE) into 4-byte keys
-// (event index within the group << 8 | pixel within the tile) + timestamps:
-// per-slice LDS histograms -> scan -> per-slice scatter.  Then per group:
-//   tile_build(g): one 1024-lane workgroup per tile OWNS that tile's 256 pixels: it folds group
-//                  g-1 into B, accumulates mask/M of its bin with LDS atomics and writes them
-//                  back with plain stores — no global atomics and no reset pass (M is only ever
-//                  read where the same group's mask bit is set);
-//   arc_test(g):   one workgroup per WORK ITEM (<= 4096 events of one tile): it stages the
-//                  tile's 24x24 neighbourhood — mask, B and the set M entries compacted per
-//                  pixel as u32 offsets from the group's first timestamp — in LDS, then tests
-//                  one event per lane against LDS only.  Hot tiles split into several items.
-// Two ping-pong buffer sets: tile_build(g) reads set (g-1)&1 and writes set g&1.
+// Pipeline (every launch covers the whole batch):
+//   bin_hist / scan / bin_scatter: counting sort by (group, 14x14-pixel TILE) into 4-byte keys
+//       (event index within the group << 8 | pixel within the tile) + group-relative timestamps;
+//   pair_build: per (group, tile) the distinct (slice, pixel) pairs with the value an arc test
+//               reads there, in sub-region order; the slices that touched each pixel and its
+//               last timestamp;
+//   sae_prefix: per pixel, B_g for every group (prefix over groups) and the final SAE;
+//   arc:        one 512-lane workgroup per (group, tile) for ALL groups at once: it stores the
+//               pairs of the sub-regions its 22x22 window covers into per-slice LDS planes,
+//               forward-fills them from B_g, and tests each distinct (slice, pixel) pair of
+//               its tile once against LDS only;
+//   flags:      per event in stream order, eligibility (Q11, Q15, border) && its pair's result.
 //
 // Arc test: the reference loop "exists i,s: T[c(i)]>=T[c(i-1)], T[c(i+s-1)]>=T[c(i+s)], and
 // every T outside the streak < min(streak)" reduces to "the s largest values are strictly
@@ -42,26 +39,17 @@
 #include <map>
 #include <mutex>
 
-// Development instrumentation (make CORNER_PROFILE=1): per-workgroup s_memrealtime stamps of one
-// group launch (ECC_CORNER_TS=<group>, ECC_CORNER_TS_FILE) and phase cut-offs (ECC_CORNER_DBG),
-// read by scripts/ts_analyze.py / ts_phases.py.  Compiled out by default.
-#ifndef ECC_CORNER_PROFILE
-#define ECC_CORNER_PROFILE 0
-#endif
-
 namespace {
 
 constexpr int kThreads = 256;
 constexpr int kBuildUnroll = 8;
 constexpr int kArcThreads = 512;  // 8 waves: one lane per window pixel (484) when staging
-constexpr int kItemEvents = 2048;  // events per arc work item
 constexpr int kGroup = 32;         // slices per group (mask bits)
 constexpr int kTile = 14;          // tile edge (pixels): the 22x22 window fits one 8-wave workgroup
 constexpr int kTilePix = kTile * kTile;
 constexpr int kHalo = 4;           // circle radius
 constexpr int kWin = kTile + 2 * kHalo;  // 22
 constexpr int kWinPix = kWin * kWin;     // 484
-constexpr int kStageMinEvents = 128;     // smaller work items skip the window staging
 constexpr int kMaxTiles = 8191;          // bins per group = n_tiles + 1 (8192 fit an LDS histogram)
 constexpr int kMaxSlice = 1 << 19;       // group-local event index must fit 24 bits
 
@@ -69,15 +57,7 @@ struct CornerGeom {
     int W, H, S, margin, border_mode, first_detect;
     int tiles_x, n_tiles;  // bin n_tiles of each group holds the events outside the sensor
     float inv_S;
-    int dbg;                 // ECC_CORNER_PROFILE only
-    unsigned long long *ts;  // ECC_CORNER_PROFILE only
-    int64_t ts_grp;
     int64_t n, n_slices;
-};
-
-struct GroupBufs {
-    uint32_t *mask;  // [H*W]
-    int64_t *M;      // [kGroup][H*W]
 };
 
 // Batch sorted by (group, tile): bin b of group g is [bin_off[g*nb+b], bin_off[g*nb+b+1]).
@@ -87,11 +67,6 @@ struct Sorted {
     int32_t *bin_count;  // [n_bins]
     int32_t *rel;        // [n_slices * nb] slice's offset inside each bin it touches
     int64_t *bin_off;    // [n_bins + 1]
-    int32_t *n_items;    // [n_bins] work items per bin
-    int64_t *item_off;   // [n_bins + 1]
-    uint4 *items;        // [n_groups][max_items] {tile, first event, end event, -}
-    int32_t *grp_items;  // [n_groups] work items per group
-    int max_items;       // per-group stride of items
 };
 
 __constant__ int8_t c3dy[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -111,6 +86,11 @@ __device__ __forceinline__ int tile_of(uint32_t v, const CornerGeom &g) {
 
 __device__ __forceinline__ uint32_t tile_key(uint32_t v, uint32_t e_local) {
     return (e_local << 8) | (uint32_t)((ecc::xy_y(v) % kTile) * kTile + ecc::xy_x(v) % kTile);
+}
+
+__device__ __forceinline__ void tile_origin(const CornerGeom &g, int tile, int &x0, int &y0) {
+    x0 = (tile % g.tiles_x) * kTile;
+    y0 = (tile / g.tiles_x) * kTile;
 }
 
 // The group's events span < 2^32 - 1 ticks: t - t(first event) fits a u32 (+1 still fits).
@@ -272,133 +252,166 @@ bin_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ 
     }
 }
 
-// 3a. Work items of the arc test: ceil(count / kItemEvents) per in-sensor bin.
-__global__ void __launch_bounds__(kThreads)
-item_count_kernel(CornerGeom g, Sorted so, int64_t n_bins) {
-    const int64_t gb = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (gb >= n_bins) return;
-    const int b = (int)(gb % (g.n_tiles + 1));
-    so.n_items[gb] = (b == g.n_tiles) ? 0 : (so.bin_count[gb] + kItemEvents - 1) / kItemEvents;
-}
+// Group time reference: L = t_last(group) - (2^27 - 1).  In a narrow group (span < 2^27 - 1
+// ticks) every value v of the group maps exactly to v' = v - L in [1, 2^27 - 1]; in a wide group
+// the stored value is the event index within the group + 1 (the exact test gathers t).
+constexpr int kVBits = 27;
+constexpr uint32_t kVMax = (1u << kVBits) - 1u;
 
-__device__ __forceinline__ int64_t i1_of(int64_t i0, int64_t b1) {
-    return (i0 + kItemEvents < b1) ? i0 + kItemEvents : b1;
-}
-
-__global__ void __launch_bounds__(kThreads)
-item_fill_kernel(CornerGeom g, Sorted so, int64_t n_bins) {
-    const int64_t gb = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (gb >= n_bins) return;
-    const int nb = g.n_tiles + 1;
-    const int64_t grp = gb / nb;
-    const uint32_t b = (uint32_t)(gb % nb);
-    const int m = so.n_items[gb];
-    const int64_t first = so.item_off[grp * nb];
-    const int64_t o = so.item_off[gb] - first;
-    const int64_t b0 = so.bin_off[gb], b1 = so.bin_off[gb + 1];
-    for (int c = 0; c < m; ++c) {
-        const int64_t i0 = b0 + (int64_t)c * kItemEvents;
-        so.items[grp * so.max_items + o + c] = make_uint4(b, (uint32_t)i0, (uint32_t)(i1_of(i0, b1)), 0u);
-    }
-    if (b == (uint32_t)(nb - 1)) so.grp_items[grp] = (int32_t)(so.item_off[gb + 1] - first);
-}
-
-__device__ __forceinline__ void tile_origin(const CornerGeom &g, int tile, int &x0, int &y0) {
-    x0 = (tile % g.tiles_x) * kTile;
-    y0 = (tile / g.tiles_x) * kTile;
-}
-
-// 3. Build group `grp` for one tile: fold group grp-1 (set `prv`) into B_out = fold(B_in) for
-// the tile's pixels (dense; grp > 0), then accumulate mask/M of the tile's bin and store them
-// into set `cur`.  The LDS keeps a u32 per (slice, pixel): the max group-relative timestamp + 1
-// (narrow groups, from the sorted t32), else the max event index + 1 — timestamps are
-// non-decreasing, so the last event carries the max t, gathered once per set pair at the end.
-struct BuildLds {
-    uint32_t mlast[kGroup][kTilePix];  // value + 1 (0 = none), 24.5 KiB
-    uint32_t mask_l[kTilePix];
+struct GroupRef {
+    int64_t first, t_first, Lt;
+    bool narrow;
+    uint32_t dlt;  // t32 + dlt = t - Lt (narrow)
 };
 
-__device__ __forceinline__ void build_tile(const int64_t *__restrict__ t, const CornerGeom &g, int64_t grp,
-                                           int tile, const Sorted &so,
-                                           const GroupBufs &cur, const GroupBufs &prv,
-                                           const int64_t *__restrict__ B_in, int64_t *__restrict__ B_out,
-                                           BuildLds &L) {
-    constexpr int kHalves = 2;  // 2 lanes per pixel (lanes >= 2 * kTilePix only load events)
-    static_assert(kArcThreads >= kHalves * kTilePix, "build lanes");
-    constexpr int kPlanes = kGroup / kHalves;
-    const int tid = threadIdx.x;
-    const int p = tid % kTilePix, part = tid / kTilePix;
-    const bool pix_lane = part < kHalves;  // lanes beyond 2 x 256 only help with the events
-    int x0, y0;
-    tile_origin(g, tile, x0, y0);
-    const int px = x0 + p % kTile, py = y0 + p / kTile;
-    const bool own = pix_lane && px < g.W && py < g.H;
-    const int64_t HW = (int64_t)g.H * g.W;
-    const int64_t q = (int64_t)py * g.W + px;
-    if (part == 0) {
-        if (own && grp > 0) {
-            const uint32_t mk = prv.mask[q];
-            B_out[q] = mk ? prv.M[(int64_t)(31 - __clz(mk)) * HW + q] : B_in[q];
-        }
-        L.mask_l[p] = 0u;
+__device__ __forceinline__ GroupRef group_ref(const int64_t *__restrict__ t, const CornerGeom &g, int64_t grp) {
+    GroupRef r;
+    r.first = grp * kGroup * (int64_t)g.S;
+    const int64_t end = (grp + 1) * kGroup * (int64_t)g.S;
+    r.t_first = t[r.first];
+    r.Lt = t[(end < g.n ? end : g.n) - 1] - (int64_t)kVMax;
+    r.narrow = (r.Lt + (int64_t)kVMax) - r.t_first < (int64_t)kVMax;
+    r.dlt = r.narrow ? (uint32_t)(r.t_first - r.Lt) : 0u;
+    return r;
+}
+
+// Sub-regions of a tile: rows/cols {0-3, 4-9, 10-13} -> r = ry * 3 + rx.  A neighbouring tile's
+// window reaches only the 4-pixel strips facing it, so the entries of each tile are stored in
+// sub-region order and a window reads exactly the sub-regions it covers.
+constexpr int kSub = 9;
+__host__ __device__ constexpr int sub_band(int c) { return c < kHalo ? 0 : (c < kTile - kHalo ? 1 : 2); }
+__host__ __device__ constexpr int sub_of(int lp) { return sub_band(lp / kTile) * 3 + sub_band(lp % kTile); }
+
+// Tile pixels in (sub-region, pixel) order.
+struct SubOrder {
+    uint8_t pix[kTilePix];
+    uint8_t end[kSub];  // exclusive end of each sub-region in pix[]
+};
+constexpr SubOrder make_sub_order() {
+    SubOrder o{};
+    int k = 0;
+    for (int r = 0; r < kSub; ++r) {
+        for (int lp = 0; lp < kTilePix; ++lp)
+            if (sub_of(lp) == r) o.pix[k++] = (uint8_t)lp;
+        o.end[r] = (uint8_t)k;
     }
-    if (pix_lane) {
-#pragma unroll
-        for (int jj = 0; jj < kPlanes; ++jj) L.mlast[part * kPlanes + jj][p] = 0u;
+    return o;
+}
+__constant__ SubOrder c_sub = make_sub_order();
+
+// 3. Per (group, tile): the distinct (slice, pixel) pairs the tile's events touch, each with the
+// value an arc test reads there (max over the slice's events at the pixel: v' or index + 1),
+// written as entries {j << 8 | pixel, value} in sub-region order at the bin's own offsets (a
+// bin holds at least as many events as pairs), with the sub-region ends in sub_end[bin][9].
+// Also the slices that touched each pixel (gmask) and its last timestamp (glast).
+struct PairEntry {
+    uint32_t meta;  // j << 8 | pixel in tile
+    uint32_t v;
+};
+
+__global__ void __launch_bounds__(kThreads)
+pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEntry *__restrict__ entries,
+                  int32_t *__restrict__ sub_end, uint32_t *__restrict__ gmask, int64_t *__restrict__ glast) {
+    __shared__ uint32_t tab[kGroup][kTilePix];  // 24.5 KiB
+    __shared__ int32_t wtot[kThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t grp = blockIdx.x / g.n_tiles;
+    const int tile = (int)(blockIdx.x % g.n_tiles);
+    {
+        uint4 *z = reinterpret_cast<uint4 *>(&tab[0][0]);
+        for (int i = tid; i < (int)(sizeof(tab) / 16); i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
     }
-    __syncthreads();
+    const GroupRef gr = group_ref(t, g, grp);
     const int nb = g.n_tiles + 1;
-    const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
-    int64_t t_first;
-    const bool narrow = group_narrow(t, g, grp, &t_first);  // uniform
-    for (int64_t i0 = b0; i0 < b1; i0 += kBuildUnroll * kArcThreads) {
-        uint32_t k[kBuildUnroll], tv32[kBuildUnroll];
+    const int64_t bin = grp * nb + tile;
+    const int64_t b0 = so.bin_off[bin], b1 = so.bin_off[bin + 1];
+    __syncthreads();
+    for (int64_t i0 = b0; i0 < b1; i0 += kBuildUnroll * kThreads) {
+        uint32_t k[kBuildUnroll], tv[kBuildUnroll];
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u) {
-            const int64_t i = i0 + u * kArcThreads + tid;
+            const int64_t i = i0 + u * kThreads + tid;
             k[u] = (i < b1) ? so.key[i] : 0xffffffffu;
-            tv32[u] = (i < b1 && narrow) ? so.t32[i] : 0u;
+            tv[u] = (i < b1 && gr.narrow) ? so.t32[i] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u) {
             if (k[u] == 0xffffffffu) continue;
-            const int lp = (int)(k[u] & 255u);
-            const int j = slice_in_group(k[u] >> 8, g);
-            atomicOr(&L.mask_l[lp], 1u << j);
-            atomicMax(&L.mlast[j][lp], (narrow ? tv32[u] : (k[u] >> 8)) + 1u);
+            const uint32_t el = k[u] >> 8;
+            atomicMax(&tab[slice_in_group(el, g)][k[u] & 255u], gr.narrow ? tv[u] + gr.dlt : el + 1u);
         }
     }
     __syncthreads();
-    if (own) {
-        const uint32_t mk_all = L.mask_l[p];
-        if (part == 0) cur.mask[q] = mk_all;
-        const int64_t grp_first = grp * kGroup * (int64_t)g.S;
-        int64_t tv[kPlanes];  // all gathers in flight, then the stores
+    // lane k owns pixel c_sub.pix[k]: slice mask, entry count, exclusive prefix in sub-region order
+    const int lp = tid < kTilePix ? c_sub.pix[tid] : 0;
+    uint32_t m = 0u;
+    if (tid < kTilePix) {
 #pragma unroll
-        for (int jj = 0; jj < kPlanes; ++jj) {
-            const int j = part * kPlanes + jj;
-            const uint32_t m = L.mlast[j][p] - 1u;
-            tv[jj] = !((mk_all >> j) & 1u) ? 0 : narrow ? t_first + (int64_t)m : t[grp_first + m];
-        }
+        for (int j = 0; j < kGroup; ++j) m |= (tab[j][lp] != 0u ? 1u : 0u) << j;
+    }
+    const int cnt = __popc(m);
+    int incl = cnt;
 #pragma unroll
-        for (int jj = 0; jj < kPlanes; ++jj) {
-            const int j = part * kPlanes + jj;
-            if ((mk_all >> j) & 1u) cur.M[(int64_t)j * HW + q] = tv[jj];
-        }
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    int off = incl - cnt;
+    for (int w = 0; w < wave; ++w) off += wtot[w];
+    if (tid >= kTilePix) return;
+    for (int r = 0; r < kSub; ++r)
+        if (tid + 1 == c_sub.end[r]) sub_end[bin * kSub + r] = off + cnt;
+    PairEntry *out = entries + b0 + off;
+    for (uint32_t mm = m; mm; mm &= mm - 1u) {
+        const int j = __ffs(mm) - 1;
+        *out++ = PairEntry{(uint32_t)(j << 8 | lp), tab[j][lp]};
+    }
+    int x0, y0;
+    tile_origin(g, tile, x0, y0);
+    const int px = x0 + lp % kTile, py = y0 + lp / kTile;
+    if (px >= g.W || py >= g.H) return;
+    const int64_t q = grp * (int64_t)g.H * g.W + (int64_t)py * g.W + px;
+    gmask[q] = m;
+    if (m) {
+        const uint32_t v = tab[31 - __clz(m)][lp];
+        glast[q] = gr.narrow ? gr.Lt + (int64_t)v : t[gr.first + v - 1u];
     }
 }
 
-// Final fold of the last group: B_out = fold(B_in) (dense; may be in place).
+// 4. Per pixel, in place over the groups: gB[g] := B_g, the SAE before group g (the caller's
+// `sae` for g = 0, then overwritten by the last event of every group that touched the pixel —
+// the reference's `sae.at(y,x) = t`, :921-923); the caller's `sae` receives the final surface.
+constexpr int kPrefixUnroll = 8;
+
 __global__ void __launch_bounds__(kThreads)
-tile_fold_kernel(CornerGeom g, GroupBufs buf, const int64_t *B_in, int64_t *B_out) {
-    int x0, y0;
-    tile_origin(g, blockIdx.x, x0, y0);
-    if (threadIdx.x >= kTilePix) return;
-    const int px = x0 + threadIdx.x % kTile, py = y0 + threadIdx.x / kTile;
-    if (px >= g.W || py >= g.H) return;
-    const int64_t q = (int64_t)py * g.W + px;
-    const uint32_t mk = buf.mask[q];
-    B_out[q] = mk ? buf.M[(int64_t)(31 - __clz(mk)) * (int64_t)g.H * g.W + q] : B_in[q];
+sae_prefix_kernel(CornerGeom g, int64_t n_groups, const uint32_t *__restrict__ gmask, int64_t *__restrict__ gB,
+                  int64_t *__restrict__ sae) {
+    const int64_t HW = (int64_t)g.H * g.W;
+    for (int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x; q < HW; q += (int64_t)gridDim.x * kThreads) {
+        int64_t run = sae[q];
+        for (int64_t g0 = 0; g0 < n_groups; g0 += kPrefixUnroll) {
+            uint32_t m[kPrefixUnroll];
+            int64_t lt[kPrefixUnroll];
+#pragma unroll
+            for (int u = 0; u < kPrefixUnroll; ++u) m[u] = (g0 + u < n_groups) ? gmask[(g0 + u) * HW + q] : 0u;
+#pragma unroll
+            for (int u = 0; u < kPrefixUnroll; ++u) lt[u] = m[u] ? gB[(g0 + u) * HW + q] : 0;
+#pragma unroll
+            for (int u = 0; u < kPrefixUnroll; ++u) {
+                if (g0 + u >= n_groups) break;
+                gB[(g0 + u) * HW + q] = run;
+                if (m[u]) run = lt[u];
+            }
+        }
+        sae[q] = run;
+    }
+}
+
+__device__ __forceinline__ void tile_origin_xy(const CornerGeom &g, int tile, int &tx, int &ty) {
+    tx = tile % g.tiles_x;
+    ty = tile / g.tiles_x;
 }
 
 template <int N, int SMIN, int SMAX>
@@ -435,9 +448,6 @@ __device__ __forceinline__ bool arc_streak(const int64_t (&v)[N]) {
 // outside the arc) has <= SMAX values above it, so it and its arc are unclamped and compare as
 // before, while a clamped k' has every unclamped value (> SMAX of them) above it in both
 // forms.  Otherwise (or when some value exceeds t_last) the exact int64 test runs.
-constexpr int kVBits = 27;
-constexpr uint32_t kVMax = (1u << kVBits) - 1u;
-
 // Batcher odd-even merge sort, descending; with compile-time padding and only the top outputs
 // used, dead compare-exchanges fold away.
 template <int N>
@@ -482,26 +492,29 @@ __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
     return ok ? 1 : 0;
 }
 
-// Staged neighbourhood of one work item: T[j][wp] = V'(window pixel wp, slice j of the group) —
-// the clamped value the arc test of an event in slice j sees — so every circle lookup is one
-// independent LDS read.  mask[] (the group mask per window pixel) serves the exact fallback.
+// Staged neighbourhood of one (group, tile) item: T[j][wp] = the value the arc test of an event
+// in slice j of the group sees at window pixel wp — v' = t - L for values set inside the group
+// (narrow groups, exact) or the clamped B_g, forward-filled along j; in wide groups the index + 1
+// of the last event (timestamps gathered by the exact test).  mask[wp]: the slices of the group
+// that touched wp (the exact test needs it to tell group values from B_g).
+constexpr int kPairWords = kGroup * kTilePix / 32;  // 196: one bit per (slice, tile pixel)
+
 struct ArcLds {
-    uint32_t T[kGroup][kWinPix];  // 60.5 KiB
-    union {
-        uint32_t mask[kWinPix];  // staging: group mask per window pixel
-        struct {                 // tests: bit j*256 + pixel-in-tile
-            uint32_t pairs[kGroup * kTilePix / 32];  // (slice, pixel) pairs with an eligible event
-            uint32_t res[kGroup * kTilePix / 32];    // ... that are corners
-        } bits;
-    } u;
-    uint16_t word_off[kGroup * kTilePix / 32];  // exclusive prefix of popc(pairs)
-    uint16_t q4[kItemEvents];                    // pairs that passed circle 3
+    uint32_t T[kGroup][kWinPix];          // 60.5 KiB
+    uint32_t mask[kWinPix];
+    uint32_t pairs[kPairWords];           // (slice, pixel) pairs with an eligible event
+    uint32_t res[kPairWords];             // ... that are corners
+    uint16_t word_off[kPairWords];        // exclusive prefix of popc(pairs)
+    uint16_t q4[kGroup * kTilePix];       // pairs that passed circle 3
     int64_t wave_min[kArcThreads / 64];
     int32_t wave_tot[kArcThreads / 64];
     int32_t exact_only;  // a value above t_last: clamped keys unusable
     int32_t mixed;       // clamped values not all equal to the window minimum of B
     int32_t q4n;
     int32_t n_tasks;
+    int64_t seg_lo[16];   // window segments: first entry (absolute) ...
+    int32_t seg_pref[16]; // ... exclusive prefix of their lengths ...
+    int32_t seg_off[16];  // ... and the window offset of the neighbour tile's origin
 };
 
 __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, int32_t *exact_flag,
@@ -515,112 +528,155 @@ __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, 
     return (uint32_t)d;
 }
 
-// Exact int64 V(q_k, j) of N circle pixels from the global images in two dependent levels:
-// all masks, then one selected address per pixel (no branch between a mask and its load).
+// Exact int64 arc test of one circle around window pixel wp0 (global pixel q0) for slice j:
+// V = the group value (from T: v' + L, or the timestamp of the stored event index) where a slice
+// <= j of the group touched the pixel, else B_g.  Rare fallback; out of line so its registers do
+// not raise the pressure of the main kernel body.
+struct ExactCtx {
+    const int64_t *Bg;  // B_g image of the group
+    const int64_t *t;
+    int64_t grp_first, Lt;
+    int W;
+    bool narrow;
+};
+
 template <int N>
-__device__ __forceinline__ void sae_gather(int64_t q0, const int8_t *dy, const int8_t *dx, int W, uint32_t below,
-                                           const GroupBufs &cur, const int64_t *__restrict__ B, int64_t HW,
-                                           int64_t (&v)[N]) {
-    uint32_t mk[N];
-#pragma unroll
-    for (int k = 0; k < N; ++k) mk[k] = cur.mask[q0 + (int64_t)dy[k] * W + dx[k]] & below;
+__device__ __forceinline__ void exact_values(const ArcLds *L, int wp0, int64_t q0, uint32_t below, int j,
+                                             const int8_t *dy, const int8_t *dx, const ExactCtx &c, int64_t (&v)[N]) {
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        const int64_t q = q0 + (int64_t)dy[k] * W + dx[k];
-        const int64_t *p = mk[k] ? cur.M + (int64_t)(31 - __clz(mk[k])) * HW + q : B + q;
-        v[k] = *p;
+        const int wp = wp0 + dy[k] * kWin + dx[k];
+        const uint32_t tv = L->T[j][wp];
+        v[k] = !(L->mask[wp] & below) ? c.Bg[q0 + (int64_t)dy[k] * c.W + dx[k]]
+               : c.narrow            ? c.Lt + (int64_t)tv
+                                     : c.t[c.grp_first + tv - 1u];
     }
 }
 
-// Exact int64 arc test of one circle from the global images (rare fallback; out of line so its
-// registers do not raise the pressure of the main kernel body).
-__device__ __noinline__ bool exact_circle_test(int x, int y, int j, bool c3, int W, const GroupBufs cur,
-                                               const int64_t *__restrict__ B, int64_t HW) {
+__device__ __noinline__ bool exact_circle_test(const ArcLds *L, int wp0, int64_t q0, int j, bool c3, const ExactCtx c) {
     const uint32_t below = (j == 31) ? 0xffffffffu : ((2u << j) - 1u);
-    const int64_t q0 = (int64_t)y * W + x;
     if (c3) {
         int64_t v3[16];
-        sae_gather<16>(q0, c3dy, c3dx, W, below, cur, B, HW, v3);
+        exact_values<16>(L, wp0, q0, below, j, c3dy, c3dx, c, v3);
         return arc_streak<16, 3, 6>(v3);
     }
     int64_t v4[20];
-    sae_gather<20>(q0, c4dy, c4dx, W, below, cur, B, HW, v4);
+    exact_values<20>(L, wp0, q0, below, j, c4dy, c4dx, c, v4);
     return arc_streak<20, 4, 8>(v4);
 }
 
-// 4. Arc test of one work item (<= kItemEvents tile-sorted events of group `grp`).
-#define ARC_STAMP(k)                                                                              \
-    do {                                                                                          \
-        if (ECC_CORNER_PROFILE && g.ts && grp == g.ts_grp && threadIdx.x == 0)                    \
-            g.ts[(size_t)item_idx * 16 + 4 + (k)] = __builtin_amdgcn_s_memrealtime();             \
-    } while (0)
-__device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const CornerGeom &g, int64_t grp,
-                                         int item_idx, const Sorted &so, const GroupBufs &cur,
-                                         const int64_t *__restrict__ B, const int32_t *__restrict__ first_border,
-                                         uint8_t *__restrict__ flags, ArcLds &L) {
-    const uint4 rec = so.items[grp * so.max_items + item_idx];  // one load resolves the item
-    if (item_idx >= so.grp_items[grp]) return;
-    const int tile = (int)rec.x;
-    const int64_t i0 = rec.y, i1 = rec.z;
+// 5. Arc test of one (group, tile) item, all items of all groups in one launch.  The item's
+// corner pairs go to res[item][kPairWords] (bit j*196 + pixel); flags_kernel applies them.
+constexpr int kStageUnroll = 8;
+
+// Window segments: the sub-regions of the 3x3 tiles around the item's tile that its window
+// covers (own tile: all; edge neighbours: the 3 facing sub-regions; corners: 1) — 13 at most.
+constexpr int kMaxSeg = 13;
+
+__global__ void __launch_bounds__(kArcThreads, 2)  // two 8-wave workgroups per CU (LDS)
+arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, Sorted so,
+           const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
+           const int64_t *__restrict__ gB, uint32_t *__restrict__ res) {
+    __shared__ ArcLds L;
+    // XCD-aware order: workgroup b runs on XCD b % 8, so XCD x takes the contiguous item range
+    // [x * per, (x + 1) * per) — neighbouring tiles of one group share that XCD's L2.
+    const int64_t per = gridDim.x / 8;
+    const int64_t item = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (item >= n_items) return;
+    const int64_t grp = item / g.n_tiles;
+    const int tile = (int)(item % g.n_tiles);
+    if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
+    const int nb = g.n_tiles + 1;
+    if (so.bin_off[grp * nb + tile] == so.bin_off[grp * nb + tile + 1]) return;  // no events to flag
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t HW = (int64_t)g.H * g.W;
-    int x0, y0;
-    tile_origin(g, tile, x0, y0);
+    int tx, ty;
+    tile_origin_xy(g, tile, tx, ty);
+    const int x0 = tx * kTile, y0 = ty * kTile;
     const int wx0 = x0 - kHalo, wy0 = y0 - kHalo;
-    const int64_t grp_first = grp * kGroup * (int64_t)g.S;
-    const int64_t grp_end = (grp + 1) * kGroup * (int64_t)g.S;
-    const int64_t Lt = t[(grp_end < g.n ? grp_end : g.n) - 1] - (int64_t)kVMax;
-    if (ECC_CORNER_PROFILE && (g.dbg & 4)) return;
-    if (i1 - i0 < kStageMinEvents) {
-        // small item (sparse tile): staging 576 pixels would cost more than the events — exact
-        // int64 test straight from the global images, one event per lane
-        for (int64_t i = i0 + tid; i < i1; i += kArcThreads) {
-            const uint32_t key = so.key[i];
-            const int lp = (int)(key & 255u);
-            const uint32_t el = key >> 8;
-            const int x = x0 + lp % kTile, y = y0 + lp / kTile;
-            const int j = slice_in_group(el, g);
-            const int64_t s = grp * kGroup + j;
-            bool test = s >= g.first_detect && !is_border(x, y, g);
-            if (test && g.border_mode == 1) test = (int64_t)el - (int64_t)j * g.S < first_border[s];
-            if (!test) continue;
-            if (exact_circle_test(x, y, j, true, g.W, cur, B, HW) && exact_circle_test(x, y, j, false, g.W, cur, B, HW))
-                flags[grp_first + el] = 1;
-        }
-        return;
-    }
-    if (tid == 0) {
-        L.exact_only = 0;
-        L.mixed = 0;
-    }
+    const GroupRef gr = group_ref(t, g, grp);
+    const int64_t grp_first = gr.first, Lt = gr.Lt;
+    const bool narrow = gr.narrow;
+    const int64_t *Bg = gB + grp * HW;
 
-    // keys of the item (preloaded; the loads overlap the staging)
-    constexpr int kPerLane = (kItemEvents + kArcThreads - 1) / kArcThreads;
-    uint32_t keys[kPerLane];
-#pragma unroll
-    for (int u = 0; u < kPerLane; ++u) {
-        const int64_t i = i0 + tid + (int64_t)u * kArcThreads;
-        keys[u] = (i < i1) ? so.key[i] : 0xffffffffu;
-    }
-    // (a) one lane per window pixel: its group mask and B, then the low 32 bits of its set M
-    //     planes, issued before the barrier.  When the group spans < 2^27 ticks every M lies in
-    //     (Lt, t_last], so M' = M - Lt is exact from the low words.  (Loading all 32 planes
-    //     without waiting for the mask was measured slower: ~73 KB of extra L2 traffic per item.)
+    // (a) the window pixel's B_g (issued first; lane wp < 484), zeroed LDS
     static_assert(kArcThreads >= kWinPix, "one lane per window pixel");
     const int wp = tid;
     const bool win_lane = wp < kWinPix;
     const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
     const bool in = win_lane && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
-    const int64_t qq = (int64_t)wy * g.W + wx;
-    const uint32_t mk = in ? cur.mask[qq] : 0u;
-    const int64_t bq = in ? B[qq] : INT64_MAX;  // INT64_MAX: outside the sensor (never read)
-    uint32_t v[kGroup];
-    {  // only the planes whose mask bit is set (issued before the barrier below)
-        const uint32_t *M32 = reinterpret_cast<const uint32_t *>(cur.M + (in ? qq : 0));
-#pragma unroll
-        for (int j = 0; j < kGroup; ++j) v[j] = ((mk >> j) & 1u) ? M32[(int64_t)j * HW * 2] : 0u;
+    const int64_t bq = in ? Bg[(int64_t)wy * g.W + wx] : INT64_MAX;  // INT64_MAX: outside (never read)
+    {
+        uint4 *z = reinterpret_cast<uint4 *>(&L.T[0][0]);
+        for (int i = tid; i < (int)(sizeof(L.T) / 16); i += kArcThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (int w = tid; w < 2 * kPairWords; w += kArcThreads) (&L.pairs[0])[w] = 0u;  // pairs + res
+        if (tid == 0) {
+            L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
+            L.mixed = 0;
+            L.q4n = 0;
+        }
     }
-    if (win_lane) L.u.mask[wp] = mk;
+    // segments (lanes 0..12): absolute entry range + the window offset of the neighbour tile
+    if (tid < kMaxSeg) {
+        // own tile: every sub-region; above/below: their facing rows; corners: one sub-region;
+        // left/right: their facing columns (3 sub-regions, one segment each)
+        constexpr int8_t sx[kMaxSeg] = {0, 0, 0, -1, 1, -1, 1, -1, 1, -1, 1, -1, 1};
+        constexpr int8_t sy[kMaxSeg] = {0, -1, 1, -1, -1, 1, 1, 0, 0, 0, 0, 0, 0};
+        constexpr int8_t r0[kMaxSeg] = {0, 6, 0, 8, 6, 2, 0, 2, 0, 5, 3, 8, 6};
+        constexpr int8_t r1[kMaxSeg] = {8, 8, 2, 8, 6, 2, 0, 2, 0, 5, 3, 8, 6};
+        const int nx = tx + sx[tid], ny = ty + sy[tid];
+        int64_t b0 = 0;
+        int len = 0;
+        if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
+            const int64_t bi = grp * nb + (int64_t)ny * g.tiles_x + nx;
+            const int s0 = r0[tid] ? sub_end[bi * kSub + r0[tid] - 1] : 0;
+            b0 = so.bin_off[bi] + s0;
+            len = sub_end[bi * kSub + r1[tid]] - s0;
+        }
+        int incl = len;  // prefix over lanes 0..12 of wave 0
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const int v = __shfl_up(incl, o, 16);
+            if (tid >= o) incl += v;
+        }
+        L.seg_lo[tid] = b0;
+        L.seg_pref[tid + 1] = incl;
+        L.seg_off[tid] = (sy[tid] * kTile) * kWin + sx[tid] * kTile + kHalo * kWin + kHalo;
+        if (tid == 0) L.seg_pref[0] = 0;
+    }
+    __syncthreads();
+    const int total = L.seg_pref[kMaxSeg];
+    int pref[kMaxSeg + 1];
+#pragma unroll
+    for (int c = 0; c <= kMaxSeg; ++c) pref[c] = L.seg_pref[c];  // uniform (SGPRs)
+
+    // (b) each entry is a distinct (slice, pixel) pair of one tile: plain LDS stores of its value;
+    //     the own tile's pairs (segment 0) are the test candidates when the pixel and slice are
+    //     eligible (the per-event cut of border mode 1 is applied when flagging)
+    for (int i0 = 0; i0 < total; i0 += kStageUnroll * kArcThreads) {
+        PairEntry ent[kStageUnroll];
+        int sg[kStageUnroll];
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; ++u) {
+            const int i = i0 + u * kArcThreads + tid;
+            int r = 0;
+#pragma unroll
+            for (int c = 1; c < kMaxSeg; ++c) r += (i >= pref[c]) ? 1 : 0;
+            sg[u] = (i < total) ? r : -1;
+            ent[u] = (i < total) ? entries[L.seg_lo[r] + (i - L.seg_pref[r])] : PairEntry{0u, 0u};
+        }
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; ++u) {
+            if (sg[u] < 0) continue;
+            const int lp = (int)(ent[u].meta & 255u), j = (int)(ent[u].meta >> 8);
+            L.T[j][L.seg_off[sg[u]] + (lp / kTile) * kWin + lp % kTile] = ent[u].v;
+            if (sg[u] == 0 && (int64_t)grp * kGroup + j >= g.first_detect &&
+                !is_border(x0 + lp % kTile, y0 + lp / kTile, g)) {
+                const uint32_t pi = (uint32_t)(j * kTilePix + lp);
+                atomicOr(&L.pairs[pi >> 5], 1u << (pi & 31u));
+            }
+        }
+    }
     int64_t bmin = bq;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -629,64 +685,27 @@ __device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const Co
     }
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
-    int64_t vz = INT64_MAX;
+
+    // (c) forward fill along j: T[j] = (set) ? T[j] : T[j-1], T[-1] = clamped B_g; a (slice, pixel)
+    //     value is set iff nonzero (values are >= 1), which also yields the pixel's slice mask
+    if (win_lane) {
+        int64_t vz = INT64_MAX;
 #pragma unroll
-    for (int w = 0; w < kArcThreads / 64; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
-    ARC_STAMP(0);
-    if (ECC_CORNER_PROFILE && (g.dbg & 2)) return;
-    // (b) forward fill along j in registers: T[j] = bit j set ? M'_j : T[j-1], T[-1] = B'
-    const int64_t t_first = t[grp_first];
-    const bool narrow = (Lt + (int64_t)kVMax) - t_first < (int64_t)kVMax;  // uniform
-    uint32_t cur_v = (bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
-    if (!win_lane) {
-    } else if (narrow) {
-        const uint32_t lt32 = (uint32_t)Lt;
+        for (int w = 0; w < kArcThreads / 64; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
+        uint32_t cur_v = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
+        uint32_t mk = 0u;
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
-            cur_v = ((mk >> j) & 1u) ? v[j] - lt32 : cur_v;
+            const uint32_t v = L.T[j][wp];
+            mk |= (v != 0u ? 1u : 0u) << j;
+            cur_v = v ? v : cur_v;
             L.T[j][wp] = cur_v;
         }
-    } else {
-#pragma unroll 4
-        for (int j = 0; j < kGroup; ++j) {
-            if ((mk >> j) & 1u) cur_v = clamp_rel(cur.M[(int64_t)j * HW + qq], Lt, vz, &L.exact_only, &L.mixed);
-            L.T[j][wp] = cur_v;
-        }
+        L.mask[wp] = mk;
     }
-    __syncthreads();
-    const bool fast = !L.exact_only;
-    ARC_STAMP(1);
-    if (ECC_CORNER_PROFILE && (g.dbg & 1)) return;
-    const bool ties_exact = !L.mixed;
-    // (d) the test depends only on (slice j, pixel): eligible events mark their pair in a bitmap,
-    //     each distinct pair is tested once (one per lane; ~2.5x fewer tests than events on
-    //     dense tiles), circle-3 survivors are queued so circle 4 runs densely, and every event
-    //     finally reads its pair's result.  Eligibility (first slice, border, the border-mode-1
-    //     cut at the slice's first border event) stays per event.
-    constexpr int kPairWords = kGroup * kTilePix / 32;  // 196
-    for (int w = tid; w < 2 * kPairWords; w += kArcThreads) (&L.u.bits.pairs[0])[w] = 0u;
-    if (tid == 0) L.q4n = 0;
-    __syncthreads();
-    uint32_t pidx[kPerLane];
-#pragma unroll
-    for (int u = 0; u < kPerLane; ++u) {
-        pidx[u] = 0xffffffffu;
-        const uint32_t key = keys[u];
-        if (key == 0xffffffffu) continue;
-        const int lp = (int)(key & 255u);
-        const uint32_t el = key >> 8;
-        const int j = slice_in_group(el, g);
-        const int64_t s = grp * kGroup + j;
-        bool test = s >= g.first_detect && !is_border(x0 + lp % kTile, y0 + lp / kTile, g);
-        if (test && g.border_mode == 1) test = (int64_t)el - (int64_t)j * g.S < first_border[s];
-        if (!test) continue;
-        pidx[u] = (uint32_t)(j * kTilePix + lp);
-        atomicOr(&L.u.bits.pairs[pidx[u] >> 5], 1u << (pidx[u] & 31u));
-    }
-    __syncthreads();
     int wcnt = 0, wincl = 0;
     if (tid < kPairWords) {  // exclusive prefix of the words' popcounts (waves 0-3)
-        wcnt = __popc(L.u.bits.pairs[tid]);
+        wcnt = __popc(L.pairs[tid]);
         wincl = wcnt;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -703,47 +722,47 @@ __device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const Co
         if (tid == kPairWords - 1) L.n_tasks = before + wincl;
     }
     __syncthreads();
+    // (d) each distinct pair is tested once; circle-3 survivors are queued so circle 4 runs densely
     const int n_tasks = L.n_tasks;
-    ARC_STAMP(2);
+    const bool fast = !L.exact_only;
+    const bool ties_exact = !L.mixed;
+    const ExactCtx ec{Bg, t, grp_first, Lt, g.W, narrow};
     auto task_pair = [&](int ti) {  // ti-th set bit of the pair bitmap
-        int lo = 0, hi = kPairWords;
+        int lo_w = 0, hi_w = kPairWords;
 #pragma unroll
         for (int step = 0; step < 8; ++step) {  // 2^8 >= kPairWords
-            const int mid = (lo + hi) >> 1;
-            if ((int)L.word_off[mid] <= ti) lo = mid; else hi = mid;
+            const int mid = (lo_w + hi_w) >> 1;
+            if ((int)L.word_off[mid] <= ti) lo_w = mid; else hi_w = mid;
         }
-        uint32_t m = L.u.bits.pairs[lo];
-        for (int r = ti - (int)L.word_off[lo]; r > 0; --r) m &= m - 1;
-        return lo * 32 + (__ffs(m) - 1);
-    };
-    auto exact_circle = [&](int x, int y, int j, bool c3) {
-        return exact_circle_test(x, y, j, c3, g.W, cur, B, HW);
+        uint32_t m = L.pairs[lo_w];
+        for (int r = ti - (int)L.word_off[lo_w]; r > 0; --r) m &= m - 1;
+        return lo_w * 32 + (__ffs(m) - 1);
     };
     for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
         const int pi = task_pair(ti);
         const int j = pi / kTilePix, lp = pi % kTilePix;
-        const int x = x0 + lp % kTile, y = y0 + lp / kTile;
-        const int wp0 = (y - wy0) * kWin + (x - wx0);
-        int res = -1;
+        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        int r3 = -1;
         if (fast) {
             const uint32_t *Tj = L.T[j];
             uint32_t k3[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) k3[k] = (Tj[wp0 + c3dy[k] * kWin + c3dx[k]] << 4) | k;
-            res = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+            r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
         }
-        if (res < 0) res = exact_circle(x, y, j, true) ? 1 : 0;
-        if (res == 1) L.q4[atomicAdd(&L.q4n, 1)] = (uint16_t)pi;
+        if (r3 < 0) {
+            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
+            r3 = exact_circle_test(&L, wp0, q0, j, true, ec) ? 1 : 0;
+        }
+        if (r3 == 1) L.q4[atomicAdd(&L.q4n, 1)] = (uint16_t)pi;
     }
     __syncthreads();
     const int n4 = L.q4n;
-    ARC_STAMP(3);
     for (int qi = tid; qi < n4; qi += kArcThreads) {
         const int pi = L.q4[qi];
         const int j = pi / kTilePix, lp = pi % kTilePix;
-        const int x = x0 + lp % kTile, y = y0 + lp / kTile;
-        const int wp0 = (y - wy0) * kWin + (x - wx0);
-        int res = -1;
+        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        int r4 = -1;
         if (fast) {
             const uint32_t *Tj = L.T[j];
             uint32_t k4[32];
@@ -751,50 +770,54 @@ __device__ __forceinline__ void arc_item(const int64_t *__restrict__ t, const Co
             for (int k = 0; k < 20; ++k) k4[k] = (Tj[wp0 + c4dy[k] * kWin + c4dx[k]] << 5) | k;
 #pragma unroll
             for (int k = 20; k < 32; ++k) k4[k] = 0u;
-            res = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
+            r4 = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
         }
-        if (res < 0) res = exact_circle(x, y, j, false) ? 1 : 0;
-        if (res == 1) atomicOr(&L.u.bits.res[pi >> 5], 1u << (pi & 31));
+        if (r4 < 0) {
+            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
+            r4 = exact_circle_test(&L, wp0, q0, j, false, ec) ? 1 : 0;
+        }
+        if (r4 == 1) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
     }
     __syncthreads();
-    ARC_STAMP(4);
-#pragma unroll
-    for (int u = 0; u < kPerLane; ++u)
-        if (pidx[u] != 0xffffffffu && ((L.u.bits.res[pidx[u] >> 5] >> (pidx[u] & 31u)) & 1u))
-            flags[grp_first + (keys[u] >> 8)] = 1;
+    if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
 }
 
-// One launch per group g: workgroups [0, n_arc) test the work items of group g, the rest build
-// group g+1 (one tile each).  Both read set g&1; the build writes set (g+1)&1 and
-// B_{g+1} = fold(B_g) into the other B buffer, so nothing the arc test reads changes under it.
-union GroupLds {
-    ArcLds arc;
-    BuildLds build;
-};
-
-__global__ void __launch_bounds__(kArcThreads, 4)  // two 8-wave workgroups per CU
-group_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t grp, int n_arc, Sorted so,
-             GroupBufs cur, GroupBufs nxt, const int64_t *B_in, int64_t *B_out,
+// 6. Corner flags: per (group, tile) item, its events (sorted keys, coalesced) look up their
+// pair's result; only corner events are stored (flags are cleared beforehand).  The per-event
+// eligibility of the reference loop is applied here: the slice's first-detect rule (Q15), the
+// border margin, and in ref_compat mode (Q11) "before the slice's first border event".
+__global__ void __launch_bounds__(kThreads)
+flags_kernel(CornerGeom g, int64_t n_items, Sorted so, const uint32_t *__restrict__ res,
              const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags) {
-    __shared__ GroupLds L;
-    const bool rec = ECC_CORNER_PROFILE && g.ts && grp == g.ts_grp && threadIdx.x == 0;
-    unsigned long long t_start = rec ? __builtin_amdgcn_s_memrealtime() : 0;
-    if ((int)blockIdx.x < n_arc) {  // long arc items first, short build workgroups fill in after
-        if (!(ECC_CORNER_PROFILE && (g.dbg & 8))) arc_item(t, g, grp, (int)blockIdx.x, so, cur, B_in, first_border, flags, L.arc);
-    } else {
-        build_tile(t, g, grp + 1, (int)blockIdx.x - n_arc, so, nxt, cur, B_in, B_out, L.build);
+    __shared__ uint32_t r_l[kPairWords];
+    const int64_t item = blockIdx.x;
+    const int64_t grp = item / g.n_tiles;
+    const int tile = (int)(item % g.n_tiles);
+    if ((grp + 1) * kGroup <= g.first_detect) return;
+    const int nb = g.n_tiles + 1;
+    const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
+    if (b0 == b1) return;
+    uint32_t any = 0u;
+    for (int w = threadIdx.x; w < kPairWords; w += kThreads) {
+        const uint32_t v = res[item * kPairWords + w];
+        r_l[w] = v;
+        any |= v;
     }
-    if (rec) {
-        unsigned int hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        unsigned int xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        g.ts[blockIdx.x * 16 + 0] = t_start;
-        g.ts[blockIdx.x * 16 + 1] = __builtin_amdgcn_s_memrealtime();
-        g.ts[blockIdx.x * 16 + 2] = ((int)blockIdx.x < n_arc && (int)blockIdx.x < so.grp_items[grp])
-                                       ? (so.items[grp * so.max_items + blockIdx.x].z - so.items[grp * so.max_items + blockIdx.x].y)
-                                       : 0xfffff;
-        g.ts[blockIdx.x * 16 + 3] = xcc;
+    if (!__syncthreads_or(any != 0u)) return;  // no corner in this item
+    int x0, y0;
+    tile_origin(g, tile, x0, y0);
+    const int64_t grp_first = grp * kGroup * (int64_t)g.S;
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += kThreads) {
+        const uint32_t key = so.key[i];
+        const int lp = (int)(key & 255u);
+        const uint32_t el = key >> 8;
+        const int j = slice_in_group(el, g);
+        const uint32_t pi = (uint32_t)(j * kTilePix + lp);
+        if (!((r_l[pi >> 5] >> (pi & 31u)) & 1u)) continue;  // a corner pair is never a border pixel
+        const int64_t s = grp * kGroup + j;
+        if (s < g.first_detect) continue;
+        if (g.border_mode == 1 && (int64_t)el - (int64_t)j * g.S >= first_border[s]) continue;
+        flags[grp_first + el] = 1;
     }
 }
 
@@ -822,13 +845,9 @@ sae_max_combine_kernel(const int64_t *__restrict__ images, int n_images, int64_t
     }
 }
 
-// Per-context corner workspace: group images (sized by the sensor) and the sorted batch with
-// its bin tables (sized by the batch; grown, never shrunk).
+// Per-context corner workspace: the sorted batch with its bin tables and the per-group images
+// (sized by batch and sensor; grown, never shrunk).
 struct CornerState {
-    int W = 0, H = 0;
-    void *img = nullptr;
-    GroupBufs set[2]{};
-    int64_t *b_alt = nullptr;  // second SAE buffer (B ping-pong with the caller's `sae`)
     void *evt = nullptr;
     size_t evt_bytes = 0;
 };
@@ -856,51 +875,34 @@ struct Carve {
     }
 };
 
-Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_bins, int32_t **first_border,
-                    int64_t **scan_scratch) {
+struct GroupImages {
+    uint32_t *mask;  // [n_groups][H*W] slices of the group that touched the pixel
+    int64_t *B;      // [n_groups][H*W] last t of the group, then (in place) B_g
+    uint32_t *res;   // [n_groups * n_tiles][kPairWords] corner (slice, pixel) pairs per item
+    PairEntry *entries;  // [n] distinct (slice, pixel) pairs per bin, at the bin's offsets
+    int32_t *sub_end;    // [n_bins][kSub] sub-region ends inside each bin's entries
+};
+
+Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_bins, int64_t n_groups, int32_t **first_border,
+                    int64_t **scan_scratch, GroupImages *gi) {
     Sorted so{};
     so.key = cv.take<uint32_t>((size_t)g.n);
     so.t32 = cv.take<uint32_t>((size_t)g.n);
     so.bin_count = cv.take<int32_t>((size_t)n_bins);
     so.rel = cv.take<int32_t>((size_t)g.n_slices * (g.n_tiles + 1));
     so.bin_off = cv.take<int64_t>((size_t)n_bins + 1);
-    so.n_items = cv.take<int32_t>((size_t)n_bins);
-    so.item_off = cv.take<int64_t>((size_t)n_bins + 1);
-    const int64_t n_groups = (g.n_slices + kGroup - 1) / kGroup;
-    so.max_items = (int)(g.n_tiles + std::min<int64_t>((int64_t)kGroup * g.S, g.n) / kItemEvents);
-    so.items = cv.take<uint4>((size_t)n_groups * so.max_items);
-    so.grp_items = cv.take<int32_t>((size_t)n_groups);
     *first_border = cv.take<int32_t>((size_t)g.n_slices);
     *scan_scratch = cv.take<int64_t>((ecc::scan_scratch_bytes(n_bins) + 7) / 8);
+    const size_t img = (size_t)n_groups * g.W * g.H;
+    gi->mask = cv.take<uint32_t>(img);
+    gi->B = cv.take<int64_t>(img);
+    gi->res = cv.take<uint32_t>((size_t)n_groups * g.n_tiles * kPairWords);
+    gi->entries = cv.take<PairEntry>((size_t)g.n);
+    gi->sub_end = cv.take<int32_t>((size_t)n_bins * kSub);
     return so;
 }
 
-int corner_state_reserve(ecc_ctx *ctx, CornerState *st, const CornerGeom &g, size_t evt_need) {
-    if (st->W != g.W || st->H != g.H || !st->img) {
-        if (st->img) {
-            ECC_CHECK_HIP(ctx, hipDeviceSynchronize(), "sync(corner images)");
-            (void)hipFree(st->img);
-            st->img = nullptr;
-        }
-        const size_t HW = (size_t)g.W * g.H;
-        const size_t mask_b = ecc::align_up(HW * 4, 256);
-        const size_t m_b = ecc::align_up(HW * 8 * kGroup, 256);
-        const size_t b_b = ecc::align_up(HW * 8, 256);
-        hipError_t e = hipMalloc(&st->img, 2 * mask_b + 2 * m_b + b_b);
-        if (e != hipSuccess) {
-            st->img = nullptr;
-            ecc::hip_fail(ctx, e, "hipMalloc(corner images)");
-            return ECC_ERR_NOMEM;
-        }
-        char *p = static_cast<char *>(st->img);
-        for (int b = 0; b < 2; ++b) {
-            st->set[b].mask = reinterpret_cast<uint32_t *>(p + b * mask_b);
-            st->set[b].M = reinterpret_cast<int64_t *>(p + 2 * mask_b + b * m_b);
-        }
-        st->b_alt = reinterpret_cast<int64_t *>(p + 2 * mask_b + 2 * m_b);
-        st->W = g.W;
-        st->H = g.H;
-    }
+int corner_state_reserve(ecc_ctx *ctx, CornerState *st, size_t evt_need) {
     if (evt_need > st->evt_bytes) {
         if (st->evt) {
             ECC_CHECK_HIP(ctx, hipDeviceSynchronize(), "sync(corner batch)");
@@ -934,7 +936,6 @@ void corner_state_release(const ecc_ctx *ctx) {
         st = it->second;
         g_states.erase(it);
     }
-    if (st->img) (void)hipFree(st->img);
     if (st->evt) (void)hipFree(st->evt);
     delete st;
 }
@@ -967,19 +968,6 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     g.H = cfg->height;
     g.S = cfg->slice_events;
     g.inv_S = 1.0f / (float)g.S;
-    g.dbg = 0;
-    g.ts = nullptr;
-    g.ts_grp = -1;
-#if ECC_CORNER_PROFILE
-    g.dbg = getenv("ECC_CORNER_DBG") ? atoi(getenv("ECC_CORNER_DBG")) : 0;
-    static unsigned long long *ts_buf = nullptr;
-    g.ts_grp = getenv("ECC_CORNER_TS") ? atoi(getenv("ECC_CORNER_TS")) : -1;
-    if (g.ts_grp >= 0) {
-        if (!ts_buf) (void)hipMalloc(&ts_buf, 1 << 20);
-        (void)hipMemset(ts_buf, 0, 1 << 20);
-        g.ts = ts_buf;
-    }
-#endif
     g.margin = cfg->margin;
     g.border_mode = cfg->border_mode;
     g.first_detect = cfg->first_detect_slice;
@@ -996,15 +984,18 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     const int nb = g.n_tiles + 1;
     const int64_t n_groups = (g.n_slices + kGroup - 1) / kGroup;
     const int64_t n_bins = n_groups * nb;
+    const int64_t n_items = n_groups * g.n_tiles;  // arc work items: (group, tile)
+    if (n_items > (int64_t)INT32_MAX - 8) return ECC_ERR_INVALID;
     CornerState *st = state_of(ctx);
     int32_t *first_border = nullptr;
     int64_t *scan_scratch = nullptr;
+    GroupImages gi{};
     Carve measure{nullptr};
-    carve_sorted(measure, g, n_bins, &first_border, &scan_scratch);
-    int rc = corner_state_reserve(ctx, st, g, measure.used);
+    carve_sorted(measure, g, n_bins, n_groups, &first_border, &scan_scratch, &gi);
+    int rc = corner_state_reserve(ctx, st, measure.used);
     if (rc) return rc;
     Carve cv{static_cast<char *>(st->evt)};
-    const Sorted so = carve_sorted(cv, g, n_bins, &first_border, &scan_scratch);
+    const Sorted so = carve_sorted(cv, g, n_bins, n_groups, &first_border, &scan_scratch, &gi);
 
     ECC_CHECK_HIP(ctx, hipMemsetAsync(corner_flags, 0, (size_t)n, s), "memset(flags)");
     ECC_CHECK_HIP(ctx, hipMemsetAsync(so.bin_count, 0, (size_t)n_bins * 4, s), "memset(bins)");
@@ -1028,50 +1019,29 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
                                xy, t, g, so);
     }
     {
-        ECC_TIMED(ctx, s, "item_count_kernel");
-        hipLaunchKernelGGL(item_count_kernel, dim3(blocks_for(n_bins, kThreads)), dim3(kThreads), 0, s, g,
-                           so, n_bins);
-    }
-    rc = ecc::exclusive_scan_i32_i64(ctx, so.n_items, n_bins, so.item_off, scan_scratch, s);
-    if (rc) return rc;
-    {
-        ECC_TIMED(ctx, s, "item_fill_kernel");
-        hipLaunchKernelGGL(item_fill_kernel, dim3(blocks_for(n_bins, kThreads)), dim3(kThreads), 0, s, g,
-                           so, n_bins);
-    }
-    // upper bound of the work items of one group: one partial item per tile + full items
-    const int64_t grp_events = std::min<int64_t>((int64_t)kGroup * g.S, n);
-    const int64_t arc_blocks = g.n_tiles + grp_events / kItemEvents;
-    if (arc_blocks > INT32_MAX) return ECC_ERR_INVALID;
-    // B_g lives in bufB[g & 1]: B_0 = the caller's sae, B_1 = b_alt, ...
-    int64_t *bufB[2] = {sae, st->b_alt};
-    {
-        ECC_TIMED(ctx, s, "group_kernel");  // build(0) only
-        hipLaunchKernelGGL(group_kernel, dim3(g.n_tiles), dim3(kArcThreads), 0, s, t, g, (int64_t)-1, 0, so, st->set[1], st->set[0], (const int64_t *)bufB[0], bufB[1], (const int32_t *)first_border,
-                           corner_flags);
-    }
-    for (int64_t gi = 0; gi < n_groups; ++gi) {
-        const int n_build = (gi + 1 < n_groups) ? g.n_tiles : 0;
-        ECC_TIMED(ctx, s, "group_kernel");
-        hipLaunchKernelGGL(group_kernel, dim3((unsigned)(n_build + arc_blocks)), dim3(kArcThreads), 0, s, t, g, gi,
-                           (int)arc_blocks, so, st->set[gi & 1], st->set[(gi + 1) & 1], (const int64_t *)bufB[gi & 1],
-                           bufB[(gi + 1) & 1], (const int32_t *)first_border, corner_flags);
+        ECC_TIMED(ctx, s, "pair_build_kernel");
+        hipLaunchKernelGGL(pair_build_kernel, dim3((unsigned)n_items), dim3(kThreads), 0, s, t, g, so, gi.entries,
+                           gi.sub_end, gi.mask, gi.B);
     }
     {
-        ECC_TIMED(ctx, s, "tile_fold_kernel");  // B_G into the caller's buffer
-        hipLaunchKernelGGL(tile_fold_kernel, dim3(g.n_tiles), dim3(kThreads), 0, s, g, st->set[(n_groups - 1) & 1],
-                           (const int64_t *)bufB[(n_groups - 1) & 1], sae);
+        ECC_TIMED(ctx, s, "sae_prefix_kernel");
+        const int64_t HW = (int64_t)g.W * g.H;
+        const unsigned blocks = (unsigned)std::min<int64_t>((HW + kThreads - 1) / kThreads, 8192);
+        hipLaunchKernelGGL(sae_prefix_kernel, dim3(blocks), dim3(kThreads), 0, s, g, n_groups,
+                           (const uint32_t *)gi.mask, gi.B, sae);
+    }
+    {
+        ECC_TIMED(ctx, s, "arc_kernel");
+        const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
+        hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items, so,
+                           (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end, (const int64_t *)gi.B, gi.res);
+    }
+    {
+        ECC_TIMED(ctx, s, "flags_kernel");
+        hipLaunchKernelGGL(flags_kernel, dim3((unsigned)n_items), dim3(kThreads), 0, s, g, n_items, so,
+                           (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
     }
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
-#if ECC_CORNER_PROFILE
-    if (g.ts) {
-        (void)hipStreamSynchronize(s);
-        static unsigned long long hb[1 << 17];
-        (void)hipMemcpy(hb, g.ts, 1 << 20, hipMemcpyDeviceToHost);
-        FILE *f = fopen(getenv("ECC_CORNER_TS_FILE") ? getenv("ECC_CORNER_TS_FILE") : "/tmp/ts.bin", "wb");
-        if (f) { fwrite(hb, 1, 1 << 20, f); fclose(f); }
-    }
-#endif
     return ECC_OK;
 }
 
