@@ -60,13 +60,13 @@ struct CornerGeom {
     int64_t n, n_slices;
 };
 
-// Batch sorted by (group, tile): bin b of group g is [bin_off[g*nb+b], bin_off[g*nb+b+1]).
+// Batch sorted per slice by tile: slice s keeps its own range [s*S, s*S + len_s), and tile b of
+// slice s is [s*S + toff[s][b], s*S + toff[s][b+1]) (row length n_tiles + 2: the outside-sensor
+// bin n_tiles, then len_s).  A (group, tile) item's events are the 32 segments of its slices.
 struct Sorted {
-    uint32_t *key;       // (event index - first event of the group) << 8 | pixel in tile
-    uint32_t *t32;       // t - t(first event of the group), written for groups spanning < 2^32 - 1
-    int32_t *bin_count;  // [n_bins]
-    int32_t *rel;        // [n_slices * nb] slice's offset inside each bin it touches
-    int64_t *bin_off;    // [n_bins + 1]
+    uint32_t *key;   // (event index - first event of the group) << 8 | pixel in tile
+    uint32_t *t32;   // t - t(first event of the group), written for groups spanning < 2^32 - 1
+    int32_t *toff;   // [n_slices][n_tiles + 2]
 };
 
 __constant__ int8_t c3dy[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -111,60 +111,22 @@ __device__ __forceinline__ int slice_in_group(uint32_t el, const CornerGeom &g) 
     return (int)q;
 }
 
-// 1. Per-slice tile histogram (+ time-order check, first border index per slice for Q11).  The
-// value returned by the bin-total atomic is the slice's offset inside the bin (kept in rel[]).
-constexpr int kHistUnroll = 8;
+// 1. Per slice, one 1024-lane workgroup: counting sort of the slice's events by tile into the
+// slice's own range (keys + group-relative timestamps), the per-slice tile offsets, the
+// time-order check (Metavision stream order: t non-decreasing) and, for Q11, the slice's first
+// border event.  Slices of <= 16384 events stay in registers (one read); longer ones take a
+// counting pass and a placing pass.
+constexpr int kSortThreads = 1024;
+constexpr int kSortEPT = 16;
+constexpr int kSortChunk = kSortThreads * kSortEPT;
 
-__global__ void __launch_bounds__(kThreads)
-bin_hist_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g,
-                Sorted so, int32_t *__restrict__ first_border, int32_t *__restrict__ err) {
-    extern __shared__ int32_t hist[];  // [nb]
-    const int64_t s = blockIdx.x;
-    const int64_t lo = s * g.S, hi = (lo + g.S < g.n) ? lo + g.S : g.n;
-    const int64_t grp = s / kGroup;
-    const int nb = g.n_tiles + 1;
-    for (int b = threadIdx.x; b < nb; b += kThreads) hist[b] = 0;
-    __syncthreads();
-    bool bad = false;
-    int fb = 0x7fffffff;
-    for (int64_t e0 = lo; e0 < hi; e0 += kHistUnroll * kThreads) {
-        uint32_t v[kHistUnroll];
-        int64_t tc[kHistUnroll], tp[kHistUnroll];
-#pragma unroll
-        for (int u = 0; u < kHistUnroll; ++u) {
-            const int64_t e = e0 + u * kThreads + threadIdx.x;
-            v[u] = (e < hi) ? xy[e] : 0u;
-            tc[u] = (e < hi) ? t[e] : 0;
-            tp[u] = (e < hi && e > 0) ? t[e - 1] : INT64_MIN;
-        }
-#pragma unroll
-        for (int u = 0; u < kHistUnroll; ++u) {
-            const int64_t e = e0 + u * kThreads + threadIdx.x;
-            if (e < hi) {
-                atomicAdd(&hist[tile_of(v[u], g)], 1);
-                bad |= tp[u] > tc[u];
-                if (is_border(ecc::xy_x(v[u]), ecc::xy_y(v[u]), g)) fb = min(fb, (int)(e - lo));
-            }
-        }
-    }
-    if (__any(bad) && (threadIdx.x & 63) == 0) *err = 1;
-    if (g.border_mode == 1) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) fb = min(fb, __shfl_xor(fb, o));
-        if ((threadIdx.x & 63) == 0 && fb != 0x7fffffff) atomicMin(&first_border[s], fb);
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += kThreads)
-        if (hist[b]) so.rel[s * nb + b] = atomicAdd(&so.bin_count[grp * nb + b], hist[b]);
-}
-
-// Block-wide exclusive scan of in[0, n) into out (256 threads, each owning a contiguous run).
-__device__ __forceinline__ void block_excl_scan(const int32_t *in, int32_t *out, int n, int32_t *wsum) {
+// Block-wide exclusive scan in place of a[0, n) (kSortThreads threads, each a contiguous run).
+__device__ __forceinline__ void block_excl_scan_inplace(int32_t *a, int n, int32_t *wsum) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int per = (n + kThreads - 1) / kThreads;
+    const int per = (n + kSortThreads - 1) / kSortThreads;
     const int b0 = min(n, tid * per), b1 = min(n, b0 + per);
     int sum = 0;
-    for (int i = b0; i < b1; ++i) sum += in[i];
+    for (int i = b0; i < b1; ++i) sum += a[i];
     int incl = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -176,80 +138,146 @@ __device__ __forceinline__ void block_excl_scan(const int32_t *in, int32_t *out,
     int run = incl - sum;
     for (int w = 0; w < wave; ++w) run += wsum[w];
     for (int i = b0; i < b1; ++i) {
-        const int c = in[i];
-        out[i] = run;
+        const int c = a[i];
+        a[i] = run;
         run += c;
     }
 }
 
-// 2. Scatter 4-byte keys (+ 4-byte group-relative timestamps when the group spans < 2^32 - 1
-// ticks) into (group, tile) order; order inside a bin is irrelevant.
-// The slice's range of every bin comes from bin_hist (rel[]); each chunk of C events is counting-
-// sorted by bin in LDS and written out in bin order, so consecutive lanes store to
-// consecutive addresses (a direct scatter stores every lane to a different line).
-template <int C>
-__global__ void __launch_bounds__(kThreads)
-bin_scatter_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g, Sorted so) {
-    extern __shared__ int64_t lds64[];
-    __shared__ int32_t wsum[kThreads / 64];
-    const int nb = g.n_tiles + 1;
-    int64_t *base = lds64;                                    // [nb] next free slot per bin
-    int32_t *cnt = reinterpret_cast<int32_t *>(base + nb);    // [nb]
-    int32_t *loff = cnt + nb;                                 // [nb]
-    uint32_t *st_key = reinterpret_cast<uint32_t *>(loff + nb);  // [C]
-    uint32_t *st_t = st_key + C;                                  // [C]
-    uint16_t *st_bin = reinterpret_cast<uint16_t *>(st_t + C);    // [C]
-    const int tid = threadIdx.x;
+__global__ void __launch_bounds__(kSortThreads)
+slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g, Sorted so,
+                  int32_t *__restrict__ first_border, int32_t *__restrict__ err) {
+    extern __shared__ int32_t hist[];  // [nb]: counts, then offsets, then (long slices) cursors;
+                                       // then [kSortChunk] staging of the sorted slice
+    __shared__ int32_t wsum[kSortThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63;
     const int64_t s = blockIdx.x;
-    const int64_t lo = s * g.S, hi = (lo + g.S < g.n) ? lo + g.S : g.n;
+    const int64_t lo = s * g.S;
+    const int len = (int)((lo + g.S < g.n ? lo + g.S : g.n) - lo);
     const int64_t grp = s / kGroup;
     const int64_t grp_first = grp * kGroup * (int64_t)g.S;
     int64_t t_first;
     const bool narrow = group_narrow(t, g, grp, &t_first);  // uniform
-    for (int b = tid; b < nb; b += kThreads) {  // rel[] is only defined for bins the slice touches
-        base[b] = so.bin_off[grp * nb + b] + so.rel[s * nb + b];
-        cnt[b] = 0;
+    const int nb = g.n_tiles + 1;
+    for (int b = tid; b < nb; b += kSortThreads) hist[b] = 0;
+    __syncthreads();
+    bool bad = false;
+    int fb = 0x7fffffff;
+    const bool single = len <= kSortChunk;
+    uint32_t v[kSortEPT], tv[kSortEPT];
+    uint32_t br[kSortEPT];  // tile << 16 | rank within the tile (single slices: rank < 2^14)
+    for (int c0 = 0; c0 < len; c0 += kSortChunk) {  // one iteration for single slices
+#pragma unroll
+        for (int u = 0; u < kSortEPT; ++u) {
+            const int i = c0 + u * kSortThreads + tid;
+            const int64_t e = lo + i;
+            const bool ok = i < len;
+            v[u] = ok ? xy[e] : 0u;
+            const int64_t tc = ok ? t[e] : INT64_MAX;
+            int64_t tp = __shfl_up(tc, 1);  // the previous event is the previous lane's ...
+            if (lane == 0) tp = (ok && e > 0) ? t[e - 1] : INT64_MIN;  // ... except at a wave's start
+            bad |= ok && tp > tc;
+            tv[u] = (uint32_t)(tc - t_first);
+            br[u] = ok ? (uint32_t)tile_of(v[u], g) << 16 : 0xffffffffu;
+        }
+#pragma unroll
+        for (int u = 0; u < kSortEPT; ++u) {
+            if (br[u] == 0xffffffffu) continue;
+            br[u] |= (uint32_t)atomicAdd(&hist[br[u] >> 16], 1) & 0xffffu;
+            if (is_border(ecc::xy_x(v[u]), ecc::xy_y(v[u]), g)) fb = min(fb, c0 + u * kSortThreads + tid);
+        }
+    }
+    if (__any(bad) && lane == 0) *err = 1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) fb = min(fb, __shfl_xor(fb, o));
+    if (lane == 0) wsum[tid >> 6] = fb;
+    __syncthreads();
+    if (tid == 0) {
+        int m = 0x7fffffff;
+        for (int w = 0; w < kSortThreads / 64; ++w) m = min(m, wsum[w]);
+        first_border[s] = m;
     }
     __syncthreads();
-    constexpr int kPer = C / kThreads;
-    for (int64_t c0 = lo; c0 < hi; c0 += C) {
-        const int cn = (int)((hi - c0) < C ? (hi - c0) : C);
-        uint32_t v[kPer];
-        int bb[kPer], rr[kPer];
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            const int i = u * kThreads + tid;
-            v[u] = (i < cn) ? xy[c0 + i] : 0u;
-            bb[u] = (i < cn) ? tile_of(v[u], g) : -1;
-            rr[u] = (i < cn) ? atomicAdd(&cnt[bb[u]], 1) : 0;
-        }
-        __syncthreads();
-        block_excl_scan(cnt, loff, nb, wsum);
+    block_excl_scan_inplace(hist, nb, wsum);
+    __syncthreads();
+    int32_t *row = so.toff + s * (int64_t)(nb + 1);
+    for (int b = tid; b < nb; b += kSortThreads) row[b] = hist[b];
+    if (tid == 0) row[nb] = len;
+    if (single) {  // place keys, then timestamps, in tile order in LDS; write both out contiguously
+        uint32_t *stage = reinterpret_cast<uint32_t *>(hist + nb);
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            const int i = u * kThreads + tid;
-            if (i < cn) {
-                const int pos = loff[bb[u]] + rr[u];
-                st_key[pos] = tile_key(v[u], (uint32_t)(c0 + i - grp_first));
-                if (narrow) st_t[pos] = (uint32_t)(t[c0 + i] - t_first);
-                st_bin[pos] = (uint16_t)bb[u];
-            }
+        for (int u = 0; u < kSortEPT; ++u) {
+            if (br[u] == 0xffffffffu) continue;
+            const int i = u * kSortThreads + tid;
+            stage[hist[br[u] >> 16] + (br[u] & 0xffffu)] = tile_key(v[u], (uint32_t)(lo + i - grp_first));
         }
         __syncthreads();
-        for (int i = tid; i < cn; i += kThreads) {
-            const int b = st_bin[i];
-            const int64_t gpos = base[b] + (i - loff[b]);
-            so.key[gpos] = st_key[i];
-            if (narrow) so.t32[gpos] = st_t[i];
-        }
+        for (int i = tid; i < len; i += kSortThreads) so.key[lo + i] = stage[i];
+        if (!narrow) return;
         __syncthreads();
-        for (int b = tid; b < nb; b += kThreads) {
-            base[b] += cnt[b];
-            cnt[b] = 0;
-        }
+#pragma unroll
+        for (int u = 0; u < kSortEPT; ++u)
+            if (br[u] != 0xffffffffu) stage[hist[br[u] >> 16] + (br[u] & 0xffffu)] = tv[u];
         __syncthreads();
+        for (int i = tid; i < len; i += kSortThreads) so.t32[lo + i] = stage[i];
+        return;
     }
+    __syncthreads();  // row written before the offsets turn into cursors
+    for (int c0 = 0; c0 < len; c0 += kSortThreads) {
+        const int i = c0 + tid;
+        if (i >= len) continue;
+        const uint32_t vv = xy[lo + i];
+        const int64_t pos = lo + atomicAdd(&hist[tile_of(vv, g)], 1);
+        so.key[pos] = tile_key(vv, (uint32_t)(lo + i - grp_first));
+        if (narrow) so.t32[pos] = (uint32_t)(t[lo + i] - t_first);
+    }
+}
+
+// The 32 slice segments of one (group, tile) item, built by wave 0 into LDS (caller syncs):
+// segment r = slice grp*32 + r; events are addressed by a flattened index i in [0, pref[32]).
+// base = sum over the slices of toff[s][tile] = the item's offset inside the group's range when
+// the group's items are laid out in tile order (used for its pair entries).
+struct TileSegs {
+    int64_t start[kGroup];
+    int32_t pref[kGroup + 1];
+    int64_t base;
+};
+
+__device__ __forceinline__ void tile_segs(const CornerGeom &g, const Sorted &so, int64_t grp, int tile, TileSegs &T) {
+    const int tid = threadIdx.x;
+    if (tid >= 64) return;
+    const int64_t s = grp * kGroup + tid;
+    int a = 0, len = 0;
+    if (tid < kGroup && s < g.n_slices) {
+        const int32_t *row = so.toff + s * (int64_t)(g.n_tiles + 2);
+        a = row[tile];
+        len = row[tile + 1] - a;
+    }
+    int incl = len;
+    int64_t asum = a;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (tid >= o) incl += v;
+        asum += __shfl_xor(asum, o);
+    }
+    if (tid < kGroup) {
+        T.start[tid] = s * g.S + a;
+        T.pref[tid + 1] = incl;
+    }
+    if (tid == 0) {
+        T.pref[0] = 0;
+        T.base = asum;
+    }
+}
+
+__device__ __forceinline__ int64_t seg_at(const TileSegs &T, int i) {
+    int r = 0;
+#pragma unroll
+    for (int step = kGroup / 2; step > 0; step >>= 1)
+        if (T.pref[r + step] <= i) r += step;
+    return T.start[r] + (i - T.pref[r]);
 }
 
 // Group time reference: L = t_last(group) - (2^27 - 1).  In a narrow group (span < 2^27 - 1
@@ -301,8 +329,9 @@ __constant__ SubOrder c_sub = make_sub_order();
 
 // 3. Per (group, tile): the distinct (slice, pixel) pairs the tile's events touch, each with the
 // value an arc test reads there (max over the slice's events at the pixel: v' or index + 1),
-// written as entries {j << 8 | pixel, value} in sub-region order at the bin's own offsets (a
-// bin holds at least as many events as pairs), with the sub-region ends in sub_end[bin][9].
+// written as entries {j << 8 | pixel, value} in sub-region order at item_base[item] = the item's
+// place in its group's range with the group's items in tile order (an item has at least as many
+// events as pairs), with the sub-region ends in sub_end[item][9].
 // Also the slices that touched each pixel (gmask) and its last timestamp (glast).
 struct PairEntry {
     uint32_t meta;  // j << 8 | pixel in tile
@@ -311,28 +340,31 @@ struct PairEntry {
 
 __global__ void __launch_bounds__(kThreads)
 pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEntry *__restrict__ entries,
-                  int32_t *__restrict__ sub_end, uint32_t *__restrict__ gmask, int64_t *__restrict__ glast) {
+                  int64_t *__restrict__ item_base, int32_t *__restrict__ sub_end, uint32_t *__restrict__ gmask,
+                  int64_t *__restrict__ glast) {
     __shared__ uint32_t tab[kGroup][kTilePix];  // 24.5 KiB
     __shared__ int32_t wtot[kThreads / 64];
+    __shared__ TileSegs segs;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t grp = blockIdx.x / g.n_tiles;
-    const int tile = (int)(blockIdx.x % g.n_tiles);
+    const int64_t item = blockIdx.x;
+    const int64_t grp = item / g.n_tiles;
+    const int tile = (int)(item % g.n_tiles);
     {
         uint4 *z = reinterpret_cast<uint4 *>(&tab[0][0]);
         for (int i = tid; i < (int)(sizeof(tab) / 16); i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
     }
+    tile_segs(g, so, grp, tile, segs);
     const GroupRef gr = group_ref(t, g, grp);
-    const int nb = g.n_tiles + 1;
-    const int64_t bin = grp * nb + tile;
-    const int64_t b0 = so.bin_off[bin], b1 = so.bin_off[bin + 1];
     __syncthreads();
-    for (int64_t i0 = b0; i0 < b1; i0 += kBuildUnroll * kThreads) {
+    const int total = segs.pref[kGroup];
+    for (int i0 = 0; i0 < total; i0 += kBuildUnroll * kThreads) {
         uint32_t k[kBuildUnroll], tv[kBuildUnroll];
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u) {
-            const int64_t i = i0 + u * kThreads + tid;
-            k[u] = (i < b1) ? so.key[i] : 0xffffffffu;
-            tv[u] = (i < b1 && gr.narrow) ? so.t32[i] : 0u;
+            const int i = i0 + u * kThreads + tid;
+            const int64_t gi = (i < total) ? seg_at(segs, i) : 0;
+            k[u] = (i < total) ? so.key[gi] : 0xffffffffu;
+            tv[u] = (i < total && gr.narrow) ? so.t32[gi] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u) {
@@ -361,9 +393,11 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
     int off = incl - cnt;
     for (int w = 0; w < wave; ++w) off += wtot[w];
     if (tid >= kTilePix) return;
+    const int64_t base = gr.first + segs.base;  // the item's events range = room for its pairs
+    if (tid == 0) item_base[item] = base;
     for (int r = 0; r < kSub; ++r)
-        if (tid + 1 == c_sub.end[r]) sub_end[bin * kSub + r] = off + cnt;
-    PairEntry *out = entries + b0 + off;
+        if (tid + 1 == c_sub.end[r]) sub_end[item * kSub + r] = off + cnt;
+    PairEntry *out = entries + base + off;
     for (uint32_t mm = m; mm; mm &= mm - 1u) {
         const int j = __ffs(mm) - 1;
         *out++ = PairEntry{(uint32_t)(j << 8 | lp), tab[j][lp]};
@@ -574,7 +608,7 @@ constexpr int kStageUnroll = 8;
 constexpr int kMaxSeg = 13;
 
 __global__ void __launch_bounds__(kArcThreads, 2)  // two 8-wave workgroups per CU (LDS)
-arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, Sorted so,
+arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
            const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
            const int64_t *__restrict__ gB, uint32_t *__restrict__ res) {
     __shared__ ArcLds L;
@@ -586,8 +620,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, Sorted 
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
     if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
-    const int nb = g.n_tiles + 1;
-    if (so.bin_off[grp * nb + tile] == so.bin_off[grp * nb + tile + 1]) return;  // no events to flag
+    if (sub_end[item * kSub + kSub - 1] == 0) return;  // no events in the tile: nothing to flag
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t HW = (int64_t)g.H * g.W;
     int tx, ty;
@@ -628,9 +661,9 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, Sorted 
         int64_t b0 = 0;
         int len = 0;
         if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
-            const int64_t bi = grp * nb + (int64_t)ny * g.tiles_x + nx;
+            const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
             const int s0 = r0[tid] ? sub_end[bi * kSub + r0[tid] - 1] : 0;
-            b0 = so.bin_off[bi] + s0;
+            b0 = item_base[bi] + s0;
             len = sub_end[bi * kSub + r1[tid]] - s0;
         }
         int incl = len;  // prefix over lanes 0..12 of wave 0
@@ -787,37 +820,43 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, Sorted 
 // eligibility of the reference loop is applied here: the slice's first-detect rule (Q15), the
 // border margin, and in ref_compat mode (Q11) "before the slice's first border event".
 __global__ void __launch_bounds__(kThreads)
-flags_kernel(CornerGeom g, int64_t n_items, Sorted so, const uint32_t *__restrict__ res,
+flags_kernel(CornerGeom g, Sorted so, const int32_t *__restrict__ sub_end, const uint32_t *__restrict__ res,
              const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags) {
     __shared__ uint32_t r_l[kPairWords];
+    __shared__ TileSegs segs;
     const int64_t item = blockIdx.x;
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
-    if ((grp + 1) * kGroup <= g.first_detect) return;
-    const int nb = g.n_tiles + 1;
-    const int64_t b0 = so.bin_off[grp * nb + tile], b1 = so.bin_off[grp * nb + tile + 1];
-    if (b0 == b1) return;
+    if ((grp + 1) * kGroup <= g.first_detect || sub_end[item * kSub + kSub - 1] == 0) return;
     uint32_t any = 0u;
     for (int w = threadIdx.x; w < kPairWords; w += kThreads) {
         const uint32_t v = res[item * kPairWords + w];
         r_l[w] = v;
         any |= v;
     }
+    tile_segs(g, so, grp, tile, segs);
     if (!__syncthreads_or(any != 0u)) return;  // no corner in this item
-    int x0, y0;
-    tile_origin(g, tile, x0, y0);
     const int64_t grp_first = grp * kGroup * (int64_t)g.S;
-    for (int64_t i = b0 + threadIdx.x; i < b1; i += kThreads) {
-        const uint32_t key = so.key[i];
-        const int lp = (int)(key & 255u);
-        const uint32_t el = key >> 8;
-        const int j = slice_in_group(el, g);
-        const uint32_t pi = (uint32_t)(j * kTilePix + lp);
-        if (!((r_l[pi >> 5] >> (pi & 31u)) & 1u)) continue;  // a corner pair is never a border pixel
-        const int64_t s = grp * kGroup + j;
-        if (s < g.first_detect) continue;
-        if (g.border_mode == 1 && (int64_t)el - (int64_t)j * g.S >= first_border[s]) continue;
-        flags[grp_first + el] = 1;
+    const int total = segs.pref[kGroup];
+    for (int i0 = 0; i0 < total; i0 += kBuildUnroll * kThreads) {
+        uint32_t k[kBuildUnroll];
+#pragma unroll
+        for (int u = 0; u < kBuildUnroll; ++u) {
+            const int i = i0 + u * kThreads + threadIdx.x;
+            k[u] = (i < total) ? so.key[seg_at(segs, i)] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int u = 0; u < kBuildUnroll; ++u) {
+            if (k[u] == 0xffffffffu) continue;
+            const uint32_t el = k[u] >> 8;
+            const int j = slice_in_group(el, g);
+            const uint32_t pi = (uint32_t)(j * kTilePix + (k[u] & 255u));
+            if (!((r_l[pi >> 5] >> (pi & 31u)) & 1u)) continue;  // corner pairs are never border pixels
+            const int64_t s = grp * kGroup + j;
+            if (s < g.first_detect) continue;
+            if (g.border_mode == 1 && (int64_t)el - (int64_t)j * g.S >= first_border[s]) continue;
+            flags[grp_first + el] = 1;
+        }
     }
 }
 
@@ -845,7 +884,7 @@ sae_max_combine_kernel(const int64_t *__restrict__ images, int n_images, int64_t
     }
 }
 
-// Per-context corner workspace: the sorted batch with its bin tables and the per-group images
+// Per-context corner workspace: the sorted batch with its offset tables and the per-group images
 // (sized by batch and sensor; grown, never shrunk).
 struct CornerState {
     void *evt = nullptr;
@@ -876,29 +915,28 @@ struct Carve {
 };
 
 struct GroupImages {
-    uint32_t *mask;  // [n_groups][H*W] slices of the group that touched the pixel
-    int64_t *B;      // [n_groups][H*W] last t of the group, then (in place) B_g
-    uint32_t *res;   // [n_groups * n_tiles][kPairWords] corner (slice, pixel) pairs per item
-    PairEntry *entries;  // [n] distinct (slice, pixel) pairs per bin, at the bin's offsets
-    int32_t *sub_end;    // [n_bins][kSub] sub-region ends inside each bin's entries
+    uint32_t *mask;       // [n_groups][H*W] slices of the group that touched the pixel
+    int64_t *B;           // [n_groups][H*W] last t of the group, then (in place) B_g
+    uint32_t *res;        // [n_items][kPairWords] corner (slice, pixel) pairs per item
+    PairEntry *entries;   // [n] distinct (slice, pixel) pairs per item, at item_base[item]
+    int64_t *item_base;   // [n_items]
+    int32_t *sub_end;     // [n_items][kSub] sub-region ends inside each item's entries
 };
 
-Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_bins, int64_t n_groups, int32_t **first_border,
-                    int64_t **scan_scratch, GroupImages *gi) {
+Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_items, int64_t n_groups, int32_t **first_border,
+                    GroupImages *gi) {
     Sorted so{};
     so.key = cv.take<uint32_t>((size_t)g.n);
     so.t32 = cv.take<uint32_t>((size_t)g.n);
-    so.bin_count = cv.take<int32_t>((size_t)n_bins);
-    so.rel = cv.take<int32_t>((size_t)g.n_slices * (g.n_tiles + 1));
-    so.bin_off = cv.take<int64_t>((size_t)n_bins + 1);
+    so.toff = cv.take<int32_t>((size_t)g.n_slices * (g.n_tiles + 2));
     *first_border = cv.take<int32_t>((size_t)g.n_slices);
-    *scan_scratch = cv.take<int64_t>((ecc::scan_scratch_bytes(n_bins) + 7) / 8);
     const size_t img = (size_t)n_groups * g.W * g.H;
     gi->mask = cv.take<uint32_t>(img);
     gi->B = cv.take<int64_t>(img);
-    gi->res = cv.take<uint32_t>((size_t)n_groups * g.n_tiles * kPairWords);
+    gi->res = cv.take<uint32_t>((size_t)n_items * kPairWords);
     gi->entries = cv.take<PairEntry>((size_t)g.n);
-    gi->sub_end = cv.take<int32_t>((size_t)n_bins * kSub);
+    gi->item_base = cv.take<int64_t>((size_t)n_items);
+    gi->sub_end = cv.take<int32_t>((size_t)n_items * kSub);
     return so;
 }
 
@@ -983,45 +1021,32 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     if (n == 0) return ECC_OK;
     const int nb = g.n_tiles + 1;
     const int64_t n_groups = (g.n_slices + kGroup - 1) / kGroup;
-    const int64_t n_bins = n_groups * nb;
-    const int64_t n_items = n_groups * g.n_tiles;  // arc work items: (group, tile)
+    const int64_t n_items = n_groups * g.n_tiles;  // work items: (group, tile)
     if (n_items > (int64_t)INT32_MAX - 8) return ECC_ERR_INVALID;
     CornerState *st = state_of(ctx);
     int32_t *first_border = nullptr;
-    int64_t *scan_scratch = nullptr;
     GroupImages gi{};
     Carve measure{nullptr};
-    carve_sorted(measure, g, n_bins, n_groups, &first_border, &scan_scratch, &gi);
+    carve_sorted(measure, g, n_items, n_groups, &first_border, &gi);
     int rc = corner_state_reserve(ctx, st, measure.used);
     if (rc) return rc;
     Carve cv{static_cast<char *>(st->evt)};
-    const Sorted so = carve_sorted(cv, g, n_bins, n_groups, &first_border, &scan_scratch, &gi);
+    const Sorted so = carve_sorted(cv, g, n_items, n_groups, &first_border, &gi);
 
     ECC_CHECK_HIP(ctx, hipMemsetAsync(corner_flags, 0, (size_t)n, s), "memset(flags)");
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(so.bin_count, 0, (size_t)n_bins * 4, s), "memset(bins)");
-    if (g.border_mode == 1)
-        ECC_CHECK_HIP(ctx, hipMemsetAsync(first_border, 0x7f, (size_t)g.n_slices * 4, s), "memset(fb)");
     {
-        ECC_TIMED(ctx, s, "bin_hist_kernel");
-        hipLaunchKernelGGL(bin_hist_kernel, dim3((unsigned)g.n_slices), dim3(kThreads), nb * 4, s, xy, t,
-                           g, so, first_border, ctx->flags);
-    }
-    rc = ecc::exclusive_scan_i32_i64(ctx, so.bin_count, n_bins, so.bin_off, scan_scratch, s);
-    if (rc) return rc;
-    {
-        ECC_TIMED(ctx, s, "bin_scatter_kernel");
-        const size_t lds_big = (size_t)nb * 16 + 2048 * 10, lds_small = (size_t)nb * 16 + 1024 * 10;
-        if (lds_big <= 40 * 1024)  // 4 workgroups per CU
-            hipLaunchKernelGGL(bin_scatter_kernel<2048>, dim3((unsigned)g.n_slices), dim3(kThreads), lds_big, s, xy,
-                               t, g, so);
-        else
-            hipLaunchKernelGGL(bin_scatter_kernel<1024>, dim3((unsigned)g.n_slices), dim3(kThreads), lds_small, s,
-                               xy, t, g, so);
+        const size_t lds = (size_t)nb * 4 + kSortChunk * 4;  // > 64 KiB: opt in (gfx950 has 160 KiB)
+        ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&slice_sort_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                      "slice_sort LDS");
+        ECC_TIMED(ctx, s, "slice_sort_kernel");
+        hipLaunchKernelGGL(slice_sort_kernel, dim3((unsigned)g.n_slices), dim3(kSortThreads), lds, s, xy, t, g,
+                           so, first_border, ctx->flags);
     }
     {
         ECC_TIMED(ctx, s, "pair_build_kernel");
         hipLaunchKernelGGL(pair_build_kernel, dim3((unsigned)n_items), dim3(kThreads), 0, s, t, g, so, gi.entries,
-                           gi.sub_end, gi.mask, gi.B);
+                           gi.item_base, gi.sub_end, gi.mask, gi.B);
     }
     {
         ECC_TIMED(ctx, s, "sae_prefix_kernel");
@@ -1033,13 +1058,13 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     {
         ECC_TIMED(ctx, s, "arc_kernel");
         const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
-        hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items, so,
-                           (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end, (const int64_t *)gi.B, gi.res);
+        hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
+                           (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end, (const int64_t *)gi.B, gi.res);
     }
     {
         ECC_TIMED(ctx, s, "flags_kernel");
-        hipLaunchKernelGGL(flags_kernel, dim3((unsigned)n_items), dim3(kThreads), 0, s, g, n_items, so,
-                           (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
+        hipLaunchKernelGGL(flags_kernel, dim3((unsigned)n_items), dim3(kThreads), 0, s, g, so,
+                           (const int32_t *)gi.sub_end, (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
     }
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
     return ECC_OK;
