@@ -57,6 +57,8 @@ struct CornerGeom {
     int W, H, S, margin, border_mode, first_detect;
     int tiles_x, n_tiles;  // bin n_tiles of each group holds the events outside the sensor
     float inv_S;
+    int dbg;  // development: arc phase cut-off (ECC_ARC_DBG)
+    void *dbg_cnt;
     int64_t n, n_slices;
 };
 
@@ -526,26 +528,31 @@ __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
     return ok ? 1 : 0;
 }
 
-// Staged neighbourhood of one (group, tile) item: T[j][wp] = the value the arc test of an event
-// in slice j of the group sees at window pixel wp — v' = t - L for values set inside the group
-// (narrow groups, exact) or the clamped B_g, forward-filled along j; in wide groups the index + 1
-// of the last event (timestamps gathered by the exact test).  mask[wp]: the slices of the group
-// that touched wp (the exact test needs it to tell group values from B_g).
+// Staged neighbourhood of one (group, tile) item.  T[j][wp] holds the value set at window pixel
+// wp by slice j of the group — v' = t - L (narrow groups, exact) or the event index + 1 (wide
+// groups) — and is valid only where bit j of mb[wp].mask is set; mb[wp].bc is the clamped B_g.
+// The value an event of slice j sees at wp is T[j*][wp] with j* the highest set bit of
+// mask & ((2 << j) - 1), else bc: no forward fill, and T is never cleared.
 constexpr int kPairWords = kGroup * kTilePix / 32;  // 196: one bit per (slice, tile pixel)
+constexpr int kWaves = kArcThreads / 64;
+constexpr int kQ4Cap = 1024;  // two 8-wave workgroups per CU fit the 160 KiB LDS
+
+struct MaskB {
+    uint32_t mask;
+    uint32_t bc;
+};
 
 struct ArcLds {
-    uint32_t T[kGroup][kWinPix];          // 60.5 KiB
-    uint32_t mask[kWinPix];
-    uint32_t pairs[kPairWords];           // (slice, pixel) pairs with an eligible event
-    uint32_t res[kPairWords];             // ... that are corners
-    uint16_t word_off[kPairWords];        // exclusive prefix of popc(pairs)
-    uint16_t q4[kGroup * kTilePix];       // pairs that passed circle 3
-    int64_t wave_min[kArcThreads / 64];
-    int32_t wave_tot[kArcThreads / 64];
+    uint32_t T[kGroup][kWinPix];      // 60.5 KiB
+    MaskB mb[kWinPix];
+    uint32_t res[kPairWords];         // corner (slice, pixel) pairs of the tile
+    uint16_t tasks[kGroup * kTilePix]; // the tile's eligible pairs (j * 196 + pixel)
+    uint16_t q4[kQ4Cap];               // circle-3 survivors (beyond the cap: tested inline)
+    int64_t wave_min[kWaves];
     int32_t exact_only;  // a value above t_last: clamped keys unusable
     int32_t mixed;       // clamped values not all equal to the window minimum of B
-    int32_t q4n;
     int32_t n_tasks;
+    int32_t q4n;
     int64_t seg_lo[16];   // window segments: first entry (absolute) ...
     int32_t seg_pref[16]; // ... exclusive prefix of their lengths ...
     int32_t seg_off[16];  // ... and the window offset of the neighbour tile's origin
@@ -562,10 +569,19 @@ __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, 
     return (uint32_t)d;
 }
 
+__device__ __forceinline__ uint32_t below_mask(int j) { return (j == 31) ? 0xffffffffu : ((2u << j) - 1u); }
+
+// Clamped value at window pixel wp for slice j (fast path).
+__device__ __forceinline__ uint32_t win_value(const ArcLds &L, int wp, uint32_t below) {
+    const MaskB m = L.mb[wp];
+    const uint32_t mk = m.mask & below;
+    return mk ? L.T[31 - __clz(mk)][wp] : m.bc;
+}
+
 // Exact int64 arc test of one circle around window pixel wp0 (global pixel q0) for slice j:
-// V = the group value (from T: v' + L, or the timestamp of the stored event index) where a slice
-// <= j of the group touched the pixel, else B_g.  Rare fallback; out of line so its registers do
-// not raise the pressure of the main kernel body.
+// V = the group value (v' + L, or the timestamp of the stored event index) where a slice <= j of
+// the group touched the pixel, else B_g.  Rare fallback; out of line so its registers do not
+// raise the pressure of the main kernel body.
 struct ExactCtx {
     const int64_t *Bg;  // B_g image of the group
     const int64_t *t;
@@ -575,33 +591,34 @@ struct ExactCtx {
 };
 
 template <int N>
-__device__ __forceinline__ void exact_values(const ArcLds *L, int wp0, int64_t q0, uint32_t below, int j,
+__device__ __forceinline__ void exact_values(const ArcLds *L, int wp0, int64_t q0, uint32_t below,
                                              const int8_t *dy, const int8_t *dx, const ExactCtx &c, int64_t (&v)[N]) {
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         const int wp = wp0 + dy[k] * kWin + dx[k];
-        const uint32_t tv = L->T[j][wp];
-        v[k] = !(L->mask[wp] & below) ? c.Bg[q0 + (int64_t)dy[k] * c.W + dx[k]]
-               : c.narrow            ? c.Lt + (int64_t)tv
-                                     : c.t[c.grp_first + tv - 1u];
+        const uint32_t mk = L->mb[wp].mask & below;
+        const uint32_t tv = mk ? L->T[31 - __clz(mk)][wp] : 0u;
+        v[k] = !mk      ? c.Bg[q0 + (int64_t)dy[k] * c.W + dx[k]]
+               : c.narrow ? c.Lt + (int64_t)tv
+                          : c.t[c.grp_first + tv - 1u];
     }
 }
 
 __device__ __noinline__ bool exact_circle_test(const ArcLds *L, int wp0, int64_t q0, int j, bool c3, const ExactCtx c) {
-    const uint32_t below = (j == 31) ? 0xffffffffu : ((2u << j) - 1u);
+    const uint32_t below = below_mask(j);
     if (c3) {
         int64_t v3[16];
-        exact_values<16>(L, wp0, q0, below, j, c3dy, c3dx, c, v3);
+        exact_values<16>(L, wp0, q0, below, c3dy, c3dx, c, v3);
         return arc_streak<16, 3, 6>(v3);
     }
     int64_t v4[20];
-    exact_values<20>(L, wp0, q0, below, j, c4dy, c4dx, c, v4);
+    exact_values<20>(L, wp0, q0, below, c4dy, c4dx, c, v4);
     return arc_streak<20, 4, 8>(v4);
 }
 
 // 5. Arc test of one (group, tile) item, all items of all groups in one launch.  The item's
 // corner pairs go to res[item][kPairWords] (bit j*196 + pixel); flags_kernel applies them.
-constexpr int kStageUnroll = 8;
+constexpr int kStageUnroll = 4;
 
 // Window segments: the sub-regions of the 3x3 tiles around the item's tile that its window
 // covers (own tile: all; edge neighbours: the 3 facing sub-regions; corners: 1) — 13 at most.
@@ -620,7 +637,6 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
     if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
-    if (sub_end[item * kSub + kSub - 1] == 0) return;  // no events in the tile: nothing to flag
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t HW = (int64_t)g.H * g.W;
     int tx, ty;
@@ -632,24 +648,21 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     const bool narrow = gr.narrow;
     const int64_t *Bg = gB + grp * HW;
 
-    // (a) the window pixel's B_g (issued first; lane wp < 484), zeroed LDS
+    // (a) the window pixel's B_g (lane wp < 484), the segment table (lanes 0..12), cleared masks
     static_assert(kArcThreads >= kWinPix, "one lane per window pixel");
     const int wp = tid;
     const bool win_lane = wp < kWinPix;
     const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
     const bool in = win_lane && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
     const int64_t bq = in ? Bg[(int64_t)wy * g.W + wx] : INT64_MAX;  // INT64_MAX: outside (never read)
-    {
-        uint4 *z = reinterpret_cast<uint4 *>(&L.T[0][0]);
-        for (int i = tid; i < (int)(sizeof(L.T) / 16); i += kArcThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
-        for (int w = tid; w < 2 * kPairWords; w += kArcThreads) (&L.pairs[0])[w] = 0u;  // pairs + res
-        if (tid == 0) {
-            L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
-            L.mixed = 0;
-            L.q4n = 0;
-        }
+    if (win_lane) L.mb[wp].mask = 0u;
+    for (int w = tid; w < kPairWords; w += kArcThreads) L.res[w] = 0u;
+    if (tid == 0) {
+        L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
+        L.mixed = 0;
+        L.n_tasks = 0;
+        L.q4n = 0;
     }
-    // segments (lanes 0..12): absolute entry range + the window offset of the neighbour tile
     if (tid < kMaxSeg) {
         // own tile: every sub-region; above/below: their facing rows; corners: one sub-region;
         // left/right: their facing columns (3 sub-regions, one segment each)
@@ -678,14 +691,16 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         if (tid == 0) L.seg_pref[0] = 0;
     }
     __syncthreads();
+    if (L.seg_pref[1] == 0) return;  // no events in the tile: nothing to flag
     const int total = L.seg_pref[kMaxSeg];
+    if (g.dbg == 3) return;
     int pref[kMaxSeg + 1];
 #pragma unroll
     for (int c = 0; c <= kMaxSeg; ++c) pref[c] = L.seg_pref[c];  // uniform (SGPRs)
 
-    // (b) each entry is a distinct (slice, pixel) pair of one tile: plain LDS stores of its value;
-    //     the own tile's pairs (segment 0) are the test candidates when the pixel and slice are
-    //     eligible (the per-event cut of border mode 1 is applied when flagging)
+    // (b) each entry is a distinct (slice, pixel) pair of one tile: its value goes to T, its slice
+    //     bit to the pixel's mask; the own tile's pairs (segment 0) with an eligible slice and
+    //     pixel are the test tasks (the per-event cut of border mode 1 is applied when flagging)
     for (int i0 = 0; i0 < total; i0 += kStageUnroll * kArcThreads) {
         PairEntry ent[kStageUnroll];
         int sg[kStageUnroll];
@@ -702,12 +717,12 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         for (int u = 0; u < kStageUnroll; ++u) {
             if (sg[u] < 0) continue;
             const int lp = (int)(ent[u].meta & 255u), j = (int)(ent[u].meta >> 8);
-            L.T[j][L.seg_off[sg[u]] + (lp / kTile) * kWin + lp % kTile] = ent[u].v;
+            const int ewp = L.seg_off[sg[u]] + (lp / kTile) * kWin + lp % kTile;
+            L.T[j][ewp] = ent[u].v;
+            atomicOr(&L.mb[ewp].mask, 1u << j);
             if (sg[u] == 0 && (int64_t)grp * kGroup + j >= g.first_detect &&
-                !is_border(x0 + lp % kTile, y0 + lp / kTile, g)) {
-                const uint32_t pi = (uint32_t)(j * kTilePix + lp);
-                atomicOr(&L.pairs[pi >> 5], 1u << (pi & 31u));
-            }
+                !is_border(x0 + lp % kTile, y0 + lp / kTile, g))
+                L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)(j * kTilePix + lp);
         }
     }
     int64_t bmin = bq;
@@ -718,89 +733,33 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     }
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
+    if (g.dbg == 2) return;
 
-    // (c) forward fill along j: T[j] = (set) ? T[j] : T[j-1], T[-1] = clamped B_g; a (slice, pixel)
-    //     value is set iff nonzero (values are >= 1), which also yields the pixel's slice mask
+    // (c) clamped B_g per window pixel
     if (win_lane) {
         int64_t vz = INT64_MAX;
 #pragma unroll
-        for (int w = 0; w < kArcThreads / 64; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
-        uint32_t cur_v = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
-        uint32_t mk = 0u;
-#pragma unroll
-        for (int j = 0; j < kGroup; ++j) {
-            const uint32_t v = L.T[j][wp];
-            mk |= (v != 0u ? 1u : 0u) << j;
-            cur_v = v ? v : cur_v;
-            L.T[j][wp] = cur_v;
-        }
-        L.mask[wp] = mk;
-    }
-    int wcnt = 0, wincl = 0;
-    if (tid < kPairWords) {  // exclusive prefix of the words' popcounts (waves 0-3)
-        wcnt = __popc(L.pairs[tid]);
-        wincl = wcnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(wincl, o);
-            if (lane >= o) wincl += v;
-        }
-        if (lane == 63) L.wave_tot[wave] = wincl;
+        for (int w = 0; w < kWaves; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
+        L.mb[wp].bc = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
     }
     __syncthreads();
-    if (tid < kPairWords) {
-        int before = 0;
-        for (int w = 0; w < wave; ++w) before += L.wave_tot[w];
-        L.word_off[tid] = (uint16_t)(before + wincl - wcnt);
-        if (tid == kPairWords - 1) L.n_tasks = before + wincl;
-    }
-    __syncthreads();
-    // (d) each distinct pair is tested once; circle-3 survivors are queued so circle 4 runs densely
+    if (g.dbg == 1) return;
+
+    // (d) each eligible pair of the tile is tested once; circle-3 survivors are queued so that
+    //     circle 4 runs on as few waves as possible
     const int n_tasks = L.n_tasks;
     const bool fast = !L.exact_only;
     const bool ties_exact = !L.mixed;
     const ExactCtx ec{Bg, t, grp_first, Lt, g.W, narrow};
-    auto task_pair = [&](int ti) {  // ti-th set bit of the pair bitmap
-        int lo_w = 0, hi_w = kPairWords;
-#pragma unroll
-        for (int step = 0; step < 8; ++step) {  // 2^8 >= kPairWords
-            const int mid = (lo_w + hi_w) >> 1;
-            if ((int)L.word_off[mid] <= ti) lo_w = mid; else hi_w = mid;
-        }
-        uint32_t m = L.pairs[lo_w];
-        for (int r = ti - (int)L.word_off[lo_w]; r > 0; --r) m &= m - 1;
-        return lo_w * 32 + (__ffs(m) - 1);
-    };
-    for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
-        const int pi = task_pair(ti);
+    auto circle4 = [&](int pi) {
         const int j = pi / kTilePix, lp = pi % kTilePix;
         const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-        int r3 = -1;
-        if (fast) {
-            const uint32_t *Tj = L.T[j];
-            uint32_t k3[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) k3[k] = (Tj[wp0 + c3dy[k] * kWin + c3dx[k]] << 4) | k;
-            r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
-        }
-        if (r3 < 0) {
-            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
-            r3 = exact_circle_test(&L, wp0, q0, j, true, ec) ? 1 : 0;
-        }
-        if (r3 == 1) L.q4[atomicAdd(&L.q4n, 1)] = (uint16_t)pi;
-    }
-    __syncthreads();
-    const int n4 = L.q4n;
-    for (int qi = tid; qi < n4; qi += kArcThreads) {
-        const int pi = L.q4[qi];
-        const int j = pi / kTilePix, lp = pi % kTilePix;
-        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        const uint32_t below = below_mask(j);
         int r4 = -1;
         if (fast) {
-            const uint32_t *Tj = L.T[j];
             uint32_t k4[32];
 #pragma unroll
-            for (int k = 0; k < 20; ++k) k4[k] = (Tj[wp0 + c4dy[k] * kWin + c4dx[k]] << 5) | k;
+            for (int k = 0; k < 20; ++k) k4[k] = (win_value(L, wp0 + c4dy[k] * kWin + c4dx[k], below) << 5) | k;
 #pragma unroll
             for (int k = 20; k < 32; ++k) k4[k] = 0u;
             r4 = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
@@ -810,7 +769,32 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
             r4 = exact_circle_test(&L, wp0, q0, j, false, ec) ? 1 : 0;
         }
         if (r4 == 1) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
+    };
+    for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+        const int pi = L.tasks[ti];
+        const int j = pi / kTilePix, lp = pi % kTilePix;
+        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        const uint32_t below = below_mask(j);
+        int r3 = -1;
+        if (fast) {
+            uint32_t k3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) k3[k] = (win_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
+            r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+        }
+        if (r3 < 0) {
+            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
+            r3 = exact_circle_test(&L, wp0, q0, j, true, ec) ? 1 : 0;
+        }
+        if (r3 == 1) {
+            const int qi = atomicAdd(&L.q4n, 1);
+            if (qi < kQ4Cap) L.q4[qi] = (uint16_t)pi;
+            else circle4(pi);  // queue full (rare): test here
+        }
     }
+    __syncthreads();
+    const int n4 = min(L.q4n, kQ4Cap);
+    for (int qi = tid; qi < n4; qi += kArcThreads) circle4(L.q4[qi]);
     __syncthreads();
     if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
 }
@@ -1006,6 +990,13 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     g.H = cfg->height;
     g.S = cfg->slice_events;
     g.inv_S = 1.0f / (float)g.S;
+    g.dbg = getenv("ECC_ARC_DBG") ? atoi(getenv("ECC_ARC_DBG")) : 0;
+    g.dbg_cnt = nullptr;
+    static unsigned long long *dbg_buf = nullptr;
+    if (g.dbg == 4) {
+        if (!dbg_buf) { (void)hipMalloc(&dbg_buf, 64); (void)hipMemset(dbg_buf, 0, 64); }
+        g.dbg_cnt = dbg_buf;
+    }
     g.margin = cfg->margin;
     g.border_mode = cfg->border_mode;
     g.first_detect = cfg->first_detect_slice;
@@ -1067,6 +1058,11 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
                            (const int32_t *)gi.sub_end, (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
     }
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
+    if (g.dbg == 4) {
+        unsigned long long h[2];
+        (void)hipMemcpy(h, g.dbg_cnt, 16, hipMemcpyDeviceToHost);
+        fprintf(stderr, "arc tasks %llu circle4 %llu (cumulative)\n", h[0], h[1]);
+    }
     return ECC_OK;
 }
 
