@@ -470,6 +470,107 @@ kmeans_extent_kernel(const uint32_t *__restrict__ xy, Segs segs, uint32_t *__res
     }
 }
 
+// Per-pixel point counts: the assignment depends on a point's pixel only, so a Lloyd pass can
+// visit each occupied pixel once with its multiplicity n, adding (n, n*x, n*y) — the same
+// integer sums as adding every point.  Counts are compact over the bounding box (w x h from the
+// extent kernel): cnt[y * w + x].  No global atomics (they execute at the memory side): workgroup
+// (chunk c, part m) counts the points of its part falling in pixel chunk c into LDS and stores
+// the chunk densely into partial[m]; kmeans_count_sum_kernel adds the parts.  Part 0's
+// workgroups of chunk 0 also list the points outside the kImgSide^2 image.
+constexpr int kHistThreads = 1024;
+constexpr int kHistChunk = 32768;  // pixels per LDS chunk (128 KiB)
+constexpr int kHistParts = 128;
+constexpr int64_t kHistBudget = 16 << 20;  // partial-count entries (64 MiB): parts used = budget / cells
+
+__host__ __device__ inline int parts_used(int parts, int64_t cells) {
+    const int64_t p = cells > 0 ? kHistBudget / cells : parts;
+    return (int)(p < 1 ? 1 : (p < parts ? p : parts));
+}
+constexpr int kHistUnroll = 4;
+
+__device__ __forceinline__ void reduce_extent(const uint32_t *__restrict__ ext, int n_ext, uint32_t *s_red,
+                                              uint32_t &w, uint32_t &h) {
+    uint32_t p = 0, q = 0;
+    for (int i = threadIdx.x; i < n_ext; i += blockDim.x) { p = max(p, ext[2 * i]); q = max(q, ext[2 * i + 1]); }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        p = max(p, (uint32_t)__shfl_xor((int)p, o));
+        q = max(q, (uint32_t)__shfl_xor((int)q, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_red[2 * (threadIdx.x >> 6)] = p;
+        s_red[2 * (threadIdx.x >> 6) + 1] = q;
+    }
+    __syncthreads();
+    w = 0;
+    h = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { w = max(w, s_red[2 * i]); h = max(h, s_red[2 * i + 1]); }
+}
+
+__global__ void __launch_bounds__(kHistThreads)
+kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *__restrict__ ext, int n_ext,
+                    int parts, uint32_t *__restrict__ partial, uint32_t *__restrict__ wh,
+                    uint32_t *__restrict__ outside, uint32_t *__restrict__ n_outside) {
+    extern __shared__ uint32_t hist[];  // [kHistChunk]
+    __shared__ uint32_t s_red[2 * kHistThreads / 64];
+    const int m = blockIdx.y, tid = threadIdx.x;
+    uint32_t w, h;
+    reduce_extent(ext, n_ext, s_red, w, h);
+    const int64_t cells = (int64_t)w * h;
+    if (blockIdx.x == 0 && m == 0 && tid == 0) {
+        wh[0] = w;
+        wh[1] = h;
+    }
+    parts = parts_used(parts, cells);
+    if (m >= parts) return;
+    const int64_t s0 = segs.n_segs * m / parts, s1 = segs.n_segs * (m + 1) / parts;
+    const int64_t n_chunks = (cells + kHistChunk - 1) / kHistChunk;
+    for (int64_t c = blockIdx.x; c < (n_chunks > 0 ? n_chunks : 1); c += gridDim.x) {
+        const int64_t lo = c * kHistChunk;
+        const int n_loc = (int)((cells - lo) < kHistChunk ? (cells - lo) : kHistChunk);
+        for (int i = tid; i < kHistChunk; i += kHistThreads) hist[i] = 0u;
+        __syncthreads();
+        for (int64_t sg = s0; sg < s1; ++sg) {
+            const int64_t cnt = segs.count(sg), base = sg * segs.stride;
+            for (int64_t j0 = 0; j0 < cnt; j0 += kHistUnroll * kHistThreads) {
+                uint32_t v[kHistUnroll];
+#pragma unroll
+                for (int u = 0; u < kHistUnroll; ++u) {
+                    const int64_t j = j0 + u * kHistThreads + tid;
+                    v[u] = j < cnt ? xy[base + j] : 0xffffffffu;
+                }
+#pragma unroll
+                for (int u = 0; u < kHistUnroll; ++u) {
+                    if (j0 + u * kHistThreads + tid >= cnt) continue;
+                    const uint32_t x = v[u] & 0xffffu, y = v[u] >> 16;
+                    if (x < kImgSide && y < kImgSide) {
+                        const int64_t idx = (int64_t)y * w + x - lo;
+                        if (idx >= 0 && idx < n_loc) atomicAdd(&hist[idx], 1u);
+                    } else if (c == 0) {
+                        outside[atomicAdd(n_outside, 1u)] = v[u];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t *out = partial + (int64_t)m * cells + lo;
+        for (int i = tid; i < n_loc; i += kHistThreads) out[i] = hist[i];
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+kmeans_count_sum_kernel(const uint32_t *__restrict__ partial, int parts, const uint32_t *__restrict__ wh,
+                        uint32_t *__restrict__ cnt) {
+    const int64_t cells = (int64_t)wh[0] * wh[1];
+    parts = parts_used(parts, cells);
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < cells; i += (int64_t)gridDim.x * kThreads) {
+        uint32_t t = 0;
+        for (int m = 0; m < parts; ++m) t += partial[(int64_t)m * cells + i];
+        cnt[i] = t;
+    }
+}
+
 // One kmeans_step_kernel per Lloyd pass replaces "update, then label image": every workgroup
 // re-derives the centroid update from the previous pass's accumulator replicas (a few hundred
 // L2 reads), so no second launch and no grid-wide hand-off is needed.  Buffers alternate by pass:
@@ -489,10 +590,19 @@ struct StepArgs {
     bool want_image;
 };
 
-template <int K>
+// kPix: instead of a label image, the pass itself — (n, n*x, n*y) of every occupied pixel (cnt)
+// and (1, x, y) of every outside point, into acc_out; WG 0 zeroes acc_zero, the replicas the
+// NEXT pass accumulates into (three sets rotate: read by this pass's update, written, zeroed).
+struct PixArgs {
+    const uint32_t *cnt, *outside, *n_outside;
+    unsigned long long *acc_out;
+    const uint32_t *wh;  // bounding box (w, h), or null: reduce the per-WG extents
+};
+
+template <int K, bool kPix>
 __global__ void __launch_bounds__(kThreads)
 kmeans_step_kernel(StepArgs a, const uint32_t *__restrict__ ext, int n_ext, uint8_t *__restrict__ img,
-                   KmState *st) {
+                   KmState *st, PixArgs px) {
     const bool done_in = st->done != 0;
     if (done_in && !a.final_pass) return;
     const int tid = threadIdx.x;
@@ -554,7 +664,13 @@ kmeans_step_kernel(StepArgs a, const uint32_t *__restrict__ ext, int n_ext, uint
         }
         if (tid == 0) s_done = done_in ? 1 : 0;
     }
-    {  // bounding box = max over the extent kernel's per-WG maxima
+    if (px.wh) {  // bounding box stored by kmeans_count_kernel
+        if (tid == 0) {
+            s_wh[0][0] = px.wh[0];
+            s_wh[1][0] = px.wh[1];
+        }
+        __syncthreads();
+    } else {  // bounding box = max over the extent kernel's per-WG maxima
         uint32_t p = 0, q = 0;
         for (int i = tid; i < n_ext; i += kThreads) { p = max(p, ext[2 * i]); q = max(q, ext[2 * i + 1]); }
         s_wh[0][tid] = p;
@@ -578,16 +694,47 @@ kmeans_step_kernel(StepArgs a, const uint32_t *__restrict__ ext, int n_ext, uint
     }
     const uint32_t w = s_wh[0][0], h = s_wh[1][0];
     const int64_t cells = (int64_t)w * h;
-    for (int64_t c = (int64_t)blockIdx.x * kThreads + tid; c < cells; c += (int64_t)gridDim.x * kThreads) {
-        const uint32_t x = (uint32_t)(c % w), y = (uint32_t)(c / w);
-        img[(int64_t)y * kImgSide + x] = (uint8_t)assign_fast<K>((float)x, (float)y, cx, cy, a.thr);
+    if constexpr (!kPix) {
+        for (int64_t c = (int64_t)blockIdx.x * kThreads + tid; c < cells; c += (int64_t)gridDim.x * kThreads) {
+            const uint32_t x = (uint32_t)(c % w), y = (uint32_t)(c / w);
+            img[(int64_t)y * kImgSide + x] = (uint8_t)assign_fast<K>((float)x, (float)y, cx, cy, a.thr);
+        }
+    } else {
+        __shared__ unsigned long long w_acc[3][K];
+        for (int i = tid; i < 3 * K; i += kThreads) (&w_acc[0][0])[i] = 0ull;
+        __syncthreads();
+        for (int64_t c = (int64_t)blockIdx.x * kThreads + tid; c < cells; c += (int64_t)gridDim.x * kThreads) {
+            const uint32_t x = (uint32_t)(c % w), y = (uint32_t)(c / w);
+            const uint32_t n = px.cnt[c];
+            if (!n) continue;
+            const uint32_t l = assign_fast<K>((float)x, (float)y, cx, cy, a.thr);
+            if (l >= (uint32_t)K) continue;
+            atomicAdd(&w_acc[0][l], (unsigned long long)n);
+            atomicAdd(&w_acc[1][l], (unsigned long long)n * x);
+            atomicAdd(&w_acc[2][l], (unsigned long long)n * y);
+        }
+        const uint32_t n_out = *px.n_outside;  // (cnt is compact: cnt[y * w + x])
+        for (uint32_t i = blockIdx.x * kThreads + tid; i < n_out; i += gridDim.x * kThreads) {
+            const uint32_t v = px.outside[i], x = v & 0xffffu, y = v >> 16;
+            const uint32_t l = assign_fast<K>((float)x, (float)y, cx, cy, a.thr);
+            if (l >= (uint32_t)K) continue;
+            atomicAdd(&w_acc[0][l], 1ull);
+            atomicAdd(&w_acc[1][l], (unsigned long long)x);
+            atomicAdd(&w_acc[2][l], (unsigned long long)y);
+        }
+        __syncthreads();
+        if (tid < 3 * a.k) {
+            const int f = tid / a.k, c = tid - f * a.k;
+            const unsigned long long sum = w_acc[f][c];
+            if (sum) atomicAdd(&px.acc_out[(int)(blockIdx.x % a.n_copies) * kAccStride + 3 * c + f], sum);
+        }
     }
 }
 
-template <int K>
+template <int K, bool kPix>
 void launch_step(dim3 grid, hipStream_t s, const StepArgs &a, const uint32_t *ext, int n_ext, uint8_t *img,
-                 KmState *st) {
-    hipLaunchKernelGGL(kmeans_step_kernel<K>, grid, dim3(kThreads), 0, s, a, ext, n_ext, img, st);
+                 KmState *st, const PixArgs &px) {
+    hipLaunchKernelGGL((kmeans_step_kernel<K, kPix>), grid, dim3(kThreads), 0, s, a, ext, n_ext, img, st, px);
 }
 
 // Launch helpers for the fast path (k <= kFastMaxK); false when k needs the generic kernel.
@@ -653,24 +800,36 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
     // per-WG packed counts must stay < 2^24 points (sum_x < 2^40)
     const int grid = grid_for(segs.n_segs);
     if (segs.n_segs * segs.stride / grid >= (1ll << 24)) return ECC_ERR_INVALID;
-    // workspace: two sets of kAccCopies accumulator replicas (pass parity; the generic path uses
-    // copy 0 of set 0), the state, the centroid history cb[2], the per-WG extents, the label image
+    // workspace: three sets of kAccCopies accumulator replicas (rotating by pass; the generic path
+    // uses copy 0 of set 0), the state, the centroid history cb[2], the per-WG extents, the label
+    // image, the per-pixel counts and the outside-point list
     constexpr size_t kAccBytes = (size_t)kAccCopies * kAccStride * 8;
-    const size_t off_st = 2 * kAccBytes;
+    const size_t off_st = 3 * kAccBytes;
     const size_t off_cb = off_st + 64;
     const size_t off_ext = ecc::align_up(off_cb + 2 * 2 * kMaxK * sizeof(float), 256);
     const size_t off_img = ecc::align_up(off_ext + (size_t)grid * 8, 256);
-    rc = ecc::ws_reserve(ctx, off_img + (size_t)kImgSide * kImgSide);
+    const size_t off_cnt = ecc::align_up(off_img + (size_t)kImgSide * kImgSide, 256);
+    const size_t off_part = off_cnt + (size_t)kImgSide * kImgSide * 4;
+    const int parts = (int)std::min<int64_t>(kHistParts, std::max<int64_t>(segs.n_segs, 1));
+    const size_t off_out = off_part + (size_t)kHistBudget * 4;
+    const int64_t n_pts_max = segs.n_segs * segs.stride;
+    rc = ecc::ws_reserve(ctx, off_out + 256 + (size_t)n_pts_max * 4);
     if (rc) return rc;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t s = ecc::as_stream(stream);
     char *ws = static_cast<char *>(ctx->ws);
-    unsigned long long *accb[2] = {reinterpret_cast<unsigned long long *>(ws),
-                                   reinterpret_cast<unsigned long long *>(ws + kAccBytes)};
+    unsigned long long *accb[3] = {reinterpret_cast<unsigned long long *>(ws),
+                                   reinterpret_cast<unsigned long long *>(ws + kAccBytes),
+                                   reinterpret_cast<unsigned long long *>(ws + 2 * kAccBytes)};
     auto *st = reinterpret_cast<KmState *>(ws + off_st);
     float *cb[2] = {reinterpret_cast<float *>(ws + off_cb), reinterpret_cast<float *>(ws + off_cb) + 2 * kMaxK};
     auto *ext = reinterpret_cast<uint32_t *>(ws + off_ext);
     auto *img = reinterpret_cast<uint8_t *>(ws + off_img);
+    auto *cnt = reinterpret_cast<uint32_t *>(ws + off_cnt);
+    auto *partial = reinterpret_cast<uint32_t *>(ws + off_part);
+    auto *n_out = reinterpret_cast<uint32_t *>(ws + off_out);
+    auto *wh = n_out + 1;
+    auto *outside = reinterpret_cast<uint32_t *>(ws + off_out + 256);
     ECC_CHECK_HIP(ctx, hipMemsetAsync(ws, 0, off_st + 64, s), "memset(kmeans acc)");
     if (segs.n_segs == 0) {
         if (iters_out)
@@ -698,16 +857,35 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
             ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 labels");
         }
     } else {
-        // label-image passes: one WG per segment (<= 32 waves/CU resident at 8 waves/SIMD)
+        // per-pixel passes: the points are counted per pixel once, every Lloyd pass is ONE launch
+        // over the occupied pixels of the bounding box (+ the outside list); labels come from the
+        // final label image
         const int grid_pts = (int)std::min<int64_t>(segs.n_segs, kMaxGridPts);
+        ECC_CHECK_HIP(ctx, hipMemsetAsync(n_out, 0, 4, s), "memset(kmeans outside)");
         {
             ECC_TIMED(ctx, s, "kmeans_extent_kernel");
             hipLaunchKernelGGL(kmeans_extent_kernel, dim3(grid), dim3(kThreads), 0, s, xy, segs, ext);
         }
+        {
+            ECC_TIMED(ctx, s, "kmeans_count_kernel");
+            static bool lds_ok = false;
+            if (!lds_ok) {
+                ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&kmeans_count_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kHistChunk * 4),
+                              "kmeans_count LDS");
+                lds_ok = true;
+            }
+            hipLaunchKernelGGL(kmeans_count_kernel, dim3(4, parts), dim3(kHistThreads), kHistChunk * 4, s, xy,
+                               segs, ext, grid, parts, partial, wh, outside, n_out);
+        }
+        {
+            ECC_TIMED(ctx, s, "kmeans_count_sum_kernel");
+            hipLaunchKernelGGL(kmeans_count_sum_kernel, dim3(1024), dim3(kThreads), 0, s, partial, parts, wh, cnt);
+        }
         auto step = [&](int it, bool final_pass) {
             StepArgs a{};
-            a.acc_in = it ? accb[(it - 1) & 1] : nullptr;
-            a.acc_zero = accb[it & 1];
+            a.acc_in = it ? accb[(it - 1) % 3] : nullptr;
+            a.acc_zero = accb[(it + 1) % 3];
             a.c_prev = it ? cb[(it - 1) & 1] : centroids;
             a.c_next = cb[it & 1];
             a.cent = centroids;
@@ -717,16 +895,18 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
             a.tol = cfg->tol;
             a.final_pass = final_pass;
             a.want_image = labels != nullptr;
-            ECC_TIMED(ctx, s, "kmeans_step_kernel");
-            if (cfg->k <= 16) launch_step<16>(dim3(512), s, a, ext, grid, img, st);
-            else launch_step<32>(dim3(512), s, a, ext, grid, img, st);
+            const PixArgs px{cnt, outside, n_out, accb[it % 3], wh};
+            if (final_pass) {
+                ECC_TIMED(ctx, s, "kmeans_step_kernel");
+                if (cfg->k <= 16) launch_step<16, false>(dim3(512), s, a, ext, grid, img, st, px);
+                else launch_step<32, false>(dim3(512), s, a, ext, grid, img, st, px);
+            } else {
+                ECC_TIMED(ctx, s, "kmeans_pixel_pass");
+                if (cfg->k <= 16) launch_step<16, true>(dim3(256), s, a, ext, grid, img, st, px);
+                else launch_step<32, true>(dim3(256), s, a, ext, grid, img, st, px);
+            }
         };
-        for (int it = 0; it < cfg->max_iters; ++it) {
-            step(it, false);
-            ECC_TIMED(ctx, s, "kmeans_xy16_kernel");
-            launch_fast<true>(cfg->k, dim3(grid_pts), s, xy, segs, cb[it & 1], cfg->threshold, accb[it & 1],
-                              kAccCopies, st, nullptr, img);
-        }
+        for (int it = 0; it < cfg->max_iters; ++it) step(it, false);
         if (cfg->max_iters > 0 || labels) step(cfg->max_iters, true);  // last update (+ image for labels)
         ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 iteration");
         if (labels) {
