@@ -184,18 +184,23 @@ def main():
     launches = stats[dominant]["launches"]
     avg_ms = kern_ms[dominant] / launches
     per_step_launches = launches / args.steps
-    # algorithmic bytes per launch (DESIGN.md "Measurement"): what the kernel must move at minimum
+    # algorithmic bytes per launch: what the kernel must move at minimum
+    geo = corner_geometry(xy_h, n, W, H)
     bytes_per_launch = {
         "downsample_hash_kernel": 4.0 * n + 4.0 * n_reps + 8.0 * n_win,   # xy in, reps + counts out
         "kmeans_xy16_kernel": 4.0 * n_reps,                               # packed u16 xy per point
         "kmeans_xy16_labels": 5.0 * n_reps,                               # + u8 label out
-        "bin_hist_kernel": 12.0 * n,                                      # xy + t
-        "bin_scatter_kernel": 20.0 * n,                                   # xy + t in, key + relative t out
-        # group_kernel: key + relative t of group g+1 (build), key of group g (arc), corner flag
-        # out; n_groups + 1 launches
-        "group_kernel": 13.0 * n / per_step_launches,
+        "kmeans_count_kernel": 4.0 * n_reps,                              # packed u16 xy per point
+        "kmeans_pixel_pass": 4.0 * W * H,                                 # per-pixel counts (bbox <= sensor)
+        # corner stage: xy + t in, key + t32 out (+ per-slice tile offsets)
+        "slice_sort_kernel": 20.0 * n + 4.0 * geo["slices"] * (geo["tiles"] + 2),
+        # key + t32 in, pair entries out, per-(group, pixel) slice mask + last t out
+        "pair_build_kernel": 8.0 * n + 8.0 * geo["pairs"] + 12.0 * geo["hw_groups"],
+        # each pair entry read once, B_g per (group, pixel), corner-pair bits out
+        "arc_kernel": 8.0 * geo["pairs"] + 8.0 * geo["hw_groups"] + 784.0 * geo["items"],
+        "flags_kernel": 5.0 * n,                                          # keys in, flags out
+        "sae_prefix_kernel": 20.0 * geo["hw_groups"] + 16.0 * W * H,
         "nms_kernel": 1.0 * n,                                            # corner flags
-        "kmeans_step_kernel": 0.0,
     }.get(dominant, 0.0)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     # HBM bytes per launch of the same kernel from the newest committed PMC summary
@@ -297,6 +302,20 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def corner_geometry(xy, n, W, H, S=16384, group=32, tile=14):
+    """Counts the corner stage's byte table needs: distinct (slice, pixel) pairs of in-sensor
+    events (= pair entries), (group, tile) items, (group, pixel) image cells."""
+    x = (xy & 0xFFFF).astype(np.int64)
+    y = (xy >> 16).astype(np.int64)
+    inside = (x < W) & (y < H)
+    s = np.arange(n, dtype=np.int64) // S
+    pairs = int(np.unique((s * (W * H) + y * W + x)[inside]).size)
+    slices = (n + S - 1) // S
+    groups = (slices + group - 1) // group
+    tiles = ((W + tile - 1) // tile) * ((H + tile - 1) // tile)
+    return {"pairs": pairs, "slices": slices, "tiles": tiles, "items": groups * tiles, "hw_groups": groups * W * H}
 
 
 def cpu_baseline(args, W, H, K, I):

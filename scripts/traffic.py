@@ -22,6 +22,8 @@ def short(name: str) -> str:
         return "kmeans_xy16_labels" if re.search(r"<(\d+, )?false[,>]", name) else "kmeans_xy16_kernel"
     if base == "nms_grid_kernel":
         return "nms_kernel"
+    if base == "kmeans_step_kernel" and re.search(r"<\d+, true>", name):
+        return "kmeans_pixel_pass"
     return base
 
 
