@@ -487,6 +487,7 @@ __host__ __device__ inline int parts_used(int parts, int64_t cells) {
     return (int)(p < 1 ? 1 : (p < parts ? p : parts));
 }
 constexpr int kHistUnroll = 4;
+constexpr int kPixGrid = 256;  // pixel-pass workgroups (64 measured slower: the per-pixel assignment dominates)
 
 __device__ __forceinline__ void reduce_extent(const uint32_t *__restrict__ ext, int n_ext, uint32_t *s_red,
                                               uint32_t &w, uint32_t &h) {
@@ -566,7 +567,15 @@ kmeans_count_sum_kernel(const uint32_t *__restrict__ partial, int parts, const u
     parts = parts_used(parts, cells);
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < cells; i += (int64_t)gridDim.x * kThreads) {
         uint32_t t = 0;
-        for (int m = 0; m < parts; ++m) t += partial[(int64_t)m * cells + i];
+        int m = 0;
+        for (; m + 8 <= parts; m += 8) {  // eight independent loads in flight
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = partial[(int64_t)(m + u) * cells + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t += v[u];
+        }
+        for (; m < parts; ++m) t += partial[(int64_t)m * cells + i];
         cnt[i] = t;
     }
 }
@@ -902,8 +911,8 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
                 else launch_step<32, false>(dim3(512), s, a, ext, grid, img, st, px);
             } else {
                 ECC_TIMED(ctx, s, "kmeans_pixel_pass");
-                if (cfg->k <= 16) launch_step<16, true>(dim3(256), s, a, ext, grid, img, st, px);
-                else launch_step<32, true>(dim3(256), s, a, ext, grid, img, st, px);
+                if (cfg->k <= 16) launch_step<16, true>(dim3(kPixGrid), s, a, ext, grid, img, st, px);
+                else launch_step<32, true>(dim3(kPixGrid), s, a, ext, grid, img, st, px);
             }
         };
         for (int it = 0; it < cfg->max_iters; ++it) step(it, false);
