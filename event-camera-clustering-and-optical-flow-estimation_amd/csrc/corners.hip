@@ -776,7 +776,8 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
         const uint32_t below = below_mask(j);
         int r3 = -1;
-        if (fast) {
+        if (g.dbg == 6) r3 = (pi & 7) == 0;  // profiling: circle 3 replaced by a trivial predicate
+        else if (fast) {
             uint32_t k3[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) k3[k] = (win_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
@@ -793,7 +794,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         }
     }
     __syncthreads();
-    const int n4 = min(L.q4n, kQ4Cap);
+    const int n4 = g.dbg == 5 ? 0 : min(L.q4n, kQ4Cap);
     for (int qi = tid; qi < n4; qi += kArcThreads) circle4(L.q4[qi]);
     __syncthreads();
     if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
