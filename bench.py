@@ -4,8 +4,8 @@
 
 One step = one pass of the hot path over one resident batch of synthetic events:
   hash downsample (8192-event windows)  ->  k-means k=16 on the representatives (10 Lloyd
-  iterations + final labels)  ->  SAE + FAST/arc corner detection (16384-event slices)  ->
-  greedy 15x15 box NMS per slice.
+  iterations + final labels), and SAE + FAST/arc corner detection (16384-event slices)  ->
+  greedy 15x15 box NMS per slice.  On one GPU the two chains run on two HIP streams.
 The corner tracker (sequential over slices) is timed separately and reported in µs/slice.
 
 Single GPU:  python bench.py [--steps K --warmup W]
@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the RAW (EVT 3.0 / 2.0) decode measurement")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the single-GPU step as a captured HIP graph (measured equal to eager)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for rehearsal")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on device 0 (with --dist-backend gloo)")
@@ -128,16 +130,29 @@ def main():
         ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
         ctx.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, nms_out, nms_cnt)
 
+    # single GPU: downsample -> k-means and the corner chain read the same resident batch and are
+    # independent, so they run on two streams (fork/join with events) and overlap
+    s2, ev_fork, ev_join = ecc.P(), ecc.P(), ecc.P()
+    if not dist:
+        ecc.check(lib.ecc_stream_create(ecc.C.byref(s2)), "stream")
+        ecc.check(lib.ecc_event_create(ecc.C.byref(ev_fork)), "event")
+        ecc.check(lib.ecc_event_create(ecc.C.byref(ev_join)), "event")
+
     def step():
         if dist:
             return step_sharded()
+        ecc.check(lib.ecc_event_record(ev_fork, ctx.stream))
+        ecc.check(lib.ecc_stream_wait_event(s2, ev_fork))
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
-                                          uniq.ptr, rep.ptr, ctx.stream), "downsample")
-        ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, ctx.stream))
-        ctx.kmeans_xy16(rep_xy, n_win, 8192, uniq, d_c, kcfg, labels)
+                                          uniq.ptr, rep.ptr, s2), "downsample")
+        ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, s2))
+        ecc.check(lib.ecc_kmeans_run_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, ecc.C.byref(kcfg), d_c.ptr,
+                                          labels.ptr, None, s2), "kmeans")
+        ecc.check(lib.ecc_event_record(ev_join, s2))
         ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
         ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
         ctx.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, nms_out, nms_cnt)
+        ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_join))
 
     for _ in range(args.warmup):
         step()
@@ -145,6 +160,25 @@ def main():
     if ctx.fast_detect_status() != 0:
         raise RuntimeError("fast_detect reported a status error")
     n_reps = int(uniq.numpy().sum())
+    # --graph: the step's ~40 launches and memsets are captured once into a HIP graph
+    # (ecc_graph_*) and replayed — the same kernels on the same buffers, without per-launch
+    # host dispatch (measured equal to eager: the GPU is the bottleneck).  The sharded step
+    # interleaves RCCL collectives and stays eager.
+    graph = None
+    if not dist and args.graph:
+        gp = ecc.P()
+        ecc.check(lib.ecc_graph_begin(ctx.stream), "ecc_graph_begin")
+        step()
+        ecc.check(lib.ecc_graph_end(ctx.stream, ecc.C.byref(gp)), "ecc_graph_end")
+        graph = gp.value
+        ecc.check(lib.ecc_graph_launch(graph, ctx.stream), "ecc_graph_launch")  # one untimed replay
+        ctx.sync()
+
+    def timed_step():
+        if graph is not None:
+            ecc.check(lib.ecc_graph_launch(graph, ctx.stream), "ecc_graph_launch")
+        else:
+            step()
 
     # 1. the timed region: K steps, uninstrumented (a timestamped HIP event around every launch
     #    drains the queue between kernels and costs ~0.6 ms/step here)
@@ -153,7 +187,7 @@ def main():
     ctx.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        timed_step()
     ctx.sync()
     if dist:
         dist.barrier()
@@ -265,6 +299,8 @@ def main():
             del d_words, d_oxy, d_ot, d_op, d_on
 
     value = world * args.steps * n / elapsed / 1e6
+    if graph is not None:
+        lib.ecc_graph_destroy(graph)
     result = {
         "metric": "Mevents/s (downsample+cluster+corner)",
         "value": round(value, 2),
@@ -284,12 +320,13 @@ def main():
                         f"{n} events/GPU/step (BASELINE configs C2-C4)",
             "events_per_gpu": n, "reps_per_gpu": n_reps, "width": W, "height": H, "k": K,
             "kmeans_iters": I, "parallelism": f"time-window shards x{world}",
+            "launch": "hipGraph replay of the captured step" if graph is not None else "eager launches",
         },
         "roofline": {
             "kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "avg_launch_ms": round(avg_ms, 5), "algorithmic_bytes_per_launch": bytes_per_launch,
-            "timing": f"HIP events around every launch in a second {args.steps}-step pass "
+            "timing": f"HIP events around every launch in a second, eager {args.steps}-step pass "
                       f"({instrumented / args.steps * 1e3:.3f} ms/step instrumented)",
         },
         "stages_ms_per_step": {k: round(v / args.steps, 4) for k, v in sorted(kern_ms.items())},

@@ -1028,9 +1028,14 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     ECC_CHECK_HIP(ctx, hipMemsetAsync(corner_flags, 0, (size_t)n, s), "memset(flags)");
     {
         const size_t lds = (size_t)nb * 4 + kSortChunk * 4;  // > 64 KiB: opt in (gfx950 has 160 KiB)
-        ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&slice_sort_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                      "slice_sort LDS");
+        static int lds_set = 0;
+        if ((int)lds > lds_set) {
+            ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&slice_sort_kernel),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)((size_t)kMaxTiles * 4 + 4 + kSortChunk * 4)),
+                          "slice_sort LDS");
+            lds_set = kMaxTiles * 4 + 4 + kSortChunk * 4;
+        }
         ECC_TIMED(ctx, s, "slice_sort_kernel");
         hipLaunchKernelGGL(slice_sort_kernel, dim3((unsigned)g.n_slices), dim3(kSortThreads), lds, s, xy, t, g,
                            so, first_border, ctx->flags);

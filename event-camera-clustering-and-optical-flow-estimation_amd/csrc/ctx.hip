@@ -216,6 +216,10 @@ ECC_API int ecc_event_destroy(void *event) { ECC_RT(hipEventDestroy(reinterpret_
 ECC_API int ecc_event_record(void *event, ecc_stream_t s) {
     ECC_RT(hipEventRecord(reinterpret_cast<hipEvent_t>(event), ecc::as_stream(s)));
 }
+ECC_API int ecc_stream_wait_event(ecc_stream_t s, void *event) {
+    if (!event) return ECC_ERR_INVALID;
+    ECC_RT(hipStreamWaitEvent(ecc::as_stream(s), reinterpret_cast<hipEvent_t>(event), 0));
+}
 ECC_API int ecc_event_elapsed_ms(float *ms, void *start, void *stop) {
     if (!ms) return ECC_ERR_INVALID;
     if (hipEventSynchronize(reinterpret_cast<hipEvent_t>(stop)) != hipSuccess) return ECC_ERR_HIP;
@@ -236,5 +240,44 @@ ECC_API int ecc_util_sqrt_f32(ecc_ctx *ctx, const float *in, float *out, int64_t
     const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(util_sqrt_kernel, dim3((unsigned)blocks), dim3(256), 0, ecc::as_stream(stream), in, out, n);
     ECC_CHECK_LAUNCH(ctx, "util_sqrt_kernel");
+    return ECC_OK;
+}
+
+// ---- step capture (HIP graphs) --------------------------------------------------------------
+struct ecc_graph {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+};
+
+ECC_API int ecc_graph_begin(ecc_stream_t stream) {
+    if (!stream) return ECC_ERR_INVALID;
+    return hipStreamBeginCapture(ecc::as_stream(stream), hipStreamCaptureModeRelaxed) == hipSuccess ? ECC_OK
+                                                                                                  : ECC_ERR_HIP;
+}
+
+ECC_API int ecc_graph_end(ecc_stream_t stream, ecc_graph **out) {
+    if (!stream || !out) return ECC_ERR_INVALID;
+    *out = nullptr;
+    auto *g = new ecc_graph();
+    if (hipStreamEndCapture(ecc::as_stream(stream), &g->graph) != hipSuccess || !g->graph ||
+        hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0) != hipSuccess) {
+        if (g->graph) (void)hipGraphDestroy(g->graph);
+        delete g;
+        return ECC_ERR_HIP;
+    }
+    *out = g;
+    return ECC_OK;
+}
+
+ECC_API int ecc_graph_launch(ecc_graph *graph, ecc_stream_t stream) {
+    if (!graph) return ECC_ERR_INVALID;
+    return hipGraphLaunch(graph->exec, ecc::as_stream(stream)) == hipSuccess ? ECC_OK : ECC_ERR_HIP;
+}
+
+ECC_API int ecc_graph_destroy(ecc_graph *graph) {
+    if (!graph) return ECC_OK;
+    if (graph->exec) (void)hipGraphExecDestroy(graph->exec);
+    if (graph->graph) (void)hipGraphDestroy(graph->graph);
+    delete graph;
     return ECC_OK;
 }

@@ -119,10 +119,15 @@ _sigs = {
     "ecc_event_destroy": (C.c_int, [P]),
     "ecc_event_record": (C.c_int, [P, P]),
     "ecc_event_elapsed_ms": (C.c_int, [C.POINTER(C.c_float), P, P]),
+    "ecc_stream_wait_event": (C.c_int, [P, P]),
     "ecc_ctx_set_timing": (C.c_int, [P, C.c_int]),
     "ecc_ctx_timing_reset": (C.c_int, [P]),
     "ecc_ctx_timing_report": (C.c_int, [P, C.c_char_p, C.c_size_t]),
     "ecc_util_sqrt_f32": (C.c_int, [P, P, P, i64, P]),
+    "ecc_graph_begin": (C.c_int, [P]),
+    "ecc_graph_end": (C.c_int, [P, C.POINTER(P)]),
+    "ecc_graph_launch": (C.c_int, [P, P]),
+    "ecc_graph_destroy": (C.c_int, [P]),
     "ecc_hash_cfg_default": (None, [C.POINTER(HashCfg)]),
     "ecc_downsample_hash": (C.c_int, [P, P, i64, C.POINTER(HashCfg), P, P, P, P, P]),
     "ecc_kmeans_cfg_default": (None, [C.POINTER(KmeansCfg)]),

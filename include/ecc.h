@@ -74,6 +74,7 @@ int ecc_event_create(void **event);
 int ecc_event_destroy(void *event);
 int ecc_event_record(void *event, ecc_stream_t stream);
 int ecc_event_elapsed_ms(float *ms, void *start, void *stop); /* synchronises `stop` */
+int ecc_stream_wait_event(ecc_stream_t stream, void *event); /* stream waits for `event` */
 
 /* Per-kernel timing (the reference's CL_QUEUE_PROFILING_ENABLE + clGetEventProfilingInfo,
  * SMP/…opencl_store.cpp:263-264, 406-412): when enabled, every kernel this context launches
@@ -82,6 +83,18 @@ int ecc_event_elapsed_ms(float *ms, void *start, void *stop); /* synchronises `s
 int ecc_ctx_set_timing(ecc_ctx *ctx, int enable);
 int ecc_ctx_timing_reset(ecc_ctx *ctx);
 int ecc_ctx_timing_report(ecc_ctx *ctx, char *buf, size_t cap);
+
+/* Step capture with HIP graphs (no reference counterpart: the reference re-issues every OpenCL
+ * command per slice, SMP/…opencl_store.cpp:370-459).  Work issued on `stream` between
+ * ecc_graph_begin and ecc_graph_end is recorded, not run; ecc_graph_launch replays it with the
+ * same pointers and sizes.  Run the sequence once eagerly first (workspaces are allocated
+ * outside the capture) and keep per-kernel timing off while capturing.  `stream` must be a
+ * created stream, not the null stream. */
+typedef struct ecc_graph ecc_graph;
+int ecc_graph_begin(ecc_stream_t stream);
+int ecc_graph_end(ecc_stream_t stream, ecc_graph **out);
+int ecc_graph_launch(ecc_graph *graph, ecc_stream_t stream);
+int ecc_graph_destroy(ecc_graph *graph);
 
 /* Numerics self-check: out[i] = correctly rounded fp32 sqrt(in[i]) as used by every bit-exact
  * kernel of this library (device pointers).  Lets tests pin the device arithmetic against

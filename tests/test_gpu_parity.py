@@ -660,3 +660,56 @@ def test_dbscan_extract_rejects_short_lists(ecc, gpu):
     gpu.dbscan_extract(1, n, None, d_off, d_nbr, 3, 1, 1 << 30, d_lab, d_nc, None, 0, d_nd)
     assert gpu.dbscan_status() == ecc.ERR_CAPACITY
     assert (d_lab.numpy() == -1).all() and int(d_nc.numpy()[0]) == 0
+
+
+# ------------------------------------------------------------------------------ HIP graph replay
+def test_graph_replay_matches_eager(ecc, orc, gpu):
+    """ecc_graph_begin/end/launch: a captured downsample -> k-means -> corners -> NMS step replays
+    to the same outputs as the eager calls (and as the oracle's corner flags)."""
+    W, H = 346, 260
+    n = 16384 * 40
+    xy, t, _ = ecc.gen_events(n, seed=77, width=W, height=H)
+    d_xy, d_t = dev(ecc, xy), dev(ecc, t)
+    n_win = (n + 8191) // 8192
+    hcfg = ecc.hash_cfg(window=8192)
+    rep_xy, uniq, rep = ecc.DeviceArray(n_win * 8192, np.uint32), ecc.DeviceArray(n_win, np.int32), ecc.DeviceArray(n_win, np.int32)
+    K = 16
+    c0 = np.stack([np.linspace(20, W - 20, K), np.linspace(20, H - 20, K)[::-1]], 1).astype(np.float32).ravel()
+    d_c0, d_c = dev(ecc, c0), ecc.DeviceArray(2 * K, np.float32)
+    labels = ecc.DeviceArray(n_win * 8192, np.uint8)
+    kcfg = ecc.kmeans_cfg(k=K, max_iters=5, tol=-1.0)
+    ccfg = ecc.corner_cfg(width=W, height=H)
+    sae, flags = ecc.DeviceArray(W * H, np.int64), ecc.DeviceArray(n, np.uint8)
+    ns, cap = n // 16384, 4096
+    nms_out, nms_cnt = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE), ecc.DeviceArray(ns, np.int32)
+    lib = ecc.lib
+
+    def step():
+        ecc.check(lib.ecc_downsample_hash(gpu.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None, uniq.ptr,
+                                          rep.ptr, gpu.stream))
+        ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, gpu.stream))
+        gpu.kmeans_xy16(rep_xy, n_win, 8192, uniq, d_c, kcfg, labels)
+        ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, gpu.stream))
+        gpu.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
+        gpu.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, nms_out, nms_cnt)
+
+    step()
+    gpu.sync()
+    eager = [a.numpy().copy() for a in (rep_xy, d_c, labels, sae, flags, nms_cnt)]
+    o_flags, _ = orc.fast_detect(xy, t, W, H)
+    assert (eager[4] == o_flags).all()
+    gp = ecc.P()
+    ecc.check(lib.ecc_graph_begin(gpu.stream))
+    step()
+    ecc.check(lib.ecc_graph_end(gpu.stream, ecc.C.byref(gp)))
+    for a in (rep_xy, d_c, labels, sae, flags, nms_cnt):  # poison the outputs, then replay twice
+        ecc.check(lib.ecc_memset_async(a.ptr, 0xA5, a.nbytes, gpu.stream))
+    for _ in range(2):
+        ecc.check(lib.ecc_graph_launch(gp.value, gpu.stream))
+    gpu.sync()
+    ecc.check(lib.ecc_graph_destroy(gp.value))
+    u = uniq.numpy()
+    valid = (np.arange(8192)[None, :] < u[:, None]).ravel()  # written slots of the windowed outputs
+    for e, a, windowed in zip(eager, (rep_xy, d_c, labels, sae, flags, nms_cnt), (1, 0, 1, 0, 0, 0)):
+        got = a.numpy()
+        assert (got[valid] == e[valid]).all() if windowed else (got == e).all()
