@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the RAW (EVT 3.0 / 2.0) decode measurement")
+    ap.add_argument("--serial", action="store_true",
+                    help="one stream for the whole step (isolated per-kernel times for profiling)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the single-GPU step as a captured HIP graph (measured equal to eager)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for rehearsal")
@@ -133,8 +135,11 @@ def main():
     # single GPU: downsample -> k-means and the corner chain read the same resident batch and are
     # independent, so they run on two streams (fork/join with events) and overlap
     s2, ev_fork, ev_join = ecc.P(), ecc.P(), ecc.P()
+    if args.serial:
+        s2 = ecc.P(ctx.stream)
     if not dist:
-        ecc.check(lib.ecc_stream_create(ecc.C.byref(s2)), "stream")
+        if not args.serial:
+            ecc.check(lib.ecc_stream_create(ecc.C.byref(s2)), "stream")
         ecc.check(lib.ecc_event_create(ecc.C.byref(ev_fork)), "event")
         ecc.check(lib.ecc_event_create(ecc.C.byref(ev_join)), "event")
 
@@ -142,13 +147,13 @@ def main():
         if dist:
             return step_sharded()
         ecc.check(lib.ecc_event_record(ev_fork, ctx.stream))
-        ecc.check(lib.ecc_stream_wait_event(s2, ev_fork))
+        ecc.check(lib.ecc_stream_wait_event(s2.value, ev_fork))
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
-                                          uniq.ptr, rep.ptr, s2), "downsample")
-        ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, s2))
+                                          uniq.ptr, rep.ptr, s2.value), "downsample")
+        ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, s2.value))
         ecc.check(lib.ecc_kmeans_run_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, ecc.C.byref(kcfg), d_c.ptr,
-                                          labels.ptr, None, s2), "kmeans")
-        ecc.check(lib.ecc_event_record(ev_join, s2))
+                                          labels.ptr, None, s2.value), "kmeans")
+        ecc.check(lib.ecc_event_record(ev_join, s2.value))
         ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
         ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
         ctx.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, nms_out, nms_cnt)
