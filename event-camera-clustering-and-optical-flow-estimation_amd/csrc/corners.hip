@@ -624,16 +624,10 @@ constexpr int kStageUnroll = 4;
 // covers (own tile: all; edge neighbours: the 3 facing sub-regions; corners: 1) — 13 at most.
 constexpr int kMaxSeg = 13;
 
-__global__ void __launch_bounds__(kArcThreads, 2)  // two 8-wave workgroups per CU (LDS)
-arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
-           const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
-           const int64_t *__restrict__ gB, uint32_t *__restrict__ res) {
-    __shared__ ArcLds L;
-    // XCD-aware order: workgroup b runs on XCD b % 8, so XCD x takes the contiguous item range
-    // [x * per, (x + 1) * per) — neighbouring tiles of one group share that XCD's L2.
-    const int64_t per = gridDim.x / 8;
-    const int64_t item = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (item >= n_items) return;
+__device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const int64_t *__restrict__ t, const CornerGeom &g,
+                                               const int64_t *__restrict__ item_base,
+                                               const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
+                                               const int64_t *__restrict__ gB, uint32_t *__restrict__ res) {
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
     if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
@@ -693,7 +687,6 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     __syncthreads();
     if (L.seg_pref[1] == 0) return;  // no events in the tile: nothing to flag
     const int total = L.seg_pref[kMaxSeg];
-    if (g.dbg == 3) return;
     int pref[kMaxSeg + 1];
 #pragma unroll
     for (int c = 0; c <= kMaxSeg; ++c) pref[c] = L.seg_pref[c];  // uniform (SGPRs)
@@ -733,7 +726,6 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     }
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
-    if (g.dbg == 2) return;
 
     // (c) clamped B_g per window pixel
     if (win_lane) {
@@ -743,7 +735,6 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         L.mb[wp].bc = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
     }
     __syncthreads();
-    if (g.dbg == 1) return;
 
     // (d) each eligible pair of the tile is tested once; circle-3 survivors are queued so that
     //     circle 4 runs on as few waves as possible
@@ -776,8 +767,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
         const uint32_t below = below_mask(j);
         int r3 = -1;
-        if (g.dbg == 6) r3 = (pi & 7) == 0;  // profiling: circle 3 replaced by a trivial predicate
-        else if (fast) {
+        if (fast) {
             uint32_t k3[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) k3[k] = (win_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
@@ -794,10 +784,282 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         }
     }
     __syncthreads();
-    const int n4 = g.dbg == 5 ? 0 : min(L.q4n, kQ4Cap);
+    const int n4 = min(L.q4n, kQ4Cap);
     for (int qi = tid; qi < n4; qi += kArcThreads) circle4(L.q4[qi]);
     __syncthreads();
     if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
+}
+
+// ---- compact window values (the common case) -------------------------------------------------
+// Window pixel wp keeps the values of the slices that touched it, ascending j, at
+// vals[pix[wp].off ...]; the value an event of slice j sees is vals[off + popc(mask & ((2 << j)
+// - 1)) - 1], or the clamped B_g when no slice <= j touched it.  ~36 KB of LDS instead of the
+// dense planes' ~80 KB: three 8-wave workgroups per CU.  Windows with more than kValCap values
+// go to the overflow list (arc_dense_kernel).
+constexpr int kValCap = 4096;
+
+struct PixInfo {
+    uint32_t mask;  // slices of the group that touched the pixel
+    uint32_t bc;    // clamped B_g
+    uint32_t off;   // first value in vals[]
+    uint32_t pad;
+};
+
+struct SparseLds {
+    uint32_t vals[kValCap];             // 16 KiB
+    PixInfo pix[kWinPix];               // 7.6 KiB
+    uint32_t res[kPairWords];
+    uint16_t tasks[kGroup * kTilePix];  // the tile's eligible pairs (j * 196 + pixel)
+    uint16_t q4[kQ4Cap];
+    int64_t wave_min[kWaves];
+    int32_t wave_tot[kWaves];
+    int32_t exact_only, mixed, n_tasks, q4n;
+    int64_t seg_lo[16];
+    int32_t seg_pref[16];
+    int32_t seg_off[16];
+};
+
+__device__ __forceinline__ uint32_t sparse_value(const SparseLds &L, int wp, uint32_t below) {
+    const PixInfo p = L.pix[wp];
+    const uint32_t mk = p.mask & below;
+    return mk ? L.vals[p.off + __popc(mk) - 1] : p.bc;
+}
+
+template <int N>
+__device__ __forceinline__ void sparse_exact_values(const SparseLds *L, int wp0, int64_t q0, uint32_t below,
+                                                    const int8_t *dy, const int8_t *dx, const ExactCtx &c,
+                                                    int64_t (&v)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int wp = wp0 + dy[k] * kWin + dx[k];
+        const uint32_t mk = L->pix[wp].mask & below;
+        const uint32_t tv = mk ? L->vals[L->pix[wp].off + __popc(mk) - 1] : 0u;
+        v[k] = !mk      ? c.Bg[q0 + (int64_t)dy[k] * c.W + dx[k]]
+               : c.narrow ? c.Lt + (int64_t)tv
+                          : c.t[c.grp_first + tv - 1u];
+    }
+}
+
+__device__ __noinline__ bool sparse_exact_test(const SparseLds *L, int wp0, int64_t q0, int j, bool c3, const ExactCtx c) {
+    const uint32_t below = below_mask(j);
+    if (c3) {
+        int64_t v3[16];
+        sparse_exact_values<16>(L, wp0, q0, below, c3dy, c3dx, c, v3);
+        return arc_streak<16, 3, 6>(v3);
+    }
+    int64_t v4[20];
+    sparse_exact_values<20>(L, wp0, q0, below, c4dy, c4dx, c, v4);
+    return arc_streak<20, 4, 8>(v4);
+}
+
+constexpr int kSparseHold = kValCap / kArcThreads;  // entries per lane, held between the two passes
+
+__global__ void __launch_bounds__(kArcThreads, 6)  // 6 waves/SIMD: three 8-wave workgroups per CU
+arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
+           const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
+           const int64_t *__restrict__ gB, uint32_t *__restrict__ res, int64_t *__restrict__ over,
+           uint32_t *__restrict__ n_over) {
+    __shared__ SparseLds L;
+    // XCD-aware order: workgroup b runs on XCD b % 8, so XCD x takes the contiguous item range
+    // [x * per, (x + 1) * per) — neighbouring tiles of one group share that XCD's L2.
+    const int64_t per = gridDim.x / 8;
+    const int64_t item = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (item >= n_items) return;
+    const int64_t grp = item / g.n_tiles;
+    const int tile = (int)(item % g.n_tiles);
+    if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t HW = (int64_t)g.H * g.W;
+    int tx, ty;
+    tile_origin_xy(g, tile, tx, ty);
+    const int x0 = tx * kTile, y0 = ty * kTile;
+    const int wx0 = x0 - kHalo, wy0 = y0 - kHalo;
+    const GroupRef gr = group_ref(t, g, grp);
+    const int64_t grp_first = gr.first, Lt = gr.Lt;
+    const bool narrow = gr.narrow;
+    const int64_t *Bg = gB + grp * HW;
+
+    // (a) the window pixel's B_g (lane wp < 484), the segment table (lanes 0..12), cleared masks
+    const int wp = tid;
+    const bool win_lane = wp < kWinPix;
+    const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
+    const bool in = win_lane && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
+    const int64_t bq = in ? Bg[(int64_t)wy * g.W + wx] : INT64_MAX;  // INT64_MAX: outside (never read)
+    if (win_lane) L.pix[wp].mask = 0u;
+    for (int w = tid; w < kPairWords; w += kArcThreads) L.res[w] = 0u;
+    if (tid == 0) {
+        L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
+        L.mixed = 0;
+        L.n_tasks = 0;
+        L.q4n = 0;
+    }
+    if (tid < kMaxSeg) {
+        constexpr int8_t sx[kMaxSeg] = {0, 0, 0, -1, 1, -1, 1, -1, 1, -1, 1, -1, 1};
+        constexpr int8_t sy[kMaxSeg] = {0, -1, 1, -1, -1, 1, 1, 0, 0, 0, 0, 0, 0};
+        constexpr int8_t r0[kMaxSeg] = {0, 6, 0, 8, 6, 2, 0, 2, 0, 5, 3, 8, 6};
+        constexpr int8_t r1[kMaxSeg] = {8, 8, 2, 8, 6, 2, 0, 2, 0, 5, 3, 8, 6};
+        const int nx = tx + sx[tid], ny = ty + sy[tid];
+        int64_t b0 = 0;
+        int len = 0;
+        if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
+            const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
+            const int s0 = r0[tid] ? sub_end[bi * kSub + r0[tid] - 1] : 0;
+            b0 = item_base[bi] + s0;
+            len = sub_end[bi * kSub + r1[tid]] - s0;
+        }
+        int incl = len;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const int v = __shfl_up(incl, o, 16);
+            if (tid >= o) incl += v;
+        }
+        L.seg_lo[tid] = b0;
+        L.seg_pref[tid + 1] = incl;
+        L.seg_off[tid] = (sy[tid] * kTile) * kWin + sx[tid] * kTile + kHalo * kWin + kHalo;
+        if (tid == 0) L.seg_pref[0] = 0;
+    }
+    __syncthreads();
+    if (L.seg_pref[1] == 0) return;  // no events in the tile: nothing to flag
+    const int total = L.seg_pref[kMaxSeg];
+    if (total > kValCap) {  // too many values for the compact list: the dense kernel takes it
+        if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
+        return;
+    }
+    int pref[kMaxSeg + 1];
+#pragma unroll
+    for (int c = 0; c <= kMaxSeg; ++c) pref[c] = L.seg_pref[c];  // uniform
+
+    // (b) pass 1: slice bits of every window pixel; the own tile's eligible pairs become tasks;
+    //     the entries stay in registers for pass 2
+    PairEntry ent[kSparseHold];
+    int ewp[kSparseHold];
+#pragma unroll
+    for (int u = 0; u < kSparseHold; ++u) {
+        const int i = u * kArcThreads + tid;
+        int r = 0;
+#pragma unroll
+        for (int c = 1; c < kMaxSeg; ++c) r += (i >= pref[c]) ? 1 : 0;
+        ent[u] = (i < total) ? entries[L.seg_lo[r] + (i - L.seg_pref[r])] : PairEntry{0u, 0u};
+        ewp[u] = (i < total) ? r : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kSparseHold; ++u) {
+        if (ewp[u] < 0) continue;
+        const int r = ewp[u];
+        const int lp = (int)(ent[u].meta & 255u), j = (int)(ent[u].meta >> 8);
+        ewp[u] = L.seg_off[r] + (lp / kTile) * kWin + lp % kTile;
+        atomicOr(&L.pix[ewp[u]].mask, 1u << j);
+        if (r == 0 && (int64_t)grp * kGroup + j >= g.first_detect && !is_border(x0 + lp % kTile, y0 + lp / kTile, g))
+            L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)(j * kTilePix + lp);
+    }
+    int64_t bmin = bq;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t x = __shfl_xor(bmin, o);
+        bmin = x < bmin ? x : bmin;
+    }
+    if (lane == 0) L.wave_min[wave] = bmin;
+    __syncthreads();
+
+    // (c) per window pixel: clamped B_g, value count, wave prefix of the counts
+    const uint32_t mk_w = win_lane ? L.pix[wp].mask : 0u;
+    const int cnt = __popc(mk_w);
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) L.wave_tot[wave] = incl;
+    if (win_lane) {
+        int64_t vz = INT64_MAX;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
+        L.pix[wp].bc = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
+    }
+    __syncthreads();
+    if (win_lane) {
+        int off = incl - cnt;
+        for (int w = 0; w < wave; ++w) off += L.wave_tot[w];
+        L.pix[wp].off = (uint32_t)off;
+    }
+    __syncthreads();
+    // (d) pass 2: each value at its pixel's list position (ascending slice)
+#pragma unroll
+    for (int u = 0; u < kSparseHold; ++u) {
+        if (ewp[u] < 0) continue;
+        const int j = (int)(ent[u].meta >> 8);
+        const PixInfo p = L.pix[ewp[u]];
+        L.vals[p.off + __popc(p.mask & ((1u << j) - 1u))] = ent[u].v;
+    }
+    __syncthreads();
+
+    // (e) tests, as the dense kernel's (lookups through the compact lists)
+    const int n_tasks = L.n_tasks;
+    const bool fast = !L.exact_only;
+    const bool ties_exact = !L.mixed;
+    const ExactCtx ec{Bg, t, grp_first, Lt, g.W, narrow};
+    auto circle4 = [&](int pi) {
+        const int j = pi / kTilePix, lp = pi % kTilePix;
+        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        const uint32_t below = below_mask(j);
+        int r4 = -1;
+        if (fast) {
+            uint32_t k4[32];
+#pragma unroll
+            for (int k = 0; k < 20; ++k) k4[k] = (sparse_value(L, wp0 + c4dy[k] * kWin + c4dx[k], below) << 5) | k;
+#pragma unroll
+            for (int k = 20; k < 32; ++k) k4[k] = 0u;
+            r4 = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
+        }
+        if (r4 < 0) {
+            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
+            r4 = sparse_exact_test(&L, wp0, q0, j, false, ec) ? 1 : 0;
+        }
+        if (r4 == 1) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
+    };
+    for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+        const int pi = L.tasks[ti];
+        const int j = pi / kTilePix, lp = pi % kTilePix;
+        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        const uint32_t below = below_mask(j);
+        int r3 = -1;
+        if (fast) {
+            uint32_t k3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) k3[k] = (sparse_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
+            r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+        }
+        if (r3 < 0) {
+            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
+            r3 = sparse_exact_test(&L, wp0, q0, j, true, ec) ? 1 : 0;
+        }
+        if (r3 == 1) {
+            const int qi = atomicAdd(&L.q4n, 1);
+            if (qi < kQ4Cap) L.q4[qi] = (uint16_t)pi;
+            else circle4(pi);  // queue full (rare): test here
+        }
+    }
+    __syncthreads();
+    const int n4 = min(L.q4n, kQ4Cap);
+    for (int qi = tid; qi < n4; qi += kArcThreads) circle4(L.q4[qi]);
+    __syncthreads();
+    if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
+}
+
+// The windows above the compact list's capacity (arc_kernel's overflow list), each with the
+// dense per-slice planes.
+__global__ void __launch_bounds__(kArcThreads, 4)  // 4 waves/SIMD: two 8-wave workgroups per CU
+arc_dense_kernel(const int64_t *__restrict__ t, CornerGeom g, const int64_t *__restrict__ over,
+                 const uint32_t *__restrict__ n_over, const int64_t *__restrict__ item_base,
+                 const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
+                 const int64_t *__restrict__ gB, uint32_t *__restrict__ res) {
+    __shared__ ArcLds L;
+    const uint32_t n = *n_over;
+    for (uint32_t li = blockIdx.x; li < n; li += gridDim.x) {
+        arc_dense_item(L, over[li], t, g, item_base, entries, sub_end, gB, res);
+        __syncthreads();
+    }
 }
 
 // 6. Corner flags: per (group, tile) item, its events (sorted keys, coalesced) look up their
@@ -906,6 +1168,8 @@ struct GroupImages {
     PairEntry *entries;   // [n] distinct (slice, pixel) pairs per item, at item_base[item]
     int64_t *item_base;   // [n_items]
     int32_t *sub_end;     // [n_items][kSub] sub-region ends inside each item's entries
+    int64_t *over;        // [n_items] items whose windows exceed the compact list (arc_dense_kernel)
+    uint32_t *n_over;
 };
 
 Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_items, int64_t n_groups, int32_t **first_border,
@@ -922,6 +1186,8 @@ Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_items, int64_t n_g
     gi->entries = cv.take<PairEntry>((size_t)g.n);
     gi->item_base = cv.take<int64_t>((size_t)n_items);
     gi->sub_end = cv.take<int32_t>((size_t)n_items * kSub);
+    gi->over = cv.take<int64_t>((size_t)n_items);
+    gi->n_over = cv.take<uint32_t>(64);
     return so;
 }
 
@@ -1026,6 +1292,7 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     const Sorted so = carve_sorted(cv, g, n_items, n_groups, &first_border, &gi);
 
     ECC_CHECK_HIP(ctx, hipMemsetAsync(corner_flags, 0, (size_t)n, s), "memset(flags)");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
     {
         const size_t lds = (size_t)nb * 4 + kSortChunk * 4;  // > 64 KiB: opt in (gfx950 has 160 KiB)
         static int lds_set = 0;
@@ -1056,7 +1323,14 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
         ECC_TIMED(ctx, s, "arc_kernel");
         const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
         hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
-                           (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end, (const int64_t *)gi.B, gi.res);
+                           (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
+                           (const int64_t *)gi.B, gi.res, gi.over, gi.n_over);
+    }
+    {
+        ECC_TIMED(ctx, s, "arc_dense_kernel");  // the overflow list, dense planes
+        hipLaunchKernelGGL(arc_dense_kernel, dim3(512), dim3(kArcThreads), 0, s, t, g, (const int64_t *)gi.over,
+                           (const uint32_t *)gi.n_over, (const int64_t *)gi.item_base, (const PairEntry *)gi.entries,
+                           (const int32_t *)gi.sub_end, (const int64_t *)gi.B, gi.res);
     }
     {
         ECC_TIMED(ctx, s, "flags_kernel");
