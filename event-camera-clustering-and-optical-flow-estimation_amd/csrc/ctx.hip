@@ -150,6 +150,7 @@ ECC_API int ecc_ctx_destroy(ecc_ctx *ctx) {
     for (auto &p : ctx->pending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
     for (auto e : ctx->event_pool) hipEventDestroy(e);
     ecc::corner_state_release(ctx);
+    ecc::nms_state_release(ctx);
     if (ctx->ws) hipFree(ctx->ws);
     if (ctx->flags) hipFree(ctx->flags);
     delete ctx;

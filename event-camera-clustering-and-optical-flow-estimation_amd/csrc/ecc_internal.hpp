@@ -68,6 +68,8 @@ int exclusive_scan_i32_i64(ecc_ctx *ctx, const int32_t *in, int64_t n, int64_t *
 
 // Frees the per-context corner-stage workspace (corners.hip); called by ecc_ctx_destroy.
 void corner_state_release(const ecc_ctx *ctx);
+// Frees the per-context NMS candidate buffer (nms.hip); called by ecc_ctx_destroy.
+void nms_state_release(const ecc_ctx *ctx);
 
 // Launch-error check: kernel launches are asynchronous; this surfaces configuration errors.
 #define ECC_CHECK_LAUNCH(ctx, what)                                  \

@@ -13,15 +13,18 @@
 // (LDS broadcast reads), then the within-chunk order dependency is resolved on a 64x64
 // overlap bitmask with scalar bit logic.  Output label = rank in the kept list (:140).
 //
-// Grid form (nms_grid_kernel, used whenever the grid fits LDS): two boxes [c±h] overlap iff
-// their centres are within Chebyshev distance 2h (clipping to the image never separates two
-// boxes whose centres lie inside it), so kept boxes are pairwise disjoint and a grid of
-// (2h+1)-pixel cells holds at most ONE kept centre per cell.  "Overlaps an earlier kept box"
-// is then 9 LDS probes.  One wave per slice streams the flags 1024 events at a time; within a
-// chunk of 64 candidates the kept ones are found by a scalar loop over the surviving lanes
-// (each kept lane's centre is broadcast and kills the later lanes it overlaps).  ~6 KiB of LDS
-// per slice, so many slices run per CU.
+// Grid form (used whenever the grid fits LDS): two boxes [c±h] overlap iff their centres are
+// within Chebyshev distance 2h (clipping to the image never separates two boxes whose centres
+// lie inside it), so kept boxes are pairwise disjoint and a grid of (2h+1)-pixel cells holds at
+// most ONE kept centre per cell.  "Overlaps an earlier kept box" is then 9 LDS probes.  A
+// parallel compaction kernel (256 lanes per slice) first lists each slice's flagged events in
+// event order; one wave per slice then takes them 64 at a time, and within a chunk the kept ones
+// are found by a scalar loop over the surviving lanes (each kept lane's centre is broadcast and
+// kills the later lanes it overlaps).  ~2 KiB of LDS per slice, so many slices run per CU.
 #include "ecc_internal.hpp"
+
+#include <map>
+#include <mutex>
 
 namespace {
 
@@ -158,25 +161,23 @@ __device__ __forceinline__ bool near_centre(uint32_t a, uint32_t b, int reach) {
     return abs(ecc::xy_x(a) - ecc::xy_x(b)) <= reach && abs(ecc::xy_y(a) - ecc::xy_y(b)) <= reach;
 }
 
-__global__ void __launch_bounds__(kGridThreads)
-nms_grid_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ flags, int64_t n, int S, int W,
-                int H, int half, int gw, int gh, int cap, ecc_corner *__restrict__ out,
-                int32_t *__restrict__ out_count, int32_t *__restrict__ err) {
-    extern __shared__ uint32_t grid[];  // [gh][gw] kept centre per cell
-    __shared__ uint32_t cbuf[kChunkEvents];
-    const int lane = threadIdx.x;
+// Two-kernel grid form (bench sizes): candidates first, greedy second.
+// nms_compact_kernel: one 256-lane workgroup per slice (chunks of 4096 events): 16-B flag loads,
+// a block scan of the per-lane flag counts, and the flagged events' xy gathered into the slice's
+// candidate list in event order (cand[s*S ...], count n_cand[s]).
+constexpr int kCompactThreads = 256;
+
+__global__ void __launch_bounds__(kCompactThreads)
+nms_compact_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ flags, int64_t n, int S,
+                   uint32_t *__restrict__ cand, int32_t *__restrict__ n_cand) {
+    __shared__ int wtot[kCompactThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t s = blockIdx.x;
     const int64_t lo = s * (int64_t)S;
     const int64_t len = ((lo + S < n) ? lo + S : n) - lo;
-    const int cs = 2 * half + 1, reach = 2 * half;
-    for (int i = lane; i < gw * gh; i += kGridThreads) grid[i] = kNoCentre;
-    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    int n_kept = 0;
-    bool overflow = false, bad_input = false;
-    __syncthreads();
-    for (int64_t c0 = 0; c0 < len; c0 += kChunkEvents) {
-        // (a) compact the chunk's flagged events in event order
-        const int64_t my0 = c0 + (int64_t)lane * 16;
+    int run = 0;
+    for (int64_t c0 = 0; c0 < len; c0 += kCompactThreads * 16) {
+        const int64_t my0 = c0 + (int64_t)tid * 16;
         uint32_t bits = 0;
         if (my0 + 15 < len && ((lo + my0) & 15) == 0) {
             const uint4 q = *reinterpret_cast<const uint4 *>(flags + lo + my0);
@@ -194,52 +195,80 @@ nms_grid_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ fla
             const int y = __shfl_up(incl, o);
             if (lane >= o) incl += y;
         }
-        const int total = __shfl(incl, 63);
-        int off = incl - cnt;
+        if (lane == 63) wtot[wave] = incl;
+        __syncthreads();
+        int off = run + incl - cnt, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kCompactThreads / 64; ++w) {
+            off += w < wave ? wtot[w] : 0;
+            tot += wtot[w];
+        }
         while (bits) {
             const int k = __ffs(bits) - 1;
             bits &= bits - 1;
-            cbuf[off++] = xy[lo + my0 + k];
+            cand[lo + off++] = xy[lo + my0 + k];
         }
+        run += tot;
         __syncthreads();
-        // (b) greedy over the chunk's candidates, 64 at a time
-        for (int p0 = 0; p0 < total; p0 += kGridThreads) {
-            uint32_t v = (p0 + lane < total) ? cbuf[p0 + lane] : 0u;
-            int x = ecc::xy_x(v), y = ecc::xy_y(v);
-            const bool outside = p0 + lane < total && (x >= W || y >= H);
-            if (outside) bad_input = true;  // skipped and reported (ecc_corner_nms_status)
-            const bool valid = p0 + lane < total && !outside;
-            if (!valid) { v = 0u; x = 0; y = 0; }
-            const int cx = x / cs, cy = y / cs;
-            bool alive = valid;
+    }
+    if (tid == 0) n_cand[s] = run;
+}
+
+// nms_greedy_kernel: one wave per slice over its candidate list (the next 64 candidates are
+// requested before the current 64 are decided); the kept-centre grid as in nms_grid_kernel.
+__global__ void __launch_bounds__(kGridThreads)
+nms_greedy_kernel(const uint32_t *__restrict__ cand, const int32_t *__restrict__ n_cand, int S, int W, int H,
+                  int half, int gw, int gh, int cap, ecc_corner *__restrict__ out, int32_t *__restrict__ out_count,
+                  int32_t *__restrict__ err) {
+    extern __shared__ uint32_t grid[];  // [gh][gw] kept centre per cell
+    const int lane = threadIdx.x;
+    const int64_t s = blockIdx.x;
+    const uint32_t *c = cand + s * (int64_t)S;
+    const int total = n_cand[s];
+    const int cs = 2 * half + 1, reach = 2 * half;
+    for (int i = lane; i < gw * gh; i += kGridThreads) grid[i] = kNoCentre;
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int n_kept = 0;
+    bool overflow = false, bad_input = false;
+    uint32_t nxt = lane < total ? c[lane] : 0u;
+    __syncthreads();
+    for (int p0 = 0; p0 < total; p0 += kGridThreads) {
+        uint32_t v = nxt;
+        const bool have = p0 + lane < total;
+        nxt = (p0 + kGridThreads + lane < total) ? c[p0 + kGridThreads + lane] : 0u;
+        int x = ecc::xy_x(v), y = ecc::xy_y(v);
+        const bool outside = have && (x >= W || y >= H);
+        if (outside) bad_input = true;  // skipped and reported (ecc_corner_nms_status)
+        const bool valid = have && !outside;
+        if (!valid) { v = 0u; x = 0; y = 0; }
+        const int cx = x / cs, cy = y / cs;
+        bool alive = valid;
 #pragma unroll
-            for (int dy = -1; dy <= 1; ++dy) {
+        for (int dy = -1; dy <= 1; ++dy) {
 #pragma unroll
-                for (int dx = -1; dx <= 1; ++dx) {
-                    const int gx = cx + dx, gy = cy + dy;
-                    if (gx >= 0 && gy >= 0 && gx < gw && gy < gh) {
-                        const uint32_t k = grid[gy * gw + gx];
-                        if (k != kNoCentre && near_centre(k, v, reach)) alive = false;
-                    }
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int gx = cx + dx, gy = cy + dy;
+                if (gx >= 0 && gy >= 0 && gx < gw && gy < gh) {
+                    const uint32_t k = grid[gy * gw + gx];
+                    if (k != kNoCentre && near_centre(k, v, reach)) alive = false;
                 }
             }
-            uint64_t am = __ballot(alive), keepm = 0;
-            while (am) {  // wave-uniform: each step keeps the first surviving lane
-                const int i0 = __ffsll((unsigned long long)am) - 1;
-                keepm |= 1ull << i0;
-                am &= am - 1;
-                const uint32_t vi = (uint32_t)__builtin_amdgcn_readlane((int)v, i0);
-                am &= ~__ballot(lane > i0 && near_centre(vi, v, reach));
-            }
-            if ((keepm >> lane) & 1ull) {
-                const int rank = n_kept + __popcll(keepm & lt_mask);
-                grid[cy * gw + cx] = v;
-                if (rank < cap) out[s * (int64_t)cap + rank] = ecc_corner{x, y, rank};
-                else overflow = true;
-            }
-            n_kept += __popcll(keepm);
-            __syncthreads();
         }
+        uint64_t am = __ballot(alive), keepm = 0;
+        while (am) {  // wave-uniform: each step keeps the first surviving lane
+            const int i0 = __ffsll((unsigned long long)am) - 1;
+            keepm |= 1ull << i0;
+            am &= am - 1;
+            const uint32_t vi = (uint32_t)__builtin_amdgcn_readlane((int)v, i0);
+            am &= ~__ballot(lane > i0 && near_centre(vi, v, reach));
+        }
+        if ((keepm >> lane) & 1ull) {
+            const int rank = n_kept + __popcll(keepm & lt_mask);
+            grid[cy * gw + cx] = v;
+            if (rank < cap) out[s * (int64_t)cap + rank] = ecc_corner{x, y, rank};
+            else overflow = true;
+        }
+        n_kept += __popcll(keepm);
         __syncthreads();
     }
     overflow = __any(overflow);
@@ -250,6 +279,13 @@ nms_grid_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ fla
         if (bad_input) atomicOr(err, 2);
     }
 }
+
+struct NmsState {
+    void *buf = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_nms_mu;
+std::map<const ecc_ctx *, NmsState> g_nms;
 
 }  // namespace
 
@@ -270,10 +306,38 @@ ECC_API int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corn
     const int half = box_size / 2, cs = 2 * half + 1;
     const int gw = (width + cs - 1) / cs, gh = (height + cs - 1) / cs;
     if ((int64_t)gw * gh <= kGridMaxCells) {
+        // candidate lists: n xy words + n_slices counts, per context (grown, never shrunk)
+        const size_t need = ecc::align_up((size_t)n * 4, 256) + (size_t)n_slices * 4;
+        NmsState *st;
+        {
+            std::lock_guard<std::mutex> lk(g_nms_mu);
+            st = &g_nms[ctx];
+        }
+        if (need > st->bytes) {
+            if (st->buf) {
+                ECC_CHECK_HIP(ctx, hipDeviceSynchronize(), "sync(nms buffer)");
+                (void)hipFree(st->buf);
+                st->buf = nullptr;
+                st->bytes = 0;
+            }
+            const size_t want = ecc::align_up(need + need / 8, 1 << 20);
+            if (hipMalloc(&st->buf, want) != hipSuccess) {
+                st->buf = nullptr;
+                return ECC_ERR_NOMEM;
+            }
+            st->bytes = want;
+        }
+        auto *cand = static_cast<uint32_t *>(st->buf);
+        auto *n_cand = reinterpret_cast<int32_t *>(static_cast<char *>(st->buf) + ecc::align_up((size_t)n * 4, 256));
+        {
+            ECC_TIMED(ctx, s, "nms_compact_kernel");
+            hipLaunchKernelGGL(nms_compact_kernel, dim3((unsigned)n_slices), dim3(kCompactThreads), 0, s, xy,
+                               corner_flags, n, slice_events, cand, n_cand);
+        }
         ECC_TIMED(ctx, s, "nms_kernel");
-        hipLaunchKernelGGL(nms_grid_kernel, dim3((unsigned)n_slices), dim3(kGridThreads), (size_t)gw * gh * 4, s,
-                           xy, corner_flags, n, slice_events, width, height, half, gw, gh, cap, out, out_count,
-                           ctx->flags + 1);
+        hipLaunchKernelGGL(nms_greedy_kernel, dim3((unsigned)n_slices), dim3(kGridThreads), (size_t)gw * gh * 4, s,
+                           (const uint32_t *)cand, (const int32_t *)n_cand, slice_events, width, height, half, gw, gh,
+                           cap, out, out_count, ctx->flags + 1);
     } else {
         ECC_TIMED(ctx, s, "nms_kernel");
         hipLaunchKernelGGL(nms_kernel, dim3((unsigned)n_slices), dim3(kThreads), 0, s, xy,
@@ -293,3 +357,13 @@ ECC_API int ecc_corner_nms_status(ecc_ctx *ctx, ecc_stream_t stream) {
     if (f & 2) return ECC_ERR_INVALID;
     return (f & 1) ? ECC_ERR_CAPACITY : ECC_OK;
 }
+
+namespace ecc {
+void nms_state_release(const ecc_ctx *ctx) {
+    std::lock_guard<std::mutex> lk(g_nms_mu);
+    auto it = g_nms.find(ctx);
+    if (it == g_nms.end()) return;
+    if (it->second.buf) (void)hipFree(it->second.buf);
+    g_nms.erase(it);
+}
+}  // namespace ecc
