@@ -154,7 +154,6 @@ nms_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ flags, i
 
 constexpr int kGridThreads = 64;
 constexpr int kGridMaxCells = 16384;  // 64 KiB of LDS
-constexpr int kChunkEvents = kGridThreads * 16;
 constexpr uint32_t kNoCentre = 0xffffffffu;
 
 __device__ __forceinline__ bool near_centre(uint32_t a, uint32_t b, int reach) {
