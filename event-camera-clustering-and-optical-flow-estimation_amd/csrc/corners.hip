@@ -351,6 +351,9 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
     const int64_t item = blockIdx.x;
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
+    // this lane's pixel in sub-region order: a per-lane constant-memory read is a vector load,
+    // issued here so that it completes during the setup
+    const int lp = tid < kTilePix ? c_sub.pix[tid] : 0;
     {
         uint4 *z = reinterpret_cast<uint4 *>(&tab[0][0]);
         for (int i = tid; i < (int)(sizeof(tab) / 16); i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -377,7 +380,6 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
     }
     __syncthreads();
     // lane k owns pixel c_sub.pix[k]: slice mask, entry count, exclusive prefix in sub-region order
-    const int lp = tid < kTilePix ? c_sub.pix[tid] : 0;
     uint32_t m = 0u;
     if (tid < kTilePix) {
 #pragma unroll
