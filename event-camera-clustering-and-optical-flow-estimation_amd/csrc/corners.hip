@@ -662,18 +662,18 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     if (tid < kMaxSeg) {
         // own tile: every sub-region; above/below: their facing rows; corners: one sub-region;
         // left/right: their facing columns (3 sub-regions, one segment each)
-        constexpr int8_t sx[kMaxSeg] = {0, 0, 0, -1, 1, -1, 1, -1, 1, -1, 1, -1, 1};
-        constexpr int8_t sy[kMaxSeg] = {0, -1, 1, -1, -1, 1, 1, 0, 0, 0, 0, 0, 0};
-        constexpr int8_t r0[kMaxSeg] = {0, 6, 0, 8, 6, 2, 0, 2, 0, 5, 3, 8, 6};
-        constexpr int8_t r1[kMaxSeg] = {8, 8, 2, 8, 6, 2, 0, 2, 0, 5, 3, 8, 6};
-        const int nx = tx + sx[tid], ny = ty + sy[tid];
+        // segment geometry packed into integer constants (a per-lane table read would be a load):
+        // dx, dy in {-1,0,1} (2 bits + 1), first/last sub-region (4 bits)
+        const int sxt = (int)((0x2222215u >> (2 * tid)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * tid)) & 3u) - 1;
+        const int r0t = (int)((0x6835020268060ull >> (4 * tid)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * tid)) & 15u);
+        const int nx = tx + sxt, ny = ty + syt;
         int64_t b0 = 0;
         int len = 0;
         if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
             const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
-            const int s0 = r0[tid] ? sub_end[bi * kSub + r0[tid] - 1] : 0;
+            const int s0 = r0t ? sub_end[bi * kSub + r0t - 1] : 0;
             b0 = item_base[bi] + s0;
-            len = sub_end[bi * kSub + r1[tid]] - s0;
+            len = sub_end[bi * kSub + r1t] - s0;
         }
         int incl = len;  // prefix over lanes 0..12 of wave 0
 #pragma unroll
@@ -683,7 +683,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         }
         L.seg_lo[tid] = b0;
         L.seg_pref[tid + 1] = incl;
-        L.seg_off[tid] = (sy[tid] * kTile) * kWin + sx[tid] * kTile + kHalo * kWin + kHalo;
+        L.seg_off[tid] = (syt * kTile) * kWin + sxt * kTile + kHalo * kWin + kHalo;
         if (tid == 0) L.seg_pref[0] = 0;
     }
     __syncthreads();
@@ -896,18 +896,18 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         L.q4n = 0;
     }
     if (tid < kMaxSeg) {
-        constexpr int8_t sx[kMaxSeg] = {0, 0, 0, -1, 1, -1, 1, -1, 1, -1, 1, -1, 1};
-        constexpr int8_t sy[kMaxSeg] = {0, -1, 1, -1, -1, 1, 1, 0, 0, 0, 0, 0, 0};
-        constexpr int8_t r0[kMaxSeg] = {0, 6, 0, 8, 6, 2, 0, 2, 0, 5, 3, 8, 6};
-        constexpr int8_t r1[kMaxSeg] = {8, 8, 2, 8, 6, 2, 0, 2, 0, 5, 3, 8, 6};
-        const int nx = tx + sx[tid], ny = ty + sy[tid];
+        // segment geometry packed into integer constants (a per-lane table read would be a load):
+        // dx, dy in {-1,0,1} (2 bits + 1), first/last sub-region (4 bits)
+        const int sxt = (int)((0x2222215u >> (2 * tid)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * tid)) & 3u) - 1;
+        const int r0t = (int)((0x6835020268060ull >> (4 * tid)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * tid)) & 15u);
+        const int nx = tx + sxt, ny = ty + syt;
         int64_t b0 = 0;
         int len = 0;
         if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
             const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
-            const int s0 = r0[tid] ? sub_end[bi * kSub + r0[tid] - 1] : 0;
+            const int s0 = r0t ? sub_end[bi * kSub + r0t - 1] : 0;
             b0 = item_base[bi] + s0;
-            len = sub_end[bi * kSub + r1[tid]] - s0;
+            len = sub_end[bi * kSub + r1t] - s0;
         }
         int incl = len;
 #pragma unroll
@@ -917,7 +917,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         }
         L.seg_lo[tid] = b0;
         L.seg_pref[tid + 1] = incl;
-        L.seg_off[tid] = (sy[tid] * kTile) * kWin + sx[tid] * kTile + kHalo * kWin + kHalo;
+        L.seg_off[tid] = (syt * kTile) * kWin + sxt * kTile + kHalo * kWin + kHalo;
         if (tid == 0) L.seg_pref[0] = 0;
     }
     __syncthreads();
