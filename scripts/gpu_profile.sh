@@ -4,7 +4,7 @@
 # --kernel-trace only (never sys/runtime traces with --pmc).
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${1:-r01}"; shift
-ARGS="--steps 3 --warmup 1 --no-cpu --no-tracker $*"
+ARGS="--steps 3 --warmup 1 --no-cpu --no-tracker --serial $*"
 OUT="$REPO/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
