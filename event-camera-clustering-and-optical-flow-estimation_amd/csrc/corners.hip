@@ -935,8 +935,11 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     //     the entries stay in registers for pass 2
     PairEntry ent[kSparseHold];
     int ewp[kSparseHold];
+    const int slots = (total + kArcThreads - 1) / kArcThreads;  // uniform: the slots in use
 #pragma unroll
     for (int u = 0; u < kSparseHold; ++u) {
+        ewp[u] = -1;
+        if (u >= slots) continue;
         const int i = u * kArcThreads + tid;
         int r = 0;
 #pragma unroll
@@ -946,6 +949,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     }
 #pragma unroll
     for (int u = 0; u < kSparseHold; ++u) {
+        if (u >= slots) break;
         if (ewp[u] < 0) continue;
         const int r = ewp[u];
         const int lp = (int)(ent[u].meta & 255u), j = (int)(ent[u].meta >> 8);
@@ -989,6 +993,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     // (d) pass 2: each value at its pixel's list position (ascending slice)
 #pragma unroll
     for (int u = 0; u < kSparseHold; ++u) {
+        if (u >= slots) break;
         if (ewp[u] < 0) continue;
         const int j = (int)(ent[u].meta >> 8);
         const PixInfo p = L.pix[ewp[u]];
