@@ -11,9 +11,10 @@ The corner tracker (sequential over slices) is timed separately and reported in 
 Single GPU:  python bench.py [--steps K --warmup W]
 Multi GPU:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
   Each rank owns one contiguous time window (shard) of the stream: downsample and detection are
-  shard-local, k-means is global (RCCL all-reduce of the integer partial sums every iteration)
-  and the SAE is handed over exactly (all-gather of the shards' local time surfaces; rank r
-  starts from the elementwise max over ranks < r).  Weak scaling: events per rank fixed.
+  shard-local; k-means is global from ONE RCCL all-reduce of the shards' per-pixel count images
+  (every rank then runs the Lloyd passes locally); the SAE is handed over exactly (all-gather
+  of the shards' own last-timestamp images; rank r starts from the elementwise max over ranks
+  < r).  Weak scaling: events per rank fixed.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -105,31 +106,28 @@ def main():
     lib = ecc.lib
     if dist:
         # exchange buffers are torch tensors (RCCL operates on them); libecc gets their pointers
-        t_acc = torch.zeros(3 * K, dtype=torch.int64, device=f"cuda:{local}")
-        t_state = torch.zeros(2, dtype=torch.int32, device=f"cuda:{local}")
+        t_counts = torch.zeros(W * H, dtype=torch.int32, device=f"cuda:{local}")
         t_local = torch.zeros(W * H, dtype=torch.int64, device=f"cuda:{local}")
         t_all = torch.zeros(world * W * H, dtype=torch.int64, device=f"cuda:{local}")
 
     def step_sharded():
-        """Shard-local downsample/detection/NMS + global k-means + exact SAE hand-off."""
+        """Shard-local downsample/detection/NMS; global k-means from ONE all-reduce of the
+        shards' per-pixel count images; exact SAE hand-off (all-gather of the shards' own last-t
+        images, computed by the detection's prepare phase)."""
         S = ctx.stream
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
                                           uniq.ptr, rep.ptr, S), "downsample")
+        ecc.check(lib.ecc_kmeans_counts_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, W, H, t_counts.data_ptr(), S))
+        ecc.check(lib.ecc_fast_detect_prepare(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), t_local.data_ptr(), S))
+        dist.all_reduce(t_counts)
+        dist.all_gather_into_tensor(t_all, t_local)
         ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, S))
-        t_acc.zero_()
-        t_state.zero_()
-        for _ in range(I):  # exact integer partial sums, all-reduced every iteration
-            ecc.check(lib.ecc_kmeans_accumulate_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, d_c.ptr, K,
-                                                     kcfg.threshold, t_acc.data_ptr(), t_state.data_ptr(), S))
-            dist.all_reduce(t_acc)
-            ecc.check(lib.ecc_kmeans_update(ctx.ctx, t_acc.data_ptr(), d_c.ptr, K, kcfg.tol, t_state.data_ptr(), S))
+        ecc.check(lib.ecc_kmeans_run_counts(ctx.ctx, t_counts.data_ptr(), W, H, ecc.C.byref(kcfg), d_c.ptr, None, S))
         ecc.check(lib.ecc_kmeans_labels_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, d_c.ptr, K,
                                              kcfg.threshold, labels.ptr, S))
-        t_local.zero_()
-        ecc.check(lib.ecc_sae_scatter(ctx.ctx, d_xy.ptr, d_t.ptr, n, W, H, t_local.data_ptr(), S))
-        dist.all_gather(list(t_all.view(world, -1).unbind(0)), t_local)
         ecc.check(lib.ecc_sae_max_combine(ctx.ctx, t_all.data_ptr(), rank, W * H, sae.ptr, S))
-        ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
+        ecc.check(lib.ecc_fast_detect_finish(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), sae.ptr,
+                                             flags.ptr, S), "fast_detect_finish")
         ctx.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, nms_out, nms_cnt)
 
     # single GPU: downsample -> k-means and the corner chain read the same resident batch and are
@@ -162,6 +160,8 @@ def main():
     ctx.sync()
     if ctx.fast_detect_status() != 0:
         raise RuntimeError("fast_detect reported a status error")
+    if dist and lib.ecc_kmeans_counts_status(ctx.ctx, ctx.stream) != 0:
+        raise RuntimeError("a representative lies outside the k-means count frame")
     n_reps = int(uniq.numpy().sum())
     # --graph: the step's ~40 launches and memsets are captured once into a HIP graph
     # (ecc_graph_*) and replayed — the same kernels on the same buffers, without per-launch

@@ -57,8 +57,6 @@ struct CornerGeom {
     int W, H, S, margin, border_mode, first_detect;
     int tiles_x, n_tiles;  // bin n_tiles of each group holds the events outside the sensor
     float inv_S;
-    int dbg;  // development: arc phase cut-off (ECC_ARC_DBG)
-    void *dbg_cnt;
     int64_t n, n_slices;
 };
 
@@ -444,6 +442,21 @@ sae_prefix_kernel(CornerGeom g, int64_t n_groups, const uint32_t *__restrict__ g
             }
         }
         sae[q] = run;
+    }
+}
+
+// The shard's own final time surface for the multi-GPU hand-off (ecc_fast_detect_prepare): per
+// pixel the last timestamp of the batch, 0 where no event touched it — from the per-group images,
+// no global atomics.
+__global__ void __launch_bounds__(kThreads)
+sae_local_last_kernel(CornerGeom g, int64_t n_groups, const uint32_t *__restrict__ gmask,
+                      const int64_t *__restrict__ glast, int64_t *__restrict__ out) {
+    const int64_t HW = (int64_t)g.H * g.W;
+    for (int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x; q < HW; q += (int64_t)gridDim.x * kThreads) {
+        int64_t run = 0;
+        for (int64_t gi = n_groups - 1; gi >= 0; --gi)
+            if (gmask[gi * HW + q]) { run = glast[gi * HW + q]; break; }
+        out[q] = run;
     }
 }
 
@@ -1247,11 +1260,15 @@ ECC_API void ecc_corner_cfg_default(ecc_corner_cfg *cfg) {
     cfg->first_detect_slice = 1;  // time_surface_flag (Q15)
 }
 
-ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
-                            const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
-                            ecc_stream_t stream) {
-    if (!ctx || !cfg || !sae || n < 0) return ECC_ERR_INVALID;
-    if (n > 0 && (!xy || !t || !corner_flags)) return ECC_ERR_INVALID;
+// phase bit 1: sort + pair entries (+ the shard-local last-t image when local_last != null);
+// phase bit 2: SAE prefix from `sae` + arc tests + flags.  Both phases see the same workspace
+// carve (same n and cfg), so prepare/finish may be separate calls with a collective between.
+static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                              const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags, int64_t *local_last,
+                              int phases, ecc_stream_t stream) {
+    if (!ctx || !cfg || n < 0) return ECC_ERR_INVALID;
+    if ((phases & 2) && !sae) return ECC_ERR_INVALID;
+    if (n > 0 && (!xy || !t || ((phases & 2) && !corner_flags))) return ECC_ERR_INVALID;
     if (cfg->width < 1 || cfg->height < 1 || cfg->width > 65536 || cfg->height > 65536)
         return ECC_ERR_INVALID;
     if (cfg->margin < 4 || 2 * cfg->margin >= cfg->width || 2 * cfg->margin >= cfg->height)
@@ -1264,13 +1281,6 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     g.H = cfg->height;
     g.S = cfg->slice_events;
     g.inv_S = 1.0f / (float)g.S;
-    g.dbg = getenv("ECC_ARC_DBG") ? atoi(getenv("ECC_ARC_DBG")) : 0;
-    g.dbg_cnt = nullptr;
-    static unsigned long long *dbg_buf = nullptr;
-    if (g.dbg == 4) {
-        if (!dbg_buf) { (void)hipMalloc(&dbg_buf, 64); (void)hipMemset(dbg_buf, 0, 64); }
-        g.dbg_cnt = dbg_buf;
-    }
     g.margin = cfg->margin;
     g.border_mode = cfg->border_mode;
     g.first_detect = cfg->first_detect_slice;
@@ -1282,8 +1292,11 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     if (g.n_slices > INT32_MAX) return ECC_ERR_INVALID;
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags, 0, 4, s), "memset(err flag)");
-    if (n == 0) return ECC_OK;
+    if (phases & 1) ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags, 0, 4, s), "memset(err flag)");
+    if (n == 0) {
+        if (local_last) ECC_CHECK_HIP(ctx, hipMemsetAsync(local_last, 0, (size_t)g.W * g.H * 8, s), "memset(local)");
+        return ECC_OK;
+    }
     const int nb = g.n_tiles + 1;
     const int64_t n_groups = (g.n_slices + kGroup - 1) / kGroup;
     const int64_t n_items = n_groups * g.n_tiles;  // work items: (group, tile)
@@ -1293,13 +1306,13 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     GroupImages gi{};
     Carve measure{nullptr};
     carve_sorted(measure, g, n_items, n_groups, &first_border, &gi);
-    int rc = corner_state_reserve(ctx, st, measure.used);
+    if (!(phases & 1) && measure.used > st->evt_bytes) return ECC_ERR_INVALID;  // finish without prepare
+    int rc = (phases & 1) ? corner_state_reserve(ctx, st, measure.used) : ECC_OK;
     if (rc) return rc;
     Carve cv{static_cast<char *>(st->evt)};
     const Sorted so = carve_sorted(cv, g, n_items, n_groups, &first_border, &gi);
 
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(corner_flags, 0, (size_t)n, s), "memset(flags)");
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
+    if (phases & 1) {
     {
         const size_t lds = (size_t)nb * 4 + kSortChunk * 4;  // > 64 KiB: opt in (gfx950 has 160 KiB)
         static int lds_set = 0;
@@ -1319,6 +1332,20 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
         hipLaunchKernelGGL(pair_build_kernel, dim3((unsigned)n_items), dim3(kThreads), 0, s, t, g, so, gi.entries,
                            gi.item_base, gi.sub_end, gi.mask, gi.B);
     }
+    if (local_last) {
+        ECC_TIMED(ctx, s, "sae_local_last_kernel");
+        const int64_t HW = (int64_t)g.W * g.H;
+        const unsigned blocks = (unsigned)std::min<int64_t>((HW + kThreads - 1) / kThreads, 8192);
+        hipLaunchKernelGGL(sae_local_last_kernel, dim3(blocks), dim3(kThreads), 0, s, g, n_groups,
+                           (const uint32_t *)gi.mask, (const int64_t *)gi.B, local_last);
+    }
+    }  // phase 1
+    if (!(phases & 2)) {
+        ECC_CHECK_LAUNCH(ctx, "fast_detect_prepare");
+        return ECC_OK;
+    }
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(corner_flags, 0, (size_t)n, s), "memset(flags)");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
     {
         ECC_TIMED(ctx, s, "sae_prefix_kernel");
         const int64_t HW = (int64_t)g.W * g.H;
@@ -1345,12 +1372,24 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
                            (const int32_t *)gi.sub_end, (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
     }
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
-    if (g.dbg == 4) {
-        unsigned long long h[2];
-        (void)hipMemcpy(h, g.dbg_cnt, 16, hipMemcpyDeviceToHost);
-        fprintf(stderr, "arc tasks %llu circle4 %llu (cumulative)\n", h[0], h[1]);
-    }
     return ECC_OK;
+}
+
+ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                            const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
+                            ecc_stream_t stream) {
+    return fast_detect_phases(ctx, xy, t, n, cfg, sae, corner_flags, nullptr, 3, stream);
+}
+
+ECC_API int ecc_fast_detect_prepare(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                                    const ecc_corner_cfg *cfg, int64_t *local_last, ecc_stream_t stream) {
+    return fast_detect_phases(ctx, xy, t, n, cfg, nullptr, nullptr, local_last, 1, stream);
+}
+
+ECC_API int ecc_fast_detect_finish(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                                   const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
+                                   ecc_stream_t stream) {
+    return fast_detect_phases(ctx, xy, t, n, cfg, sae, corner_flags, nullptr, 2, stream);
 }
 
 ECC_API int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream) {

@@ -511,12 +511,17 @@ __device__ __forceinline__ void reduce_extent(const uint32_t *__restrict__ ext, 
 __global__ void __launch_bounds__(kHistThreads)
 kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *__restrict__ ext, int n_ext,
                     int parts, uint32_t *__restrict__ partial, uint32_t *__restrict__ wh,
-                    uint32_t *__restrict__ outside, uint32_t *__restrict__ n_outside) {
+                    uint32_t *__restrict__ outside, uint32_t *__restrict__ n_outside, uint32_t fixed_w,
+                    uint32_t fixed_h, int32_t *__restrict__ err) {
     extern __shared__ uint32_t hist[];  // [kHistChunk]
     __shared__ uint32_t s_red[2 * kHistThreads / 64];
     const int m = blockIdx.y, tid = threadIdx.x;
-    uint32_t w, h;
-    reduce_extent(ext, n_ext, s_red, w, h);
+    // fixed frame (multi-GPU count images, ecc_kmeans_counts_xy16): points outside it are an
+    // error; otherwise the bounding box of the points inside the kImgSide^2 image
+    const bool fixed = fixed_w > 0;
+    uint32_t w = fixed_w, h = fixed_h;
+    if (!fixed) reduce_extent(ext, n_ext, s_red, w, h);
+    const uint32_t lim_x = fixed ? w : kImgSide, lim_y = fixed ? h : kImgSide;
     const int64_t cells = (int64_t)w * h;
     if (blockIdx.x == 0 && m == 0 && tid == 0) {
         wh[0] = w;
@@ -544,11 +549,12 @@ kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *
                 for (int u = 0; u < kHistUnroll; ++u) {
                     if (j0 + u * kHistThreads + tid >= cnt) continue;
                     const uint32_t x = v[u] & 0xffffu, y = v[u] >> 16;
-                    if (x < kImgSide && y < kImgSide) {
+                    if (x < lim_x && y < lim_y) {
                         const int64_t idx = (int64_t)y * w + x - lo;
                         if (idx >= 0 && idx < n_loc) atomicAdd(&hist[idx], 1u);
                     } else if (c == 0) {
-                        outside[atomicAdd(n_outside, 1u)] = v[u];
+                        if (fixed) *err = 1;
+                        else outside[atomicAdd(n_outside, 1u)] = v[u];
                     }
                 }
             }
@@ -885,7 +891,7 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
                 lds_ok = true;
             }
             hipLaunchKernelGGL(kmeans_count_kernel, dim3(4, parts), dim3(kHistThreads), kHistChunk * 4, s, xy,
-                               segs, ext, grid, parts, partial, wh, outside, n_out);
+                               segs, ext, grid, parts, partial, wh, outside, n_out, 0u, 0u, (int32_t *)nullptr);
         }
         {
             ECC_TIMED(ctx, s, "kmeans_count_sum_kernel");
@@ -1061,5 +1067,129 @@ ECC_API int ecc_kmeans_labels_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_s
                                threshold, (unsigned long long *)nullptr, (const KmState *)nullptr, labels);
     }
     ECC_CHECK_LAUNCH(ctx, "kmeans labels");
+    return ECC_OK;
+}
+
+// ---- count images (multi-GPU k-means: one all-reduce of the counts instead of one per pass) ----
+// A shard's representatives counted per pixel of a caller-given frame (counts[y * w + x], u32).
+// Counts are additive over shards, and a Lloyd pass over a count image adds exactly the integer
+// sums of the points it counts, so summing the shards' images once and running every pass
+// locally gives each rank the single-GPU centroids.
+constexpr int kKmFlagWord = 5;  // ctx->flags[5]: a point outside the count frame (3: evt, 4: dbscan)
+
+__global__ void kmeans_set_wh_kernel(uint32_t *wh, uint32_t w, uint32_t h) {
+    wh[0] = w;
+    wh[1] = h;
+}
+
+ECC_API int ecc_kmeans_counts_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                                   const int32_t *seg_counts, int32_t frame_w, int32_t frame_h, uint32_t *counts,
+                                   ecc_stream_t stream) {
+    if (!ctx || !counts || n_segs < 0 || seg_stride < 1 || frame_w < 1 || frame_h < 1 || frame_w > 65536 ||
+        frame_h > 65536)
+        return ECC_ERR_INVALID;
+    const Segs segs = make_segs(n_segs, seg_stride, seg_counts);
+    const int64_t cells = (int64_t)frame_w * frame_h;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + kKmFlagWord, 0, 4, s), "memset(kmeans err)");
+    if (segs.n_segs == 0) {
+        ECC_CHECK_HIP(ctx, hipMemsetAsync(counts, 0, (size_t)cells * 4, s), "memset(counts)");
+        return ECC_OK;
+    }
+    if (!xy) return ECC_ERR_INVALID;
+    const int parts = (int)std::min<int64_t>(kHistParts, segs.n_segs);
+    const size_t off_part = 256;
+    int rc = ecc::ws_reserve(ctx, off_part + (size_t)kHistBudget * 4);
+    if (rc) return rc;
+    char *ws = static_cast<char *>(ctx->ws);
+    auto *wh = reinterpret_cast<uint32_t *>(ws);
+    auto *partial = reinterpret_cast<uint32_t *>(ws + off_part);
+    static bool lds_ok = false;
+    if (!lds_ok) {
+        ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&kmeans_count_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kHistChunk * 4),
+                      "kmeans_count LDS");
+        lds_ok = true;
+    }
+    {
+        ECC_TIMED(ctx, s, "kmeans_count_kernel");
+        hipLaunchKernelGGL(kmeans_count_kernel, dim3(4, parts), dim3(kHistThreads), kHistChunk * 4, s, xy, segs,
+                           (const uint32_t *)nullptr, 0, parts, partial, wh, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                           (uint32_t)frame_w, (uint32_t)frame_h, ctx->flags + kKmFlagWord);
+    }
+    {
+        ECC_TIMED(ctx, s, "kmeans_count_sum_kernel");
+        hipLaunchKernelGGL(kmeans_count_sum_kernel, dim3(1024), dim3(kThreads), 0, s, (const uint32_t *)partial, parts,
+                           (const uint32_t *)wh, counts);
+    }
+    ECC_CHECK_LAUNCH(ctx, "kmeans counts");
+    return ECC_OK;
+}
+
+ECC_API int ecc_kmeans_counts_status(ecc_ctx *ctx, ecc_stream_t stream) {
+    if (!ctx) return ECC_ERR_INVALID;
+    int32_t f = 0;
+    ECC_CHECK_HIP(ctx, hipMemcpyAsync(&f, ctx->flags + kKmFlagWord, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
+                  "read kmeans flag");
+    ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
+    return f ? ECC_ERR_INVALID : ECC_OK;
+}
+
+ECC_API int ecc_kmeans_run_counts(ecc_ctx *ctx, const uint32_t *counts, int32_t frame_w, int32_t frame_h,
+                                  const ecc_kmeans_cfg *cfg, float *centroids, int32_t *iters_out,
+                                  ecc_stream_t stream) {
+    int rc = kmeans_check(ctx, cfg, centroids);
+    if (rc) return rc;
+    if (!counts || frame_w < 1 || frame_h < 1 || frame_w > 65536 || frame_h > 65536) return ECC_ERR_INVALID;
+    if (cfg->k > kFastMaxK) return ECC_ERR_INVALID;  // pixel passes: k <= 32
+    constexpr size_t kAccBytes = (size_t)kAccCopies * kAccStride * 8;
+    const size_t off_st = 3 * kAccBytes;
+    const size_t off_cb = off_st + 64;
+    const size_t off_wh = ecc::align_up(off_cb + 2 * 2 * kMaxK * sizeof(float), 256);
+    rc = ecc::ws_reserve(ctx, off_wh + 256);
+    if (rc) return rc;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    char *ws = static_cast<char *>(ctx->ws);
+    unsigned long long *accb[3] = {reinterpret_cast<unsigned long long *>(ws),
+                                   reinterpret_cast<unsigned long long *>(ws + kAccBytes),
+                                   reinterpret_cast<unsigned long long *>(ws + 2 * kAccBytes)};
+    auto *st = reinterpret_cast<KmState *>(ws + off_st);
+    float *cb[2] = {reinterpret_cast<float *>(ws + off_cb), reinterpret_cast<float *>(ws + off_cb) + 2 * kMaxK};
+    auto *wh = reinterpret_cast<uint32_t *>(ws + off_wh);
+    auto *n_out = wh + 2;
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ws, 0, off_st + 64, s), "memset(kmeans acc)");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(n_out, 0, 4, s), "memset(kmeans outside)");
+    hipLaunchKernelGGL(kmeans_set_wh_kernel, dim3(1), dim3(1), 0, s, wh, (uint32_t)frame_w, (uint32_t)frame_h);
+    auto step = [&](int it, bool final_pass) {
+        StepArgs a{};
+        a.acc_in = it ? accb[(it - 1) % 3] : nullptr;
+        a.acc_zero = accb[(it + 1) % 3];
+        a.c_prev = it ? cb[(it - 1) & 1] : centroids;
+        a.c_next = cb[it & 1];
+        a.cent = centroids;
+        a.n_copies = kAccCopies;
+        a.k = cfg->k;
+        a.thr = cfg->threshold;
+        a.tol = cfg->tol;
+        a.final_pass = final_pass;
+        a.want_image = false;
+        const PixArgs px{counts, (const uint32_t *)n_out, n_out, accb[it % 3], wh};
+        if (final_pass) {
+            ECC_TIMED(ctx, s, "kmeans_step_kernel");
+            if (cfg->k <= 16) launch_step<16, false>(dim3(1), s, a, nullptr, 0, nullptr, st, px);
+            else launch_step<32, false>(dim3(1), s, a, nullptr, 0, nullptr, st, px);
+        } else {
+            ECC_TIMED(ctx, s, "kmeans_pixel_pass");
+            if (cfg->k <= 16) launch_step<16, true>(dim3(kPixGrid), s, a, nullptr, 0, nullptr, st, px);
+            else launch_step<32, true>(dim3(kPixGrid), s, a, nullptr, 0, nullptr, st, px);
+        }
+    };
+    for (int it = 0; it < cfg->max_iters; ++it) step(it, false);
+    if (cfg->max_iters > 0) step(cfg->max_iters, true);  // the last pass's update
+    ECC_CHECK_LAUNCH(ctx, "kmeans run_counts");
+    if (iters_out)
+        ECC_CHECK_HIP(ctx, hipMemcpyAsync(iters_out, &st->iters, 4, hipMemcpyDeviceToDevice, s), "copy iters");
     return ECC_OK;
 }

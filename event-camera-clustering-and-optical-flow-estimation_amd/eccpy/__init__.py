@@ -137,9 +137,14 @@ _sigs = {
     "ecc_kmeans_accumulate_xy16": (C.c_int, [P, P, i64, i64, P, P, i32, C.c_float, P, P, P]),
     "ecc_kmeans_update": (C.c_int, [P, P, P, i32, C.c_float, P, P]),
     "ecc_kmeans_labels_xy16": (C.c_int, [P, P, i64, i64, P, P, i32, C.c_float, P, P]),
+    "ecc_kmeans_counts_xy16": (C.c_int, [P, P, i64, i64, P, i32, i32, P, P]),
+    "ecc_kmeans_counts_status": (C.c_int, [P, P]),
+    "ecc_kmeans_run_counts": (C.c_int, [P, P, i32, i32, C.POINTER(KmeansCfg), P, P, P]),
     "ecc_sae_max_combine": (C.c_int, [P, P, i32, i64, P, P]),
     "ecc_corner_cfg_default": (None, [C.POINTER(CornerCfg)]),
     "ecc_fast_detect": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, P]),
+    "ecc_fast_detect_prepare": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P]),
+    "ecc_fast_detect_finish": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, P]),
     "ecc_fast_detect_status": (C.c_int, [P, P]),
     "ecc_sae_scatter": (C.c_int, [P, P, P, i64, i32, i32, P, P]),
     "ecc_corner_nms": (C.c_int, [P, P, P, i64, i32, i32, i32, i32, i32, P, P, P]),

@@ -1,9 +1,11 @@
 """Multi-GPU time-window sharding of the event stream.
 
 One process per GPU.  Rank r owns events [r*n, (r+1)*n) of the stream.  The exchanges:
-  * k-means: every iteration, the shards' exact integer partial sums (count, sum x, sum y per
-    centre) are all-reduced (SUM) and every rank applies the same update -> identical
-    centroids on all ranks, bit-identical to the single-GPU run;
+  * k-means (bench.py): ONE all-reduce (SUM) of the shards' per-pixel count images, then every
+    rank runs the Lloyd passes locally over the summed image (global_kmeans_counts) -> the
+    same integer sums, hence identical centroids on all ranks, bit-identical to single-GPU;
+    the per-iteration form (all-reduce of the partial sums every pass, global_kmeans) is kept
+    for points that are not pixel coordinates;
   * SAE hand-off: the shards' local final time surfaces are all-gathered and rank r starts from
     the element-wise max over ranks < r (time is non-decreasing across shards, so max == last
     writer) -> corner flags identical to the single-GPU run; only rank 0 skips the first slice.
@@ -60,6 +62,14 @@ def global_kmeans(accumulate: Callable[[], object], allreduce: Callable[[object]
         if update(acc):
             break
     return it
+
+
+def global_kmeans_counts(local_counts, allreduce: Callable[[object], None], run_counts: Callable[[object], object]):
+    """K-means over sharded integer points with ONE collective: local_counts is this rank's
+    per-pixel count image (additive over shards); after the all-reduce every rank runs the
+    Lloyd passes over the global image (run_counts) and returns its result."""
+    allreduce(local_counts)
+    return run_counts(local_counts)
 
 
 def sae_base_for_rank(local_images_all, rank: int, combine: Callable[[object, int], object]):

@@ -177,6 +177,18 @@ int ecc_kmeans_update(ecc_ctx *ctx, uint64_t *acc, float *centroids, int32_t k, 
 int ecc_kmeans_labels_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
                            const int32_t *seg_counts, const float *centroids, int32_t k,
                            float threshold, uint8_t *labels, ecc_stream_t stream);
+/* Count-image form (multi-GPU: ONE all-reduce per k-means instead of one per Lloyd pass).
+ * ecc_kmeans_counts_xy16 writes counts[y*frame_w + x] (u32) = the number of points at (x, y)
+ * (a point outside the frame sets the flag ecc_kmeans_counts_status reports as
+ * ECC_ERR_INVALID).  Count images are additive over shards; ecc_kmeans_run_counts runs the
+ * Lloyd passes ("fixed" mode, k <= 32) over a (summed) image: the same integer sums, hence the
+ * same centroids, as ecc_kmeans_run_xy16 over all the points.  Labels: ecc_kmeans_labels_xy16. */
+int ecc_kmeans_counts_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                           const int32_t *seg_counts, int32_t frame_w, int32_t frame_h, uint32_t *counts,
+                           ecc_stream_t stream);
+int ecc_kmeans_counts_status(ecc_ctx *ctx, ecc_stream_t stream);
+int ecc_kmeans_run_counts(ecc_ctx *ctx, const uint32_t *counts, int32_t frame_w, int32_t frame_h,
+                          const ecc_kmeans_cfg *cfg, float *centroids, int32_t *iters_out, ecc_stream_t stream);
 /* One assignment pass only (assign_to_centers): labels[i] in [0,k) or 255. */
 int ecc_kmeans_assign_f32(ecc_ctx *ctx, const float *xy, int64_t n_points, const float *centroids,
                           int32_t k, float threshold, uint8_t *labels, ecc_stream_t stream);
@@ -211,6 +223,15 @@ void ecc_corner_cfg_default(ecc_corner_cfg *cfg);
 int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
                     const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
                     ecc_stream_t stream);
+/* The same in two calls, for the multi-GPU SAE hand-off: prepare sorts the batch and writes
+ * local_last[H*W] = the batch's own last timestamp per pixel (0 where untouched; no SAE input
+ * needed), finish then runs the detection from the initial SAE `sae` (updated in place) with
+ * the same xy/t/n/cfg on the same context.  prepare + finish == ecc_fast_detect. */
+int ecc_fast_detect_prepare(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                            const ecc_corner_cfg *cfg, int64_t *local_last, ecc_stream_t stream);
+int ecc_fast_detect_finish(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                           const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
+                           ecc_stream_t stream);
 /* Synchronises `stream` and reports ECC_ERR_UNSORTED_TIME if the last ecc_fast_detect on
  * this context saw decreasing timestamps, else ECC_OK. */
 int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream);

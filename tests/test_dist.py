@@ -1,6 +1,7 @@
 """Multi-process (world_size 2, gloo on CPU) tests of the sharded path (eccpy/dist.py): sharded
-k-means with an all-reduce of the integer partial sums and the exact SAE hand-off reproduce the
-single-process results.  Compute backend here: the oracle (CPU)."""
+k-means (an all-reduce of the integer partial sums every pass, and ONE all-reduce of per-pixel
+count images) and the exact SAE hand-off reproduce the single-process results.  Compute backend
+here: the oracle (CPU)."""
 import os
 import socket
 
@@ -56,6 +57,17 @@ def _worker(rank, world, port, q):
             return False
 
         edist.global_kmeans(accumulate, comm.allreduce_sum, update, 6)
+        # ---- the same k-means from ONE all-reduce of per-pixel count images (bench.py's form)
+        xs_, ys_ = ecc.unpack_xy(pts)
+        cnt = torch.from_numpy(np.bincount(ys_.astype(np.int64) * W + xs_, minlength=W * H).astype(np.int64))
+
+        def run_counts(c_img):
+            img = c_img.numpy()
+            pix = np.repeat(np.arange(W * H), img)  # the global points, by pixel
+            gpts = (pix % W).astype(np.uint32) | ((pix // W).astype(np.uint32) << 16)
+            return orc.kmeans_run_xy16(gpts, c, 6)[0]
+
+        c_counts = edist.global_kmeans_counts(cnt, comm.allreduce_sum, run_counts)
         # ---- exact SAE hand-off + shard-local detection
         local = np.zeros(W * H, np.int64)
         xs, ys = ecc.unpack_xy(sx)
@@ -65,7 +77,7 @@ def _worker(rank, world, port, q):
         base = edist.sae_base_for_rank(allimg.view(world, -1).numpy(), rank,
                                        lambda imgs, r: imgs[:r].max(0) if r > 0 else np.zeros(W * H, np.int64))
         flags, _ = orc.fast_detect(sx, st, W, H, first_detect=1 if rank == 0 else 0, sae=base)
-        q.put((rank, state["c"], flags, pts))
+        q.put((rank, state["c"], flags, pts, c_counts))
     finally:
         tdist.destroy_process_group()
 
@@ -77,7 +89,7 @@ def test_two_rank_sharded_pipeline_matches_single_process(orc, ecc):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (c, f, pts)) for r, c, f, pts in (q.get(timeout=240) for _ in range(world)))
+    res = dict((r, (c, f, pts, cc)) for r, c, f, pts, cc in (q.get(timeout=240) for _ in range(world)))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
@@ -89,6 +101,7 @@ def test_two_rank_sharded_pipeline_matches_single_process(orc, ecc):
     o_c, _, _ = orc.kmeans_run_xy16(allpts, c0, 6)
     for r in range(world):
         assert np.array_equal(res[r][0].view(np.uint32), o_c.view(np.uint32))
+        assert np.array_equal(res[r][3].view(np.uint32), o_c.view(np.uint32))  # count-image form
     # corner flags of the sharded run == the single-process run over the whole stream
     o_flags, _ = orc.fast_detect(xy, t, W, H)
     assert (np.concatenate([res[0][1], res[1][1]]) == o_flags).all()

@@ -713,3 +713,63 @@ def test_graph_replay_matches_eager(ecc, orc, gpu):
     for e, a, windowed in zip(eager, (rep_xy, d_c, labels, sae, flags, nms_cnt), (1, 0, 1, 0, 0, 0)):
         got = a.numpy()
         assert (got[valid] == e[valid]).all() if windowed else (got == e).all()
+
+
+# ------------------------------------------------------------------------------ multi-GPU forms
+def test_fast_detect_prepare_finish_matches_one_call(ecc, orc, gpu):
+    """prepare (sort + pair entries + the batch's own last-t image) then finish (from a given
+    initial SAE) == ecc_fast_detect; the last-t image == per-pixel max t of the batch."""
+    W, H = 346, 260
+    n = 16384 * 45 + 1234
+    xy, t, _ = ecc.gen_events(n, seed=91, width=W, height=H)
+    sae0 = np.zeros(W * H, np.int64)
+    sae0[::7] = 5  # a non-trivial initial surface
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H, first_detect=0, sae=sae0.copy())
+    cfg = ecc.corner_cfg(width=W, height=H, first_detect_slice=0)
+    d_xy, d_t = dev(ecc, xy), dev(ecc, t)
+    local = ecc.DeviceArray(W * H, np.int64)
+    sae, flags = dev(ecc, sae0), ecc.DeviceArray(n, np.uint8)
+    lib = ecc.lib
+    ecc.check(lib.ecc_fast_detect_prepare(gpu.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(cfg), local.ptr, gpu.stream))
+    ecc.check(lib.ecc_fast_detect_finish(gpu.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(cfg), sae.ptr, flags.ptr,
+                                         gpu.stream))
+    assert gpu.fast_detect_status() == 0
+    assert (flags.numpy() == o_flags).all()
+    assert (sae.numpy() == o_sae).all()
+    x, y = ecc.unpack_xy(xy)
+    ref = np.zeros(W * H, np.int64)
+    np.maximum.at(ref, y.astype(np.int64) * W + x, t)
+    assert (local.numpy() == ref).all()
+
+
+def test_kmeans_count_images_sum_over_shards(ecc, orc, gpu):
+    """Two shards' per-pixel count images, summed, then ecc_kmeans_run_counts == the oracle's
+    k-means over the union of the shards' points (bit-identical centroids)."""
+    W, H, K = 346, 260, 16
+    xy, _, _ = ecc.gen_events(16384 * 30, seed=33, width=W, height=H)
+    rx, _, u, _ = orc.downsample_hash(xy)
+    pts = np.concatenate([rx[w * 8192: w * 8192 + u[w]] for w in range(len(u))])
+    half = len(pts) // 2
+    c0 = np.stack([np.linspace(20, W - 20, K), np.linspace(20, H - 20, K)[::-1]], 1).astype(np.float32).ravel()
+    lib = ecc.lib
+    total = np.zeros(W * H, np.uint32)
+    for part in (pts[:half], pts[half:]):
+        cnt = ecc.DeviceArray(W * H, np.uint32)
+        ecc.check(lib.ecc_kmeans_counts_xy16(gpu.ctx, dev(ecc, part).ptr, 1, len(part), None, W, H, cnt.ptr,
+                                             gpu.stream))
+        assert lib.ecc_kmeans_counts_status(gpu.ctx, gpu.stream) == 0
+        total += cnt.numpy()
+    xs, ys = ecc.unpack_xy(pts)
+    assert (total == np.bincount(ys.astype(np.int64) * W + xs, minlength=W * H)).all()
+    kcfg = ecc.kmeans_cfg(k=K, max_iters=10, tol=-1.0)
+    d_c = dev(ecc, c0)
+    ecc.check(lib.ecc_kmeans_run_counts(gpu.ctx, dev(ecc, total).ptr, W, H, ecc.C.byref(kcfg), d_c.ptr, None,
+                                        gpu.stream))
+    gpu.sync()
+    o_c, _, _ = orc.kmeans_run_xy16(pts, c0, 10)
+    assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
+    # a point outside the frame is reported
+    bad = np.array([ecc.pack_xy(W, 3)], np.uint32)
+    cnt = ecc.DeviceArray(W * H, np.uint32)
+    ecc.check(lib.ecc_kmeans_counts_xy16(gpu.ctx, dev(ecc, bad).ptr, 1, 1, None, W, H, cnt.ptr, gpu.stream))
+    assert lib.ecc_kmeans_counts_status(gpu.ctx, gpu.stream) == ecc.ERR_INVALID
