@@ -255,7 +255,7 @@ def main():
     # tracker (sequential over slices): reported separately, µs per slice
     tracker_us = None
     if not args.no_tracker and rank == 0:
-        tr = ecc.Tracker(ctx, max_tracks=16384)
+        tr = ecc.Tracker(ctx)
         tmr = ecc.Timer(ctx.stream)
         tmr.start()
         tr.update(nms_out, nms_cnt, ns, cap)

@@ -5,26 +5,45 @@
 // damping 0.8, velocity/direction blend 0.3, group-velocity blend 0.3).  It runs on the CPU
 // once per 16384-event slice (:847), O(T*C) matching + O(T^2) grouping.
 //
-// MI355X design: the whole multi-slice update runs in ONE launch of one workgroup (a single
-// wave64 — the algorithm is order-dependent: greedy matching in track order, greedy grouping
-// in seed order), so a batch of slices costs one kernel instead of one host round trip each.
-// Parallel phases use one lane per track / per detection (prediction, state update, new-track
-// creation with ballot prefix sums, stable erase by compaction into a ping-pong buffer, group
-// membership tests, velocity blend); the sequential phases (match claim per track, member
-// sums per group) keep the reference's order.  Every fp32 expression is written in the
-// reference's operation order and compiled without FMA contraction, so positions, velocities
-// and directions are bit-identical to oracle/oracle.cpp (std::pow(0.8f, i-1) is a host-side
-// table, :254).
+// MI355X design: the whole multi-slice update runs in ONE launch of one workgroup (the
+// algorithm is sequential over slices and order-dependent inside one: greedy matching in track
+// order, greedy grouping in seed order), so a batch of slices costs one kernel instead of one
+// host round trip each.  A slice's working set (detections, predictions, match states, the
+// grouping candidates) lives in LDS, so the per-track state is read and written once per
+// slice; matching runs as parallel conflict-free rounds that provably reproduce the greedy
+// order (see tracker_kernel), update + erase + append is one block-scan pass, and only the
+// grouping's ordered sums stay sequential.  Every fp32 expression is written in the
+// reference's operation order and compiled without FMA contraction, so positions,
+// velocities and directions are bit-identical to oracle/oracle.cpp (std::pow(0.8f, i-1) is a
+// host-side table, :254).
 #include "ecc_internal.hpp"
 
 #include <cmath>
 #include <vector>
 
+#ifndef ECC_TRACKER_PROFILE
+#define ECC_TRACKER_PROFILE 0
+#endif
+
 namespace {
 
-constexpr int kLanes = 64;
+#if ECC_TRACKER_PROFILE
+// wall-clock ticks per phase (thread 0, after the phase's barrier) + matching rounds
+__device__ unsigned long long g_trk_prof[12];
+#define TRK_MARK(k)                                                  \
+    do {                                                             \
+        const unsigned long long now_ = wall_clock64();              \
+        prof[k] += now_ - last_;                                     \
+        last_ = now_;                                                \
+    } while (0)
+#else
+#define TRK_MARK(k) do { } while (0)
+#endif
+
+constexpr int kNT = 1024;                        // one workgroup of 16 waves (4 per SIMD)
 constexpr int kH = ECC_TRACK_HIST_MAX;
-constexpr int kMaxDet = 4096;  // detections per slice held in LDS
+constexpr int kMaxTrk = ECC_TRACKER_MAX_TRACKS;  // active tracks of a slice held in LDS
+constexpr int kMaxDet = ECC_TRACKER_MAX_DETECTIONS;
 
 struct DevTrack {
     int x, y, label, frame_count, is_matched, fsld, hist_len;
@@ -123,216 +142,607 @@ __device__ __forceinline__ F2 predict(const DevTrack &t, const TrackerParams &p)
     return pred;
 }
 
-__global__ void __launch_bounds__(kLanes)
-tracker_kernel(DevTrack *__restrict__ buf0, DevTrack *__restrict__ buf1, int max_tracks,
-               DevGroup *__restrict__ groups, int *__restrict__ group_labels,
-               uint8_t *__restrict__ work, TrackerCounters *__restrict__ ctr, TrackerParams p,
-               const ecc_corner *__restrict__ corners, const int32_t *__restrict__ counts,
-               int n_slices, int cap) {
-    __shared__ int s_dx[kMaxDet], s_dy[kMaxDet];
-    __shared__ uint8_t s_dmatched[kMaxDet];
-    const int lane = threadIdx.x;
-    // per-track scratch in global memory: pred x/y, best match, processed flag
-    float *w_px = reinterpret_cast<float *>(work);
-    float *w_py = w_px + max_tracks;
-    int *w_best = reinterpret_cast<int *>(w_py + max_tracks);
-    uint8_t *w_proc = reinterpret_cast<uint8_t *>(w_best + max_tracks);
+// ---- LDS plan.  A slice's working set lives in LDS, in distinct __shared__ arrays (so the
+// compiler can keep loads of one in flight across atomics on another); an array is reused once
+// its phase is over (P0 detections, P1 predictions, P2 matching rounds, P3 update/erase/append,
+// P4 grouping).  Candidates (tracks with fsld == 0 after P3) each own a distinct detection, so
+// there are at most C of them.
+static_assert(kMaxTrk == kMaxDet, "ck_x/ck_y overlay the prediction arrays");
+static_assert(kMaxTrk <= 4096, "track index packs into 12 bits of the matching tag");
+static_assert(64 * 16 <= 2 * kMaxTrk, "member staging fits the st array");
 
+// Detection grid for the matching scans: cells of kCell >= 2 * (max_distance + 1) + 2 pixels
+// hashed into kBuckets buckets, so every detection a prediction can reach lies in at most 2 x 2
+// cells.  Collisions only add candidates (the argmin is taken over (dist, index) explicitly).
+constexpr int kBuckets = 1024;
+constexpr int kBrute = 384;
+constexpr int kLaneList = 4;  // in-range detections a matching lane keeps in registers  // up to this many detections a scan walks all of them (uniform, no grid)  // per-track candidate list held in registers during the matching rounds
+__device__ __forceinline__ int floor_div(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+__device__ __forceinline__ int cell_bucket(int cx, int cy) {
+    return (int)(((uint32_t)cx * 0x9E3779B1u ^ (uint32_t)cy * 0x85EBCA77u) >> (32 - 10));
+}
+static_assert(kBuckets == 1 << 10, "bucket hash takes the top 10 bits");
+
+// Exclusive scan of v[0..kBuckets) in place (one entry per thread); v[kBuckets] = total.
+__device__ __forceinline__ void block_scan_buckets(int *v, int *ws) {
+    static_assert(kBuckets == kNT, "one bucket per thread");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int a = v[threadIdx.x];
+    int inc = a;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(inc, d);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    int pre = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kNT / 64; ++w) {
+        pre += w < wave ? ws[w] : 0;
+        all += ws[w];
+    }
+    v[threadIdx.x] = pre + inc - a;
+    if (threadIdx.x == 0) v[kBuckets] = all;
+    __syncthreads();
+}
+
+// Compiler-only ordering point for wave-synchronous LDS exchanges (no hardware wait needed:
+// one wave's LDS instructions execute in issue order).
+__device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
+
+__device__ __forceinline__ uint64_t lanes_below() {
+    const int lane = threadIdx.x & 63;
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// Exclusive block-wide ranks of two per-thread flags (thread order); totals through *t0, *t1.
+__device__ __forceinline__ void block_rank2(bool f0, bool f1, int *ws, int &r0, int &r1, int &t0, int &t1) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
+    if (lane == 0) {
+        ws[wave] = __popcll(m0);
+        ws[16 + wave] = __popcll(m1);
+    }
+    __syncthreads();
+    int p0 = 0, p1 = 0;
+    t0 = 0;
+    t1 = 0;
+#pragma unroll
+    for (int w = 0; w < kNT / 64; ++w) {
+        const int c0 = ws[w], c1 = ws[16 + w];
+        p0 += w < wave ? c0 : 0;
+        p1 += w < wave ? c1 : 0;
+        t0 += c0;
+        t1 += c1;
+    }
+    __syncthreads();  // ws reusable
+    r0 = p0 + __popcll(m0 & lanes_below());
+    r1 = p1 + __popcll(m1 & lanes_below());
+}
+
+// Track stores: a grouping candidate's vx, vy and group_id are written once, after grouping.
+__device__ __forceinline__ void store_track(DevTrack *dst, const DevTrack &t, bool cand) {
+    dst->x = t.x; dst->y = t.y; dst->label = t.label; dst->frame_count = t.frame_count;
+    dst->is_matched = t.is_matched; dst->fsld = t.fsld; dst->hist_len = t.hist_len;
+#pragma unroll
+    for (int k = 0; k < kH; ++k) { dst->hx[k] = t.hx[k]; dst->hy[k] = t.hy[k]; }
+    dst->dcx = t.dcx; dst->dcy = t.dcy; dst->dtx = t.dtx; dst->dty = t.dty;
+    if (!cand) { dst->vx = t.vx; dst->vy = t.vy; dst->group_id = t.group_id; }
+}
+
+// One workgroup processes the slices in order (the algorithm is sequential over slices); inside
+// a slice every phase is parallel over tracks / detections / candidates except the greedy
+// grouping (wave 0).
+//   P1  prediction per track (:451), is_matched reset (:438-441).
+//   P2  greedy matching in track order (:446-487) as conflict-free rounds: every unresolved
+//       track takes its nearest unclaimed detection with dist < max_distance (first minimum),
+//       and keeps it iff no earlier unresolved track has that detection in range (the
+//       smallest such track index per detection is an LDS atomicMin of a round-tagged key).
+//       Earlier tracks can then never claim it, and the argmin over a shrinking set that
+//       still holds it is unchanged, so the result equals the sequential loop; the first
+//       unresolved track always resolves, so rounds terminate.
+//   P3  matched / missed update (:471-497), new tracks for unmatched detections in detection
+//       order (:501-514) and the stable erase (:517-526) in one pass: kept tracks are written
+//       to the other buffer at their block-scan rank; candidates (fsld == 0) are listed in LDS.
+//   P4  greedy grouping in seed order over the candidates (:321-398) with ordered fp32 sums,
+//       then the group-velocity blend (:388-397).
+__global__ void __launch_bounds__(kNT)
+tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restrict__ groups,
+               int *__restrict__ group_labels, TrackerCounters *__restrict__ ctr, TrackerParams p,
+               const ecc_corner *__restrict__ corners, const int32_t *__restrict__ counts, int n_slices,
+               int cap) {
+    __shared__ int2 s_det[kMaxDet + 4];              // P0-P3 detections; P4 group average velocity
+    __shared__ uint32_t s_claim[kMaxDet / 32];       // P0-P3 claimed detections (bits)
+    __shared__ int s_want[kMaxDet];                  // P2 matching tags; P3-P4 candidate label
+    __shared__ float s_px[kMaxTrk], s_py[kMaxTrk];   // P1-P2 predictions; P3-P4 candidate x, y
+    __shared__ __attribute__((aligned(16))) int16_t s_st[kMaxTrk];  // P1-P3 match state; P4 member staging
+    __shared__ __attribute__((aligned(16))) float s_cv[2 * kMaxDet];  // P3-P4 candidate velocity; P0-P2 grid entries
+    __shared__ __attribute__((aligned(16))) int16_t s_ctidx[kMaxDet];  // candidate's index in the new list; P0-P2 bucket ends
+    __shared__ int s_cgid[kMaxDet];                  // candidate's group id (stale until grouped)
+    __shared__ uint8_t s_cproc[kMaxDet];             // grouped
+    __shared__ int s_ws[32];                         // wave counts
+    __shared__ unsigned s_rad;                       // group radius (fp32 bits, >= 0)
+    int2 *const det = s_det;
+    float2 *const gav = reinterpret_cast<float2 *>(s_det);
+    uint32_t *const claim = s_claim;
+    int *const want = s_want, *const ck_label = s_want;
+    float *const px = s_px, *const py = s_py;
+    int *const ck_x = reinterpret_cast<int *>(s_px), *const ck_y = reinterpret_cast<int *>(s_py);
+    int16_t *const st = s_st;
+    float4 *const stage = reinterpret_cast<float4 *>(s_st);
+    float *const ck_vx = s_cv, *const ck_vy = s_cv + kMaxDet;
+    int16_t *const ck_tidx = s_ctidx;
+    int *const ck_gid = s_cgid;
+    uint8_t *const ck_proc = s_cproc;
+    int *const ws = s_ws;
+    // grid entries {x | y << 16 (int16 each), index} by bucket; g_end[b] = end of bucket b
+    uint2 *const g_ent = reinterpret_cast<uint2 *>(s_cv);
+    int *const g_end = reinterpret_cast<int *>(s_ctidx);
+    static_assert(sizeof(uint2) * kMaxDet <= sizeof(s_cv), "grid entries fit s_cv");
+    static_assert((kBuckets + 1) * sizeof(int) <= sizeof(s_ctidx), "bucket ends fit s_ctidx");
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // |dx| or |dy| above max_distance + 1 cannot give dist < max_distance (for sane radii)
+    const bool prefilter = p.max_distance < 1.0e6f;
+    const float reach = __fadd_rn(p.max_distance, 1.0f);
+    // grid matching for sane radii; otherwise every scan walks all detections
+    const bool grid_ok = p.max_distance >= 0.0f && p.max_distance < 1.0e5f;
+    const int cell = grid_ok ? (int)ceilf(reach) + 1 : 1;
     int T = ctr->n_tracks, next_label = ctr->next_label, cur = ctr->cur, err = ctr->err;
     int n_groups = 0, n_glabels = 0;
+#if ECC_TRACKER_PROFILE
+    unsigned long long prof[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, last_ = wall_clock64();
+    const unsigned long long c0_ = clock64(), w0_ = last_;
+#endif
     for (int s = 0; s < n_slices; ++s) {
-        DevTrack *A = cur ? buf1 : buf0;  // active tracks
-        DevTrack *Bf = cur ? buf0 : buf1; // compaction target
+        DevTrack *A = cur ? buf1 : buf0;   // active tracks
+        DevTrack *Bf = cur ? buf0 : buf1;  // next active list
         int C = counts[s];
         if (C > cap) C = cap;
-        if (C > kMaxDet) { C = kMaxDet; err = ECC_ERR_CAPACITY; }
-        for (int d = lane; d < C; d += kLanes) {
+        if (C < 0) C = 0;
+        // P0: detections
+        bool wide = false;  // a coordinate outside int16: this slice scans without the grid
+        for (int d = tid; d < C; d += kNT) {
             const ecc_corner c = corners[(int64_t)s * cap + d];
-            s_dx[d] = c.x;
-            s_dy[d] = c.y;
-            s_dmatched[d] = 0;
+            det[d] = make_int2(c.x, c.y);
+            want[d] = 0x7fffffff;
+            wide |= c.x < -32768 || c.x > 32767 || c.y < -32768 || c.y > 32767;
         }
-        // 1. prediction for every active track (:451) + reset is_matched (:438-441)
-        for (int i = lane; i < T; i += kLanes) {
-            const F2 pp = predict(A[i], p);
-            w_px[i] = pp.x;
-            w_py[i] = pp.y;
-            A[i].is_matched = 0;
+        for (int w = tid; w < (C + 31) / 32; w += kNT) claim[w] = 0u;
+        const bool any_wide = __syncthreads_or(wide);
+        const bool use_grid = grid_ok && C > kBrute && !any_wide;
+        if (use_grid) {
+            for (int b = tid; b <= kBuckets; b += kNT) g_end[b] = 0;
+            __syncthreads();
+            for (int d = tid; d < C; d += kNT) {
+                const int2 q = det[d];
+                atomicAdd(&g_end[cell_bucket(floor_div(q.x, cell), floor_div(q.y, cell))], 1);
+            }
         }
-        __syncthreads();
-        // 2. greedy matching in track order (:446-487): first nearest unmatched with dist < max
-        for (int i = 0; i < T; ++i) {
-            const bool skip = A[i].fsld > p.frames_to_skip;
-            const F2 pp{w_px[i], w_py[i]};
-            float bd = p.max_distance;
-            int bi = 0x7fffffff;
-            if (!skip) {
-                for (int d = lane; d < C; d += kLanes) {
-                    if (s_dmatched[d]) continue;
-                    const float dd = dist(pp, F2{(float)s_dx[d], (float)s_dy[d]});
-                    if (dd < bd) { bd = dd; bi = d; }
-                }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const float ob = __shfl_xor(bd, o);
-                const int oi = __shfl_xor(bi, o);
-                if (ob < bd || (ob == bd && oi < bi)) { bd = ob; bi = oi; }
-            }
-            if (lane == 0) {
-                w_best[i] = skip ? -2 : (bi == 0x7fffffff ? -1 : bi);
-                if (!skip && bi != 0x7fffffff) s_dmatched[bi] = 1;
+        // P1: predictions
+        bool open = false;
+        for (int i = tid; i < T; i += kNT) {
+            const DevTrack &t = A[i];
+            DevTrack q;
+            q.x = t.x; q.y = t.y; q.vx = t.vx; q.vy = t.vy; q.dcx = t.dcx; q.dcy = t.dcy; q.fsld = t.fsld;
+            const F2 pp = predict(q, p);
+            px[i] = pp.x;
+            py[i] = pp.y;
+            const bool skip = q.fsld > p.frames_to_skip;
+            st[i] = skip ? (int16_t)-2 : (int16_t)-3;
+            open |= !skip;
+        }
+        // P2: matching rounds
+        int round = 0;
+        bool pending = __syncthreads_or(open) && C > 0;
+        if (use_grid && pending) {
+            TRK_MARK(0);
+            block_scan_buckets(g_end, ws);  // bucket starts
+            for (int d = tid; d < C; d += kNT) {  // scatter; afterwards g_end[b] = end of bucket b
+                const int2 q = det[d];
+                const int at = atomicAdd(&g_end[cell_bucket(floor_div(q.x, cell), floor_div(q.y, cell))], 1);
+                g_ent[at] = make_uint2(((uint32_t)q.x & 0xFFFFu) | ((uint32_t)q.y << 16), (uint32_t)d);
             }
             __syncthreads();
         }
-        // 3. update matched / missed tracks (:471-497)
-        for (int i = lane; i < T; i += kLanes) {
-            const int b = w_best[i];
-            if (b == -2) continue;
-            DevTrack t = A[i];
-            if (b >= 0) {
-                t.x = s_dx[b];
-                t.y = s_dy[b];
-                t.is_matched = 1;
-                t.fsld = 0;
-                t.frame_count++;
-                push_hist(t, p.history);
-                const F2 nd = calc_direction(t, p);
-                t.dtx = nd.x;                                          // DirectionVector::update
-                t.dty = nd.y;
-                t.dcx = __fadd_rn(__fmul_rn(t.dcx, p.damping), __fmul_rn(t.dtx, __fsub_rn(1.0f, p.damping)));
-                t.dcy = __fadd_rn(__fmul_rn(t.dcy, p.damping), __fmul_rn(t.dty, __fsub_rn(1.0f, p.damping)));
-                const F2 v = estimate_velocity(t, p);
-                t.vx = v.x;
-                t.vy = v.y;
-            } else {
-                t.x = (int)w_px[i];                                    // Q16 truncation
-                t.y = (int)w_py[i];
-                t.fsld++;
-                push_hist(t, p.history);
-                const F2 v = estimate_velocity(t, p);
-                t.vx = v.x;
-                t.vy = v.y;
+        TRK_MARK(7);
+        if (C == 0)
+            for (int i = tid; i < T; i += kNT)
+                if (st[i] == -3) st[i] = -1;
+        // Grid visitor (large C, one lane per track): f(d, dd) for every unclaimed detection with
+        // dist < max_distance from the prediction pp.
+        auto visit_grid = [&](const F2 pp, bool check_claims, auto &&f) {
+            // the cells of the integer box [pp - reach, pp + reach]: at most 3 x 3
+            const int cx0 = floor_div((int)floorf(__fsub_rn(pp.x, reach)), cell);
+            const int cx1 = floor_div((int)ceilf(__fadd_rn(pp.x, reach)), cell);
+            const int cy0 = floor_div((int)floorf(__fsub_rn(pp.y, reach)), cell);
+            const int cy1 = floor_div((int)ceilf(__fadd_rn(pp.y, reach)), cell);
+            int seen[9], ns = 0;
+            for (int cy = cy0; cy <= cy1; ++cy)
+                for (int cx = cx0; cx <= cx1; ++cx) {
+                    const int b = cell_bucket(cx, cy);
+                    bool dup = false;
+                    for (int k = 0; k < ns; ++k) dup |= seen[k] == b;  // hash collision
+                    if (dup) continue;
+                    seen[ns++] = b;
+                    const int e1 = g_end[b];
+                    for (int e = b ? g_end[b - 1] : 0; e < e1; ++e) {
+                        const uint2 g = g_ent[e];
+                        const float fx = (float)(int16_t)(g.x & 0xFFFFu), fy = (float)(int16_t)(g.x >> 16);
+                        if (fabsf(__fsub_rn(pp.x, fx)) > reach || fabsf(__fsub_rn(pp.y, fy)) > reach) continue;
+                        const int d = (int)g.y;
+                        if (check_claims && ((claim[d >> 5] >> (d & 31)) & 1u)) continue;
+                        const float dd = dist(pp, F2{fx, fy});
+                        if (dd < p.max_distance) f(d, dd);
+                    }
+                }
+        };
+        // L lanes per track (a power of two, T * L <= kNT): lane jl of a track's group scans
+        // detections jl, jl + L, ...; the group combines its (dist, index) minima with shuffles.
+        int L = 1;
+        if (!use_grid)
+            while (L < 64 && T * L * 2 <= kNT) L <<= 1;
+        const int jl = tid & (L - 1);
+        // Each lane's in-range detections of the first round stay in registers (the lane owns one
+        // track when T * L <= kNT), so later rounds only re-check claims; a lane with more than
+        // kLaneList of them rescans its share instead.
+        const bool lists_ok = T <= kNT / L;
+        float l_d[kLaneList];
+        int l_i[kLaneList];
+        int l_n = 0;
+        bool l_ovf = false;
+        while (pending) {
+            const int tag = (8191 - round) << 12;
+            for (int i = tid / L; i < T; i += kNT / L) {
+                if (st[i] != -3) continue;  // uniform over the lane group
+                float bd = p.max_distance;
+                int bi = -1;
+                auto take = [&](int d, float dd) {
+                    atomicMin(&want[d], tag | i);
+                    // first minimum in detection order == smallest (dist, index)
+                    if (bi < 0 || dd < bd || (dd == bd && d < bi)) { bd = dd; bi = d; }
+                };
+                if (lists_ok && round > 0 && !l_ovf) {
+#pragma unroll
+                    for (int k = 0; k < kLaneList; ++k)
+                        if (k < l_n && !((claim[l_i[k] >> 5] >> (l_i[k] & 31)) & 1u)) take(l_i[k], l_d[k]);
+                } else {
+                    const F2 pp{px[i], py[i]};
+                    const bool record = lists_ok && round == 0;
+                    auto take_rec = [&](int d, float dd) {
+                        take(d, dd);
+                        if (record) {
+#pragma unroll
+                            for (int k = 0; k < kLaneList; ++k)
+                                if (k == l_n) { l_d[k] = dd; l_i[k] = d; }
+                            l_ovf |= l_n == kLaneList;
+                            l_n += l_n < kLaneList ? 1 : 0;
+                        }
+                    };
+                    if (use_grid && fabsf(pp.x) < 1.0e9f && fabsf(pp.y) < 1.0e9f) {
+                        visit_grid(pp, round > 0, take_rec);
+                    } else {
+                        for (int d = jl; d < C; d += L) {
+                            if (round > 0 && ((claim[d >> 5] >> (d & 31)) & 1u)) continue;
+                            const int2 q = det[d];
+                            const float fx = (float)q.x, fy = (float)q.y;
+                            if (prefilter && (fabsf(__fsub_rn(pp.x, fx)) > reach || fabsf(__fsub_rn(pp.y, fy)) > reach))
+                                continue;
+                            const float dd = dist(pp, F2{fx, fy});
+                            if (dd < p.max_distance) take_rec(d, dd);
+                        }
+                    }
+                }
+                for (int o = L >> 1; o > 0; o >>= 1) {
+                    const float od = __shfl_xor(bd, o);
+                    const int oi = __shfl_xor(bi, o);
+                    if (oi >= 0 && (bi < 0 || od < bd || (od == bd && oi < bi))) { bd = od; bi = oi; }
+                }
+                if (jl == 0) st[i] = bi < 0 ? (int16_t)-1 : (int16_t)(-4 - bi);
             }
-            A[i] = t;
+            __syncthreads();
+            if (round == 0) TRK_MARK(8); else TRK_MARK(1);
+            bool again = false;
+            for (int i = tid; i < T; i += kNT) {
+                const int sv = st[i];
+                if (sv > -4) continue;
+                const int b = -4 - sv;
+                if (want[b] == (tag | i)) {
+                    st[i] = (int16_t)b;
+                    atomicOr(&claim[b >> 5], 1u << (b & 31));
+                } else {
+                    st[i] = -3;
+                    again = true;
+                }
+            }
+            ++round;
+            pending = __syncthreads_or(again);
+            TRK_MARK(5);
         }
         __syncthreads();
-        // 4. new tracks for unmatched detections, in detection order (:501-514)
-        for (int d0 = 0; d0 < C; d0 += kLanes) {
-            const int d = d0 + lane;
-            const bool nw = d < C && !s_dmatched[d];
-            const uint64_t m = __ballot(nw);
-            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-            const int slot = T + __popcll(m & lt);
-            if (nw) {
-                if (slot < max_tracks) {
-                    DevTrack t;
-                    t.x = s_dx[d];
-                    t.y = s_dy[d];
-                    t.label = next_label + __popcll(m & lt);
-                    t.frame_count = 1;
-                    t.is_matched = 0;
+        TRK_MARK(1);
+#if ECC_TRACKER_PROFILE
+        prof[6] += round;
+#endif
+        // P3: update, erase, append
+        int T2 = 0, G = 0;
+        for (int base = 0; base < T; base += kNT) {
+            const int i = base + tid;
+            DevTrack t;
+            bool keep = false, cand = false;
+            if (i < T) {
+                t = A[i];
+                const int sv = st[i];
+                t.is_matched = 0;
+                if (sv >= 0) {  // matched (:471-485)
+                    t.x = det[sv].x;
+                    t.y = det[sv].y;
+                    t.is_matched = 1;
                     t.fsld = 0;
-                    t.hist_len = 0;
-#pragma unroll
-                    for (int k = 0; k < kH; ++k) { t.hx[k] = 0; t.hy[k] = 0; }
+                    t.frame_count++;
                     push_hist(t, p.history);
-                    t.vx = t.vy = 0.f;
-                    t.dcx = t.dcy = t.dtx = t.dty = 0.f;
-                    t.group_id = -1;                                   // Q17
-                    A[slot] = t;
+                    const F2 nd = calc_direction(t, p);
+                    t.dtx = nd.x;                                          // DirectionVector::update
+                    t.dty = nd.y;
+                    t.dcx = __fadd_rn(__fmul_rn(t.dcx, p.damping), __fmul_rn(t.dtx, __fsub_rn(1.0f, p.damping)));
+                    t.dcy = __fadd_rn(__fmul_rn(t.dcy, p.damping), __fmul_rn(t.dty, __fsub_rn(1.0f, p.damping)));
+                    const F2 v = estimate_velocity(t, p);
+                    t.vx = v.x;
+                    t.vy = v.y;
+                } else if (sv == -1) {  // missed (:488-497): move to the prediction
+                    const F2 pp = predict(t, p);
+                    t.x = (int)pp.x;                                       // Q16 truncation
+                    t.y = (int)pp.y;
+                    t.fsld++;
+                    push_hist(t, p.history);
+                    const F2 v = estimate_velocity(t, p);
+                    t.vx = v.x;
+                    t.vy = v.y;
+                }
+                keep = !(t.fsld > p.frames_to_skip || t.frame_count > p.max_frames);
+                cand = keep && t.fsld == 0;
+            }
+            int rk, rc, tk, tc;
+            block_rank2(keep, cand, ws, rk, rc, tk, tc);
+            if (keep) store_track(Bf + T2 + rk, t, cand);
+            if (cand) {
+                const int k = G + rc;
+                ck_x[k] = t.x;
+                ck_y[k] = t.y;
+                ck_vx[k] = t.vx;
+                ck_vy[k] = t.vy;
+                ck_label[k] = t.label;
+                ck_tidx[k] = (int16_t)(T2 + rk);
+                ck_gid[k] = t.group_id;
+            }
+            T2 += tk;
+            G += tc;
+        }
+        TRK_MARK(2);
+        // new tracks for the unmatched detections, in detection order; slots past max_tracks
+        // (counted before the erase, like the reference's append-then-erase) are dropped
+        const int room = max_tracks - T;
+        const bool keep_new = !(0 > p.frames_to_skip || 1 > p.max_frames);
+        int n_unm = 0;
+        for (int base = 0; base < C; base += kNT) {
+            const int d = base + tid;
+            const bool un = d < C && !((claim[d >> 5] >> (d & 31)) & 1u);
+            int r, r_unused, tot, tot_unused;
+            block_rank2(un, false, ws, r, r_unused, tot, tot_unused);
+            r += n_unm;
+            if (un) {
+                if (r < room) {
+                    if (keep_new) {
+                        DevTrack t;
+                        t.x = det[d].x;
+                        t.y = det[d].y;
+                        t.label = next_label + r;
+                        t.frame_count = 1;
+                        t.is_matched = 0;
+                        t.fsld = 0;
+                        t.hist_len = 0;
+#pragma unroll
+                        for (int k = 0; k < kH; ++k) { t.hx[k] = 0; t.hy[k] = 0; }
+                        push_hist(t, p.history);
+                        t.vx = t.vy = 0.f;
+                        t.dcx = t.dcy = t.dtx = t.dty = 0.f;
+                        t.group_id = -1;                                   // Q17
+                        store_track(Bf + T2 + r, t, true);
+                        const int k = G + r;
+                        ck_x[k] = t.x;
+                        ck_y[k] = t.y;
+                        ck_vx[k] = 0.f;
+                        ck_vy[k] = 0.f;
+                        ck_label[k] = t.label;
+                        ck_tidx[k] = (int16_t)(T2 + r);
+                        ck_gid[k] = -1;
+                    }
                 } else {
                     err = ECC_ERR_CAPACITY;
                 }
             }
-            const int added = __popcll(m);
-            next_label += added;
-            T = min(T + added, max_tracks);
+            n_unm += tot;
         }
-        __syncthreads();
-        // 5. stable erase of lost / expired tracks (:517-526) into the other buffer
-        int T2 = 0;
-        for (int i0 = 0; i0 < T; i0 += kLanes) {
-            const int i = i0 + lane;
-            bool keep = false;
-            if (i < T) keep = !(A[i].fsld > p.frames_to_skip || A[i].frame_count > p.max_frames);
-            const uint64_t m = __ballot(keep);
-            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-            if (keep) Bf[T2 + __popcll(m & lt)] = A[i];
-            T2 += __popcll(m);
+        next_label += n_unm;
+        const int added = room > 0 ? min(n_unm, room) : 0;
+        if (keep_new) {
+            T2 += added;
+            G += added;
         }
         T = T2;
         cur ^= 1;
-        DevTrack *R = Bf;  // now the active buffer
         __syncthreads();
-        // 6. greedy grouping in seed order (:321-398)
-        for (int i = lane; i < T; i += kLanes) w_proc[i] = 0;
-        __syncthreads();
-        n_groups = 0;
-        n_glabels = 0;
-        for (int i = 0; i < T; ++i) {
-            if (w_proc[i] || R[i].fsld > 0) continue;          // uniform: all lanes read the same
-            const F2 pi{(float)R[i].x, (float)R[i].y};
-            // membership: unprocessed, detected this slice, within radius (self included)
-            int cnt = 0;
-            F2 sp{0.f, 0.f}, sv{0.f, 0.f};
-            const int gid = n_groups;
-            for (int j0 = 0; j0 < T; j0 += kLanes) {
-                const int j = j0 + lane;
-                bool mem = false;
-                if (j < T && !w_proc[j] && R[j].fsld == 0)
-                    mem = dist(pi, F2{(float)R[j].x, (float)R[j].y}) <= p.group_radius;
-                uint64_t m = __ballot(mem);
-                int mx = 0, my = 0, mlab = 0;
-                float mvx = 0.f, mvy = 0.f;
+        TRK_MARK(3);
+        // P4: greedy grouping in seed order over the candidates, then the velocity blend (wave 0).
+        // Wave-synchronous: a wave's LDS operations execute in issue order, so only compiler
+        // reordering has to be fenced (wave_sync).
+        if (wave == 0 && G <= 64) {
+            // one candidate per lane, in registers: seed search and membership are ballots,
+            // the ordered sums walk the member lanes with readlane
+            const bool valid = lane < G;
+            const int mx = valid ? ck_x[lane] : 0, my = valid ? ck_y[lane] : 0;
+            const float mvx = valid ? ck_vx[lane] : 0.f, mvy = valid ? ck_vy[lane] : 0.f;
+            const int mlab = valid ? ck_label[lane] : 0, mtidx = valid ? ck_tidx[lane] : 0;
+            int mgid = valid ? ck_gid[lane] : -1;
+            float gax = 0.f, gay = 0.f;  // the lane's group average velocity
+            bool proc = !valid;
+            n_groups = 0;
+            n_glabels = 0;
+            int next = 0;
+            for (;;) {
+                const uint64_t open_ = __ballot(!proc && lane >= next);
+                if (!open_) break;
+                const int sl = __ffsll((unsigned long long)open_) - 1;
+                next = sl + 1;
+                const F2 pi{(float)__builtin_amdgcn_readlane(mx, sl), (float)__builtin_amdgcn_readlane(my, sl)};
+                const bool mem = !proc && dist(pi, F2{(float)mx, (float)my}) <= p.group_radius;
+                const uint64_t m = __ballot(mem);
+                if (!m) continue;
+                const int gid = n_groups, cnt = __popcll(m);
                 if (mem) {
-                    w_proc[j] = 1;
-                    R[j].group_id = gid;
-                    mx = R[j].x; my = R[j].y; mlab = R[j].label;
-                    mvx = R[j].vx; mvy = R[j].vy;
+                    proc = true;
+                    mgid = gid;
+                    const int r = __popcll(m & lanes_below());
+                    if (n_glabels + r < max_tracks) group_labels[n_glabels + r] = mlab;
                 }
-                // ordered fp32 sums over members (j ascending), evaluated redundantly per lane
-                while (m) {
-                    const int l = __ffsll((unsigned long long)m) - 1;
-                    m &= m - 1;
-                    const int xj = __shfl(mx, l), yj = __shfl(my, l), lab = __shfl(mlab, l);
-                    const float vxj = __shfl(mvx, l), vyj = __shfl(mvy, l);
-                    sp = add(sp, F2{(float)xj, (float)yj});
-                    sv = add(sv, F2{vxj, vyj});
-                    if (lane == 0 && n_glabels + cnt < max_tracks) group_labels[n_glabels + cnt] = lab;
-                    cnt++;
+                // ordered fp32 sums over the members (lane = candidate order)
+                F2 sp{0.f, 0.f}, sv{0.f, 0.f};
+                for (uint64_t mm = m; mm; mm &= mm - 1) {
+                    const int l = __ffsll((unsigned long long)mm) - 1;
+                    sp = add(sp, F2{(float)__builtin_amdgcn_readlane(mx, l), (float)__builtin_amdgcn_readlane(my, l)});
+                    sv = add(sv, F2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mvx), l)),
+                                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mvy), l))});
                 }
-            }
-            __syncthreads();
-            if (cnt > 0) {
                 const F2 cen = mul(sp, __fdiv_rn(1.0f, (float)cnt));
                 const F2 av = mul(sv, __fdiv_rn(1.0f, (float)cnt));
-                // radius = max distance of the group's members to the centroid
+                const float dm = mem ? dist(F2{(float)mx, (float)my}, cen) : 0.f;
                 float mr = 0.f;
-                for (int j = lane; j < T; j += kLanes)
-                    if (R[j].fsld == 0 && R[j].group_id == gid && w_proc[j])
-                        mr = fmaxf(mr, dist(F2{(float)R[j].x, (float)R[j].y}, cen));
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) mr = fmaxf(mr, __shfl_xor(mr, o));
-                if (lane == 0 && gid < max_tracks)
-                    groups[gid] = DevGroup{gid, cnt, n_glabels, av.x, av.y, cen.x, cen.y, mr};
+                for (uint64_t mm = m; mm; mm &= mm - 1)
+                    mr = fmaxf(mr, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dm), __ffsll((unsigned long long)mm) - 1)));
+                if (mem) {
+                    gax = av.x;
+                    gay = av.y;
+                }
+                if (lane == 0 && gid < max_tracks) groups[gid] = DevGroup{gid, cnt, n_glabels, av.x, av.y, cen.x, cen.y, mr};
                 n_glabels += cnt;
                 n_groups++;
             }
-            __syncthreads();
-        }
-        // velocity blend with the group average (:388-397)
-        for (int i = lane; i < T; i += kLanes) {
-            if (R[i].fsld == 0 && R[i].group_id >= 0 && R[i].group_id < n_groups) {
-                const DevGroup &g = groups[R[i].group_id];
-                R[i].vx = __fadd_rn(__fmul_rn(R[i].vx, 0.7f), __fmul_rn(g.avx, 0.3f));
-                R[i].vy = __fadd_rn(__fmul_rn(R[i].vy, 0.7f), __fmul_rn(g.avy, 0.3f));
+            // velocity blend with the group average (:388-397); candidates' last fields.  With
+            // group_radius >= 0 every candidate joins a group this slice; otherwise none forms.
+            if (valid) {
+                float vx = mvx, vy = mvy;
+                if (mgid >= 0 && mgid < n_groups) {
+                    vx = __fadd_rn(__fmul_rn(vx, 0.7f), __fmul_rn(gax, 0.3f));
+                    vy = __fadd_rn(__fmul_rn(vy, 0.7f), __fmul_rn(gay, 0.3f));
+                }
+                DevTrack *dst = Bf + mtidx;
+                dst->vx = vx;
+                dst->vy = vy;
+                dst->group_id = mgid;
+            }
+        } else if (wave == 0) {
+            for (int k = lane; k < G; k += 64) ck_proc[k] = 0;
+            wave_sync();
+            n_groups = 0;
+            n_glabels = 0;
+            int next = 0;
+            for (;;) {
+                int seed = -1;
+                for (int b0 = next; b0 < G; b0 += 64) {
+                    const int k = b0 + lane;
+                    const uint64_t m = __ballot(k < G && !ck_proc[k]);
+                    if (m) {
+                        seed = b0 + __ffsll((unsigned long long)m) - 1;
+                        break;
+                    }
+                }
+                if (seed < 0) break;
+                next = seed + 1;
+                const F2 pi{(float)ck_x[seed], (float)ck_y[seed]};
+                const int gid = n_groups;
+                int cnt = 0;
+                uint64_t mine = 0;  // bit c: this lane is a member in chunk c
+                F2 sp{0.f, 0.f}, sv{0.f, 0.f};
+                for (int b0 = 0, c = 0; b0 < G; b0 += 64, ++c) {
+                    const int k = b0 + lane;
+                    bool mem = false;
+                    if (k < G && !ck_proc[k]) mem = dist(pi, F2{(float)ck_x[k], (float)ck_y[k]}) <= p.group_radius;
+                    const uint64_t m = __ballot(mem);
+                    if (!m) continue;
+                    const int r = __popcll(m & lanes_below());
+                    if (mem) {
+                        mine |= 1ull << c;
+                        ck_proc[k] = 1;
+                        ck_gid[k] = gid;
+                        if (n_glabels + cnt + r < max_tracks) group_labels[n_glabels + cnt + r] = ck_label[k];
+                        stage[r] = make_float4((float)ck_x[k], (float)ck_y[k], ck_vx[k], ck_vy[k]);
+                    }
+                    wave_sync();
+                    // ordered fp32 sums over the members (k ascending), evaluated by every lane
+                    const int nm = __popcll(m);
+                    int q = 0;
+                    for (; q + 4 <= nm; q += 4) {
+                        const float4 v0 = stage[q], v1 = stage[q + 1], v2 = stage[q + 2], v3 = stage[q + 3];
+                        sp = add(add(add(add(sp, F2{v0.x, v0.y}), F2{v1.x, v1.y}), F2{v2.x, v2.y}), F2{v3.x, v3.y});
+                        sv = add(add(add(add(sv, F2{v0.z, v0.w}), F2{v1.z, v1.w}), F2{v2.z, v2.w}), F2{v3.z, v3.w});
+                    }
+                    for (; q < nm; ++q) {
+                        const float4 v = stage[q];
+                        sp = add(sp, F2{v.x, v.y});
+                        sv = add(sv, F2{v.z, v.w});
+                    }
+                    cnt += nm;
+                    wave_sync();
+                }
+                if (cnt > 0) {
+                    const F2 cen = mul(sp, __fdiv_rn(1.0f, (float)cnt));
+                    const F2 av = mul(sv, __fdiv_rn(1.0f, (float)cnt));
+                    // radius = max distance of the group's members to the centroid (fp32 >= 0
+                    // orders like its bit pattern)
+                    if (lane == 0) s_rad = 0u;
+                    wave_sync();
+                    for (uint64_t mm = mine; mm; mm &= mm - 1) {
+                        const int k = (__ffsll((unsigned long long)mm) - 1) * 64 + lane;
+                        atomicMax(&s_rad, __float_as_uint(dist(F2{(float)ck_x[k], (float)ck_y[k]}, cen)));
+                    }
+                    wave_sync();
+                    const float mr = __uint_as_float(s_rad);
+                    if (lane == 0) {
+                        if (gid < max_tracks) groups[gid] = DevGroup{gid, cnt, n_glabels, av.x, av.y, cen.x, cen.y, mr};
+                        gav[gid] = make_float2(av.x, av.y);
+                    }
+                    n_glabels += cnt;
+                    n_groups++;
+                }
+                wave_sync();
+            }
+            // velocity blend with the group average (:388-397); candidates' last fields
+            for (int k = lane; k < G; k += 64) {
+                const int gid = ck_gid[k];
+                float vx = ck_vx[k], vy = ck_vy[k];
+                if (gid >= 0 && gid < n_groups) {
+                    const float2 g = gav[gid];
+                    vx = __fadd_rn(__fmul_rn(vx, 0.7f), __fmul_rn(g.x, 0.3f));
+                    vy = __fadd_rn(__fmul_rn(vy, 0.7f), __fmul_rn(g.y, 0.3f));
+                }
+                DevTrack *dst = Bf + ck_tidx[k];
+                dst->vx = vx;
+                dst->vy = vy;
+                dst->group_id = gid;
             }
         }
         __syncthreads();
+        TRK_MARK(4);
     }
-    const bool any_err = __any(err != 0);
-    if (lane == 0) {
+#if ECC_TRACKER_PROFILE
+    prof[10] = clock64() - c0_;
+    prof[11] = wall_clock64() - w0_;
+    if (tid == 0)
+        for (int k = 0; k < 12; ++k) g_trk_prof[k] = prof[k];
+#endif
+    const bool any_err = __syncthreads_or(err != 0);
+    if (tid == 0) {
         if (any_err && err == 0) err = ECC_ERR_CAPACITY;
         ctr->n_tracks = T;
         ctr->next_label = next_label;
@@ -352,7 +762,6 @@ struct ecc_tracker {
     DevTrack *buf[2] = {nullptr, nullptr};
     DevGroup *groups = nullptr;
     int *group_labels = nullptr;
-    uint8_t *work = nullptr;
     TrackerCounters *ctr = nullptr;
 };
 
@@ -371,7 +780,7 @@ ECC_API void ecc_tracker_cfg_default(ecc_tracker_cfg *cfg) {
 ECC_API int ecc_tracker_create(ecc_ctx *ctx, const ecc_tracker_cfg *cfg, int32_t max_tracks,
                                int32_t max_detections, ecc_tracker **out) {
     if (!ctx || !cfg || !out || max_tracks < 1 || max_detections < 1 ||
-        max_detections > kMaxDet || cfg->history_size < 1 || cfg->history_size > kH ||
+        max_tracks > kMaxTrk || max_detections > kMaxDet || cfg->history_size < 1 || cfg->history_size > kH ||
         cfg->frames_to_skip < 1)
         return ECC_ERR_INVALID;
     *out = nullptr;
@@ -394,7 +803,6 @@ ECC_API int ecc_tracker_create(ecc_ctx *ctx, const ecc_tracker_cfg *cfg, int32_t
     bool ok = hipMalloc(&tr->buf[0], tb) == hipSuccess && hipMalloc(&tr->buf[1], tb) == hipSuccess &&
               hipMalloc(&tr->groups, sizeof(DevGroup) * (size_t)max_tracks) == hipSuccess &&
               hipMalloc(&tr->group_labels, sizeof(int) * (size_t)max_tracks) == hipSuccess &&
-              hipMalloc(&tr->work, (size_t)max_tracks * 16 + 256) == hipSuccess &&
               hipMalloc(&tr->ctr, sizeof(TrackerCounters)) == hipSuccess &&
               hipMemset(tr->ctr, 0, sizeof(TrackerCounters)) == hipSuccess;
     if (!ok) {
@@ -413,7 +821,6 @@ ECC_API int ecc_tracker_destroy(ecc_tracker *tr) {
     hipFree(tr->buf[1]);
     hipFree(tr->groups);
     hipFree(tr->group_labels);
-    hipFree(tr->work);
     hipFree(tr->ctr);
     delete tr;
     return ECC_OK;
@@ -428,14 +835,26 @@ ECC_API int ecc_tracker_update(ecc_tracker *tr, const ecc_corner *corners, const
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     {
         ECC_TIMED(ctx, ecc::as_stream(stream), "tracker_kernel");
-        hipLaunchKernelGGL(tracker_kernel, dim3(1), dim3(kLanes), 0, ecc::as_stream(stream),
+        hipLaunchKernelGGL(tracker_kernel, dim3(1), dim3(kNT), 0, ecc::as_stream(stream),
                            tr->buf[0], tr->buf[1], tr->max_tracks, tr->groups, tr->group_labels,
-                           tr->work, tr->ctr, tr->params, corners, counts, n_slices,
+                           tr->ctr, tr->params, corners, counts, n_slices,
                            cap < tr->max_det ? cap : tr->max_det);
     }
     ECC_CHECK_LAUNCH(ctx, "tracker_kernel");
     return ECC_OK;
 }
+
+#if ECC_TRACKER_PROFILE
+// Profiling builds only (make TRACKER_PROFILE=1): wall-clock ticks of the last update's phases
+// (P0+P1, P2, P3 update, P3 append, P4) and the matching rounds; ticks_per_us from the device.
+ECC_API int ecc_tracker_profile(unsigned long long *out8, double *ticks_per_us) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_trk_prof), 12 * sizeof(unsigned long long)) != hipSuccess) return ECC_ERR_HIP;
+    int khz = 0;
+    hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
+    *ticks_per_us = khz / 1000.0;
+    return ECC_OK;
+}
+#endif
 
 ECC_API int ecc_tracker_status(ecc_tracker *tr, ecc_stream_t stream) {
     if (!tr) return ECC_ERR_INVALID;

@@ -398,7 +398,7 @@ class Context:
 class Tracker:
     """Device-resident CornerTracker (FCT/…group_track.cpp:201-537)."""
 
-    def __init__(self, ctx: Context, cfg: TrackerCfg | None = None, max_tracks: int = 16384,
+    def __init__(self, ctx: Context, cfg: TrackerCfg | None = None, max_tracks: int = 4096,
                  max_detections: int = 4096):
         self.ctx = ctx
         self.cfg = cfg or tracker_cfg()

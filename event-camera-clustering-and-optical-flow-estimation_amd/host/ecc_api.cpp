@@ -103,7 +103,7 @@ std::vector<Corner> CornerFilter::filterCorners(Context &ctx, const std::vector<
 
 CornerTracker::CornerTracker(float max_matching_distance, int max_frames, int history_size,
                              int frames_to_skip, float damping, float smoothing, float group_rad)
-    : ctx_(&Context::default_context()), max_tracks_(16384), max_det_(4096) {
+    : ctx_(&Context::default_context()), max_tracks_(ECC_TRACKER_MAX_TRACKS), max_det_(4096) {
     ecc_tracker_cfg c{max_matching_distance, max_frames, history_size, frames_to_skip, damping,
                       smoothing, group_rad};
     check(ecc_tracker_create(ctx_->get(), &c, max_tracks_, max_det_, &tr_), "ecc_tracker_create");

@@ -271,9 +271,14 @@ int ecc_corner_nms_status(ecc_ctx *ctx, ecc_stream_t stream);
  *            (30, 30, 10, 5, 0.8, 0.3, 100) at :805-813.  fp32 arithmetic in the
  *            reference's operation order; miss path truncates to int (Q16).
  * A tracker lives on the device; ecc_tracker_update consumes n_slices NMS outputs in order
- * (one updateTrackedCorners call per slice) in a single launch.
+ * (one updateTrackedCorners call per slice) in a single launch.  A slice's working set is
+ * held in LDS, so max_tracks <= ECC_TRACKER_MAX_TRACKS and max_detections <=
+ * ECC_TRACKER_MAX_DETECTIONS (ECC_ERR_INVALID otherwise); tracks or detections beyond
+ * the tracker's capacities are dropped and reported as ECC_ERR_CAPACITY.
  * ------------------------------------------------------------------------------------- */
 #define ECC_TRACK_HIST_MAX 16
+#define ECC_TRACKER_MAX_TRACKS 4096
+#define ECC_TRACKER_MAX_DETECTIONS 4096
 
 typedef struct ecc_tracker_cfg {
     float max_distance;     /* 30 */

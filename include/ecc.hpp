@@ -152,7 +152,7 @@ class CornerTracker {  // :201-537, device-resident state
     CornerTracker(float max_matching_distance = 30.0f, int max_frames = 30, int history_size = 10,
                   int frames_to_skip = 5, float damping = 0.8f, float smoothing = 0.3f,
                   float group_rad = 50.0f);
-    CornerTracker(Context &ctx, const ecc_tracker_cfg &cfg, int max_tracks = 16384,
+    CornerTracker(Context &ctx, const ecc_tracker_cfg &cfg, int max_tracks = ECC_TRACKER_MAX_TRACKS,
                   int max_detections = 4096);
     ~CornerTracker();
     CornerTracker(const CornerTracker &) = delete;

@@ -464,6 +464,88 @@ def test_tracker_matches_oracle(ecc, orc, gpu):
     assert (gl[:nl] == ol[:nl]).all()
 
 
+def _compare_trackers(ecc, gtr, otr):
+    o_tr = otr.tracks(ecc.Track)
+    g_tr = gtr.tracks()
+    assert len(g_tr) == len(o_tr)
+    for a, b in zip(g_tr, o_tr):
+        assert _track_key(a) == _track_key(b)
+    og, ol = otr.groups(ecc.Group)
+    gg, gl = gtr.groups()
+    assert len(gg) == len(og)
+    for a, b in zip(gg, og):
+        assert (a.id, a.n_labels, a.first_label_offset) == (b.id, b.n_labels, b.first_label_offset)
+        for f in ("avg_vx", "avg_vy", "cx", "cy", "radius"):
+            assert np.float32(getattr(a, f)) == np.float32(getattr(b, f)), f
+    nl = sum(g.n_labels for g in og)
+    assert (gl[:nl] == ol[:nl]).all()
+    return len(o_tr), len(og)
+
+
+def _dense_detections(seed, n_slices, per_slice, n_centres, spread, W=346, H=260):
+    """Clustered detections drifting slowly: many tracks compete for the same detections, so
+    the matching takes several conflict rounds (order-dependent greedy claims)."""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform([20, 20], [W - 20, H - 20], size=(n_centres, 2))
+    v = rng.uniform(-3, 3, size=(n_centres, 2))
+    out = []
+    for s in range(n_slices):
+        n = int(rng.integers(per_slice // 2, per_slice + 1))
+        k = rng.integers(0, n_centres, size=n)
+        pts = np.rint(c[k] + rng.normal(0, spread, size=(n, 2))).astype(np.int32)
+        arr = np.zeros(n, np.dtype([("x", np.int32), ("y", np.int32), ("label", np.int32)]))
+        arr["x"], arr["y"] = pts[:, 0], pts[:, 1]
+        out.append(arr)
+        c += v
+    return out
+
+
+@pytest.mark.parametrize("seed,per_slice,n_centres,spread,cfg_over", [
+    (51, 120, 12, 8.0, {}),
+    (52, 400, 30, 12.0, {}),
+    (53, 60, 4, 20.0, {"max_frames": 3, "frames_to_skip": 1, "history_size": 16, "group_radius": 40.0}),
+    (54, 900, 80, 6.0, {"max_distance": 12.5, "damping": 0.5, "smoothing": 0.6}),
+])
+def test_tracker_dense_conflicts_match_oracle(ecc, orc, gpu, seed, per_slice, n_centres, spread, cfg_over):
+    cfg = ecc.tracker_cfg(**cfg_over)
+    dets = _dense_detections(seed, 36, per_slice, n_centres, spread)
+    cap = max(len(d) for d in dets)
+    ns = len(dets)
+    flat = np.zeros(ns * cap, ecc.CORNER_DTYPE)
+    cnt = np.zeros(ns, np.int32)
+    for s, d in enumerate(dets):
+        flat[s * cap: s * cap + len(d)] = d
+        cnt[s] = len(d)
+    otr = orc.OracleTracker(cfg)
+    for d in dets:
+        otr.update(d)
+    gtr = ecc.Tracker(gpu, cfg)
+    # three launches (1, 20, rest slices): state carries across launches
+    bounds = [0, 1, 21, ns]
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        gtr.update(dev(ecc, flat[a * cap: b * cap]), dev(ecc, cnt[a:b]), b - a, cap)
+    gpu.sync()
+    assert gtr.status() == 0
+    n_tr, n_gr = _compare_trackers(ecc, gtr, otr)
+    assert n_tr > 0 and n_gr > 0
+
+
+def test_tracker_capacity_flag(ecc, gpu):
+    """More new tracks than max_tracks: the overflow is dropped and reported."""
+    dets = _dense_detections(55, 4, 300, 40, 30.0)
+    cap = max(len(d) for d in dets)
+    flat = np.zeros(4 * cap, ecc.CORNER_DTYPE)
+    cnt = np.zeros(4, np.int32)
+    for s, d in enumerate(dets):
+        flat[s * cap: s * cap + len(d)] = d
+        cnt[s] = len(d)
+    gtr = ecc.Tracker(gpu, max_tracks=64)
+    gtr.update(dev(ecc, flat), dev(ecc, cnt), 4, cap)
+    gpu.sync()
+    assert gtr.status() == ecc.ERR_CAPACITY
+    assert len(gtr.tracks()) <= 64
+
+
 # ------------------------------------------------------------------------------ eps-neighbourhoods
 @pytest.mark.parametrize("eps,min_pts", [(10.0, 2), (20.0, 20), (1.01, 1), (3.5, 64)])
 def test_eps_neighbourhoods_match_oracle(ecc, orc, gpu, eps, min_pts):
