@@ -19,6 +19,7 @@
 #include "ecc_internal.hpp"
 
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 #ifndef ECC_TRACKER_PROFILE
@@ -40,7 +41,7 @@ __device__ unsigned long long g_trk_prof[12];
 #define TRK_MARK(k) do { } while (0)
 #endif
 
-constexpr int kNT = 1024;                        // one workgroup of 16 waves (4 per SIMD)
+constexpr int kNT = 512;                         // one workgroup of 8 waves (2 per SIMD)
 constexpr int kH = ECC_TRACK_HIST_MAX;
 constexpr int kMaxTrk = ECC_TRACKER_MAX_TRACKS;  // active tracks of a slice held in LDS
 constexpr int kMaxDet = ECC_TRACKER_MAX_DETECTIONS;
@@ -65,7 +66,31 @@ struct TrackerParams {
     float max_distance, damping, smoothing, group_radius;
     int max_frames, history, frames_to_skip;
     float pow_tab[kH + 1];
+    // Squared-distance thresholds equivalent to the reference's sqrt comparisons (sqrt_rn is
+    // monotone): sqrt_rn(s) < max_distance <=> s < s_match, sqrt_rn(s) <= group_radius <=>
+    // s <= s_group, for s = dx*dx + dy*dy rounded as in dist().
+    float s_match, s_group;
 };
+
+// Host: smallest float s >= 0 with pred(sqrtf(s)) false, by bisection over the (monotone)
+// bit patterns of [0, +inf]; sqrtf is correctly rounded on the host, like sqrt_rn.
+template <class Pred>
+static float first_false(Pred pred) {
+    uint32_t lo = 0u, hi = 0x7F800000u;  // pred(sqrt(+0)) .. +inf
+    if (!pred(0.0f)) return 0.0f;
+    float inf;
+    std::memcpy(&inf, &hi, 4);
+    if (pred(std::sqrt(inf))) return inf;
+    while (hi - lo > 1u) {  // pred(sqrt(lo)) true, pred(sqrt(hi)) false
+        const uint32_t mid = lo + (hi - lo) / 2;
+        float f;
+        std::memcpy(&f, &mid, 4);
+        (pred(std::sqrt(f)) ? lo : hi) = mid;
+    }
+    float r;
+    std::memcpy(&r, &hi, 4);
+    return r;
+}
 
 struct F2 { float x, y; };
 __device__ __forceinline__ F2 add(F2 a, F2 b) { return F2{__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y)}; }
@@ -73,6 +98,10 @@ __device__ __forceinline__ F2 mul(F2 a, float s) { return F2{__fmul_rn(a.x, s), 
 __device__ __forceinline__ float dist(F2 a, F2 b) {  // :217-222
     const float dx = __fsub_rn(a.x, b.x), dy = __fsub_rn(a.y, b.y);
     return ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
+}
+__device__ __forceinline__ float dist2(F2 a, F2 b) {  // dist()'s radicand, same rounding
+    const float dx = __fsub_rn(a.x, b.x), dy = __fsub_rn(a.y, b.y);
+    return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
 }
 __device__ __forceinline__ float norm(F2 a) {
     return ecc::sqrt_rn(__fadd_rn(__fmul_rn(a.x, a.x), __fmul_rn(a.y, a.y)));
@@ -152,16 +181,17 @@ static_assert(kMaxTrk <= 4096, "track index packs into 12 bits of the matching t
 static_assert(64 * 16 <= 2 * kMaxTrk, "member staging fits the st array");
 
 // Detection grid for the matching scans: cells of kCell >= 2 * (max_distance + 1) + 2 pixels
-// hashed into kBuckets buckets, so every detection a prediction can reach lies in at most 2 x 2
+// hashed into kBuckets buckets, so every detection a prediction can reach lies in at most 3 x 3
 // cells.  Collisions only add candidates (the argmin is taken over (dist, index) explicitly).
-constexpr int kBuckets = 1024;
+constexpr int kBuckets = 512;
 constexpr int kBrute = 384;
-constexpr int kLaneList = 4;  // in-range detections a matching lane keeps in registers  // up to this many detections a scan walks all of them (uniform, no grid)  // per-track candidate list held in registers during the matching rounds
+constexpr int kLaneList = 4;  // in-range detections a matching lane keeps in registers
+constexpr int kTailCap = 1024; // candidate entries of the one-wave matching tail  // up to this many detections a scan walks all of them (uniform, no grid)  // per-track candidate list held in registers during the matching rounds
 __device__ __forceinline__ int floor_div(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 __device__ __forceinline__ int cell_bucket(int cx, int cy) {
-    return (int)(((uint32_t)cx * 0x9E3779B1u ^ (uint32_t)cy * 0x85EBCA77u) >> (32 - 10));
+    return (int)(((uint32_t)cx * 0x9E3779B1u ^ (uint32_t)cy * 0x85EBCA77u) >> (32 - 9));
 }
-static_assert(kBuckets == 1 << 10, "bucket hash takes the top 10 bits");
+static_assert(kBuckets == 1 << 9, "bucket hash takes the top 9 bits");
 
 // Exclusive scan of v[0..kBuckets) in place (one entry per thread); v[kBuckets] = total.
 __device__ __forceinline__ void block_scan_buckets(int *v, int *ws) {
@@ -263,6 +293,10 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
     __shared__ uint8_t s_cproc[kMaxDet];             // grouped
     __shared__ int s_ws[32];                         // wave counts
     __shared__ unsigned s_rad;                       // group radius (fp32 bits, >= 0)
+    __shared__ int s_tail[2];                        // matching tail: list cursor, overflow
+    __shared__ int16_t t_trk[64], t_off[64], t_n[64];
+    __shared__ int16_t t_d[kTailCap];
+    __shared__ float t_dd[kTailCap];
     int2 *const det = s_det;
     float2 *const gav = reinterpret_cast<float2 *>(s_det);
     uint32_t *const claim = s_claim;
@@ -284,7 +318,6 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // |dx| or |dy| above max_distance + 1 cannot give dist < max_distance (for sane radii)
-    const bool prefilter = p.max_distance < 1.0e6f;
     const float reach = __fadd_rn(p.max_distance, 1.0f);
     // grid matching for sane radii; otherwise every scan walks all detections
     const bool grid_ok = p.max_distance >= 0.0f && p.max_distance < 1.0e5f;
@@ -369,12 +402,11 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
                     const int e1 = g_end[b];
                     for (int e = b ? g_end[b - 1] : 0; e < e1; ++e) {
                         const uint2 g = g_ent[e];
-                        const float fx = (float)(int16_t)(g.x & 0xFFFFu), fy = (float)(int16_t)(g.x >> 16);
-                        if (fabsf(__fsub_rn(pp.x, fx)) > reach || fabsf(__fsub_rn(pp.y, fy)) > reach) continue;
+                        const F2 dq{(float)(int16_t)(g.x & 0xFFFFu), (float)(int16_t)(g.x >> 16)};
+                        if (!(dist2(pp, dq) < p.s_match)) continue;
                         const int d = (int)g.y;
                         if (check_claims && ((claim[d >> 5] >> (d & 31)) & 1u)) continue;
-                        const float dd = dist(pp, F2{fx, fy});
-                        if (dd < p.max_distance) f(d, dd);
+                        f(d, dist(pp, dq));
                     }
                 }
         };
@@ -426,11 +458,9 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
                         for (int d = jl; d < C; d += L) {
                             if (round > 0 && ((claim[d >> 5] >> (d & 31)) & 1u)) continue;
                             const int2 q = det[d];
-                            const float fx = (float)q.x, fy = (float)q.y;
-                            if (prefilter && (fabsf(__fsub_rn(pp.x, fx)) > reach || fabsf(__fsub_rn(pp.y, fy)) > reach))
-                                continue;
-                            const float dd = dist(pp, F2{fx, fy});
-                            if (dd < p.max_distance) take_rec(d, dd);
+                            const F2 dq{(float)q.x, (float)q.y};
+                            // in range iff the squared distance is below s_match; sqrt only then
+                            if (dist2(pp, dq) < p.s_match) take_rec(d, dist(pp, dq));
                         }
                     }
                 }
@@ -459,6 +489,85 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
             ++round;
             pending = __syncthreads_or(again);
             TRK_MARK(5);
+            if (pending && round == 1 && lists_ok) {
+                // Tail: the tracks still unresolved (typically few) finish in one wave, without
+                // workgroup barriers.  Each track's lane group moves its register lists to LDS.
+                const int i = tid / L;
+                const bool unres = i < T && st[i] == -3;
+                int gn = unres ? l_n : 0, ex = gn;
+                int govf = unres && l_ovf ? 1 : 0;
+                for (int o = 1; o < L; o <<= 1) {  // inclusive prefix of the list sizes in the group
+                    const int v = __shfl_up(ex, o, L);
+                    if (jl >= o) ex += v;
+                }
+                const int gtot = __shfl(ex, (lane & ~(L - 1)) + L - 1);
+                ex -= gn;
+                for (int o = L >> 1; o > 0; o >>= 1) govf |= __shfl_xor(govf, o);
+                const bool head = unres && jl == 0;
+                if (tid == 0) { s_tail[0] = 0; s_tail[1] = 0; }
+                int u, u_unused, n_unres, n_unused;
+                block_rank2(head, false, ws, u, u_unused, n_unres, n_unused);  // also orders the reset
+                int off = 0;
+                if (head) {
+                    off = atomicAdd(&s_tail[0], gtot);
+                    if (govf) atomicOr(&s_tail[1], 1);
+                }
+                off = __shfl(off, lane & ~(L - 1));
+                __syncthreads();
+                const bool tail_ok = n_unres <= 64 && s_tail[1] == 0 && s_tail[0] <= kTailCap;
+                if (tail_ok) {
+                    if (head) {
+                        t_trk[u] = (int16_t)i;
+                        t_off[u] = (int16_t)off;
+                        t_n[u] = (int16_t)gtot;
+                    }
+                    if (unres) {
+#pragma unroll
+                        for (int k = 0; k < kLaneList; ++k)
+                            if (k < l_n) {
+                                t_d[off + ex + k] = (int16_t)l_i[k];
+                                t_dd[off + ex + k] = l_d[k];
+                            }
+                    }
+                    __syncthreads();
+                    if (wave == 0) {
+                        const bool act = lane < n_unres;
+                        const int ti = act ? t_trk[lane] : 0, to = act ? t_off[lane] : 0, tn = act ? t_n[lane] : 0;
+                        bool done = !act;
+                        int r = round;
+                        while (__ballot(!done)) {
+                            const int tag = (8191 - r) << 12;
+                            float bd = 0.f;
+                            int bi = -1;
+                            if (!done)
+                                for (int k = 0; k < tn; ++k) {
+                                    const int d = t_d[to + k];
+                                    if ((claim[d >> 5] >> (d & 31)) & 1u) continue;
+                                    atomicMin(&want[d], tag | ti);
+                                    const float dd = t_dd[to + k];
+                                    if (bi < 0 || dd < bd || (dd == bd && d < bi)) { bd = dd; bi = d; }
+                                }
+                            wave_sync();
+                            if (!done) {
+                                if (bi < 0) {
+                                    st[ti] = -1;
+                                    done = true;
+                                } else if (want[bi] == (tag | ti)) {
+                                    st[ti] = (int16_t)bi;
+                                    atomicOr(&claim[bi >> 5], 1u << (bi & 31));
+                                    done = true;
+                                }
+                            }
+                            wave_sync();
+                            ++r;
+                        }
+#if ECC_TRACKER_PROFILE
+                        prof[9] += r - round;
+#endif
+                    }
+                    pending = false;
+                }
+            }
         }
         __syncthreads();
         TRK_MARK(1);
@@ -596,7 +705,7 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
                 const int sl = __ffsll((unsigned long long)open_) - 1;
                 next = sl + 1;
                 const F2 pi{(float)__builtin_amdgcn_readlane(mx, sl), (float)__builtin_amdgcn_readlane(my, sl)};
-                const bool mem = !proc && dist(pi, F2{(float)mx, (float)my}) <= p.group_radius;
+                const bool mem = !proc && dist2(pi, F2{(float)mx, (float)my}) <= p.s_group;
                 const uint64_t m = __ballot(mem);
                 if (!m) continue;
                 const int gid = n_groups, cnt = __popcll(m);
@@ -616,10 +725,12 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
                 }
                 const F2 cen = mul(sp, __fdiv_rn(1.0f, (float)cnt));
                 const F2 av = mul(sv, __fdiv_rn(1.0f, (float)cnt));
-                const float dm = mem ? dist(F2{(float)mx, (float)my}, cen) : 0.f;
-                float mr = 0.f;
+                // max over members of sqrt_rn(s) == sqrt_rn(max s) (monotone)
+                const float sm = mem ? dist2(F2{(float)mx, (float)my}, cen) : 0.f;
+                float smax = 0.f;
                 for (uint64_t mm = m; mm; mm &= mm - 1)
-                    mr = fmaxf(mr, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dm), __ffsll((unsigned long long)mm) - 1)));
+                    smax = fmaxf(smax, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), __ffsll((unsigned long long)mm) - 1)));
+                const float mr = ecc::sqrt_rn(smax);
                 if (mem) {
                     gax = av.x;
                     gay = av.y;
@@ -798,6 +909,26 @@ ECC_API int ecc_tracker_create(ecc_ctx *ctx, const ecc_tracker_cfg *cfg, int32_t
     p.history = cfg->history_size;
     p.frames_to_skip = cfg->frames_to_skip;
     for (int k = 0; k <= kH; ++k) p.pow_tab[k] = (float)std::pow((double)0.8f, (double)k);  // :254
+    {
+        const float md = p.max_distance, gr = p.group_radius;
+        // s < s_match <=> sqrt(s) < md;  s <= s_group <=> sqrt(s) <= gr (NaN radii: never)
+        p.s_match = md == md ? first_false([md](float r) { return r < md; }) : -1.0f;
+        if (gr == gr) {
+            const float above = first_false([gr](float r) { return r <= gr; });
+            uint32_t b;
+            std::memcpy(&b, &above, 4);
+            if (above == 0.0f) {
+                p.s_group = -1.0f;
+            } else if (b == 0x7F800000u) {
+                p.s_group = above;  // every finite s
+            } else {
+                --b;
+                std::memcpy(&p.s_group, &b, 4);
+            }
+        } else {
+            p.s_group = -1.0f;
+        }
+    }
     hipSetDevice(ctx->device);
     const size_t tb = sizeof(DevTrack) * (size_t)max_tracks;
     bool ok = hipMalloc(&tr->buf[0], tb) == hipSuccess && hipMalloc(&tr->buf[1], tb) == hipSuccess &&
