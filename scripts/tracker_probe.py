@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Tracker timing probe on the bench stream's NMS corners (346x260, seed 1), computed on the GPU.
+
+Prints µs/slice per repetition; with a profiling library (make TRACKER_PROFILE=1 into another
+LIBDIR, selected by ECC_LIB) also the per-phase wall-clock split of tracker_kernel.
+Usage: tracker_probe.py [n_slices]
+"""
+import ctypes as C
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "event-camera-clustering-and-optical-flow-estimation_amd"))
+import eccpy as ecc  # noqa: E402
+
+W, H = 346, 260
+ns = int(sys.argv[1]) if len(sys.argv) > 1 else 600
+n, cap = ns * 16384, 4096
+ctx = ecc.Context(0)
+xy, t, _ = ecc.gen_events(n, seed=1, width=W, height=H)
+d_xy, d_t = ecc.DeviceArray.from_numpy(xy), ecc.DeviceArray.from_numpy(t)
+ccfg = ecc.corner_cfg(width=W, height=H, first_detect_slice=1)
+sae = ecc.DeviceArray(W * H, np.int64)
+flags = ecc.DeviceArray(n, np.uint8)
+d_out = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE)
+d_cnt = ecc.DeviceArray(ns, np.int32)
+ecc.check(ecc.lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
+ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
+ctx.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, d_out, d_cnt)
+ctx.sync()
+prof = getattr(ecc.lib, "ecc_tracker_profile", None)
+names = {0: "P0P1+grid", 7: "P0P1", 8: "P2scan0", 1: "P2scanN+tail", 5: "P2resolve", 2: "P3upd", 3: "P3new", 4: "P4group"}
+for rep in range(3):
+    tr = ecc.Tracker(ctx)
+    ctx.sync()
+    t0 = time.perf_counter()
+    tr.update(d_out, d_cnt, ns, cap)
+    ctx.sync()
+    line = f"rep {rep}: {(time.perf_counter() - t0) * 1e6 / ns:.2f} us/slice"
+    if prof:
+        o, tpu = (C.c_ulonglong * 12)(), C.c_double()
+        prof(o, C.byref(tpu))
+        line += "  " + " ".join(f"{k}={o[i] / tpu.value / ns:.2f}" for i, k in names.items())
+        line += f" block_rounds/slice={o[6] / ns:.2f} tail_rounds/slice={o[9] / ns:.2f}"
+        line += f" core_MHz={o[10] / (o[11] / tpu.value):.0f}"
+    print(line, "tracks", len(tr.tracks()), flush=True)
+    tr.close()
