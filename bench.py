@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the RAW (EVT 3.0 / 2.0) decode measurement")
+    ap.add_argument("--no-eps", action="store_true", help="skip the eps-neighbourhood (DBSCAN / OPTICS) measurement")
     ap.add_argument("--serial", action="store_true",
                     help="one stream for the whole step (isolated per-kernel times for profiling)")
     ap.add_argument("--graph", action="store_true",
@@ -302,6 +303,44 @@ def main():
             }
             del d_words, d_oxy, d_ot, d_op, d_on
 
+    # eps-neighbourhoods (BASELINE C4), reported beside the headline:
+    # DBSCAN eps 20 / minPts 20 (counts) and OPTICS eps 10 / min_pts 2 (counts + core distances)
+    # per 8192-event downsample window, over this step's device-resident representatives.
+    eps_res = None
+    if not args.no_eps and rank == 0:
+        eps_res = {}
+        e_cnt = ecc.DeviceArray(n_win * 8192, np.int32)
+        e_core = ecc.DeviceArray(n_win * 8192, np.float64)
+        for name, eps, mp, core in (("dbscan_eps20_minpts20", 20.0, 20, None),
+                                    ("optics_eps10_minpts2", 10.0, 2, e_core)):
+            run = lambda: ctx.eps_counts(rep_xy, n_win, 8192, uniq, eps, mp, e_cnt, core)
+            run()
+            ctx.sync()
+            reps = max(args.steps, 5)
+            tmr = ecc.Timer(ctx.stream)
+            tmr.start()
+            for _ in range(reps):
+                run()
+            call_ms = tmr.stop() / reps
+            ctx.set_timing(True)
+            ctx.timing_reset()
+            for _ in range(reps):
+                run()
+            st = ctx.timing_report()
+            ctx.set_timing(False)
+            kern = {k: v["total_ms"] / v["launches"] for k, v in st.items()}
+            ek = kern.get("eps_counts_kernel", float("nan"))
+            per_rep = 8 + (8 if core is not None else 0)  # xy in + count out [+ core distance out]
+            ach = n_reps * per_rep / (ek * 1e-3) / 1e9
+            eps_res[name] = {
+                "reps": n_reps, "windows": n_win, "mreps_s": round(n_reps / (call_ms * 1e-3) / 1e6, 1),
+                "ms_per_call": round(call_ms, 4), "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
+                "roofline": {"kernel": "eps_counts_kernel", "bound": "hbm", "achieved": round(ach, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                             "algorithmic_bytes": f"4 B/rep in + 4 B/rep out{' + 8 B/rep core distance' if core is not None else ''}"},
+            }
+        del e_cnt, e_core
+
     value = world * args.steps * n / elapsed / 1e6
     if graph is not None:
         lib.ecc_graph_destroy(graph)
@@ -336,6 +375,7 @@ def main():
         "stages_ms_per_step": {k: round(v / args.steps, 4) for k, v in sorted(kern_ms.items())},
         "tracker_us_per_slice": None if tracker_us is None else round(tracker_us, 2),
         "ingest": ingest,
+        "eps": eps_res,
     }
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, W, H, K, I)

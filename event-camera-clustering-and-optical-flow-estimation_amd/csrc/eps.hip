@@ -130,50 +130,120 @@ __device__ __forceinline__ void cell_range(const Grid &g, const uint32_t *cend, 
     hi = (int)cend[c];
 }
 
+// Counts (+ core distances): the segment's coordinates are counting-sorted by grid cell straight
+// into LDS (one 4-B read per candidate; a query's three cells of one grid row are one contiguous
+// run), and the exact test d^2 <= eps^2 (fp64 in the reference) is the integer test
+// d^2 <= floor(eps^2) on integer d^2.  Queries run in cell order too, so a wave's lanes walk
+// the same runs.  Dynamic LDS = (kCountCells + 1) cell ends + the segment stride's points and
+// indices: 56 KB at 8192, two workgroups per CU.
+constexpr int kCountCells = 2048;
+
 template <int K>
 __global__ void __launch_bounds__(kThreads)
-eps_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, double eps, int min_pts,
+eps_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, int r2i, int min_pts,
                   int32_t *__restrict__ counts, double *__restrict__ core) {
-    __shared__ uint32_t pxy[kMaxPts];
-    __shared__ uint16_t sorted[kMaxPts];
-    __shared__ uint32_t cend[kMaxCells];
+    extern __shared__ uint32_t lds_c[];
+    uint32_t *cend = lds_c;                     // [kCountCells + 1]: cell ends after the scatter
+    uint32_t *spt = lds_c + kCountCells + 1;    // [stride]: coordinates in cell order
+    uint16_t *sidx = reinterpret_cast<uint16_t *>(spt + sv.stride);  // [stride]: their indices
     __shared__ int red[32];
-    const double r2 = eps * eps;
+    const int tid = threadIdx.x, lane = tid & 63;
     for (int64_t s = blockIdx.x; s < sv.n_segs; s += gridDim.x) {
-        Grid g;
-        const int m = bin_segment(xy, sv, s, eps, pxy, sorted, cend, red, g);
+        int m = sv.counts ? sv.counts[s] : (int)sv.stride;
+        m = m < 0 ? 0 : (m > (int)sv.stride ? (int)sv.stride : m);
         const int64_t base = s * sv.stride;
-        for (int i = threadIdx.x; i < sv.stride; i += kThreads) {
-            if (i >= m) {
-                counts[base + i] = 0;
-                if (core) core[base + i] = -1.0;
-                continue;
-            }
-            const uint32_t v = pxy[i];
+        // bounding box -> grid (cell >= eps, at most kCountCells cells)
+        int xmn = 0x7fffffff, ymn = 0x7fffffff, xmx = -1, ymx = -1;
+        for (int i = tid; i < m; i += kThreads) {
+            const uint32_t v = xy[base + i];
             const int x = ecc::xy_x(v), y = ecc::xy_y(v);
-            const int cx = (x - g.xmin) / g.cs, cy = (y - g.ymin) / g.cs;
+            xmn = min(xmn, x); ymn = min(ymn, y); xmx = max(xmx, x); ymx = max(ymx, y);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            xmn = min(xmn, __shfl_xor(xmn, o)); ymn = min(ymn, __shfl_xor(ymn, o));
+            xmx = max(xmx, __shfl_xor(xmx, o)); ymx = max(ymx, __shfl_xor(ymx, o));
+        }
+        if (lane == 0) {
+            red[4 * (tid >> 6) + 0] = xmn; red[4 * (tid >> 6) + 1] = ymn;
+            red[4 * (tid >> 6) + 2] = xmx; red[4 * (tid >> 6) + 3] = ymx;
+        }
+        for (int c = tid; c <= kCountCells; c += kThreads) cend[c] = 0u;
+        __syncthreads();
+        xmn = red[0]; ymn = red[1]; xmx = red[2]; ymx = red[3];
+        for (int w = 1; w < kThreads / 64; ++w) {
+            xmn = min(xmn, red[4 * w]); ymn = min(ymn, red[4 * w + 1]);
+            xmx = max(xmx, red[4 * w + 2]); ymx = max(ymx, red[4 * w + 3]);
+        }
+        if (m == 0) { xmn = ymn = 0; xmx = ymx = 0; }
+        int cs = e_int + 1;  // > eps: a neighbour lies in the same or an adjacent cell
+        while ((int64_t)((xmx - xmn) / cs + 1) * ((ymx - ymn) / cs + 1) > kCountCells) cs *= 2;
+        const int gx = (xmx - xmn) / cs + 1, gy = (ymx - ymn) / cs + 1;
+        __syncthreads();  // red reusable
+        for (int i = tid; i < m; i += kThreads) {
+            const uint32_t v = xy[base + i];
+            atomicAdd(&cend[((ecc::xy_y(v) - ymn) / cs) * gx + (ecc::xy_x(v) - xmn) / cs], 1u);
+        }
+        __syncthreads();
+        {  // exclusive scan of the cell counts in place (kCountCells / kThreads per thread)
+            constexpr int per = kCountCells / kThreads;
+            uint32_t loc[per], sum = 0;
+#pragma unroll
+            for (int k = 0; k < per; ++k) { loc[k] = cend[tid * per + k]; sum += loc[k]; }
+            uint32_t inc = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
+            }
+            if (lane == 63) red[16 + (tid >> 6)] = (int)inc;
+            __syncthreads();
+            uint32_t off = inc - sum;
+            for (int w = 0; w < (tid >> 6); ++w) off += (uint32_t)red[16 + w];
+#pragma unroll
+            for (int k = 0; k < per; ++k) { cend[tid * per + k] = off; off += loc[k]; }
+        }
+        __syncthreads();
+        for (int i = tid; i < m; i += kThreads) {  // scatter; afterwards cend[c] = end of cell c
+            const uint32_t v = xy[base + i];
+            const uint32_t at = atomicAdd(&cend[((ecc::xy_y(v) - ymn) / cs) * gx + (ecc::xy_x(v) - xmn) / cs], 1u);
+            spt[at] = v;
+            sidx[at] = (uint16_t)i;
+        }
+        for (int i = m + tid; i < sv.stride; i += kThreads) {
+            counts[base + i] = 0;
+            if (core) core[base + i] = -1.0;
+        }
+        __syncthreads();
+        // queries in cell order: a wave's lanes walk the same or neighbouring runs (broadcast reads)
+        for (int q = tid; q < m; q += kThreads) {
+            const uint32_t v = spt[q];
+            const int i = sidx[q];
+            const int x = ecc::xy_x(v), y = ecc::xy_y(v);
+            const int cx = (x - xmn) / cs, cy = (y - ymn) / cs;
+            const int c0 = max(cx - 1, 0), c1 = min(cx + 1, gx - 1);
             int cnt = 0;
             int best[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) best[k] = 0x7fffffff;
-            for (int dy = -1; dy <= 1; ++dy) {
-                for (int dx = -1; dx <= 1; ++dx) {
-                    int lo, hi;
-                    cell_range(g, cend, cx + dx, cy + dy, lo, hi);
-                    for (int a = lo; a < hi; ++a) {
-                        const uint32_t w = pxy[sorted[a]];
-                        const int ex = ecc::xy_x(w) - x, ey = ecc::xy_y(w) - y;
-                        const int d2 = ex * ex + ey * ey;
-                        if ((double)d2 <= r2) {
-                            ++cnt;
-                            if (core) {
-                                int val = d2;  // insertion network keeps the K smallest, sorted
+            for (int ry = max(cy - 1, 0); ry <= min(cy + 1, gy - 1); ++ry) {
+                const int cl = ry * gx + c0, ch = ry * gx + c1;
+                const int hi = (int)cend[ch];
+#pragma unroll 4
+                for (int a = cl == 0 ? 0 : (int)cend[cl - 1]; a < hi; ++a) {
+                    const uint32_t w = spt[a];
+                    const uint32_t ax = (uint32_t)abs(ecc::xy_x(w) - x), ay = (uint32_t)abs(ecc::xy_y(w) - y);
+                    const uint32_t d2 = ax * ax + ay * ay;  // exact whenever ax, ay <= e_int <= 32767
+                    const bool in = ax <= (uint32_t)e_int && ay <= (uint32_t)e_int && d2 <= (uint32_t)r2i;
+                    cnt += in ? 1 : 0;
+                    if (in) {
+                        if (core) {
+                            int val = (int)d2;  // insertion network keeps the K smallest, sorted
 #pragma unroll
-                                for (int k = 0; k < K; ++k) {
-                                    const int lo2 = min(best[k], val);
-                                    val = max(best[k], val);
-                                    best[k] = lo2;
-                                }
+                            for (int k = 0; k < K; ++k) {
+                                const int lo2 = min(best[k], val);
+                                val = max(best[k], val);
+                                best[k] = lo2;
                             }
                         }
                     }
@@ -262,11 +332,22 @@ ECC_API int ecc_eps_counts(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int
     if (n_segs == 0) return ECC_OK;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     SegView sv{seg_counts, n_segs, seg_stride};
-    const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 4096);
-    auto kern = (!core_dist || min_pts <= 8) ? eps_counts_kernel<8> : eps_counts_kernel<64>;
+    // d^2 <= eps^2 (fp64) <=> d^2 <= floor(eps^2) for integer d^2; |dx|, |dy| <= floor(eps)
+    const double r2 = eps * eps;
+    const int r2i = (int)std::floor(r2), e_int = (int)std::floor(eps);
+    const int K = core_dist ? min_pts : 1;
+    auto kern = K <= 1 ? eps_counts_kernel<1> : K <= 2 ? eps_counts_kernel<2> : K <= 4 ? eps_counts_kernel<4>
+              : K <= 8 ? eps_counts_kernel<8> : K <= 16 ? eps_counts_kernel<16> : K <= 32 ? eps_counts_kernel<32>
+              : eps_counts_kernel<64>;
+    const size_t lds = (size_t)(kCountCells + 1 + seg_stride) * sizeof(uint32_t) + (size_t)seg_stride * sizeof(uint16_t);
+    ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                  "eps_counts lds");
+    // enough workgroups for every CU at the occupancy the LDS allows (segments are grid-strided)
+    const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 8192);
     {
         ECC_TIMED(ctx, ecc::as_stream(stream), "eps_counts_kernel");
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, ecc::as_stream(stream), xy, sv, eps,
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, ecc::as_stream(stream), xy, sv, e_int, r2i,
                            min_pts, counts, core_dist);
     }
     ECC_CHECK_LAUNCH(ctx, "eps_counts_kernel");
