@@ -16,11 +16,12 @@
 //   2. evt_group_kernel + evt_carry_kernel: a two-level scan of the chunk summaries into
 //      per-chunk carry-in states and int64 event offsets (advancing the caller's streaming
 //      state);
-//   3. evt_decode_kernel: each chunk re-reads its words, rebuilds the per-lane carry-in with
-//      the same wave-shuffle scan, walks its words per lane into an LDS window of decoded
-//      events and writes the window out coalesced.
+//   3. evt_decode_kernel: each chunk re-reads its words, takes every lane's carry-in (EVT 3.0:
+//      the chunk-local lane prefix the summary pass stored, 16 B per lane, combined with the
+//      chunk's carry; EVT 2.0: the same wave-shuffle scan recomputed), walks its words per lane
+//      into an LDS window of decoded events and writes the window out coalesced.
 // Algorithmic bytes: words read twice (2 x 2 B or 2 x 4 B per word) + 13 B per event out
-// (xy u32, t i64, p u8).
+// (xy u32, t i64, p u8); EVT 3.0 adds the lane prefixes (16 B per 32 words, written + read).
 #include "ecc_internal.hpp"
 
 namespace {
@@ -50,7 +51,35 @@ struct Evt3 {
     using Word = uint16_t;
     using S = S3;
     static constexpr int kPer = 32;
-    static constexpr int kOut = 4096;  // decode window (events); the EVT 3.0 walk is costly to repeat
+    static constexpr int kOut = 2048;  // decode window (events): 26.6 KB of LDS, six workgroups per CU
+    // The summary pass keeps every lane's chunk-local exclusive prefix (16 B per 64 B of words),
+    // so the decode pass skips the fold and the block scan.  Within a chunk: n < 2^17,
+    // loops < 2^15; the x advance only matters modulo 2^16 (x = (base + inc + b) & 0xFFFF).
+    static constexpr bool kLanePrefix = true;
+    __device__ static uint4 pack(const S &v) {
+        uint4 w;
+        w.x = ((uint32_t)v.y & 0x7FFu) | (v.y >= 0 ? 1u << 11 : 0u) | (((uint32_t)v.tl & 0xFFFu) << 12) |
+              (v.tl >= 0 ? 1u << 24 : 0u);
+        w.y = ((uint32_t)v.th_first & 0xFFFu) | (v.th_first >= 0 ? 1u << 12 : 0u) |
+              (((uint32_t)v.th_last & 0xFFFu) << 13) | (v.th_last >= 0 ? 1u << 25 : 0u);
+        w.z = (v.base >= 0 ? 1u : 0u) | (((uint32_t)v.base & 0x7FFu) << 1) | ((((uint32_t)v.base >> 16) & 1u) << 12) |
+              ((uint32_t)v.inc << 16);
+        w.w = ((uint32_t)v.n & 0x1FFFFu) | ((uint32_t)v.loops << 17);
+        return w;
+    }
+    __device__ static S unpack(const uint4 w) {
+        S v;
+        v.y = (w.x >> 11 & 1u) ? (int32_t)(w.x & 0x7FFu) : -1;
+        v.tl = (w.x >> 24 & 1u) ? (int32_t)(w.x >> 12 & 0xFFFu) : -1;
+        v.th_first = (w.y >> 12 & 1u) ? (int32_t)(w.y & 0xFFFu) : -1;
+        v.th_last = (w.y >> 25 & 1u) ? (int32_t)(w.y >> 13 & 0xFFFu) : -1;
+        v.base = (w.z & 1u) ? (int32_t)((w.z >> 1 & 0x7FFu) | ((w.z >> 12 & 1u) << 16)) : -1;
+        v.inc = (int32_t)(w.z >> 16);
+        v.n = (int32_t)(w.w & 0x1FFFFu);
+        v.loops = (int32_t)(w.w >> 17);
+        return v;
+    }
+    __device__ static int prefix_n(const uint4 w) { return (int)(w.w & 0x1FFFFu); }
     __device__ static S identity() { return S{-1, -1, -1, -1, 0, -1, 0, 0}; }
     __device__ static S cat(const S &a, const S &b) {  // a, then b
         S r;
@@ -137,6 +166,10 @@ struct Evt2 {
     using S = S2;
     static constexpr int kPer = 16;
     static constexpr int kOut = 1024;  // decode window (events): small LDS -> occupancy
+    static constexpr bool kLanePrefix = false;  // the EVT 2.0 fold is a few operations: recompute it
+    __device__ static uint4 pack(const S &) { return make_uint4(0u, 0u, 0u, 0u); }
+    __device__ static S unpack(const uint4) { return identity(); }
+    __device__ static int prefix_n(const uint4) { return 0; }
     __device__ static S identity() { return S{-1, 0, {0, 0, 0, 0, 0, 0}}; }
     __device__ static S cat(const S &a, const S &b) {
         S r = identity();
@@ -236,7 +269,8 @@ __device__ typename F::S block_excl_scan(const typename F::S &mine, typename F::
 
 template <class F>
 __global__ void __launch_bounds__(kThreads)
-evt_summary_kernel(const typename F::Word *__restrict__ words, int64_t n_words, typename F::S *__restrict__ sums) {
+evt_summary_kernel(const typename F::Word *__restrict__ words, int64_t n_words, typename F::S *__restrict__ sums,
+                   uint4 *__restrict__ lanepre) {
     using S = typename F::S;
     __shared__ S wtot[kThreads / 64];
     constexpr int kPer = F::kPer;
@@ -248,7 +282,8 @@ evt_summary_kernel(const typename F::Word *__restrict__ words, int64_t n_words, 
     for (int e = 0; e < kPer; ++e)
         if (e < nw) F::fold(s, w[e]);
     S tot;
-    block_excl_scan<F, kThreads>(s, wtot, &tot);
+    const S ex = block_excl_scan<F, kThreads>(s, wtot, &tot);
+    if constexpr (F::kLanePrefix) lanepre[(int64_t)blockIdx.x * kThreads + threadIdx.x] = F::pack(ex);
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
@@ -340,7 +375,8 @@ __global__ void __launch_bounds__(kThreads)
 evt_decode_kernel(const typename F::Word *__restrict__ words, int64_t n_words, const typename F::S *__restrict__ sums,
                   const typename F::S *__restrict__ carry_local, const int32_t *__restrict__ off_local,
                   const typename F::S *__restrict__ gcarry, const int64_t *__restrict__ goff,
-                  uint32_t *__restrict__ xy, int64_t *__restrict__ t, uint8_t *__restrict__ p, int64_t cap) {
+                  const uint4 *__restrict__ lanepre, uint32_t *__restrict__ xy, int64_t *__restrict__ t,
+                  uint8_t *__restrict__ p, int64_t cap) {
     using S = typename F::S;
     constexpr int kOut = F::kOut;
     __shared__ S wtot[kThreads / 64];
@@ -351,16 +387,26 @@ evt_decode_kernel(const typename F::Word *__restrict__ words, int64_t n_words, c
     uint32_t w[kPer];
     int nw;
     load_words<F>(words, n_words, blockIdx.x, w, nw);
-    S s = F::identity();
-#pragma unroll
-    for (int e = 0; e < kPer; ++e)
-        if (e < nw) F::fold(s, w[e]);
     const int g = blockIdx.x / kGroup;
-    const S cin = F::cat(gcarry[g], carry_local[blockIdx.x]);
-    const S ex = F::cat(cin, block_excl_scan<F, kThreads>(s, wtot, nullptr));
-    const int64_t base = goff[g] + off_local[blockIdx.x];
     const int64_t n_chunk = sums[blockIdx.x].n;
-    const int lane_first = ex.n - cin.n, lane_n = s.n;  // this lane's events within the chunk
+    S exl;        // the lane's exclusive prefix within the chunk
+    int lane_n;   // this lane's events
+    if constexpr (F::kLanePrefix) {
+        const int64_t li = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+        exl = F::unpack(lanepre[li]);
+        lane_n = (threadIdx.x + 1 < kThreads ? F::prefix_n(lanepre[li + 1]) : (int)n_chunk) - exl.n;
+    } else {
+        S s = F::identity();
+#pragma unroll
+        for (int e = 0; e < kPer; ++e)
+            if (e < nw) F::fold(s, w[e]);
+        exl = block_excl_scan<F, kThreads>(s, wtot, nullptr);
+        lane_n = s.n;
+    }
+    const S cin = F::cat(gcarry[g], carry_local[blockIdx.x]);
+    const S ex = F::cat(cin, exl);
+    const int64_t base = goff[g] + off_local[blockIdx.x];
+    const int lane_first = exl.n;  // this lane's first event within the chunk
     for (int64_t w0 = 0; w0 < n_chunk; w0 += kOut) {
         if (lane_first < w0 + kOut && lane_first + lane_n > w0) {
             typename F::Regs r = F::regs(ex);
@@ -398,12 +444,13 @@ int decode(ecc_ctx *ctx, const void *words_v, int64_t n_words, uint32_t *xy, int
     const int64_t n_chunks = (n_words + kChunk - 1) / kChunk;
     if (n_chunks > INT32_MAX) return ECC_ERR_INVALID;
     const int64_t n_groups = (n_chunks + kGroup - 1) / kGroup;
-    // workspace: sums | carry_local | off_local | gsum | gcarry | goff
+    // workspace: sums | carry_local | off_local | gsum | gcarry | goff | lane prefixes
     size_t o = 0;
     auto carve = [&](size_t bytes) { const size_t at = o; o = ecc::align_up(o + bytes, 256); return at; };
     const size_t o_sums = carve((size_t)n_chunks * sizeof(S)), o_cl = carve((size_t)n_chunks * sizeof(S));
     const size_t o_ol = carve((size_t)n_chunks * 4), o_gs = carve((size_t)n_groups * sizeof(S));
     const size_t o_gc = carve((size_t)n_groups * sizeof(S)), o_go = carve((size_t)n_groups * 8);
+    const size_t o_lp = carve(F::kLanePrefix ? (size_t)n_chunks * kThreads * sizeof(uint4) : 16);
     int rc = ecc::ws_reserve(ctx, o);
     if (rc) return rc;
     char *ws = static_cast<char *>(ctx->ws);
@@ -411,6 +458,7 @@ int decode(ecc_ctx *ctx, const void *words_v, int64_t n_words, uint32_t *xy, int
     int32_t *off_local = reinterpret_cast<int32_t *>(ws + o_ol);
     S *gsum = reinterpret_cast<S *>(ws + o_gs), *gcarry = reinterpret_cast<S *>(ws + o_gc);
     int64_t *goff = reinterpret_cast<int64_t *>(ws + o_go);
+    uint4 *lanepre = reinterpret_cast<uint4 *>(ws + o_lp);
     int32_t *err = ctx->flags + kFlagWord;
     ECC_CHECK_HIP(ctx, hipMemsetAsync(err, 0, 4, s), "memset(evt err)");
     if (n_chunks == 0) {
@@ -419,7 +467,7 @@ int decode(ecc_ctx *ctx, const void *words_v, int64_t n_words, uint32_t *xy, int
     }
     {
         ECC_TIMED(ctx, s, "evt_summary_kernel");
-        hipLaunchKernelGGL(evt_summary_kernel<F>, dim3((unsigned)n_chunks), dim3(kThreads), 0, s, words, n_words, sums);
+        hipLaunchKernelGGL(evt_summary_kernel<F>, dim3((unsigned)n_chunks), dim3(kThreads), 0, s, words, n_words, sums, lanepre);
     }
     {
         ECC_TIMED(ctx, s, "evt_group_kernel");
@@ -434,7 +482,7 @@ int decode(ecc_ctx *ctx, const void *words_v, int64_t n_words, uint32_t *xy, int
     {
         ECC_TIMED(ctx, s, "evt_decode_kernel");
         hipLaunchKernelGGL(evt_decode_kernel<F>, dim3((unsigned)n_chunks), dim3(kThreads), 0, s, words, n_words, sums,
-                           carry_local, off_local, gcarry, goff, xy, t, p, cap);
+                           carry_local, off_local, gcarry, goff, (const uint4 *)lanepre, xy, t, p, cap);
     }
     ECC_CHECK_LAUNCH(ctx, "evt decode");
     return ECC_OK;
