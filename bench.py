@@ -237,7 +237,7 @@ def main():
         "pair_build_kernel": 8.0 * n + 8.0 * geo["pairs"] + 12.0 * geo["hw_groups"],
         # each pair entry read once, B_g per (group, pixel), corner-pair bits out
         "arc_kernel": 8.0 * geo["pairs"] + 8.0 * geo["hw_groups"] + 784.0 * geo["items"],
-        "flags_kernel": 5.0 * n,                                          # keys in, flags out
+        "flags_kernel": 5.0 * n,                                          # xy in, flags out
         "sae_prefix_kernel": 20.0 * geo["hw_groups"] + 16.0 * W * H,
         "nms_kernel": 1.0 * n,                                            # corner flags
     }.get(dominant, 0.0)

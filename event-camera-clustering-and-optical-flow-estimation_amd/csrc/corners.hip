@@ -632,7 +632,7 @@ __device__ __noinline__ bool exact_circle_test(const ArcLds *L, int wp0, int64_t
 }
 
 // 5. Arc test of one (group, tile) item, all items of all groups in one launch.  The item's
-// corner pairs go to res[item][kPairWords] (bit j*196 + pixel); flags_kernel applies them.
+// corner pairs go to res[item][kPairWords] (bit j*196 + pixel); flags_event_kernel applies them.
 constexpr int kStageUnroll = 4;
 
 // Window segments: the sub-regions of the 3x3 tiles around the item's tile that its window
@@ -1082,49 +1082,68 @@ arc_dense_kernel(const int64_t *__restrict__ t, CornerGeom g, const int64_t *__r
     }
 }
 
-// 6. Corner flags: per (group, tile) item, its events (sorted keys, coalesced) look up their
-// pair's result; only corner events are stored (flags are cleared beforehand).  The per-event
-// eligibility of the reference loop is applied here: the slice's first-detect rule (Q15), the
-// border margin, and in ref_compat mode (Q11) "before the slice's first border event".
-__global__ void __launch_bounds__(kThreads)
-flags_kernel(CornerGeom g, Sorted so, const int32_t *__restrict__ sub_end, const uint32_t *__restrict__ res,
-             const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags) {
-    __shared__ uint32_t r_l[kPairWords];
-    __shared__ TileSegs segs;
-    const int64_t item = blockIdx.x;
-    const int64_t grp = item / g.n_tiles;
-    const int tile = (int)(item % g.n_tiles);
-    if ((grp + 1) * kGroup <= g.first_detect || sub_end[item * kSub + kSub - 1] == 0) return;
-    uint32_t any = 0u;
-    for (int w = threadIdx.x; w < kPairWords; w += kThreads) {
-        const uint32_t v = res[item * kPairWords + w];
-        r_l[w] = v;
-        any |= v;
-    }
-    tile_segs(g, so, grp, tile, segs);
-    if (!__syncthreads_or(any != 0u)) return;  // no corner in this item
-    const int64_t grp_first = grp * kGroup * (int64_t)g.S;
-    const int total = segs.pref[kGroup];
-    for (int i0 = 0; i0 < total; i0 += kBuildUnroll * kThreads) {
-        uint32_t k[kBuildUnroll];
-#pragma unroll
-        for (int u = 0; u < kBuildUnroll; ++u) {
-            const int i = i0 + u * kThreads + threadIdx.x;
-            k[u] = (i < total) ? so.key[seg_at(segs, i)] : 0xffffffffu;
+// 6. Corner flags in event order: one workgroup per slice.  Event i of slice s (group g, slice j
+// of the group) is a corner iff its (slice, pixel) pair's bit is set in the result words of its
+// (g, tile) item.  The workgroup first stages slice j's 196-bit segment of every tile's result
+// vector in LDS (7 words per tile), so each event's lookup is an LDS read; every flag is then
+// written, 0 or 1, four per lane and store.  The per-event eligibility of the reference loop: the
+// first-detect rule (Q15) and, in ref_compat mode (Q11), "before the slice's first border event";
+// corner pairs are never border pixels.
+constexpr int kFlagThreads = 512;
+constexpr int kSegWords = (kTilePix + 31) / 32 + 1;  // 7: a 196-bit segment at any bit offset
+
+// kStaged: bit lp of tile in the LDS segments; otherwise (sensors whose segments exceed the
+// LDS) straight from the group's result words.
+template <bool kStaged>
+__device__ __forceinline__ uint32_t corner_bit(uint32_t v, const CornerGeom &g, const uint32_t *sb,
+                                               const uint32_t *__restrict__ rg, int j) {
+    const int x = ecc::xy_x(v), y = ecc::xy_y(v);
+    if (x >= g.W || y >= g.H) return 0u;
+    const int tile = (y / kTile) * g.tiles_x + x / kTile;
+    const int lp = (y % kTile) * kTile + x % kTile;
+    if (kStaged) return (sb[tile * kSegWords + (lp >> 5)] >> (lp & 31)) & 1u;
+    const int pi = j * kTilePix + lp;
+    return (rg[(int64_t)tile * kPairWords + (pi >> 5)] >> (pi & 31)) & 1u;
+}
+
+template <bool kStaged>
+__global__ void __launch_bounds__(kFlagThreads)
+flags_event_kernel(const uint32_t *__restrict__ xy, CornerGeom g, const uint32_t *__restrict__ res,
+                   const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags) {
+    extern __shared__ uint32_t sb[];  // [n_tiles][kSegWords]: bit lp of tile = pair (j, lp)
+    const int64_t s = blockIdx.x;
+    const int64_t lo = s * g.S;
+    const int len = (int)((lo + g.S < g.n ? lo + g.S : g.n) - lo);
+    const int j = (int)(s % kGroup);
+    // events [0, live_end) of the slice can be corners
+    const int live_end = s < g.first_detect ? 0 : (g.border_mode == 1 ? min(len, max(first_border[s], 0)) : len);
+    const uint32_t *rg = res + (s / kGroup) * g.n_tiles * kPairWords;
+    if (kStaged && live_end > 0) {
+        const int b0 = j * kTilePix, w0 = b0 >> 5, sh = b0 & 31;
+        for (int k = threadIdx.x; k < g.n_tiles * kSegWords; k += kFlagThreads) {
+            const int tile = k / kSegWords, w = k % kSegWords;
+            const uint32_t *r = rg + (int64_t)tile * kPairWords + w0 + w;
+            const uint32_t a = w0 + w < kPairWords ? r[0] : 0u;
+            const uint32_t c = (sh && w0 + w + 1 < kPairWords) ? r[1] : 0u;
+            sb[k] = sh ? (a >> sh) | (c << (32 - sh)) : a;
         }
-#pragma unroll
-        for (int u = 0; u < kBuildUnroll; ++u) {
-            if (k[u] == 0xffffffffu) continue;
-            const uint32_t el = k[u] >> 8;
-            const int j = slice_in_group(el, g);
-            const uint32_t pi = (uint32_t)(j * kTilePix + (k[u] & 255u));
-            if (!((r_l[pi >> 5] >> (pi & 31u)) & 1u)) continue;  // corner pairs are never border pixels
-            const int64_t s = grp * kGroup + j;
-            if (s < g.first_detect) continue;
-            if (g.border_mode == 1 && (int64_t)el - (int64_t)j * g.S >= first_border[s]) continue;
-            flags[grp_first + el] = 1;
-        }
     }
+    __syncthreads();
+    const bool vec = (lo & 3) == 0;  // 4-event quads: 16-B loads, 4-B flag stores
+    const int n4 = vec ? len / 4 : 0;
+    for (int q = threadIdx.x; q < n4; q += kFlagThreads) {
+        const int i = 4 * q;
+        uint32_t f = 0u;
+        if (i < live_end) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(xy + lo + i);
+            f = corner_bit<kStaged>(v.x, g, sb, rg, j) | (i + 1 < live_end ? corner_bit<kStaged>(v.y, g, sb, rg, j) << 8 : 0u) |
+                (i + 2 < live_end ? corner_bit<kStaged>(v.z, g, sb, rg, j) << 16 : 0u) |
+                (i + 3 < live_end ? corner_bit<kStaged>(v.w, g, sb, rg, j) << 24 : 0u);
+        }
+        *reinterpret_cast<uint32_t *>(flags + lo + i) = f;
+    }
+    for (int i = 4 * n4 + threadIdx.x; i < len; i += kFlagThreads)
+        flags[lo + i] = (uint8_t)(i < live_end ? corner_bit<kStaged>(xy[lo + i], g, sb, rg, j) : 0u);
 }
 
 // Plain final-SAE scatter (no detection): sae[q] = max t.
@@ -1344,7 +1363,6 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         ECC_CHECK_LAUNCH(ctx, "fast_detect_prepare");
         return ECC_OK;
     }
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(corner_flags, 0, (size_t)n, s), "memset(flags)");
     ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
     {
         ECC_TIMED(ctx, s, "sae_prefix_kernel");
@@ -1368,8 +1386,22 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     }
     {
         ECC_TIMED(ctx, s, "flags_kernel");
-        hipLaunchKernelGGL(flags_kernel, dim3((unsigned)n_items), dim3(kThreads), 0, s, g, so,
-                           (const int32_t *)gi.sub_end, (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
+        constexpr size_t kLdsMax = 160 * 1024;
+        const size_t lds = (size_t)g.n_tiles * kSegWords * sizeof(uint32_t);
+        if (lds <= kLdsMax) {
+            static bool lds_set = false;
+            if (lds > 65536 && !lds_set) {
+                ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&flags_event_kernel<true>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax),
+                              "flags LDS");
+                lds_set = true;
+            }
+            hipLaunchKernelGGL(flags_event_kernel<true>, dim3((unsigned)g.n_slices), dim3(kFlagThreads), lds, s, xy, g,
+                               (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
+        } else {
+            hipLaunchKernelGGL(flags_event_kernel<false>, dim3((unsigned)g.n_slices), dim3(kFlagThreads), 0, s, xy, g,
+                               (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
+        }
     }
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
     return ECC_OK;

@@ -24,6 +24,8 @@ def short(name: str) -> str:
         return "nms_kernel"
     if base == "kmeans_step_kernel" and re.search(r"<\d+, true>", name):
         return "kmeans_pixel_pass"
+    if base == "flags_event_kernel":
+        return "flags_kernel"
     return base
 
 

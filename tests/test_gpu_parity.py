@@ -250,6 +250,7 @@ def test_fast_detect_wide_time_ranges(ecc, orc, gpu, scale, jump):
     (700_000, (1280, 720), 0, 3, 16384),
     (300_000, (640, 480), 1, 4, 16384),
     (100_000, (346, 260), 0, 5, 1000),   # many slices per group, ragged tail
+    (400_000, (1600, 900), 1, 6, 16384), # 7475 tiles: flags read the result words without LDS staging
 ])
 def test_fast_detect_matches_oracle(ecc, orc, gpu, n, wh, mode, seed, slice_events):
     W, H = wh
