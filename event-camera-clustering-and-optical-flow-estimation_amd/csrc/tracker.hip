@@ -294,6 +294,8 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
     __shared__ int s_ws[32];                         // wave counts
     __shared__ unsigned s_rad;                       // group radius (fp32 bits, >= 0)
     __shared__ int s_tail[2];                        // matching tail: list cursor, overflow
+    __shared__ uint64_t s_gmem[64];                  // grouping (<= 64 candidates): member masks
+    __shared__ int s_goff[64];                       //   and first label offsets
     __shared__ int16_t t_trk[64], t_off[64], t_n[64];
     __shared__ int16_t t_d[kTailCap];
     __shared__ float t_dd[kTailCap];
@@ -694,11 +696,11 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
             const float mvx = valid ? ck_vx[lane] : 0.f, mvy = valid ? ck_vy[lane] : 0.f;
             const int mlab = valid ? ck_label[lane] : 0, mtidx = valid ? ck_tidx[lane] : 0;
             int mgid = valid ? ck_gid[lane] : -1;
-            float gax = 0.f, gay = 0.f;  // the lane's group average velocity
             bool proc = !valid;
             n_groups = 0;
             n_glabels = 0;
             int next = 0;
+            // phase A: seeds in order, each group's members (ballot) and label range
             for (;;) {
                 const uint64_t open_ = __ballot(!proc && lane >= next);
                 if (!open_) break;
@@ -708,37 +710,45 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
                 const bool mem = !proc && dist2(pi, F2{(float)mx, (float)my}) <= p.s_group;
                 const uint64_t m = __ballot(mem);
                 if (!m) continue;
-                const int gid = n_groups, cnt = __popcll(m);
                 if (mem) {
                     proc = true;
-                    mgid = gid;
+                    mgid = n_groups;
                     const int r = __popcll(m & lanes_below());
                     if (n_glabels + r < max_tracks) group_labels[n_glabels + r] = mlab;
                 }
-                // ordered fp32 sums over the members (lane = candidate order)
+                if (lane == 0) {
+                    s_gmem[n_groups] = m;
+                    s_goff[n_groups] = n_glabels;
+                }
+                n_glabels += __popcll(m);
+                n_groups++;
+            }
+            wave_sync();
+            // phase B: one lane per group (<= 64 groups): ordered fp32 sums over its members
+            // (candidate order), centroid, average velocity, radius
+            if (lane < n_groups) {
+                const uint64_t m = s_gmem[lane];
+                const int cnt = __popcll(m);
                 F2 sp{0.f, 0.f}, sv{0.f, 0.f};
                 for (uint64_t mm = m; mm; mm &= mm - 1) {
-                    const int l = __ffsll((unsigned long long)mm) - 1;
-                    sp = add(sp, F2{(float)__builtin_amdgcn_readlane(mx, l), (float)__builtin_amdgcn_readlane(my, l)});
-                    sv = add(sv, F2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mvx), l)),
-                                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mvy), l))});
+                    const int k = __ffsll((unsigned long long)mm) - 1;
+                    sp = add(sp, F2{(float)ck_x[k], (float)ck_y[k]});
+                    sv = add(sv, F2{ck_vx[k], ck_vy[k]});
                 }
                 const F2 cen = mul(sp, __fdiv_rn(1.0f, (float)cnt));
                 const F2 av = mul(sv, __fdiv_rn(1.0f, (float)cnt));
-                // max over members of sqrt_rn(s) == sqrt_rn(max s) (monotone)
-                const float sm = mem ? dist2(F2{(float)mx, (float)my}, cen) : 0.f;
-                float smax = 0.f;
-                for (uint64_t mm = m; mm; mm &= mm - 1)
-                    smax = fmaxf(smax, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), __ffsll((unsigned long long)mm) - 1)));
-                const float mr = ecc::sqrt_rn(smax);
-                if (mem) {
-                    gax = av.x;
-                    gay = av.y;
+                float smax = 0.f;  // max over members of sqrt_rn(s) == sqrt_rn(max s) (monotone)
+                for (uint64_t mm = m; mm; mm &= mm - 1) {
+                    const int k = __ffsll((unsigned long long)mm) - 1;
+                    smax = fmaxf(smax, dist2(F2{(float)ck_x[k], (float)ck_y[k]}, cen));
                 }
-                if (lane == 0 && gid < max_tracks) groups[gid] = DevGroup{gid, cnt, n_glabels, av.x, av.y, cen.x, cen.y, mr};
-                n_glabels += cnt;
-                n_groups++;
+                if (lane < max_tracks)
+                    groups[lane] = DevGroup{lane, cnt, s_goff[lane], av.x, av.y, cen.x, cen.y, ecc::sqrt_rn(smax)};
+                gav[lane] = make_float2(av.x, av.y);
             }
+            wave_sync();
+            const float gax = (mgid >= 0 && mgid < n_groups) ? gav[mgid].x : 0.f;
+            const float gay = (mgid >= 0 && mgid < n_groups) ? gav[mgid].y : 0.f;
             // velocity blend with the group average (:388-397); candidates' last fields.  With
             // group_radius >= 0 every candidate joins a group this slice; otherwise none forms.
             if (valid) {
