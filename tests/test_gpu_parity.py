@@ -506,6 +506,8 @@ def _dense_detections(seed, n_slices, per_slice, n_centres, spread, W=346, H=260
     (52, 400, 30, 12.0, {}),
     (53, 60, 4, 20.0, {"max_frames": 3, "frames_to_skip": 1, "history_size": 16, "group_radius": 40.0}),
     (54, 900, 80, 6.0, {"max_distance": 12.5, "damping": 0.5, "smoothing": 0.6}),
+    (56, 500, 40, 10.0, {"max_distance": 1.0e6}),                   # radius too large for the grid
+    (57, 450, 30, 15.0, {"max_distance": 45.0, "group_radius": -1.0}),  # no group ever forms
 ])
 def test_tracker_dense_conflicts_match_oracle(ecc, orc, gpu, seed, per_slice, n_centres, spread, cfg_over):
     cfg = ecc.tracker_cfg(**cfg_over)
@@ -528,7 +530,7 @@ def test_tracker_dense_conflicts_match_oracle(ecc, orc, gpu, seed, per_slice, n_
     gpu.sync()
     assert gtr.status() == 0
     n_tr, n_gr = _compare_trackers(ecc, gtr, otr)
-    assert n_tr > 0 and n_gr > 0
+    assert n_tr > 0 and (n_gr > 0) == (cfg.group_radius >= 0)
 
 
 def test_tracker_capacity_flag(ecc, gpu):
@@ -570,6 +572,33 @@ def test_eps_neighbourhoods_match_oracle(ecc, orc, gpu, eps, min_pts):
         assert np.array_equal(g_core[sl], o_core[sl])
     assert (g_off == o_off).all()
     assert (d_nbr.numpy()[:o_off[-1]] == o_nbr[:o_off[-1]]).all()
+
+
+@pytest.mark.parametrize("eps,min_pts", [(6.0, 64), (12.5, 20), (3.0, 3)])
+def test_eps_counts_wide_segments(ecc, orc, gpu, eps, min_pts):
+    """16384-point segments (dynamic LDS above 64 KiB) and the min_pts-sized core networks."""
+    rng = np.random.default_rng(61)
+    n_segs, stride = 2, 16384
+    counts = np.array([16384, 9001], np.int32)
+    n = n_segs * stride
+    blob = rng.normal([170, 130], 9.0, size=(n, 2))
+    noise = rng.uniform([0, 0], [346, 260], size=(n, 2))
+    pick = rng.random(n) < 0.6
+    pts = np.clip(np.rint(np.where(pick[:, None], blob, noise)), 0, [345, 259]).astype(np.int64)
+    pts[100:140] = pts[99]  # duplicates
+    xy = ecc.pack_xy(pts[:, 0], pts[:, 1])
+    o_cnt, o_core, _, _ = orc.eps_neighbours(xy, n_segs, stride, counts, eps, min_pts, want_lists=False)
+    d_cnt = ecc.DeviceArray(n, np.int32)
+    d_core = ecc.DeviceArray(n, np.float64)
+    gpu.eps_counts(dev(ecc, xy), n_segs, stride, dev(ecc, counts), eps, min_pts, d_cnt, d_core)
+    gpu.sync()
+    g_cnt, g_core = d_cnt.numpy(), d_core.numpy()
+    for sgi in range(n_segs):
+        sl = slice(sgi * stride, sgi * stride + counts[sgi])
+        assert (g_cnt[sl] == o_cnt[sl]).all()
+        assert np.array_equal(g_core[sl], o_core[sl])
+        pad = slice(sgi * stride + counts[sgi], (sgi + 1) * stride)
+        assert (g_cnt[pad] == 0).all() and (g_core[pad] == -1.0).all()
 
 
 def test_eps_duplicates_and_kdtree_kat(ecc, gpu):
