@@ -834,10 +834,17 @@ struct SparseLds {
     int32_t seg_off[16];
 };
 
+// Branch-free: one 16-B pixel read, an unconditional value read (vals[0] when no slice <= j
+// touched the pixel), a select.  A conditional read compiles to an exec-mask branch per circle
+// pixel (scalar-unit bookkeeping, and every lookup's LDS round trip serialised).
+static_assert(sizeof(PixInfo) == 16, "one 16-B LDS read per pixel");
 __device__ __forceinline__ uint32_t sparse_value(const SparseLds &L, int wp, uint32_t below) {
-    const PixInfo p = L.pix[wp];
-    const uint32_t mk = p.mask & below;
-    return mk ? L.vals[p.off + __popc(mk) - 1] : p.bc;
+    uint4 p = reinterpret_cast<const uint4 *>(L.pix)[wp];  // {mask, bc, off, pad}
+    asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(p.z));   // one read, none sunk into a branch
+    const uint32_t mk = p.x & below;
+    uint32_t v = L.vals[mk ? p.z + __popc(mk) - 1u : 0u];
+    asm volatile("" : "+v"(v));  // keep the read unconditional (the compiler would sink it into a branch)
+    return mk ? v : p.y;
 }
 
 template <int N>
