@@ -806,23 +806,22 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
 }
 
 // ---- compact window values (the common case) -------------------------------------------------
-// Window pixel wp keeps the values of the slices that touched it, ascending j, at
-// vals[pix[wp].off ...]; the value an event of slice j sees is vals[off + popc(mask & ((2 << j)
-// - 1)) - 1], or the clamped B_g when no slice <= j touched it.  ~36 KB of LDS instead of the
-// dense planes' ~80 KB: three 8-wave workgroups per CU.  Windows with more than kValCap values
-// go to the overflow list (arc_dense_kernel).
+// Window pixel wp keeps its clamped B_g followed by the values of the slices that touched it,
+// ascending j, at vals[pix[wp].off ...]; the value an event of slice j sees is
+// vals[off + popc(mask & ((2 << j) - 1))] — index off (the B_g slot) when no slice <= j touched
+// the pixel, so a lookup is one 8-B pixel read and one value read, no select.  ~34 KB of LDS
+// instead of the dense planes' ~80 KB: three 8-wave workgroups per CU.  Windows with more than
+// kValCap values go to the overflow list (arc_dense_kernel).
 constexpr int kValCap = 4096;
 
 struct PixInfo {
     uint32_t mask;  // slices of the group that touched the pixel
-    uint32_t bc;    // clamped B_g
-    uint32_t off;   // first value in vals[]
-    uint32_t pad;
+    uint32_t off;   // its B_g slot in vals[], the slice values follow
 };
 
 struct SparseLds {
-    uint32_t vals[kValCap];             // 16 KiB
-    PixInfo pix[kWinPix];               // 7.6 KiB
+    uint32_t vals[kValCap + kWinPix];   // 17.9 KiB: the pairs + one B_g slot per window pixel
+    PixInfo pix[kWinPix];               // 3.8 KiB
     uint32_t res[kPairWords];
     uint16_t tasks[kGroup * kTilePix];  // the tile's eligible pairs (j * 196 + pixel)
     uint16_t q4[kQ4Cap];
@@ -834,17 +833,12 @@ struct SparseLds {
     int32_t seg_off[16];
 };
 
-// Branch-free: one 16-B pixel read, an unconditional value read (vals[0] when no slice <= j
-// touched the pixel), a select.  A conditional read compiles to an exec-mask branch per circle
-// pixel (scalar-unit bookkeeping, and every lookup's LDS round trip serialised).
-static_assert(sizeof(PixInfo) == 16, "one 16-B LDS read per pixel");
+// Branch-free by layout: one 8-B pixel read and one value read (a conditional read compiles to
+// an exec-mask branch per circle pixel: scalar-unit bookkeeping, serialised LDS round trips).
+static_assert(sizeof(PixInfo) == 8, "one 8-B LDS read per pixel");
 __device__ __forceinline__ uint32_t sparse_value(const SparseLds &L, int wp, uint32_t below) {
-    uint4 p = reinterpret_cast<const uint4 *>(L.pix)[wp];  // {mask, bc, off, pad}
-    asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(p.z));   // one read, none sunk into a branch
-    const uint32_t mk = p.x & below;
-    uint32_t v = L.vals[mk ? p.z + __popc(mk) - 1u : 0u];
-    asm volatile("" : "+v"(v));  // keep the read unconditional (the compiler would sink it into a branch)
-    return mk ? v : p.y;
+    const uint2 p = reinterpret_cast<const uint2 *>(L.pix)[wp];  // {mask, off}
+    return L.vals[p.y + __popc(p.x & below)];
 }
 
 template <int N>
@@ -855,7 +849,7 @@ __device__ __forceinline__ void sparse_exact_values(const SparseLds *L, int wp0,
     for (int k = 0; k < N; ++k) {
         const int wp = wp0 + dy[k] * kWin + dx[k];
         const uint32_t mk = L->pix[wp].mask & below;
-        const uint32_t tv = mk ? L->vals[L->pix[wp].off + __popc(mk) - 1] : 0u;
+        const uint32_t tv = mk ? L->vals[L->pix[wp].off + __popc(mk)] : 0u;
         v[k] = !mk      ? c.Bg[q0 + (int64_t)dy[k] * c.W + dx[k]]
                : c.narrow ? c.Lt + (int64_t)tv
                           : c.t[c.grp_first + tv - 1u];
@@ -987,9 +981,9 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
 
-    // (c) per window pixel: clamped B_g, value count, wave prefix of the counts
+    // (c) per window pixel: clamped B_g, value count (+ the B_g slot), wave prefix of the counts
     const uint32_t mk_w = win_lane ? L.pix[wp].mask : 0u;
-    const int cnt = __popc(mk_w);
+    const int cnt = win_lane ? __popc(mk_w) + 1 : 0;
     int incl = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -997,17 +991,19 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         if (lane >= o) incl += v;
     }
     if (lane == 63) L.wave_tot[wave] = incl;
+    uint32_t bcv = 0u;
     if (win_lane) {
         int64_t vz = INT64_MAX;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
-        L.pix[wp].bc = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
+        bcv = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
     }
     __syncthreads();
     if (win_lane) {
         int off = incl - cnt;
         for (int w = 0; w < wave; ++w) off += L.wave_tot[w];
         L.pix[wp].off = (uint32_t)off;
+        L.vals[off] = bcv;
     }
     __syncthreads();
     // (d) pass 2: each value at its pixel's list position (ascending slice)
@@ -1017,7 +1013,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         if (ewp[u] < 0) continue;
         const int j = (int)(ent[u].meta >> 8);
         const PixInfo p = L.pix[ewp[u]];
-        L.vals[p.off + __popc(p.mask & ((1u << j) - 1u))] = ent[u].v;
+        L.vals[p.off + 1u + __popc(p.mask & ((1u << j) - 1u))] = ent[u].v;
     }
     __syncthreads();
 
