@@ -870,6 +870,24 @@ __device__ __noinline__ bool sparse_exact_test(const SparseLds *L, int wp0, int6
 
 constexpr int kSparseHold = kValCap / kArcThreads;  // entries per lane, held between the two passes
 
+#ifndef ECC_ARC_PROFILE
+#define ECC_ARC_PROFILE 0
+#endif
+#if ECC_ARC_PROFILE
+// profiling builds: per-workgroup wall-clock of arc_kernel's phases, summed (thread 0); [7] = items
+__device__ unsigned long long g_arc_prof[8];
+#define ARC_MARK(k)                                                                  \
+    do {                                                                             \
+        if (tid == 0) {                                                              \
+            const unsigned long long now_ = wall_clock64();                          \
+            atomicAdd(&g_arc_prof[k], now_ - arc_t_);                                \
+            arc_t_ = now_;                                                           \
+        }                                                                            \
+    } while (0)
+#else
+#define ARC_MARK(k) do { } while (0)
+#endif
+
 __global__ void __launch_bounds__(kArcThreads, 6)  // 6 waves/SIMD: three 8-wave workgroups per CU
 arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
            const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
@@ -885,6 +903,9 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     const int tile = (int)(item % g.n_tiles);
     if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if ECC_ARC_PROFILE
+    unsigned long long arc_t_ = wall_clock64();
+#endif
     const int64_t HW = (int64_t)g.H * g.W;
     int tx, ty;
     tile_origin_xy(g, tile, tx, ty);
@@ -935,6 +956,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         if (tid == 0) L.seg_pref[0] = 0;
     }
     __syncthreads();
+    ARC_MARK(0);  // (a) segment table + B_g window
     if (L.seg_pref[1] == 0) return;  // no events in the tile: nothing to flag
     const int total = L.seg_pref[kMaxSeg];
     if (total > kValCap) {  // too many values for the compact list: the dense kernel takes it
@@ -981,6 +1003,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
 
+    ARC_MARK(1);  // (b) pass 1: entries, slice bits, tasks
     // (c) per window pixel: clamped B_g, value count (+ the B_g slot), wave prefix of the counts
     const uint32_t mk_w = win_lane ? L.pix[wp].mask : 0u;
     const int cnt = win_lane ? __popc(mk_w) + 1 : 0;
@@ -1017,6 +1040,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     }
     __syncthreads();
 
+    ARC_MARK(2);  // (c, d) list offsets, B_g slots, value scatter
     // (e) tests, as the dense kernel's (lookups through the compact lists)
     const int n_tasks = L.n_tasks;
     const bool fast = !L.exact_only;
@@ -1064,9 +1088,17 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         }
     }
     __syncthreads();
+    ARC_MARK(3);  // circle 3
     const int n4 = min(L.q4n, kQ4Cap);
+#if ECC_ARC_PROFILE
+    if (tid == 0) atomicAdd(&g_arc_prof[6], (unsigned long long)n4);
+#endif
     for (int qi = tid; qi < n4; qi += kArcThreads) circle4(L.q4[qi]);
     __syncthreads();
+    ARC_MARK(4);  // circle 4
+#if ECC_ARC_PROFILE
+    if (tid == 0) atomicAdd(&g_arc_prof[7], 1ull);
+#endif
     if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
 }
 
@@ -1409,6 +1441,20 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
     return ECC_OK;
 }
+
+#if ECC_ARC_PROFILE
+// Profiling builds only (make ARC_PROFILE=1): arc_kernel's summed per-workgroup phase ticks
+// since the last call (reset after reading); out[7] = items timed; ticks_per_us from the device.
+ECC_API int ecc_arc_profile(unsigned long long *out8, double *ticks_per_us) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_arc_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return ECC_ERR_HIP;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_arc_prof), z, sizeof(z));
+    int khz = 0;
+    hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
+    *ticks_per_us = khz / 1000.0;
+    return ECC_OK;
+}
+#endif
 
 ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
                             const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
