@@ -402,6 +402,48 @@ def test_nms_box_sizes(ecc, orc, gpu, box, wh, density):
         assert (g_out[s * cap: s * cap + k] == o_out[s * cap: s * cap + k]).all(), s
 
 
+@pytest.mark.parametrize("cap", [8192, 40])
+def test_nms_parallel_and_greedy_slices(ecc, orc, gpu, cap):
+    """Slices below and above the parallel pass's 2048-candidate limit in one call, including
+    long dependency chains (a diagonal staircase: every candidate overlaps its predecessor),
+    a slice with exactly 2048 candidates and one with 2049, and an empty slice."""
+    W, H = 346, 260
+    rng = np.random.default_rng(77)
+    S = 4096
+    xs, ys, fl = [], [], []
+    for k, m in enumerate([300, 2048, 2049, 0, 3000, 1000, 2047]):
+        if k == 5:  # staircase in event order, then random order of a second one
+            t = np.arange(m)
+            x, y = (t * 3) % 340, (t // 113) * 9 % 250
+        elif k == 6:
+            t = rng.permutation(m)
+            x, y = (t % 300), (t // 300) * 2
+        else:
+            x, y = rng.integers(0, W, S), rng.integers(0, H, S)
+        f = np.zeros(S, np.uint8)
+        if k in (5, 6):
+            x = np.concatenate([x, rng.integers(0, W, S - m)])
+            y = np.concatenate([y, rng.integers(0, H, S - m)])
+            f[:m] = 1
+        else:
+            f[rng.choice(S, m, replace=False)] = 1
+        xs.append(x), ys.append(y), fl.append(f)
+    xy = ecc.pack_xy(np.concatenate(xs), np.concatenate(ys))
+    flags = np.concatenate(fl)
+    n = len(xy)
+    o_out, o_cnt, rc = orc.corner_nms(xy, flags, W, H, cap=cap, slice_events=S)
+    ns = len(o_cnt)
+    d_out = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE)
+    d_cnt = ecc.DeviceArray(ns, np.int32)
+    gpu.corner_nms(dev(ecc, xy), dev(ecc, flags), n, S, W, H, 15, cap, d_out, d_cnt)
+    assert gpu.corner_nms_status() == (ecc.ERR_CAPACITY if rc else 0)
+    assert (d_cnt.numpy() == o_cnt).all()
+    g_out = d_out.numpy()
+    for s in range(ns):
+        k = o_cnt[s]
+        assert (g_out[s * cap: s * cap + k] == o_out[s * cap: s * cap + k]).all(), s
+
+
 def test_nms_status_capacity_and_outside(ecc, gpu):
     W, H = 346, 260
     rng = np.random.default_rng(9)
@@ -417,6 +459,11 @@ def test_nms_status_capacity_and_outside(ecc, gpu):
     xy2[5] = ecc.pack_xy(np.array([W + 3]), np.array([10]))[0]  # flagged event outside the image
     d_out = ecc.DeviceArray(4096, ecc.CORNER_DTYPE)
     gpu.corner_nms(dev(ecc, xy2), dev(ecc, flags), n, n, W, H, 15, 4096, d_out, d_cnt)
+    assert gpu.corner_nms_status() == ecc.ERR_INVALID
+    sparse = np.zeros(n, np.uint8)  # the same on the parallel pass (few candidates)
+    sparse[::64] = 1
+    sparse[5] = 1
+    gpu.corner_nms(dev(ecc, xy2), dev(ecc, sparse), n, n, W, H, 15, 4096, d_out, d_cnt)
     assert gpu.corner_nms_status() == ecc.ERR_INVALID
 
 
