@@ -225,7 +225,8 @@ nms_greedy_kernel(const uint32_t *__restrict__ cand, const int32_t *__restrict__
     const uint32_t *c = cand + s * (int64_t)S;
     const int total = n_cand[s];
     const int cs = 2 * half + 1, reach = 2 * half;
-    for (int i = lane; i < gw * gh; i += kGridThreads) grid[i] = kNoCentre;
+    const int pw = gw + 2;  // one border cell on every side: the 3x3 probes need no bounds checks
+    for (int i = lane; i < pw * (gh + 2); i += kGridThreads) grid[i] = kNoCentre;
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int n_kept = 0;
     bool overflow = false, bad_input = false;
@@ -242,17 +243,12 @@ nms_greedy_kernel(const uint32_t *__restrict__ cand, const int32_t *__restrict__
         if (!valid) { v = 0u; x = 0; y = 0; }
         const int cx = x / cs, cy = y / cs;
         bool alive = valid;
+        const int c0 = cy * pw + cx;  // padded cell (cx, cy) - (1, 1)
+        uint32_t kc[9];
 #pragma unroll
-        for (int dy = -1; dy <= 1; ++dy) {
+        for (int d = 0; d < 9; ++d) kc[d] = grid[c0 + (d / 3) * pw + d % 3];
 #pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-                const int gx = cx + dx, gy = cy + dy;
-                if (gx >= 0 && gy >= 0 && gx < gw && gy < gh) {
-                    const uint32_t k = grid[gy * gw + gx];
-                    if (k != kNoCentre && near_centre(k, v, reach)) alive = false;
-                }
-            }
-        }
+        for (int d = 0; d < 9; ++d) alive &= !(kc[d] != kNoCentre && near_centre(kc[d], v, reach));
         uint64_t am = __ballot(alive), keepm = 0;
         while (am) {  // wave-uniform: each step keeps the first surviving lane
             const int i0 = __ffsll((unsigned long long)am) - 1;
@@ -263,7 +259,7 @@ nms_greedy_kernel(const uint32_t *__restrict__ cand, const int32_t *__restrict__
         }
         if ((keepm >> lane) & 1ull) {
             const int rank = n_kept + __popcll(keepm & lt_mask);
-            grid[cy * gw + cx] = v;
+            grid[c0 + pw + 1] = v;
             if (rank < cap) out[s * (int64_t)cap + rank] = ecc_corner{x, y, rank};
             else overflow = true;
         }
@@ -304,7 +300,7 @@ ECC_API int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corn
     ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + 1, 0, 4, s), "memset(nms err)");
     const int half = box_size / 2, cs = 2 * half + 1;
     const int gw = (width + cs - 1) / cs, gh = (height + cs - 1) / cs;
-    if ((int64_t)gw * gh <= kGridMaxCells) {
+    if ((int64_t)(gw + 2) * (gh + 2) <= kGridMaxCells) {
         // candidate lists: n xy words + n_slices counts, per context (grown, never shrunk)
         const size_t need = ecc::align_up((size_t)n * 4, 256) + (size_t)n_slices * 4;
         NmsState *st;
@@ -334,7 +330,8 @@ ECC_API int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corn
                                corner_flags, n, slice_events, cand, n_cand);
         }
         ECC_TIMED(ctx, s, "nms_kernel");
-        hipLaunchKernelGGL(nms_greedy_kernel, dim3((unsigned)n_slices), dim3(kGridThreads), (size_t)gw * gh * 4, s,
+        hipLaunchKernelGGL(nms_greedy_kernel, dim3((unsigned)n_slices), dim3(kGridThreads),
+                           (size_t)(gw + 2) * (gh + 2) * 4, s,
                            (const uint32_t *)cand, (const int32_t *)n_cand, slice_events, width, height, half, gw, gh,
                            cap, out, out_count, ctx->flags + 1);
     } else {
