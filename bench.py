@@ -6,7 +6,9 @@ One step = one pass of the hot path over one resident batch of synthetic events:
   hash downsample (8192-event windows)  ->  k-means k=16 on the representatives (10 Lloyd
   iterations + final labels), and SAE + FAST/arc corner detection (16384-event slices)  ->
   greedy 15x15 box NMS per slice.  On one GPU the two chains run on two HIP streams.
-The corner tracker (sequential over slices) is timed separately and reported in µs/slice.
+The corner tracker (sequential over slices) is outside the metric's stages; it is measured
+beside it: µs per slice, and the pipelined throughput with the tracker of batch b running on a
+third stream while batch b+1 is detected (`with_tracker`).
 
 Single GPU:  python bench.py [--steps K --warmup W]
 Multi GPU:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -14,8 +16,12 @@ Multi GPU:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus 
   shard-local; k-means is global from ONE RCCL all-reduce of the shards' per-pixel count images
   (every rank then runs the Lloyd passes locally); the SAE is handed over exactly (all-gather
   of the shards' own last-timestamp images; rank r starts from the elementwise max over ranks
-  < r).  Weak scaling: events per rank fixed.
-Rank 0 prints ONE JSON line.
+  < r).  After the timed steps the shards' NMS lists are gathered in global slice order and ONE
+  tracker on rank 0 consumes them (the C5 track merge, `track_merge`).  Weak scaling: events per
+  rank fixed (--events; --preset c5 = 50 M per GPU, BASELINE config C5).
+Rank 0 prints ONE JSON line.  With the CPU leg on (default, rank 0 of a 1-GPU run), the oracle
+runs the same pipeline over exactly the step's events: that is the CPU baseline, and every GPU
+output of the step is compared with it (`parity`).
 """
 from __future__ import annotations
 
@@ -23,7 +29,6 @@ import argparse
 import json
 import os
 import platform
-import subprocess
 import sys
 import time
 from pathlib import Path
@@ -35,6 +40,13 @@ PKG = ROOT / "event-camera-clustering-and-optical-flow-estimation_amd"
 sys.path.insert(0, str(PKG))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+SLICE = 16384
+WINDOW = 8192
+CORNER_KERNELS = ("slice_sort_kernel", "pair_build_kernel", "sae_prefix_kernel", "arc_kernel",
+                  "arc_dense_kernel", "flags_kernel")
+KMEANS_KERNELS = ("kmeans_count_kernel", "kmeans_count_sum_kernel", "kmeans_extent_kernel",
+                  "kmeans_pixel_pass", "kmeans_step_kernel", "kmeans_xy16_labels")
+NMS_KERNELS = ("nms_compact_kernel", "nms_kernel")
 
 
 def parse():
@@ -42,15 +54,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--events", type=int, default=1221 * 16384,
-                    help="events per GPU per step (1221 slices of 16384 = 20.0 M, BASELINE C4)")
+    ap.add_argument("--preset", choices=("c4", "c5"), default="c4",
+                    help="c4: 20.0 M events per GPU (1221 slices, BASELINE C4, the metric's config); "
+                         "c5: 50.0 M events per GPU (3052 slices; 8 GPUs = the 400 M-event stream of C5)")
+    ap.add_argument("--events", type=int, default=None, help="events per GPU per step (overrides --preset)")
     ap.add_argument("--width", type=int, default=346)
     ap.add_argument("--height", type=int, default=260)
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--cpu-events", type=int, default=40_000_000,
-                    help="CPU-baseline sample size (~16 s of single-thread oracle work)")
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and the full-size parity leg")
     ap.add_argument("--no-tracker", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the RAW (EVT 3.0 / 2.0) decode measurement")
     ap.add_argument("--no-eps", action="store_true", help="skip the eps-neighbourhood (DBSCAN / OPTICS) measurement")
@@ -61,7 +73,10 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for rehearsal")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on device 0 (with --dist-backend gloo)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.events is None:
+        a.events = {"c4": 1221, "c5": 3052}[a.preset] * SLICE
+    return a
 
 
 def main():
@@ -82,28 +97,29 @@ def main():
     import eccpy as ecc
 
     W, H, n, K, I = args.width, args.height, args.events, args.k, args.iters
-    if n % 16384:
+    if n % SLICE:
         raise SystemExit("--events must be a multiple of the 16384-event slice (global slice alignment)")
     # one stream for libecc and the collectives (torch's current stream) when sharded
     ctx = ecc.Context(local, stream=torch.cuda.current_stream().cuda_stream) if dist else ecc.Context(local)
     xy_h, t_h, p_h = ecc.gen_events(n, first=rank * n, seed=1, width=W, height=H)
     d_xy, d_t = ecc.DeviceArray.from_numpy(xy_h, ctx.stream), ecc.DeviceArray.from_numpy(t_h, ctx.stream)
-    hcfg = ecc.hash_cfg(window=8192)  # reference bounds 0<=x<=1280, 0<=y<=720
-    n_win = (n + 8191) // 8192
-    rep_xy = ecc.DeviceArray(n_win * 8192, np.uint32)
+    hcfg = ecc.hash_cfg(window=WINDOW)  # reference bounds 0<=x<=1280, 0<=y<=720
+    n_win = (n + WINDOW - 1) // WINDOW
+    rep_xy = ecc.DeviceArray(n_win * WINDOW, np.uint32)
     uniq = ecc.DeviceArray(n_win, np.int32)
     rep = ecc.DeviceArray(n_win, np.int32)
     c0 = np.stack([np.linspace(20, W - 20, K), np.linspace(20, H - 20, K)[::-1]], 1).astype(np.float32).ravel()
     d_c0 = ecc.DeviceArray.from_numpy(c0, ctx.stream)
     d_c = ecc.DeviceArray(2 * K, np.float32)
-    labels = ecc.DeviceArray(n_win * 8192, np.uint8)
+    labels = ecc.DeviceArray(n_win * WINDOW, np.uint8)
     kcfg = ecc.kmeans_cfg(k=K, max_iters=I, tol=-1.0)
     ccfg = ecc.corner_cfg(width=W, height=H, first_detect_slice=1 if rank == 0 else 0)
     sae = ecc.DeviceArray(W * H, np.int64)
     flags = ecc.DeviceArray(n, np.uint8)
-    ns, cap = (n + 16383) // 16384, 4096
-    nms_out = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE)
-    nms_cnt = ecc.DeviceArray(ns, np.int32)
+    ns, cap = n // SLICE, 4096
+    # two NMS output buffers: the pipelined tracker pass consumes batch b's while b+1 is detected
+    nms_out = [ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE) for _ in range(2)]
+    nms_cnt = [ecc.DeviceArray(ns, np.int32) for _ in range(2)]
     lib = ecc.lib
     if dist:
         # exchange buffers are torch tensors (RCCL operates on them); libecc gets their pointers
@@ -111,25 +127,25 @@ def main():
         t_local = torch.zeros(W * H, dtype=torch.int64, device=f"cuda:{local}")
         t_all = torch.zeros(world * W * H, dtype=torch.int64, device=f"cuda:{local}")
 
-    def step_sharded():
+    def step_sharded(nb=0):
         """Shard-local downsample/detection/NMS; global k-means from ONE all-reduce of the
         shards' per-pixel count images; exact SAE hand-off (all-gather of the shards' own last-t
         images, computed by the detection's prepare phase)."""
         S = ctx.stream
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
                                           uniq.ptr, rep.ptr, S), "downsample")
-        ecc.check(lib.ecc_kmeans_counts_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, W, H, t_counts.data_ptr(), S))
+        ecc.check(lib.ecc_kmeans_counts_xy16(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, W, H, t_counts.data_ptr(), S))
         ecc.check(lib.ecc_fast_detect_prepare(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), t_local.data_ptr(), S))
         dist.all_reduce(t_counts)
         dist.all_gather_into_tensor(t_all, t_local)
         ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, S))
         ecc.check(lib.ecc_kmeans_run_counts(ctx.ctx, t_counts.data_ptr(), W, H, ecc.C.byref(kcfg), d_c.ptr, None, S))
-        ecc.check(lib.ecc_kmeans_labels_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, d_c.ptr, K,
+        ecc.check(lib.ecc_kmeans_labels_xy16(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, d_c.ptr, K,
                                              kcfg.threshold, labels.ptr, S))
         ecc.check(lib.ecc_sae_max_combine(ctx.ctx, t_all.data_ptr(), rank, W * H, sae.ptr, S))
         ecc.check(lib.ecc_fast_detect_finish(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), sae.ptr,
                                              flags.ptr, S), "fast_detect_finish")
-        ctx.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, nms_out, nms_cnt)
+        ctx.corner_nms(d_xy, flags, n, SLICE, W, H, 15, cap, nms_out[nb], nms_cnt[nb])
 
     # single GPU: downsample -> k-means and the corner chain read the same resident batch and are
     # independent, so they run on two streams (fork/join with events) and overlap
@@ -139,21 +155,21 @@ def main():
         ecc.check(lib.ecc_event_create(ecc.C.byref(ev_fork)), "event")
         ecc.check(lib.ecc_event_create(ecc.C.byref(ev_join)), "event")
 
-    def step(serial=args.serial):
+    def step(serial=args.serial, nb=0):
         if dist:
-            return step_sharded()
+            return step_sharded(nb)
         ks = ctx.stream if serial else s2.value  # the k-means chain's stream
         ecc.check(lib.ecc_event_record(ev_fork, ctx.stream))
         ecc.check(lib.ecc_stream_wait_event(ks, ev_fork))
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
                                           uniq.ptr, rep.ptr, ks), "downsample")
         ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, ks))
-        ecc.check(lib.ecc_kmeans_run_xy16(ctx.ctx, rep_xy.ptr, n_win, 8192, uniq.ptr, ecc.C.byref(kcfg), d_c.ptr,
+        ecc.check(lib.ecc_kmeans_run_xy16(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, ecc.C.byref(kcfg), d_c.ptr,
                                           labels.ptr, None, ks), "kmeans")
         ecc.check(lib.ecc_event_record(ev_join, ks))
         ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
         ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
-        ctx.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, nms_out, nms_cnt)
+        ctx.corner_nms(d_xy, flags, n, SLICE, W, H, 15, cap, nms_out[nb], nms_cnt[nb])
         ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_join))
 
     for _ in range(args.warmup):
@@ -161,6 +177,8 @@ def main():
     ctx.sync()
     if ctx.fast_detect_status() != 0:
         raise RuntimeError("fast_detect reported a status error")
+    if ctx.corner_nms_status() != 0:
+        raise RuntimeError("corner_nms reported a status error")
     if dist and lib.ecc_kmeans_counts_status(ctx.ctx, ctx.stream) != 0:
         raise RuntimeError("a representative lies outside the k-means count frame")
     n_reps = int(uniq.numpy().sum())
@@ -200,6 +218,7 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    ms_step = elapsed / args.steps * 1e3
 
     # 2. the kernel-timing pass: the same K steps again with HIP events recorded around every
     #    launch on its stream (ecc_ctx_set_timing) -> per-kernel average durations.  It runs on
@@ -213,133 +232,150 @@ def main():
     ctx.sync()
     instrumented = time.perf_counter() - t1
     lib.ecc_ctx_set_timing(ctx.ctx, 0)
-    buf = ecc.C.create_string_buffer(1 << 16)
-    ecc.check(lib.ecc_ctx_timing_report(ctx.ctx, buf, len(buf)))
-    stats = json.loads(buf.value.decode())
+    stats = ctx.timing_report()
+    detect_stats = ctx.fast_detect_stats()
 
-    # per-kernel roofline of the dominant kernel (largest total time in the timed region)
+    # ---- roofline (SURVEY.md §8d algorithmic bytes per unit) ------------------------------------
     kern_ms = {k: v["total_ms"] for k, v in stats.items()}
     dominant = max(kern_ms, key=kern_ms.get)
     launches = stats[dominant]["launches"]
     avg_ms = kern_ms[dominant] / launches
-    per_step_launches = launches / args.steps
-    # algorithmic bytes per launch: what the kernel must move at minimum
-    geo = corner_geometry(xy_h, n, W, H)
-    bytes_per_launch = {
-        "downsample_hash_kernel": 4.0 * n + 4.0 * n_reps + 8.0 * n_win,   # xy in, reps + counts out
-        "kmeans_xy16_kernel": 4.0 * n_reps,                               # packed u16 xy per point
-        "kmeans_xy16_labels": 5.0 * n_reps,                               # + u8 label out
-        "kmeans_count_kernel": 4.0 * n_reps,                              # packed u16 xy per point
-        "kmeans_pixel_pass": 4.0 * W * H,                                 # per-pixel counts (bbox <= sensor)
-        # corner stage: xy + t in, key + t32 out (+ per-slice tile offsets)
-        "slice_sort_kernel": 20.0 * n + 4.0 * geo["slices"] * (geo["tiles"] + 2),
-        # key + t32 in, pair entries out, per-(group, pixel) slice mask + last t out
-        "pair_build_kernel": 8.0 * n + 8.0 * geo["pairs"] + 12.0 * geo["hw_groups"],
-        # each pair entry read once, B_g per (group, pixel), corner-pair bits out
-        "arc_kernel": 8.0 * geo["pairs"] + 8.0 * geo["hw_groups"] + 784.0 * geo["items"],
-        "flags_kernel": 5.0 * n,                                          # xy in, flags out
-        "sae_prefix_kernel": 20.0 * geo["hw_groups"] + 16.0 * W * H,
-        "nms_kernel": 1.0 * n,                                            # corner flags
-    }.get(dominant, 0.0)
+
+    def stage_ms(names):
+        return sum(kern_ms.get(k, 0.0) for k in names) / args.steps
+
+    # §8d: downsample 4 B/event in + 4 B/rep out + 8 B/window; k-means 8 B/point/iteration
+    # (float2 read) + 1 B/point (final label); SAE + arc test 12 B/event in (xy + t) + 1 B/event
+    # out (corner flag); NMS and tracker are latency work (reported in µs, no roofline).
+    bytes_stage = {
+        "downsample": 4.0 * n + 4.0 * n_reps + 8.0 * n_win,
+        "kmeans": (8.0 * I + 1.0) * n_reps,
+        "corner": 13.0 * n,
+    }
+    t_stage = {
+        "downsample": stage_ms(("downsample_hash_kernel",)),
+        "kmeans": stage_ms(KMEANS_KERNELS),
+        "corner": stage_ms(CORNER_KERNELS),
+    }
+    stages = {}
+    for k in bytes_stage:
+        ach = bytes_stage[k] / (t_stage[k] * 1e-3) / 1e9 if t_stage[k] > 0 else 0.0
+        stages[k] = {"ms_per_step": round(t_stage[k], 4), "algorithmic_bytes": bytes_stage[k],
+                     "achieved_gbs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4)}
+    e2e_bytes = sum(bytes_stage.values())
+    stages["nms"] = {"ms_per_step": round(stage_ms(NMS_KERNELS), 4), "bound": "latency"}
+    stages["e2e"] = {"ms_per_step": round(ms_step, 4), "algorithmic_bytes": e2e_bytes,
+                     "achieved_gbs": round(e2e_bytes / (ms_step * 1e-3) / 1e9, 1),
+                     "frac": round(e2e_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "note": "wall time of the whole step (both streams) over the three stages' §8d bytes"}
+    # the dominant kernel carries its stage's §8d bytes (the corner stage's 13 B/event for the arc
+    # kernel): what that stage must move at minimum, over this one kernel's launch time
+    stage_of = {**{k: "corner" for k in CORNER_KERNELS}, **{k: "kmeans" for k in KMEANS_KERNELS},
+                "downsample_hash_kernel": "downsample"}
+    dom_stage = stage_of.get(dominant)
+    bytes_per_launch = bytes_stage[dom_stage] if dom_stage else 0.0
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     # HBM bytes per launch of the same kernel from the newest committed PMC summary
     # (scripts/gpu_profile.sh + scripts/traffic.py; PMC passes cannot run inside this process)
     traffic = None
+    traffic_src = None
     tfiles = sorted((ROOT / "profiles").glob("*_traffic.json"))
     if tfiles:
         try:
             rec = json.loads(tfiles[-1].read_text()).get(dominant)
             traffic = round(rec["bytes_per_launch"]) if rec else None
+            traffic_src = tfiles[-1].name
         except (ValueError, KeyError, TypeError):
             traffic = None
 
-    # tracker (sequential over slices): reported separately, µs per slice
-    tracker_us = None
-    if not args.no_tracker and rank == 0:
+    # ---- tracker (sequential over slices, rank 0 of a 1-GPU run) ---------------------------------
+    tracker = None
+    g_tracker = None
+    if not args.no_tracker and not dist:
         tr = ecc.Tracker(ctx)
         tmr = ecc.Timer(ctx.stream)
         tmr.start()
-        tr.update(nms_out, nms_cnt, ns, cap)
-        tracker_us = tmr.stop() * 1e3 / ns
+        tr.update(nms_out[0], nms_cnt[0], ns, cap)
+        trk_ms = tmr.stop()
+        if tr.status() != 0:
+            raise RuntimeError("tracker reported a status error")
+        g_tracker = (tr.tracks(), tr.groups()[0])
         tr.close()
+        # pipelined: the tracker of batch b (stream 3) overlaps the detection of batch b+1; the
+        # NMS buffers alternate, and batch b+2 waits for the tracker of batch b to release one
+        s3 = ecc.P()
+        ecc.check(lib.ecc_stream_create(ecc.C.byref(s3)), "stream")
+        ev_nms = [ecc.P(), ecc.P()]
+        ev_trk = [ecc.P(), ecc.P()]
+        for e in ev_nms + ev_trk:
+            ecc.check(lib.ecc_event_create(ecc.C.byref(e)), "event")
+        trp = ecc.Tracker(ctx)
+        kp = max(3, min(args.steps, 6))
+        ctx.sync()
+        tp0 = time.perf_counter()
+        for b in range(kp):
+            nb = b % 2
+            if b >= 2:
+                ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_trk[nb]))
+            step(nb=nb)
+            ecc.check(lib.ecc_event_record(ev_nms[nb], ctx.stream))
+            ecc.check(lib.ecc_stream_wait_event(s3.value, ev_nms[nb]))
+            ecc.check(lib.ecc_tracker_update(trp.tr, nms_out[nb].ptr, nms_cnt[nb].ptr, ns, cap, s3.value))
+            ecc.check(lib.ecc_event_record(ev_trk[nb], s3.value))
+        ecc.check(lib.ecc_stream_sync(s3.value))
+        ctx.sync()
+        tp = time.perf_counter() - tp0
+        trp.close()
+        tracker = {
+            "slices": ns, "us_per_slice": round(trk_ms * 1e3 / ns, 2), "ms_per_batch": round(trk_ms, 3),
+            "tracks_end": len(g_tracker[0]), "groups_end": len(g_tracker[1]),
+            "with_tracker": {"mevents_s": round(kp * n / tp / 1e6, 1), "ms_per_step": round(tp / kp * 1e3, 3),
+                             "steps": kp,
+                             "how": "tracker of batch b on a third stream overlapping detection of batch b+1"},
+        }
 
-    # RAW ingest, reported beside the headline: the same events written
-    # as EVT 3.0 / EVT 2.0 words, decoded from device-resident words.
+    # ---- C5 track merge: shard NMS lists gathered in global slice order -> ONE tracker (rank 0) ----
+    track_merge = None
+    if dist and not args.no_tracker:
+        from eccpy import dist as edist
+        comm = edist.TorchComm(dist)
+        packed = torch.zeros((ns * cap, 3), dtype=torch.int32, device=f"cuda:{local}")
+        offs = torch.zeros(ns + 1, dtype=torch.int64, device=f"cuda:{local}")
+        dist.barrier()
+        ctx.sync()
+        tm0 = time.perf_counter()
+        ctx.corner_pack(nms_out[0], nms_cnt[0], ns, cap, packed.data_ptr(), offs.data_ptr())
+        total = int(offs[-1].item())
+        cnt_t = torch.empty(ns, dtype=torch.int32, device=f"cuda:{local}")
+        ecc.check(lib.ecc_memcpy_d2d(cnt_t.data_ptr(), nms_cnt[0].ptr, 4 * ns, ctx.stream))
+        ctx.sync()
+        all_pk, starts, cnts = edist.gather_corner_lists(comm, packed[:total], cnt_t)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tm0) * 1e3
+        if rank == 0:
+            tr = ecc.Tracker(ctx)
+            tmr = ecc.Timer(ctx.stream)
+            tmr.start()
+            tr.update_lists(all_pk.data_ptr(), starts.data_ptr(), cnts.data_ptr(), int(starts.numel()))
+            merge_ms = tmr.stop()
+            if tr.status() != 0:
+                raise RuntimeError("merged tracker reported a status error")
+            track_merge = {"ranks": world, "slices": int(starts.numel()), "corners": int(cnts.sum().item()),
+                           "pack_gather_ms": round(gather_ms, 3), "tracker_ms": round(merge_ms, 3),
+                           "us_per_slice": round(merge_ms * 1e3 / int(starts.numel()), 2),
+                           "tracks_end": len(tr.tracks())}
+            tr.close()
+        dist.barrier()
+
+    # ---- RAW ingest, reported beside the headline ------------------------
     ingest = None
     if not args.no_ingest and rank == 0:
-        ingest = {}
-        for fmt, name in ((ecc.EVT3, "EVT3"), (ecc.EVT2, "EVT2")):
-            words = ecc.evt_encode(fmt, xy_h, t_h, p_h)
-            d_words = ecc.DeviceArray.from_numpy(words, ctx.stream)
-            d_oxy, d_ot = ecc.DeviceArray(n, np.uint32), ecc.DeviceArray(n, np.int64)
-            d_op, d_on = ecc.DeviceArray(n, np.uint8), ecc.DeviceArray(1, np.int64)
-            run = lambda: ctx.evt_decode(fmt, d_words, len(words), d_oxy, d_ot, d_op, n, d_on)
-            run()
-            ctx.sync()
-            reps = max(args.steps, 5)
-            tmr = ecc.Timer(ctx.stream)
-            tmr.start()
-            for _ in range(reps):
-                run()
-            dec_ms = tmr.stop() / reps
-            assert int(d_on.numpy()[0]) == n and ctx.evt_status() == 0
-            ctx.set_timing(True)
-            ctx.timing_reset()
-            for _ in range(reps):
-                run()
-            st = ctx.timing_report()
-            ctx.set_timing(False)
-            kern = {k: v["total_ms"] / v["launches"] for k, v in st.items()}
-            wbytes = words.nbytes
-            dk = kern.get("evt_decode_kernel", float("nan"))
-            ach = (wbytes + 13.0 * n) / (dk * 1e-3) / 1e9  # words in + xy/t/p out
-            ingest[name] = {
-                "words": len(words), "word_bytes": words.itemsize, "events": n,
-                "mevents_s": round(n / (dec_ms * 1e-3) / 1e6, 1), "ms_per_decode": round(dec_ms, 4),
-                "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
-                "roofline": {"kernel": "evt_decode_kernel", "bound": "hbm", "achieved": round(ach, 1),
-                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                             "algorithmic_bytes": f"{words.itemsize} B/word in + 13 B/event out"},
-            }
-            del d_words, d_oxy, d_ot, d_op, d_on
+        ingest = bench_ingest(ecc, ctx, args, xy_h, t_h, p_h, n)
 
-    # eps-neighbourhoods (BASELINE C4), reported beside the headline:
-    # DBSCAN eps 20 / minPts 20 (counts) and OPTICS eps 10 / min_pts 2 (counts + core distances)
-    # per 8192-event downsample window, over this step's device-resident representatives.
+    # ---- eps-neighbourhoods + DBSCAN (BASELINE C4) --------------------
     eps_res = None
     if not args.no_eps and rank == 0:
-        eps_res = {}
-        e_cnt = ecc.DeviceArray(n_win * 8192, np.int32)
-        e_core = ecc.DeviceArray(n_win * 8192, np.float64)
-        for name, eps, mp, core in (("dbscan_eps20_minpts20", 20.0, 20, None),
-                                    ("optics_eps10_minpts2", 10.0, 2, e_core)):
-            run = lambda: ctx.eps_counts(rep_xy, n_win, 8192, uniq, eps, mp, e_cnt, core)
-            run()
-            ctx.sync()
-            reps = max(args.steps, 5)
-            tmr = ecc.Timer(ctx.stream)
-            tmr.start()
-            for _ in range(reps):
-                run()
-            call_ms = tmr.stop() / reps
-            ctx.set_timing(True)
-            ctx.timing_reset()
-            for _ in range(reps):
-                run()
-            st = ctx.timing_report()
-            ctx.set_timing(False)
-            kern = {k: v["total_ms"] / v["launches"] for k, v in st.items()}
-            ek = kern.get("eps_counts_kernel", float("nan"))
-            per_rep = 8 + (8 if core is not None else 0)  # xy in + count out [+ core distance out]
-            ach = n_reps * per_rep / (ek * 1e-3) / 1e9
-            eps_res[name] = {
-                "reps": n_reps, "windows": n_win, "mreps_s": round(n_reps / (call_ms * 1e-3) / 1e6, 1),
-                "ms_per_call": round(call_ms, 4), "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
-                "roofline": {"kernel": "eps_counts_kernel", "bound": "hbm", "achieved": round(ach, 1),
-                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                             "algorithmic_bytes": f"4 B/rep in + 4 B/rep out{' + 8 B/rep core distance' if core is not None else ''}"},
-            }
-        del e_cnt, e_core
+        eps_res = bench_eps(ecc, ctx, args, rep_xy, uniq, n_win, n_reps)
 
     value = world * args.steps * n / elapsed / 1e6
     if graph is not None:
@@ -351,7 +387,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step": round(ms_step, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -360,7 +396,7 @@ def main():
         "config": {
             "workload": f"e2e hash-downsample(8192-event windows) -> k-means k={K} ({I} iters) on reps -> "
                         f"SAE+FAST arc corners (16384-event slices) -> 15x15 NMS; {W}x{H} sensor; "
-                        f"{n} events/GPU/step (BASELINE configs C2-C4)",
+                        f"{n} events/GPU/step (BASELINE configs C2-C4{', C5 per-GPU share' if n == 3052 * SLICE else ''})",
             "events_per_gpu": n, "reps_per_gpu": n_reps, "width": W, "height": H, "k": K,
             "kmeans_iters": I, "parallelism": f"time-window shards x{world}",
             "launch": "hipGraph replay of the captured step" if graph is not None else "eager launches",
@@ -369,61 +405,184 @@ def main():
             "kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "avg_launch_ms": round(avg_ms, 5), "algorithmic_bytes_per_launch": bytes_per_launch,
+            "algorithmic_bytes": f"SURVEY §8d bytes of the kernel's stage ({dom_stage})",
+            "traffic_source": traffic_src,
             "timing": f"HIP events around every launch in a second, eager, one-stream {args.steps}-step "
                       f"pass ({instrumented / args.steps * 1e3:.3f} ms/step instrumented)",
         },
+        "stages": stages,
         "stages_ms_per_step": {k: round(v / args.steps, 4) for k, v in sorted(kern_ms.items())},
-        "tracker_us_per_slice": None if tracker_us is None else round(tracker_us, 2),
+        "corner_items": detect_stats,
+        "tracker": tracker,
+        "track_merge": track_merge,
         "ingest": ingest,
         "eps": eps_res,
     }
-    if rank == 0 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args, W, H, K, I)
+    if rank == 0 and not dist and not args.no_cpu:
+        base, par = cpu_leg(ecc, args, W, H, K, I, xy_h, t_h, n, c0, ctx,
+                            dict(rep_xy=rep_xy, uniq=uniq, rep=rep, c=d_c, labels=labels, flags=flags, sae=sae,
+                                 nms_out=nms_out[0], nms_cnt=nms_cnt[0], cap=cap, tracker=g_tracker))
+        result["cpu_baseline"] = base
+        result["parity"] = par
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
-def corner_geometry(xy, n, W, H, S=16384, group=32, tile=14):
-    """Counts the corner stage's byte table needs: distinct (slice, pixel) pairs of in-sensor
-    events (= pair entries), (group, tile) items, (group, pixel) image cells."""
-    x = (xy & 0xFFFF).astype(np.int64)
-    y = (xy >> 16).astype(np.int64)
-    inside = (x < W) & (y < H)
-    s = np.arange(n, dtype=np.int64) // S
-    pairs = int(np.unique((s * (W * H) + y * W + x)[inside]).size)
-    slices = (n + S - 1) // S
-    groups = (slices + group - 1) // group
-    tiles = ((W + tile - 1) // tile) * ((H + tile - 1) // tile)
-    return {"pairs": pairs, "slices": slices, "tiles": tiles, "items": groups * tiles, "hw_groups": groups * W * H}
-
-
-def cpu_baseline(args, W, H, K, I):
-    """The oracle (single-thread -O2 C++ restatement of the reference algorithms) on the first
-    `--cpu-events` events of the same stream, on this host's cores."""
-    sys.path.insert(0, str(ROOT / "oracle"))
+def timed_kernels(ctx, run, reps):
+    """(ms per call over `reps` uninstrumented calls, per-kernel average ms from an instrumented
+    pass of the same calls)."""
     import eccpy as ecc
-    import orc
+    run()
+    ctx.sync()
+    tmr = ecc.Timer(ctx.stream)
+    tmr.start()
+    for _ in range(reps):
+        run()
+    call_ms = tmr.stop() / reps
+    ctx.set_timing(True)
+    ctx.timing_reset()
+    for _ in range(reps):
+        run()
+    st = ctx.timing_report()
+    ctx.set_timing(False)
+    return call_ms, {k: v["total_ms"] / v["launches"] for k, v in st.items()}
 
-    m = args.cpu_events
-    xy, t, _ = ecc.gen_events(m, seed=1, width=W, height=H)
-    c0 = np.stack([np.linspace(20, W - 20, K), np.linspace(20, H - 20, K)[::-1]], 1).astype(np.float32).ravel()
+
+def bench_ingest(ecc, ctx, args, xy_h, t_h, p_h, n):
+    """The same events written as EVT 3.0 / EVT 2.0 words, decoded from device-resident words."""
+    ingest = {}
+    for fmt, name in ((ecc.EVT3, "EVT3"), (ecc.EVT2, "EVT2")):
+        words = ecc.evt_encode(fmt, xy_h, t_h, p_h)
+        d_words = ecc.DeviceArray.from_numpy(words, ctx.stream)
+        d_oxy, d_ot = ecc.DeviceArray(n, np.uint32), ecc.DeviceArray(n, np.int64)
+        d_op, d_on = ecc.DeviceArray(n, np.uint8), ecc.DeviceArray(1, np.int64)
+        dec_ms, kern = timed_kernels(ctx, lambda: ctx.evt_decode(fmt, d_words, len(words), d_oxy, d_ot, d_op, n, d_on),
+                                     max(args.steps, 5))
+        assert int(d_on.numpy()[0]) == n and ctx.evt_status() == 0
+        dk = kern.get("evt_decode_kernel", float("nan"))
+        ach = (words.nbytes + 13.0 * n) / (dk * 1e-3) / 1e9  # words in + xy/t/p out
+        ingest[name] = {
+            "words": len(words), "word_bytes": words.itemsize, "events": n,
+            "mevents_s": round(n / (dec_ms * 1e-3) / 1e6, 1), "ms_per_decode": round(dec_ms, 4),
+            "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
+            "roofline": {"kernel": "evt_decode_kernel", "bound": "hbm", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes": f"{words.itemsize} B/word in + 13 B/event out"},
+        }
+        del d_words, d_oxy, d_ot, d_op, d_on
+    return ingest
+
+
+def bench_eps(ecc, ctx, args, rep_xy, uniq, n_win, n_reps):
+    """Per 8192-event downsample window over the step's device-resident representatives:
+    DBSCAN eps 20 / minPts 20 (PCC/pcl_cluster.cpp:113-120) — counts, lists, cluster
+    extraction — and OPTICS eps 10 / min_pts 2 (OPT/test/cluster_event_data.cpp:449) — counts
+    + core distances."""
+    res = {}
+    reps = max(args.steps, 5)
+    tot = n_win * WINDOW
+    e_cnt = ecc.DeviceArray(tot, np.int32)
+    e_core = ecc.DeviceArray(tot, np.float64)
+    for name, eps, mp, core in (("dbscan_eps20_minpts20", 20.0, 20, None),
+                                ("optics_eps10_minpts2", 10.0, 2, e_core)):
+        call_ms, kern = timed_kernels(ctx, lambda: ctx.eps_counts(rep_xy, n_win, WINDOW, uniq, eps, mp, e_cnt, core), reps)
+        ek = kern.get("eps_counts_kernel", float("nan"))
+        per_rep = 8 + (8 if core is not None else 0)  # xy in + count out [+ core distance out]
+        ach = n_reps * per_rep / (ek * 1e-3) / 1e9
+        res[name] = {
+            "reps": n_reps, "windows": n_win, "mreps_s": round(n_reps / (call_ms * 1e-3) / 1e6, 1),
+            "ms_per_call": round(call_ms, 4), "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
+            "roofline": {"kernel": "eps_counts_kernel", "bound": "hbm", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes": f"4 B/rep in + 4 B/rep out{' + 8 B/rep core distance' if core is not None else ''}"},
+        }
+    # the full DBSCAN chain (eps 20 / minPts 20, clusters of 100..25000): counts -> ascending
+    # neighbour lists -> union-find extraction (DBSCAN_simple.h:27-90)
+    ctx.eps_counts(rep_xy, n_win, WINDOW, uniq, 20.0, 20, e_cnt, None)
+    d_off = ecc.DeviceArray(tot + 1, np.int64)
+    ctx.sync()
+    cnt = e_cnt.numpy()
+    u = uniq.numpy()
+    valid = (np.arange(WINDOW)[None, :] < u[:, None]).ravel()
+    nbr_cap = int(cnt[valid].sum()) + 16
+    d_nbr = ecc.DeviceArray(nbr_cap, np.int32)
+    d_lab = ecc.DeviceArray(tot, np.int32)
+    d_nc = ecc.DeviceArray(n_win, np.int32)
+    dup_cap = 1 << 22
+    d_dups = ecc.DeviceArray(2 * dup_cap, np.int64)
+    d_nd = ecc.DeviceArray(1, np.int64)
+
+    def chain():
+        ctx.eps_counts(rep_xy, n_win, WINDOW, uniq, 20.0, 20, e_cnt, None)
+        ctx.eps_lists(rep_xy, n_win, WINDOW, uniq, 20.0, e_cnt, d_off, d_nbr, nbr_cap)
+        ctx.dbscan_extract(n_win, WINDOW, uniq, d_off, d_nbr, 20, 100, 25000, d_lab, d_nc, d_dups, dup_cap, d_nd)
+
+    chain_ms, kern = timed_kernels(ctx, chain, max(3, min(reps, 5)))
+    st = ctx.dbscan_status()
+    nc = d_nc.numpy()
+    res["dbscan_chain_eps20_minpts20"] = {
+        "reps": n_reps, "windows": n_win, "ms_per_call": round(chain_ms, 4),
+        "us_per_window": round(chain_ms * 1e3 / n_win, 3), "mreps_s": round(n_reps / (chain_ms * 1e-3) / 1e6, 1),
+        "neighbour_entries": nbr_cap - 16, "clusters": int(nc.sum()), "status": st,
+        "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
+    }
+    return res
+
+
+def cpu_leg(ecc, args, W, H, K, I, xy, t, n, c0, ctx, g):
+    """CPU baseline + full-size parity.  The oracle (single-thread C++ restatement of the
+    reference algorithms, oracle/oracle.cpp) runs the step's pipeline over exactly the step's
+    events on this host's cores (timed: the CPU baseline); every GPU output of the step is then
+    compared with it (downsample counts + representatives, k-means centroids + labels, corner
+    flags + final SAE, NMS lists, and the tracker over all slices)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import orc
+    from parity import nms_mismatches, tracker_mismatches, windowed_mismatches
+
     t0 = time.perf_counter()
-    rx, _, u, _ = orc.downsample_hash(xy)
-    dense = np.concatenate([rx[w * 8192: w * 8192 + u[w]] for w in range(len(u))])
-    orc.kmeans_run_xy16(dense, c0, I)
-    fl, _ = orc.fast_detect(xy, t, W, H)
-    orc.corner_nms(xy, fl, W, H)
+    o_rx, _, o_u, o_r = orc.downsample_hash(xy)
+    dense = np.concatenate([o_rx[w * WINDOW: w * WINDOW + o_u[w]] for w in range(len(o_u))])
+    o_c, o_lab, _ = orc.kmeans_run_xy16(dense, c0, I)
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H)
+    o_out, o_cnt, _ = orc.corner_nms(xy, o_flags, W, H, cap=g["cap"])
     dt = time.perf_counter() - t0
-    model = ""
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
         model = platform.processor()
-    return {"value": round(m / dt / 1e6, 3), "unit": "Mevents/s", "cores": 1, "kind": "port",
-            "sample": f"first {m} events of the same stream, same pipeline (oracle/oracle.cpp, 1 thread); "
-                      f"{dt:.2f} s; host {model}, nproc={os.cpu_count()}"}
+    base = {"value": round(n / dt / 1e6, 3), "unit": "Mevents/s", "cores": 1, "kind": "port",
+            "sample": f"the step's full batch: {n} events, same pipeline (oracle/oracle.cpp, 1 thread, "
+                      f"downsample + k-means + SAE/arc + NMS); {dt:.2f} s; host {model}, nproc={os.cpu_count()}"}
+
+    par = {"events": n}
+    u, r = g["uniq"].numpy(), g["rep"].numpy()
+    par["downsample_windows_mismatch"] = int(np.count_nonzero(u != o_u) + np.count_nonzero(r != o_r))
+    par["downsample_reps_mismatch"] = windowed_mismatches(g["rep_xy"].numpy(), o_rx, o_u, WINDOW)
+    gc = g["c"].numpy()
+    par["kmeans_centroids_mismatch"] = int(np.count_nonzero(gc.view(np.uint32) != o_c.view(np.uint32)))
+    gl = g["labels"].numpy()
+    g_dense = np.concatenate([gl[w * WINDOW: w * WINDOW + o_u[w]] for w in range(len(o_u))])
+    par["kmeans_labels_mismatch"] = int(np.count_nonzero(g_dense != o_lab))
+    par["corner_flags_mismatch"] = int(np.count_nonzero(g["flags"].numpy() != o_flags))
+    par["corner_flags_set"] = int(o_flags.sum())
+    par["sae_mismatch"] = int(np.count_nonzero(g["sae"].numpy() != o_sae))
+    bad, total = nms_mismatches(g["nms_out"].numpy(), g["nms_cnt"].numpy(), o_out, o_cnt, g["cap"])
+    par["nms_slices_mismatch"] = bad
+    par["nms_corners"] = total
+    if g["tracker"] is not None:
+        t1 = time.perf_counter()
+        otr = orc.OracleTracker(ecc.tracker_cfg())
+        for s in range(len(o_cnt)):
+            otr.update(o_out[s * g["cap"]: s * g["cap"] + o_cnt[s]])
+        trk_s = time.perf_counter() - t1
+        o_tracks, o_groups = otr.tracks(ecc.Track), otr.groups(ecc.Group)[0]
+        par["tracker_mismatch"] = tracker_mismatches(g["tracker"][0], o_tracks, g["tracker"][1], o_groups)
+        par["tracker_tracks"] = len(o_tracks)
+        base["tracker_us_per_slice_cpu"] = round(trk_s * 1e6 / len(o_cnt), 2)
+    par["mismatches"] = int(sum(v for k, v in par.items() if k.endswith("_mismatch")))
+    return base, par
 
 
 if __name__ == "__main__":

@@ -1210,6 +1210,9 @@ sae_max_combine_kernel(const int64_t *__restrict__ images, int n_images, int64_t
 struct CornerState {
     void *evt = nullptr;
     size_t evt_bytes = 0;
+    // diagnostics of the last detection (ecc_fast_detect_stats)
+    const uint32_t *n_over = nullptr;
+    int64_t n_items = 0, n_slices = 0, n_groups = 0;
 };
 
 std::mutex g_state_mu;
@@ -1272,6 +1275,7 @@ int corner_state_reserve(ecc_ctx *ctx, CornerState *st, size_t evt_need) {
             (void)hipFree(st->evt);
             st->evt = nullptr;
             st->evt_bytes = 0;
+            st->n_over = nullptr;
         }
         const size_t want = ecc::align_up(evt_need + evt_need / 8, 1 << 20);
         hipError_t e = hipMalloc(&st->evt, want);
@@ -1399,6 +1403,10 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         return ECC_OK;
     }
     ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
+    st->n_over = gi.n_over;
+    st->n_items = n_items;
+    st->n_slices = g.n_slices;
+    st->n_groups = n_groups;
     {
         ECC_TIMED(ctx, s, "sae_prefix_kernel");
         const int64_t HW = (int64_t)g.W * g.H;
@@ -1480,6 +1488,20 @@ ECC_API int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream) {
                   "read err flag");
     ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
     return f ? ECC_ERR_UNSORTED_TIME : ECC_OK;
+}
+
+ECC_API int ecc_fast_detect_stats(ecc_ctx *ctx, int64_t *out, int32_t n_out, ecc_stream_t stream) {
+    if (!ctx || n_out < 0 || (n_out > 0 && !out)) return ECC_ERR_INVALID;
+    CornerState *st = state_of(ctx);
+    uint32_t over = 0;
+    if (st->n_over) {
+        ECC_CHECK_HIP(ctx, hipMemcpyAsync(&over, st->n_over, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
+                      "read overflow count");
+        ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
+    }
+    const int64_t v[4] = {st->n_items, (int64_t)over, st->n_slices, st->n_groups};
+    for (int i = 0; i < n_out && i < 4; ++i) out[i] = v[i];
+    return ECC_OK;
 }
 
 ECC_API int ecc_sae_scatter(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,

@@ -275,6 +275,17 @@ nms_greedy_kernel(const uint32_t *__restrict__ cand, const int32_t *__restrict__
     }
 }
 
+// Packs per-slice corner lists (slice s at in[s * cap], counts[s] <= cap) densely at
+// out[offsets[s]]: one workgroup per slice.
+__global__ void __launch_bounds__(256)
+corner_pack_kernel(const ecc_corner *__restrict__ in, const int32_t *__restrict__ counts, int cap,
+                   const int64_t *__restrict__ offsets, ecc_corner *__restrict__ out) {
+    const int64_t s = blockIdx.x;
+    const int c = min(max(counts[s], 0), cap);
+    const int64_t o = offsets[s];
+    for (int d = threadIdx.x; d < c; d += 256) out[o + d] = in[s * cap + d];
+}
+
 struct NmsState {
     void *buf = nullptr;
     size_t bytes = 0;
@@ -341,6 +352,26 @@ ECC_API int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corn
                            out_count, ctx->flags + 1);
     }
     ECC_CHECK_LAUNCH(ctx, "nms_kernel");
+    return ECC_OK;
+}
+
+ECC_API int ecc_corner_pack(ecc_ctx *ctx, const ecc_corner *in, const int32_t *counts, int32_t n_slices,
+                            int32_t cap, ecc_corner *out, int64_t *offsets, ecc_stream_t stream) {
+    if (!ctx || n_slices < 0 || cap < 0 || !offsets || (n_slices > 0 && !counts)) return ECC_ERR_INVALID;
+    if (n_slices > 0 && cap > 0 && (!in || !out)) return ECC_ERR_INVALID;
+    hipStream_t s = ecc::as_stream(stream);
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    int rc = ecc::ws_reserve(ctx, ecc::scan_scratch_bytes(n_slices));
+    if (rc) return rc;
+    rc = ecc::exclusive_scan_i32_i64(ctx, counts, n_slices, offsets, reinterpret_cast<int64_t *>(ctx->ws), s);
+    if (rc) return rc;
+    if (n_slices == 0 || cap == 0) return ECC_OK;
+    {
+        ECC_TIMED(ctx, s, "corner_pack_kernel");
+        hipLaunchKernelGGL(corner_pack_kernel, dim3((unsigned)n_slices), dim3(256), 0, s, in, counts, cap,
+                           (const int64_t *)offsets, out);
+    }
+    ECC_CHECK_LAUNCH(ctx, "corner_pack");
     return ECC_OK;
 }
 

@@ -280,8 +280,8 @@ __device__ __forceinline__ void store_track(DevTrack *dst, const DevTrack &t, bo
 __global__ void __launch_bounds__(kNT)
 tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restrict__ groups,
                int *__restrict__ group_labels, TrackerCounters *__restrict__ ctr, TrackerParams p,
-               const ecc_corner *__restrict__ corners, const int32_t *__restrict__ counts, int n_slices,
-               int cap) {
+               const ecc_corner *__restrict__ corners, const int64_t *__restrict__ starts,
+               const int32_t *__restrict__ counts, int n_slices, int cap) {
     __shared__ int2 s_det[kMaxDet + 4];              // P0-P3 detections; P4 group average velocity
     __shared__ uint32_t s_claim[kMaxDet / 32];       // P0-P3 claimed detections (bits)
     __shared__ int s_want[kMaxDet];                  // P2 matching tags; P3-P4 candidate label
@@ -334,12 +334,13 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
         DevTrack *A = cur ? buf1 : buf0;   // active tracks
         DevTrack *Bf = cur ? buf0 : buf1;  // next active list
         int C = counts[s];
-        if (C > cap) C = cap;
+        if (C > cap) { C = cap; err = ECC_ERR_CAPACITY; }  // beyond max_detections: dropped, reported
         if (C < 0) C = 0;
+        const int64_t first = starts ? starts[s] : (int64_t)s * cap;  // slice s = corners[first, first + C)
         // P0: detections
         bool wide = false;  // a coordinate outside int16: this slice scans without the grid
         for (int d = tid; d < C; d += kNT) {
-            const ecc_corner c = corners[(int64_t)s * cap + d];
+            const ecc_corner c = corners[first + d];
             det[d] = make_int2(c.x, c.y);
             want[d] = 0x7fffffff;
             wide |= c.x < -32768 || c.x > 32767 || c.y < -32768 || c.y > 32767;
@@ -967,22 +968,35 @@ ECC_API int ecc_tracker_destroy(ecc_tracker *tr) {
     return ECC_OK;
 }
 
-ECC_API int ecc_tracker_update(ecc_tracker *tr, const ecc_corner *corners, const int32_t *counts,
-                               int32_t n_slices, int32_t cap, ecc_stream_t stream) {
-    if (!tr || n_slices < 0 || cap < 0) return ECC_ERR_INVALID;
-    if (n_slices == 0) return ECC_OK;
-    if (!counts || (cap > 0 && !corners)) return ECC_ERR_INVALID;
+static int tracker_launch(ecc_tracker *tr, const ecc_corner *corners, const int64_t *starts, const int32_t *counts,
+                          int32_t n_slices, int32_t cap, ecc_stream_t stream) {
     ecc_ctx *ctx = tr->ctx;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     {
         ECC_TIMED(ctx, ecc::as_stream(stream), "tracker_kernel");
         hipLaunchKernelGGL(tracker_kernel, dim3(1), dim3(kNT), 0, ecc::as_stream(stream),
                            tr->buf[0], tr->buf[1], tr->max_tracks, tr->groups, tr->group_labels,
-                           tr->ctr, tr->params, corners, counts, n_slices,
+                           tr->ctr, tr->params, corners, starts, counts, n_slices,
                            cap < tr->max_det ? cap : tr->max_det);
     }
     ECC_CHECK_LAUNCH(ctx, "tracker_kernel");
     return ECC_OK;
+}
+
+ECC_API int ecc_tracker_update(ecc_tracker *tr, const ecc_corner *corners, const int32_t *counts,
+                               int32_t n_slices, int32_t cap, ecc_stream_t stream) {
+    if (!tr || n_slices < 0 || cap < 0) return ECC_ERR_INVALID;
+    if (n_slices == 0) return ECC_OK;
+    if (!counts || (cap > 0 && !corners)) return ECC_ERR_INVALID;
+    return tracker_launch(tr, corners, nullptr, counts, n_slices, cap, stream);
+}
+
+ECC_API int ecc_tracker_update_lists(ecc_tracker *tr, const ecc_corner *corners, const int64_t *starts,
+                                     const int32_t *counts, int32_t n_slices, ecc_stream_t stream) {
+    if (!tr || n_slices < 0) return ECC_ERR_INVALID;
+    if (n_slices == 0) return ECC_OK;
+    if (!counts || !starts || !corners) return ECC_ERR_INVALID;
+    return tracker_launch(tr, corners, starts, counts, n_slices, tr->max_det, stream);
 }
 
 #if ECC_TRACKER_PROFILE

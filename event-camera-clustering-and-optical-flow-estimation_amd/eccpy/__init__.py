@@ -146,9 +146,12 @@ _sigs = {
     "ecc_fast_detect_prepare": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P]),
     "ecc_fast_detect_finish": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, P]),
     "ecc_fast_detect_status": (C.c_int, [P, P]),
+    "ecc_fast_detect_stats": (C.c_int, [P, P, i32, P]),
     "ecc_sae_scatter": (C.c_int, [P, P, P, i64, i32, i32, P, P]),
     "ecc_corner_nms": (C.c_int, [P, P, P, i64, i32, i32, i32, i32, i32, P, P, P]),
     "ecc_corner_nms_status": (C.c_int, [P, P]),
+    "ecc_corner_pack": (C.c_int, [P, P, P, i32, i32, P, P, P]),
+    "ecc_tracker_update_lists": (C.c_int, [P, P, P, P, i32, P]),
     "ecc_tracker_cfg_default": (None, [C.POINTER(TrackerCfg)]),
     "ecc_tracker_create": (C.c_int, [P, C.POINTER(TrackerCfg), i32, i32, C.POINTER(P)]),
     "ecc_tracker_destroy": (C.c_int, [P]),
@@ -341,6 +344,11 @@ class Context:
     def fast_detect_status(self) -> int:
         return lib.ecc_fast_detect_status(self.ctx, self.stream)
 
+    def fast_detect_stats(self) -> dict:
+        out = np.zeros(4, np.int64)
+        check(lib.ecc_fast_detect_stats(self.ctx, out.ctypes.data, 4, self.stream), "ecc_fast_detect_stats")
+        return {"items": int(out[0]), "overflow_items": int(out[1]), "slices": int(out[2]), "groups": int(out[3])}
+
     def sae_scatter(self, xy: DeviceArray, t: DeviceArray, n: int, w: int, h: int,
                     sae: DeviceArray):
         check(lib.ecc_sae_scatter(self.ctx, xy.ptr, t.ptr, n, w, h, sae.ptr, self.stream),
@@ -351,6 +359,11 @@ class Context:
                    h: int, box: int, cap: int, out: DeviceArray, counts: DeviceArray):
         check(lib.ecc_corner_nms(self.ctx, xy.ptr, flags.ptr, n, slice_events, w, h, box, cap,
                                  out.ptr, counts.ptr, self.stream), "ecc_corner_nms")
+
+    def corner_pack(self, nms_out, counts, n_slices: int, cap: int, out, offsets):
+        """Dense per-slice corner lists (DeviceArrays or raw device pointers)."""
+        check(lib.ecc_corner_pack(self.ctx, _ptr(nms_out), _ptr(counts), n_slices, cap, _ptr(out), _ptr(offsets),
+                                  self.stream), "ecc_corner_pack")
 
     def corner_nms_status(self) -> int:
         return lib.ecc_corner_nms_status(self.ctx, self.stream)
@@ -411,6 +424,11 @@ class Tracker:
     def update(self, corners: DeviceArray, counts: DeviceArray, n_slices: int, cap: int):
         check(lib.ecc_tracker_update(self.tr, corners.ptr, counts.ptr, n_slices, cap,
                                      self.ctx.stream), "ecc_tracker_update")
+
+    def update_lists(self, corners, starts, counts, n_slices: int):
+        """Slice s = corners[starts[s] .. starts[s] + counts[s]) (device pointers or DeviceArrays)."""
+        check(lib.ecc_tracker_update_lists(self.tr, _ptr(corners), _ptr(starts), _ptr(counts), n_slices,
+                                           self.ctx.stream), "ecc_tracker_update_lists")
 
     def status(self) -> int:
         return lib.ecc_tracker_status(self.tr, self.ctx.stream)

@@ -9,7 +9,11 @@ One process per GPU.  Rank r owns events [r*n, (r+1)*n) of the stream.  The exch
   * SAE hand-off: the shards' local final time surfaces are all-gathered and rank r starts from
     the element-wise max over ranks < r (time is non-decreasing across shards, so max == last
     writer) -> corner flags identical to the single-GPU run; only rank 0 skips the first slice.
-Downsample, detection and NMS are shard-local.  The tracker is sequential (replicas only).
+Downsample, detection and NMS are shard-local.  The tracker is sequential over slices, so the
+shards' per-slice NMS lists are gathered in global slice order (gather_corner_lists: the packed
+lists of every rank, all-gathered, plus each slice's start and count) and ONE tracker on rank 0
+consumes them (the track merge of BASELINE config C5; reference slice path NMS -> tracker,
+FCT/metavision_time_surface_periodic_group_track.cpp:832-850).
 
 The functions here are transport- and compute-agnostic: `comm` wraps torch.distributed (RCCL on
 GPUs, gloo in the CPU tests) and the compute callables are libecc on the GPU (bench.py) or the
@@ -28,6 +32,38 @@ def shard_bounds(n_total: int, world: int, rank: int, align: int = 16384) -> tup
     lo = rank * per
     hi = n_total if rank == world - 1 else lo + per
     return lo, hi
+
+
+def gather_corner_lists(comm, packed, counts):
+    """Track-merge exchange.  packed: this rank's int32 tensor [T_r, 3] of kept corners (x, y,
+    label), slice after slice (ecc_corner_pack); counts: int32 [ns_r] corners per slice.  Ranks
+    hold consecutive time windows, so rank order is global slice order.  Returns, on every rank,
+    (corners [world * T_max, 3] int32, starts int64 [sum ns_r], counts int32 [sum ns_r]): slice s
+    of the global order is corners[starts[s] : starts[s] + counts[s]].  Two all-gathers (sizes,
+    then the lists padded to the largest rank's); a few MB per rank at BASELINE C5."""
+    import torch
+    dev = packed.device
+    world = comm.world
+    meta = torch.tensor([packed.shape[0], counts.shape[0]], dtype=torch.int64, device=dev)
+    metas = torch.zeros(world * 2, dtype=torch.int64, device=dev)
+    comm.allgather_cat(metas, meta)
+    sizes = metas.view(world, 2).cpu().tolist()
+    t_max = max(1, max(t for t, _ in sizes))
+    ns_max = max(1, max(n for _, n in sizes))
+    pk = torch.zeros((t_max, 3), dtype=torch.int32, device=dev)
+    pk[:packed.shape[0]] = packed
+    ct = torch.zeros(ns_max, dtype=torch.int32, device=dev)
+    ct[:counts.shape[0]] = counts
+    all_pk = torch.zeros((world * t_max, 3), dtype=torch.int32, device=dev)
+    all_ct = torch.zeros(world * ns_max, dtype=torch.int32, device=dev)
+    comm.allgather_cat(all_pk.view(-1), pk.view(-1))
+    comm.allgather_cat(all_ct, ct)
+    starts, cnts = [], []
+    for r, (_, ns) in enumerate(sizes):
+        c = all_ct[r * ns_max: r * ns_max + ns].to(torch.int64)
+        starts.append(r * t_max + torch.cumsum(c, 0) - c)
+        cnts.append(all_ct[r * ns_max: r * ns_max + ns])
+    return all_pk, torch.cat(starts), torch.cat(cnts).to(torch.int32)
 
 
 class TorchComm:

@@ -235,6 +235,11 @@ int ecc_fast_detect_finish(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, i
 /* Synchronises `stream` and reports ECC_ERR_UNSORTED_TIME if the last ecc_fast_detect on
  * this context saw decreasing timestamps, else ECC_OK. */
 int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream);
+/* Diagnostics of the last ecc_fast_detect / _finish on this context (synchronises `stream`):
+ * out[0] = (group of 32 slices, 14x14 tile) work items, out[1] = items whose window held more
+ * values than the compact per-pixel lists take (tested by the dense-plane kernel), out[2] =
+ * slices, out[3] = groups.  Writes min(n_out, 4) entries. */
+int ecc_fast_detect_stats(ecc_ctx *ctx, int64_t *out, int32_t n_out, ecc_stream_t stream);
 /* Multi-GPU SAE hand-off: out[q] = max over images[i*hw + q], i < n_images (the shards'
  * local final SAEs of all LOWER ranks give a rank its exact initial SAE; max == last writer
  * because time is non-decreasing across shards). */
@@ -262,6 +267,11 @@ int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corner_flags
 /* Synchronises `stream`; ECC_ERR_CAPACITY if a slice kept more than `cap` corners in the last
  * ecc_corner_nms, ECC_ERR_INVALID if a flagged event lay outside the image (it was skipped). */
 int ecc_corner_nms_status(ecc_ctx *ctx, ecc_stream_t stream);
+/* Dense form of ecc_corner_nms' per-slice lists (multi-GPU corner gather): with
+ * counts[s] <= cap as ecc_corner_nms writes them, offsets[0..n_slices] (DEVICE int64) = the
+ * exclusive scan of counts (offsets[n_slices] = total) and out[offsets[s] + d] = in[s*cap + d]. */
+int ecc_corner_pack(ecc_ctx *ctx, const ecc_corner *in, const int32_t *counts, int32_t n_slices,
+                    int32_t cap, ecc_corner *out, int64_t *offsets, ecc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * 5. Corner tracker (damped predictor-corrector + grouping)
@@ -313,6 +323,11 @@ int ecc_tracker_create(ecc_ctx *ctx, const ecc_tracker_cfg *cfg, int32_t max_tra
 int ecc_tracker_destroy(ecc_tracker *tr);
 int ecc_tracker_update(ecc_tracker *tr, const ecc_corner *corners, const int32_t *counts,
                        int32_t n_slices, int32_t cap, ecc_stream_t stream);
+/* The same over explicit lists: slice s = corners[starts[s] .. starts[s] + counts[s]) (DEVICE
+ * int64 starts, int32 counts), e.g. ecc_corner_pack outputs of several shards gathered in global
+ * slice order (the multi-GPU track merge).  Counts above max_detections: ECC_ERR_CAPACITY. */
+int ecc_tracker_update_lists(ecc_tracker *tr, const ecc_corner *corners, const int64_t *starts,
+                             const int32_t *counts, int32_t n_slices, ecc_stream_t stream);
 /* Host copies of the current state (synchronises stream). */
 int ecc_tracker_get_tracks(ecc_tracker *tr, ecc_track *out, int32_t cap, int32_t *n_out,
                            ecc_stream_t stream);

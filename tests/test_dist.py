@@ -1,7 +1,8 @@
 """Multi-process (world_size 2, gloo on CPU) tests of the sharded path (eccpy/dist.py): sharded
 k-means (an all-reduce of the integer partial sums every pass, and ONE all-reduce of per-pixel
-count images) and the exact SAE hand-off reproduce the single-process results.  Compute backend
-here: the oracle (CPU)."""
+count images), the exact SAE hand-off and the track merge (shard NMS lists gathered in global
+slice order -> one tracker) reproduce the single-process results.  Compute backend here: the
+oracle (CPU)."""
 import os
 import socket
 
@@ -31,8 +32,9 @@ def _worker(rank, world, port, q):
         import eccpy as ecc
         from eccpy import dist as edist
         import orc
+        from parity import track_key
         comm = edist.TorchComm(tdist)
-        W, H, n_total, K = 346, 260, 16384 * 6, 8
+        W, H, n_total, K = 346, 260, 16384 * 12, 8
         xy, t, _ = ecc.gen_events(n_total, seed=4)
         lo, hi = edist.shard_bounds(n_total, world, rank)
         sx, st = xy[lo:hi], t[lo:hi]
@@ -77,7 +79,20 @@ def _worker(rank, world, port, q):
         base = edist.sae_base_for_rank(allimg.view(world, -1).numpy(), rank,
                                        lambda imgs, r: imgs[:r].max(0) if r > 0 else np.zeros(W * H, np.int64))
         flags, _ = orc.fast_detect(sx, st, W, H, first_detect=1 if rank == 0 else 0, sae=base)
-        q.put((rank, state["c"], flags, pts, c_counts))
+        # ---- track merge: shard-local NMS lists gathered in global slice order -> ONE tracker
+        cap = 4096
+        o_out, o_cnt, _ = orc.corner_nms(sx, flags, W, H, cap=cap)
+        packed = np.concatenate([o_out[s * cap: s * cap + o_cnt[s]] for s in range(len(o_cnt))])
+        pk = torch.from_numpy(packed.view(np.int32).reshape(-1, 3).copy())
+        all_pk, starts, cnts = edist.gather_corner_lists(comm, pk, torch.from_numpy(o_cnt.astype(np.int32)))
+        tracks = None
+        if rank == 0:
+            allc = all_pk.numpy().reshape(-1).view(orc.CORNER_DTYPE)
+            otr = orc.OracleTracker(ecc.tracker_cfg())
+            for s0, c in zip(starts.tolist(), cnts.tolist()):
+                otr.update(allc[s0:s0 + c])
+            tracks = [track_key(tr) for tr in otr.tracks(ecc.Track)]
+        q.put((rank, state["c"], flags, pts, c_counts, tracks))
     finally:
         tdist.destroy_process_group()
 
@@ -89,11 +104,11 @@ def test_two_rank_sharded_pipeline_matches_single_process(orc, ecc):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (c, f, pts, cc)) for r, c, f, pts, cc in (q.get(timeout=240) for _ in range(world)))
+    res = dict((r, (c, f, pts, cc, trk)) for r, c, f, pts, cc, trk in (q.get(timeout=240) for _ in range(world)))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    W, H, n_total, K = 346, 260, 16384 * 6, 8
+    W, H, n_total, K = 346, 260, 16384 * 12, 8
     xy, t, _ = ecc.gen_events(n_total, seed=4)
     # k-means over the union of both shards' representatives == each rank's sharded result
     allpts = np.concatenate([res[0][2], res[1][2]])
@@ -106,3 +121,11 @@ def test_two_rank_sharded_pipeline_matches_single_process(orc, ecc):
     o_flags, _ = orc.fast_detect(xy, t, W, H)
     assert (np.concatenate([res[0][1], res[1][1]]) == o_flags).all()
     assert o_flags.sum() > 0
+    # track merge: rank 0's tracker over the gathered shard lists == one tracker over the stream
+    from parity import track_key
+    o_out, o_cnt, _ = orc.corner_nms(xy, o_flags, W, H)
+    otr = orc.OracleTracker(ecc.tracker_cfg())
+    for s in range(len(o_cnt)):
+        otr.update(o_out[s * 4096: s * 4096 + o_cnt[s]])
+    ref = [track_key(tr) for tr in otr.tracks(ecc.Track)]
+    assert len(ref) > 0 and res[0][4] == ref

@@ -62,11 +62,13 @@ def test_downsample_matches_oracle(ecc, orc, gpu, n, window, seed, wh):
         assert (gi[sl] == o_idx[sl]).all(), f"window {w} representative indices differ"
 
 
-def test_downsample_full_size_properties(ecc, gpu):
-    """10 M events (BASELINE config C2) — size-independent properties: every representative is
-    the first event of its bucket, buckets are distinct, counts agree with the outputs."""
+@pytest.mark.parametrize("wh", [(1280, 720), (346, 260)])
+def test_downsample_full_size_properties(ecc, gpu, wh):
+    """10 M events (BASELINE config C2, both sensors) — size-independent properties: every
+    representative is the first event of its bucket, buckets are distinct, counts agree with
+    the outputs."""
     n = 10_000_000
-    xy, _, _ = ecc.gen_events(n, seed=11, width=1280, height=720)
+    xy, _, _ = ecc.gen_events(n, seed=11, width=wh[0], height=wh[1])
     d_xy = dev(ecc, xy)
     rep_xy, rep_idx, uniq, rep, nw = gpu.downsample_hash(d_xy, n)
     gpu.sync()
@@ -272,6 +274,28 @@ def test_fast_detect_stream_continuation(ecc, orc, gpu):
     f2, s2 = _fast_gpu(ecc, gpu, xy[cut:], t[cut:], W, H, first_detect=0, sae0=s1)
     assert (np.concatenate([f1, f2]) == o_flags).all()
     assert (s2 == o_sae).all()
+
+
+def test_fast_detect_dense_overflow_path(ecc, orc, gpu):
+    """>= 3 groups of 32 slices where whole slices land in a 30x30-pixel patch: every window of
+    the patch holds more values than the compact per-pixel lists take, so those items run on the
+    dense-plane kernel (asserted through ecc_fast_detect_stats) — flags and SAE still bit-exact."""
+    W, H = 346, 260
+    rng = np.random.default_rng(5)
+    n_dense = 16384 * 48
+    xd = rng.integers(150, 180, n_dense)
+    yd = rng.integers(100, 130, n_dense)
+    td = np.cumsum(rng.integers(0, 3, n_dense)).astype(np.int64)
+    xy2, t2, _ = ecc.gen_events(16384 * 50 + 333, seed=17, width=W, height=H)
+    xy = np.concatenate([ecc.pack_xy(xd, yd), xy2])
+    t = np.concatenate([td, t2 + td[-1] + 1])
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H)
+    g_flags, g_sae = _fast_gpu(ecc, gpu, xy, t, W, H)
+    st = gpu.fast_detect_stats()
+    assert st["groups"] >= 3 and st["overflow_items"] > 0, st
+    assert o_flags[:n_dense].sum() > 0 and o_flags[n_dense:].sum() > 0
+    assert (g_flags == o_flags).all(), f"{(g_flags != o_flags).sum()} corner labels differ"
+    assert (g_sae == o_sae).all()
 
 
 def test_fast_detect_rejects_decreasing_time(ecc, gpu):
@@ -578,6 +602,46 @@ def test_tracker_dense_conflicts_match_oracle(ecc, orc, gpu, seed, per_slice, n_
     assert gtr.status() == 0
     n_tr, n_gr = _compare_trackers(ecc, gtr, otr)
     assert n_tr > 0 and (n_gr > 0) == (cfg.group_radius >= 0)
+
+
+def test_corner_pack_and_tracker_lists_match_strided(ecc, orc, gpu):
+    """ecc_corner_pack == the per-slice lists packed on the host, and the tracker over explicit
+    lists (two 'shards' packed separately, at distinct bases with a gap, as the multi-GPU merge
+    gathers them) == the tracker over the cap-strided NMS output == the oracle."""
+    W, H = 346, 260
+    n = 16384 * 36
+    xy, t, _ = ecc.gen_events(n, seed=23, width=W, height=H)
+    o_flags, _ = orc.fast_detect(xy, t, W, H)
+    ns, cap = n // 16384, 4096
+    o_out, o_cnt, _ = orc.corner_nms(xy, o_flags, W, H, cap=cap)
+    d_out, d_cnt = dev(ecc, o_out), dev(ecc, o_cnt)
+    half = ns // 2
+    packed = ecc.DeviceArray(ns * cap + 1000, ecc.CORNER_DTYPE)
+    offs = ecc.DeviceArray(ns + 2, np.int64)
+    # shard A: slices [0, half) at element 0; shard B: slices [half, ns) at element base_b
+    base_b = int(o_cnt[:half].sum()) + 1000
+    gpu.corner_pack(d_out, d_cnt, half, cap, packed, offs)
+    ecc.check(ecc.lib.ecc_corner_pack(gpu.ctx, d_out.ptr + half * cap * 12, d_cnt.ptr + half * 4, ns - half, cap,
+                                      packed.ptr + base_b * 12, offs.ptr + (half + 1) * 8, gpu.stream))
+    gpu.sync()
+    off = offs.numpy()
+    assert off[half] == o_cnt[:half].sum() and off[ns + 1] == o_cnt[half:].sum()
+    starts = np.concatenate([off[:half], base_b + off[half + 1: ns + 1]]).astype(np.int64)
+    host_pk = packed.numpy()
+    for s in range(ns):
+        assert np.array_equal(host_pk[starts[s]: starts[s] + o_cnt[s]], o_out[s * cap: s * cap + o_cnt[s]])
+    g1 = ecc.Tracker(gpu)
+    g1.update(d_out, d_cnt, ns, cap)
+    g2 = ecc.Tracker(gpu)
+    g2.update_lists(packed, dev(ecc, starts), d_cnt, ns)
+    otr = orc.OracleTracker(ecc.tracker_cfg())
+    for s in range(ns):
+        otr.update(o_out[s * cap: s * cap + o_cnt[s]])
+    ref = [_track_key(tr) for tr in otr.tracks(ecc.Track)]
+    assert len(ref) > 0
+    assert [_track_key(tr) for tr in g1.tracks()] == ref
+    assert [_track_key(tr) for tr in g2.tracks()] == ref
+    assert g1.status() == 0 and g2.status() == 0
 
 
 def test_tracker_capacity_flag(ecc, gpu):
