@@ -66,11 +66,15 @@ def parse():
     ap.add_argument("--no-tracker", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the RAW (EVT 3.0 / 2.0) decode measurement")
     ap.add_argument("--no-eps", action="store_true", help="skip the eps-neighbourhood (DBSCAN / OPTICS) measurement")
+    ap.add_argument("--no-c3", action="store_true", help="skip the BASELINE C3 k-means (k=16, 50 M points) measurement")
     ap.add_argument("--serial", action="store_true",
                     help="one stream for the whole step (isolated per-kernel times for profiling)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the single-GPU step as a captured HIP graph (measured equal to eager)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for rehearsal")
+    ap.add_argument("--dist-parity", action="store_true",
+                    help="sharded runs: every rank recomputes the whole stream on the oracle and compares its "
+                         "shard's outputs, the global centroids and (rank 0) the merged tracker (rehearsal sizes)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on device 0 (with --dist-backend gloo)")
     a = ap.parse_args()
@@ -164,8 +168,8 @@ def main():
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
                                           uniq.ptr, rep.ptr, ks), "downsample")
         ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, ks))
-        ecc.check(lib.ecc_kmeans_run_xy16(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, ecc.C.byref(kcfg), d_c.ptr,
-                                          labels.ptr, None, ks), "kmeans")
+        ecc.check(lib.ecc_kmeans_run_xy16_frame(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, W, H, ecc.C.byref(kcfg),
+                                                d_c.ptr, labels.ptr, None, ks), "kmeans")
         ecc.check(lib.ecc_event_record(ev_join, ks))
         ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
         ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
@@ -336,6 +340,7 @@ def main():
 
     # ---- C5 track merge: shard NMS lists gathered in global slice order -> ONE tracker (rank 0) ----
     track_merge = None
+    merged_tracks = None
     if dist and not args.no_tracker:
         from eccpy import dist as edist
         comm = edist.TorchComm(dist)
@@ -364,8 +369,14 @@ def main():
                            "pack_gather_ms": round(gather_ms, 3), "tracker_ms": round(merge_ms, 3),
                            "us_per_slice": round(merge_ms * 1e3 / int(starts.numel()), 2),
                            "tracks_end": len(tr.tracks())}
+            merged_tracks = (tr.tracks(), tr.groups()[0])
             tr.close()
         dist.barrier()
+    dist_parity = None
+    if dist and args.dist_parity:
+        dist_parity = shard_parity(ecc, args, dist, torch, rank, world, local, W, H, I, c0,
+                                   dict(flags=flags, sae=sae, c=d_c, nms_out=nms_out[0], nms_cnt=nms_cnt[0], cap=cap,
+                                        tracker=merged_tracks))
 
     # ---- RAW ingest, reported beside the headline ------------------------
     ingest = None
@@ -376,6 +387,11 @@ def main():
     eps_res = None
     if not args.no_eps and rank == 0:
         eps_res = bench_eps(ecc, ctx, args, rep_xy, uniq, n_win, n_reps)
+
+    # ---- BASELINE C3: k-means k=16 on 50 M points (the step's representatives tiled) -------------
+    c3_res = None
+    if not args.no_c3 and rank == 0:
+        c3_res = bench_c3(ecc, ctx, args, rep_xy, uniq, c0, K)
 
     value = world * args.steps * n / elapsed / 1e6
     if graph is not None:
@@ -415,8 +431,10 @@ def main():
         "corner_items": detect_stats,
         "tracker": tracker,
         "track_merge": track_merge,
+        "dist_parity": dist_parity,
         "ingest": ingest,
         "eps": eps_res,
+        "kmeans_c3": c3_res,
     }
     if rank == 0 and not dist and not args.no_cpu:
         base, par = cpu_leg(ecc, args, W, H, K, I, xy_h, t_h, n, c0, ctx,
@@ -475,6 +493,53 @@ def bench_ingest(ecc, ctx, args, xy_h, t_h, p_h, n):
     return ingest
 
 
+def bench_c3(ecc, ctx, args, rep_xy, uniq, c0, K, n_pts=50_000_000):
+    """BASELINE C3: k-means k=16 on 50 M points (this step's C2-style representatives tiled to
+    50 M), 10 Lloyd passes + final labels, three ways: packed-u16 points through the per-pixel
+    count path, and float points through the vector and the matrix-core assignment engines.
+    Roofline per SURVEY §8d: 8 B/point/iteration (float2 read) + 1 B/point (labels)."""
+    u = uniq.numpy()
+    rx = rep_xy.numpy()
+    dense = np.concatenate([rx[w * WINDOW: w * WINDOW + u[w]] for w in range(len(u))])
+    pts = np.resize(dense, n_pts)
+    x, y = ecc.unpack_xy(pts)
+    f = np.empty(2 * n_pts, np.float32)
+    f[0::2], f[1::2] = x, y
+    d_pts, d_f = ecc.DeviceArray.from_numpy(pts, ctx.stream), ecc.DeviceArray.from_numpy(f, ctx.stream)
+    del f
+    d_c0 = ecc.DeviceArray.from_numpy(c0, ctx.stream)
+    d_c = ecc.DeviceArray(2 * K, np.float32)
+    d_lab = ecc.DeviceArray(n_pts, np.uint8)
+    I = 10
+    cfg = ecc.kmeans_cfg(k=K, max_iters=I, tol=-1.0)
+    lib = ecc.lib
+    alg = (8.0 * I + 1.0) * n_pts
+    out = {"points": n_pts, "k": K, "iters": I, "algorithmic_bytes": alg,
+           "algorithmic": "8 B/point/iteration (float2) + 1 B/point labels (SURVEY 8d)"}
+    results = {}
+    for name, run in (
+            ("xy16_count_image", lambda: ctx.kmeans_xy16_frame(d_pts, 1, n_pts, None, 346, 260, d_c, cfg, d_lab)),
+            ("f32_vector", lambda: ctx.kmeans_f32_engine(d_f, n_pts, d_c, cfg, 1, d_lab)),
+            ("f32_mfma", lambda: ctx.kmeans_f32_engine(d_f, n_pts, d_c, cfg, 2, d_lab))):
+        def full():
+            ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, ctx.stream))
+            run()
+        ms, kern = timed_kernels(ctx, full, 3)
+        cen = d_c.numpy().copy()
+        ach = alg / (ms * 1e-3) / 1e9
+        results[name] = cen
+        out[name] = {"ms": round(ms, 3), "mpoints_s": round(n_pts / (ms * 1e-3) / 1e6, 1),
+                     "achieved_gbs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())}}
+    # the three forms agree bit for bit (integer-valued points: exact fp64 / integer sums)
+    out["centroids_agree"] = bool(all(np.array_equal(results[a].view(np.uint32), results["f32_vector"].view(np.uint32))
+                                      for a in results))
+    f32 = {k: out[k]["ms"] for k in ("f32_vector", "f32_mfma")}
+    out["winner_f32"] = min(f32, key=f32.get)
+    out["winner"] = min(("xy16_count_image", "f32_vector", "f32_mfma"), key=lambda k: out[k]["ms"])
+    return out
+
+
 def bench_eps(ecc, ctx, args, rep_xy, uniq, n_win, n_reps):
     """Per 8192-event downsample window over the step's device-resident representatives:
     DBSCAN eps 20 / minPts 20 (PCC/pcl_cluster.cpp:113-120) — counts, lists, cluster
@@ -529,6 +594,44 @@ def bench_eps(ecc, ctx, args, rep_xy, uniq, n_win, n_reps):
         "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
     }
     return res
+
+
+def shard_parity(ecc, args, dist, torch, rank, world, local, W, H, I, c0, g):
+    """Sharded-run correctness (rehearsal sizes): every rank recomputes the whole stream of all
+    ranks on the oracle and compares its shard's corner flags, final SAE (= the single-run SAE after
+    its shard) and NMS lists, the global k-means centroids, and on rank 0 the merged tracker with
+    the single-run tracker; mismatches are summed over ranks."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import orc
+    from parity import nms_mismatches, tracker_mismatches
+    n = args.events
+    xy, t, _ = ecc.gen_events(world * n, seed=1, width=W, height=H)
+    o_rx, _, o_u, _ = orc.downsample_hash(xy)
+    dense = np.concatenate([o_rx[w * WINDOW: w * WINDOW + o_u[w]] for w in range(len(o_u))])
+    o_c, _, _ = orc.kmeans_run_xy16(dense, c0, I)
+    o_flags_r, o_sae_r = orc.fast_detect(xy[:(rank + 1) * n], t[:(rank + 1) * n], W, H)
+    lo = rank * n
+    cap = g["cap"]
+    o_out, o_cnt, _ = orc.corner_nms(xy[lo:lo + n], o_flags_r[lo:], W, H, cap=cap)
+    bad = {"flags": int(np.count_nonzero(g["flags"].numpy() != o_flags_r[lo:])),
+           "sae": int(np.count_nonzero(g["sae"].numpy() != o_sae_r)),
+           "centroids": int(np.count_nonzero(g["c"].numpy().view(np.uint32) != o_c.view(np.uint32))),
+           "nms_slices": nms_mismatches(g["nms_out"].numpy(), g["nms_cnt"].numpy(), o_out, o_cnt, cap)[0],
+           "tracker": 0}
+    if rank == 0 and g["tracker"] is not None:
+        f_all, _ = orc.fast_detect(xy, t, W, H)
+        a_out, a_cnt, _ = orc.corner_nms(xy, f_all, W, H, cap=cap)
+        otr = orc.OracleTracker(ecc.tracker_cfg())
+        for s in range(len(a_cnt)):
+            otr.update(a_out[s * cap: s * cap + a_cnt[s]])
+        bad["tracker"] = tracker_mismatches(g["tracker"][0], otr.tracks(ecc.Track), g["tracker"][1],
+                                            otr.groups(ecc.Group)[0])
+    vec = torch.tensor([bad[k] for k in sorted(bad)], dtype=torch.int64, device=f"cuda:{local}")
+    dist.all_reduce(vec)
+    tot = dict(zip(sorted(bad), vec.cpu().tolist()))
+    tot["mismatches"] = int(sum(tot.values()))
+    tot["events_total"] = world * n
+    return tot
 
 
 def cpu_leg(ecc, args, W, H, K, I, xy, t, n, c0, ctx, g):

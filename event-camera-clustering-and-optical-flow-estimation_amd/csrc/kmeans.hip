@@ -231,8 +231,10 @@ template <int K, bool kAccumulate, bool kImg>
 __global__ void __launch_bounds__(kThreads)
 kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__restrict__ cent, int k, float thr,
                    unsigned long long *acc, int n_copies, const KmState *st, uint8_t *__restrict__ labels,
-                   const uint8_t *__restrict__ img) {
+                   const uint8_t *__restrict__ img, const uint32_t *__restrict__ img_wh) {
     if (kAccumulate && st->done) return;
+    // the label image covers [0, img_w) x [0, img_h) (the counted frame; <= kImgSide^2)
+    const uint32_t img_w = kImg ? img_wh[0] : 0u, img_h = kImg ? img_wh[1] : 0u;
     __shared__ unsigned long long slot[kWaves][K];
     __shared__ unsigned long long w_acc[3][K];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -298,7 +300,7 @@ kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__re
                     uint32_t l;
                     if (j + e >= cnt) l = 255u;
                     else if constexpr (kImg) {
-                        if (__builtin_expect(x < kImgSide && y < kImgSide, 1)) l = img[y * kImgSide + x];
+                        if (__builtin_expect(x < img_w && y < img_h, 1)) l = img[y * kImgSide + x];
                         else l = assign_lds<K>((float)x, (float)y, s_cx, s_cy, thr);
                     } else {
                         l = assign_fast<K>((float)x, (float)y, cx, cy, thr);
@@ -390,6 +392,156 @@ kmeans_f32_kernel(const float *__restrict__ xy, int64_t n, const float *__restri
         __syncthreads();
         if (tid < 3 * k && a_s[tid] != 0.0) atomicAdd(&acc[tid], a_s[tid]);
     }
+}
+
+// ---- float points, k <= 32 (BASELINE config C3): two assignment engines, one accumulation ---------
+// Vector engine: assign_fast<K> with the centres in scalar registers (exact, ~9 VALU per centre).
+// Matrix engine: the distance part on the matrix cores.  v_mfma_f32_4x4x1f32 runs 16 blocks of
+// 4x4x1; with block b = lanes 4b..4b+3, A_b[i] = -2 cx_{4g+i} (lane 4b+i) and B_b[j] = px of
+// lane 4b+j, D_b[i][j] (lane 4b+j, register i) = C + A_b[i] B_b[j]: so two MFMAs per group g of
+// four centres give every lane s_i = |c_i|^2 - 2 c_i.p for ITS OWN point (an fma chain, one
+// rounding per step).  The argmin over s equals the argmin over d^2 = s + |p|^2 up to rounding:
+// with E bounding the error of every s (E = 2^-21 (max|c|^2 + 2 max|cx| |px| + 2 max|cy| |py|),
+// >= 4x the worst case of the three roundings), a gap between the best and second-best s above
+// 2E + 2^-19 (|s_best| + |p|^2 + E) proves the best index is the unique d^2 minimum with no
+// earlier centre inside assign_fast's square-root tie band; the winner's exact d^2 then decides
+// the threshold.  Any closer call (and NaN input) takes the exact vector path.
+// Accumulation (both engines): per wave LDS slots, u32 count and fp64 sums (ds_add_f64: exact for
+// integer-valued coordinates, 1e-16 relative otherwise); per workgroup one fp64 global atomic per
+// (cluster, field) into one of n_copies replicas that the update kernel sums.
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
+
+template <int K>
+__device__ __forceinline__ uint32_t assign_mfma(float px, float py, const float (&ax)[K / 4], const float (&ay)[K / 4],
+                                                const float (&c2)[K], float emul_c2, float emul_x, float emul_y,
+                                                const float2 *__restrict__ s_c, const float (&cx)[K],
+                                                const float (&cy)[K], float thr) {
+    floatx4_t d[K / 4];
+#pragma unroll
+    for (int g = 0; g < K / 4; ++g) {
+        d[g] = floatx4_t{c2[4 * g], c2[4 * g + 1], c2[4 * g + 2], c2[4 * g + 3]};
+        d[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(ax[g], px, d[g], 0, 0, 0);
+        d[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(ay[g], py, d[g], 0, 0, 0);
+    }
+    float b = __builtin_inff(), b2 = __builtin_inff();
+    int bi = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const float v = d[i / 4][i % 4];
+        const bool lt = v < b;
+        b2 = lt ? b : fminf(b2, v);
+        bi = lt ? i : bi;
+        b = lt ? v : b;
+    }
+    const float E = 0x1p-21f * (emul_c2 + 2.0f * (emul_x * fabsf(px) + emul_y * fabsf(py)));
+    const float P = px * px + py * py;
+    const float margin = 2.0f * E + 0x1p-19f * (fabsf(b) + P + E);
+    if (__builtin_expect(!(b2 - b > margin), 0)) return assign_fast<K>(px, py, cx, cy, thr);  // close call / NaN
+    const float2 c = s_c[bi];
+    const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
+    return ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy))) < thr ? (uint32_t)bi : 255u;
+}
+
+constexpr int kF32Unroll = 4;  // 64-point blocks per wave per trip (loads in flight together)
+
+template <int K, bool kMfma, bool kAccumulate>
+__global__ void __launch_bounds__(kThreads)
+kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__restrict__ cent, int k, float thr,
+                       double *__restrict__ acc, int n_copies, const KmState *__restrict__ st,
+                       uint8_t *__restrict__ labels) {
+    if (kAccumulate && st->done) return;
+    __shared__ uint32_t s_n[kWaves][K];
+    __shared__ double s_sx[kWaves][K], s_sy[kWaves][K];
+    __shared__ float2 s_c[K];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    float cx[K], cy[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
+        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+    }
+    // matrix-engine operands: A rows (lane & 3 = row i of every 4x4 block), |c|^2 per register
+    float ax[K / 4], ay[K / 4], c2[K];
+    float em_c2 = 0.f, em_x = 0.f, em_y = 0.f;
+    if constexpr (kMfma) {
+#pragma unroll
+        for (int g = 0; g < K / 4; ++g) {
+            const int i = 4 * g + (lane & 3);
+            const float vx = i < k ? cent[2 * i] : 0.f, vy = i < k ? cent[2 * i + 1] : 0.f;
+            ax[g] = -2.0f * vx;
+            ay[g] = -2.0f * vy;
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            c2[i] = i < k ? __fadd_rn(__fmul_rn(cx[i], cx[i]), __fmul_rn(cy[i], cy[i])) : __builtin_inff();
+            if (i < k) {
+                em_c2 = fmaxf(em_c2, c2[i]);
+                em_x = fmaxf(em_x, fabsf(cx[i]));
+                em_y = fmaxf(em_y, fabsf(cy[i]));
+            }
+        }
+    }
+    if (tid < K) s_c[tid] = make_float2(tid < k ? cent[2 * tid] : 1e30f, tid < k ? cent[2 * tid + 1] : 1e30f);
+    if (kAccumulate && lane < K) {
+        s_n[wave][lane] = 0u;
+        s_sx[wave][lane] = 0.0;
+        s_sy[wave][lane] = 0.0;
+    }
+    __syncthreads();
+    const int64_t nblk = (n + 63) / 64;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    for (int64_t b0 = (int64_t)blockIdx.x * kWaves + wave; b0 < nblk; b0 += stride * kF32Unroll) {
+        float2 q[kF32Unroll];
+#pragma unroll
+        for (int u = 0; u < kF32Unroll; ++u) {  // clamped, unconditional: all loads in flight at once
+            const int64_t p = (b0 + u * stride) * 64 + lane;
+            q[u] = xy[p < n ? p : n - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < kF32Unroll; ++u) {
+            const int64_t blk = b0 + u * stride;
+            if (blk >= nblk) break;  // wave-uniform
+            const int64_t p = blk * 64 + lane;
+            uint32_t lab;
+            if constexpr (kMfma) lab = assign_mfma<K>(q[u].x, q[u].y, ax, ay, c2, em_c2, em_x, em_y, s_c, cx, cy, thr);
+            else lab = assign_fast<K>(q[u].x, q[u].y, cx, cy, thr);
+            if (p >= n) lab = 255u;
+            if (labels && p < n) labels[p] = (uint8_t)lab;
+            if (kAccumulate && lab < (uint32_t)K) {
+                atomicAdd(&s_n[wave][lab], 1u);
+                atomicAdd(&s_sx[wave][lab], (double)q[u].x);
+                atomicAdd(&s_sy[wave][lab], (double)q[u].y);
+            }
+        }
+    }
+    if (!kAccumulate) return;
+    __syncthreads();
+    if (tid < 3 * k) {
+        const int f = tid / k, c = tid - f * k;
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) v += f == 0 ? (double)s_n[w][c] : (f == 1 ? s_sx[w][c] : s_sy[w][c]);
+        if (v != 0.0) atomicAdd(&acc[(int)(blockIdx.x % n_copies) * kAccStride + 3 * c + f], v);
+    }
+}
+
+template <bool kAccumulate>
+bool launch_f32_fast(int k, int method, dim3 grid, hipStream_t s, const float *xy, int64_t n, const float *cent,
+                     float thr, double *acc, int n_copies, const KmState *st, uint8_t *labels) {
+    if (k > kFastMaxK) return false;
+    const float2 *p = reinterpret_cast<const float2 *>(xy);
+#define ECC_F32_LAUNCH(KK, MF)                                                                               \
+    hipLaunchKernelGGL((kmeans_f32_fast_kernel<KK, MF, kAccumulate>), grid, dim3(kThreads), 0, s, p, n, cent, k, \
+                       thr, acc, n_copies, st, labels)
+    if (method == 2) {
+        if (k <= 16) ECC_F32_LAUNCH(16, true);
+        else ECC_F32_LAUNCH(32, true);
+    } else {
+        if (k <= 16) ECC_F32_LAUNCH(16, false);
+        else ECC_F32_LAUNCH(32, false);
+    }
+#undef ECC_F32_LAUNCH
+    return true;
 }
 
 // Centroid update, one wave: c = (float)(sum / n) (fp64), shift = max |new - old|.
@@ -508,6 +660,13 @@ __device__ __forceinline__ void reduce_extent(const uint32_t *__restrict__ ext, 
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { w = max(w, s_red[2 * i]); h = max(h, s_red[2 * i + 1]); }
 }
 
+// 1-D grid, XCD-aware: workgroup b runs on XCD b % 8; the kCountSlots chunk workgroups of one
+// part (point range) share b % 8 and are dispatched back to back, so the second and third reads of
+// the part's points hit that XCD's L2 instead of HBM.
+constexpr int kCountSlots = 4;
+
+__host__ __device__ inline int count_grid(int parts) { return 8 * ((parts + 7) / 8) * kCountSlots; }
+
 __global__ void __launch_bounds__(kHistThreads)
 kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *__restrict__ ext, int n_ext,
                     int parts, uint32_t *__restrict__ partial, uint32_t *__restrict__ wh,
@@ -515,15 +674,17 @@ kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *
                     uint32_t fixed_h, int32_t *__restrict__ err) {
     extern __shared__ uint32_t hist[];  // [kHistChunk]
     __shared__ uint32_t s_red[2 * kHistThreads / 64];
-    const int m = blockIdx.y, tid = threadIdx.x;
-    // fixed frame (multi-GPU count images, ecc_kmeans_counts_xy16): points outside it are an
-    // error; otherwise the bounding box of the points inside the kImgSide^2 image
+    const int xcd = (int)(blockIdx.x % 8), i8 = (int)(blockIdx.x / 8);
+    const int m = (i8 / kCountSlots) * 8 + xcd, slot = i8 % kCountSlots, tid = threadIdx.x;
+    // frame: fixed_w > 0 = the caller's frame; points outside it are an error (err != null: the
+    // multi-GPU count images) or go to the outside list; otherwise the bounding box of the points
+    // inside the kImgSide^2 image
     const bool fixed = fixed_w > 0;
     uint32_t w = fixed_w, h = fixed_h;
     if (!fixed) reduce_extent(ext, n_ext, s_red, w, h);
     const uint32_t lim_x = fixed ? w : kImgSide, lim_y = fixed ? h : kImgSide;
     const int64_t cells = (int64_t)w * h;
-    if (blockIdx.x == 0 && m == 0 && tid == 0) {
+    if (blockIdx.x == 0 && tid == 0) {
         wh[0] = w;
         wh[1] = h;
     }
@@ -531,7 +692,7 @@ kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *
     if (m >= parts) return;
     const int64_t s0 = segs.n_segs * m / parts, s1 = segs.n_segs * (m + 1) / parts;
     const int64_t n_chunks = (cells + kHistChunk - 1) / kHistChunk;
-    for (int64_t c = blockIdx.x; c < (n_chunks > 0 ? n_chunks : 1); c += gridDim.x) {
+    for (int64_t c = slot; c < (n_chunks > 0 ? n_chunks : 1); c += kCountSlots) {
         const int64_t lo = c * kHistChunk;
         const int n_loc = (int)((cells - lo) < kHistChunk ? (cells - lo) : kHistChunk);
         for (int i = tid; i < kHistChunk; i += kHistThreads) hist[i] = 0u;
@@ -553,7 +714,7 @@ kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *
                         const int64_t idx = (int64_t)y * w + x - lo;
                         if (idx >= 0 && idx < n_loc) atomicAdd(&hist[idx], 1u);
                     } else if (c == 0) {
-                        if (fixed) *err = 1;
+                        if (err) *err = 1;
                         else outside[atomicAdd(n_outside, 1u)] = v[u];
                     }
                 }
@@ -756,21 +917,21 @@ void launch_step(dim3 grid, hipStream_t s, const StepArgs &a, const uint32_t *ex
 template <bool kAccumulate>
 bool launch_fast(int k, dim3 grid, hipStream_t s, const uint32_t *xy, const Segs &segs, const float *cent,
                  float thr, unsigned long long *acc, int n_copies, const KmState *st, uint8_t *labels,
-                 const uint8_t *img = nullptr) {
+                 const uint8_t *img = nullptr, const uint32_t *img_wh = nullptr) {
     if (k > kFastMaxK) return false;
     if (img) {
         if (k <= 16)
             hipLaunchKernelGGL((kmeans_fast_kernel<16, kAccumulate, true>), grid, dim3(kThreads), 0, s, xy, segs,
-                               cent, k, thr, acc, n_copies, st, labels, img);
+                               cent, k, thr, acc, n_copies, st, labels, img, img_wh);
         else
             hipLaunchKernelGGL((kmeans_fast_kernel<32, kAccumulate, true>), grid, dim3(kThreads), 0, s, xy, segs,
-                               cent, k, thr, acc, n_copies, st, labels, img);
+                               cent, k, thr, acc, n_copies, st, labels, img, img_wh);
     } else if (k <= 16) {
         hipLaunchKernelGGL((kmeans_fast_kernel<16, kAccumulate, false>), grid, dim3(kThreads), 0, s, xy, segs,
-                           cent, k, thr, acc, n_copies, st, labels, img);
+                           cent, k, thr, acc, n_copies, st, labels, img, img_wh);
     } else {
         hipLaunchKernelGGL((kmeans_fast_kernel<32, kAccumulate, false>), grid, dim3(kThreads), 0, s, xy, segs,
-                           cent, k, thr, acc, n_copies, st, labels, img);
+                           cent, k, thr, acc, n_copies, st, labels, img, img_wh);
     }
     return true;
 }
@@ -796,13 +957,15 @@ static int kmeans_check(const ecc_ctx *ctx, const ecc_kmeans_cfg *cfg, const flo
     return ECC_OK;
 }
 
-ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs,
-                                int64_t seg_stride, const int32_t *seg_counts,
+static int kmeans_run_xy16_impl(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                                const int32_t *seg_counts, int32_t frame_w, int32_t frame_h,
                                 const ecc_kmeans_cfg *cfg, float *centroids, uint8_t *labels,
                                 int32_t *iters_out, ecc_stream_t stream) {
     int rc = kmeans_check(ctx, cfg, centroids);
     if (rc) return rc;
     if (n_segs < 0 || seg_stride < 1) return ECC_ERR_INVALID;
+    if (frame_w < 0 || frame_h < 0 || frame_w > kImgSide || frame_h > kImgSide || (frame_w == 0) != (frame_h == 0))
+        return ECC_ERR_INVALID;
     Segs segs{seg_counts, n_segs, seg_stride, n_segs * seg_stride};
     if (!seg_counts) {
         // dense array of n_segs*seg_stride points: re-cut into 16384-point segments
@@ -877,7 +1040,7 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
         // final label image
         const int grid_pts = (int)std::min<int64_t>(segs.n_segs, kMaxGridPts);
         ECC_CHECK_HIP(ctx, hipMemsetAsync(n_out, 0, 4, s), "memset(kmeans outside)");
-        {
+        if (frame_w == 0) {  // no frame given: the points' bounding box
             ECC_TIMED(ctx, s, "kmeans_extent_kernel");
             hipLaunchKernelGGL(kmeans_extent_kernel, dim3(grid), dim3(kThreads), 0, s, xy, segs, ext);
         }
@@ -890,8 +1053,9 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
                               "kmeans_count LDS");
                 lds_ok = true;
             }
-            hipLaunchKernelGGL(kmeans_count_kernel, dim3(4, parts), dim3(kHistThreads), kHistChunk * 4, s, xy,
-                               segs, ext, grid, parts, partial, wh, outside, n_out, 0u, 0u, (int32_t *)nullptr);
+            hipLaunchKernelGGL(kmeans_count_kernel, dim3(count_grid(parts)), dim3(kHistThreads), kHistChunk * 4, s,
+                               xy, segs, ext, grid, parts, partial, wh, outside, n_out, (uint32_t)frame_w,
+                               (uint32_t)frame_h, (int32_t *)nullptr);
         }
         {
             ECC_TIMED(ctx, s, "kmeans_count_sum_kernel");
@@ -927,7 +1091,7 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
         if (labels) {
             ECC_TIMED(ctx, s, "kmeans_xy16_labels");
             launch_fast<false>(cfg->k, dim3(grid_pts), s, xy, segs, centroids, cfg->threshold, nullptr, 1, st,
-                               labels, img);
+                               labels, img, wh);
             ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 labels");
         }
     }
@@ -937,29 +1101,38 @@ ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
     return ECC_OK;
 }
 
-ECC_API int ecc_kmeans_run_f32(ecc_ctx *ctx, const float *xy, int64_t n_points,
-                               const ecc_kmeans_cfg *cfg, float *centroids, uint8_t *labels,
-                               int32_t *iters_out, ecc_stream_t stream) {
+static int kmeans_run_f32_impl(ecc_ctx *ctx, const float *xy, int64_t n_points, const ecc_kmeans_cfg *cfg,
+                               int method, float *centroids, uint8_t *labels, int32_t *iters_out, ecc_stream_t stream) {
     int rc = kmeans_check(ctx, cfg, centroids);
     if (rc) return rc;
-    if (n_points < 0 || (n_points > 0 && !xy)) return ECC_ERR_INVALID;
-    rc = ecc::ws_reserve(ctx, 4096);
+    if (n_points < 0 || (n_points > 0 && !xy) || method < 0 || method > 2) return ECC_ERR_INVALID;
+    if (method != 0 && cfg->k > kFastMaxK) return ECC_ERR_INVALID;  // the engines take k <= 32
+    if ((reinterpret_cast<uintptr_t>(xy) & 7) != 0) return ECC_ERR_INVALID;  // float2 loads
+    const bool fast = cfg->k <= kFastMaxK;
+    const int n_copies = fast ? kAccCopies : 1;
+    const size_t acc_bytes = (size_t)n_copies * kAccStride * 8;
+    rc = ecc::ws_reserve(ctx, acc_bytes + 64);
     if (rc) return rc;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t s = ecc::as_stream(stream);
     auto *acc = reinterpret_cast<double *>(ctx->ws);
-    auto *st = reinterpret_cast<KmState *>(reinterpret_cast<char *>(ctx->ws) + 3 * kMaxK * 8);
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, 3 * kMaxK * 8 + 64, s), "memset(kmeans acc)");
-    const int grid = grid_for((n_points + kThreads - 1) / kThreads);
+    auto *st = reinterpret_cast<KmState *>(reinterpret_cast<char *>(ctx->ws) + acc_bytes);
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, acc_bytes + 64, s), "memset(kmeans acc)");
+    const int eng = method == 0 ? 1 : method;  // auto = the vector engine (measured faster)
+    const char *name = eng == 2 ? "kmeans_f32_mfma_kernel" : "kmeans_f32_vec_kernel";
+    const int grid = fast ? (int)std::max<int64_t>(1, std::min<int64_t>((n_points + 255) / 256, 4096))
+                          : grid_for((n_points + kThreads - 1) / kThreads);
     for (int it = 0; it < cfg->max_iters && n_points > 0; ++it) {
         {
-            ECC_TIMED(ctx, s, "kmeans_f32_kernel");
-            hipLaunchKernelGGL(kmeans_f32_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, n_points,
-                               centroids, cfg->k, cfg->threshold, acc, st, (uint8_t *)nullptr);
+            ECC_TIMED(ctx, s, fast ? name : "kmeans_f32_kernel");
+            if (!launch_f32_fast<true>(cfg->k, eng, dim3(grid), s, xy, n_points, centroids, cfg->threshold, acc,
+                                       n_copies, st, nullptr))
+                hipLaunchKernelGGL(kmeans_f32_kernel<true>, dim3(grid), dim3(kThreads), 0, s, xy, n_points,
+                                   centroids, cfg->k, cfg->threshold, acc, st, (uint8_t *)nullptr);
         }
         {
             ECC_TIMED(ctx, s, "kmeans_update_kernel");
-            hipLaunchKernelGGL(kmeans_update_kernel<double>, dim3(1), dim3(64), 0, s, acc, 1, centroids,
+            hipLaunchKernelGGL(kmeans_update_kernel<double>, dim3(1), dim3(64), 0, s, acc, n_copies, centroids,
                                cfg->k, cfg->tol, st);
         }
     }
@@ -967,8 +1140,10 @@ ECC_API int ecc_kmeans_run_f32(ecc_ctx *ctx, const float *xy, int64_t n_points,
     if (labels && n_points > 0) {
         {
             ECC_TIMED(ctx, s, "kmeans_f32_labels");
-            hipLaunchKernelGGL(kmeans_f32_kernel<false>, dim3(grid), dim3(kThreads), 0, s, xy, n_points,
-                               centroids, cfg->k, cfg->threshold, acc, st, labels);
+            if (!launch_f32_fast<false>(cfg->k, eng, dim3(grid), s, xy, n_points, centroids, cfg->threshold,
+                                        nullptr, 1, st, labels))
+                hipLaunchKernelGGL(kmeans_f32_kernel<false>, dim3(grid), dim3(kThreads), 0, s, xy, n_points,
+                                   centroids, cfg->k, cfg->threshold, acc, st, labels);
         }
         ECC_CHECK_LAUNCH(ctx, "kmeans_f32 labels");
     }
@@ -976,6 +1151,34 @@ ECC_API int ecc_kmeans_run_f32(ecc_ctx *ctx, const float *xy, int64_t n_points,
         ECC_CHECK_HIP(ctx, hipMemcpyAsync(iters_out, &st->iters, 4, hipMemcpyDeviceToDevice, s),
                       "copy iters");
     return ECC_OK;
+}
+
+ECC_API int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                                const int32_t *seg_counts, const ecc_kmeans_cfg *cfg, float *centroids,
+                                uint8_t *labels, int32_t *iters_out, ecc_stream_t stream) {
+    return kmeans_run_xy16_impl(ctx, xy, n_segs, seg_stride, seg_counts, 0, 0, cfg, centroids, labels, iters_out,
+                                stream);
+}
+
+ECC_API int ecc_kmeans_run_xy16_frame(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                                      const int32_t *seg_counts, int32_t frame_w, int32_t frame_h,
+                                      const ecc_kmeans_cfg *cfg, float *centroids, uint8_t *labels,
+                                      int32_t *iters_out, ecc_stream_t stream) {
+    if (frame_w < 1 || frame_h < 1) return ECC_ERR_INVALID;
+    return kmeans_run_xy16_impl(ctx, xy, n_segs, seg_stride, seg_counts, frame_w, frame_h, cfg, centroids, labels,
+                                iters_out, stream);
+}
+
+ECC_API int ecc_kmeans_run_f32(ecc_ctx *ctx, const float *xy, int64_t n_points,
+                               const ecc_kmeans_cfg *cfg, float *centroids, uint8_t *labels,
+                               int32_t *iters_out, ecc_stream_t stream) {
+    return kmeans_run_f32_impl(ctx, xy, n_points, cfg, 0, centroids, labels, iters_out, stream);
+}
+
+ECC_API int ecc_kmeans_run_f32_engine(ecc_ctx *ctx, const float *xy, int64_t n_points,
+                                      const ecc_kmeans_cfg *cfg, int32_t engine, float *centroids,
+                                      uint8_t *labels, int32_t *iters_out, ecc_stream_t stream) {
+    return kmeans_run_f32_impl(ctx, xy, n_points, cfg, engine, centroids, labels, iters_out, stream);
 }
 
 ECC_API int ecc_kmeans_assign_f32(ecc_ctx *ctx, const float *xy, int64_t n_points,
@@ -1114,7 +1317,7 @@ ECC_API int ecc_kmeans_counts_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_s
     }
     {
         ECC_TIMED(ctx, s, "kmeans_count_kernel");
-        hipLaunchKernelGGL(kmeans_count_kernel, dim3(4, parts), dim3(kHistThreads), kHistChunk * 4, s, xy, segs,
+        hipLaunchKernelGGL(kmeans_count_kernel, dim3(count_grid(parts)), dim3(kHistThreads), kHistChunk * 4, s, xy, segs,
                            (const uint32_t *)nullptr, 0, parts, partial, wh, (uint32_t *)nullptr, (uint32_t *)nullptr,
                            (uint32_t)frame_w, (uint32_t)frame_h, ctx->flags + kKmFlagWord);
     }

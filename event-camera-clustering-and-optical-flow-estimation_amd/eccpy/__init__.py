@@ -133,6 +133,8 @@ _sigs = {
     "ecc_kmeans_cfg_default": (None, [C.POINTER(KmeansCfg)]),
     "ecc_kmeans_run_xy16": (C.c_int, [P, P, i64, i64, P, C.POINTER(KmeansCfg), P, P, P, P]),
     "ecc_kmeans_run_f32": (C.c_int, [P, P, i64, C.POINTER(KmeansCfg), P, P, P, P]),
+    "ecc_kmeans_run_xy16_frame": (C.c_int, [P, P, i64, i64, P, i32, i32, C.POINTER(KmeansCfg), P, P, P, P]),
+    "ecc_kmeans_run_f32_engine": (C.c_int, [P, P, i64, C.POINTER(KmeansCfg), i32, P, P, P, P]),
     "ecc_kmeans_assign_f32": (C.c_int, [P, P, i64, P, i32, C.c_float, P, P]),
     "ecc_kmeans_accumulate_xy16": (C.c_int, [P, P, i64, i64, P, P, i32, C.c_float, P, P, P]),
     "ecc_kmeans_update": (C.c_int, [P, P, P, i32, C.c_float, P, P]),
@@ -325,10 +327,23 @@ class Context:
                                       C.byref(cfg), centroids.ptr, _ptr(labels), _ptr(iters),
                                       self.stream), "ecc_kmeans_run_xy16")
 
+    def kmeans_xy16_frame(self, xy: DeviceArray, n_segs: int, stride: int, counts: DeviceArray | None, w: int,
+                          h: int, centroids: DeviceArray, cfg: KmeansCfg, labels: DeviceArray | None = None,
+                          iters: DeviceArray | None = None):
+        check(lib.ecc_kmeans_run_xy16_frame(self.ctx, xy.ptr, n_segs, stride, _ptr(counts), w, h, C.byref(cfg),
+                                            centroids.ptr, _ptr(labels), _ptr(iters), self.stream),
+              "ecc_kmeans_run_xy16_frame")
+
     def kmeans_f32(self, xy: DeviceArray, n: int, centroids: DeviceArray, cfg: KmeansCfg,
                    labels: DeviceArray | None = None, iters: DeviceArray | None = None):
         check(lib.ecc_kmeans_run_f32(self.ctx, xy.ptr, n, C.byref(cfg), centroids.ptr,
                                      _ptr(labels), _ptr(iters), self.stream), "ecc_kmeans_run_f32")
+
+    def kmeans_f32_engine(self, xy: DeviceArray, n: int, centroids: DeviceArray, cfg: KmeansCfg, engine: int,
+                          labels: DeviceArray | None = None, iters: DeviceArray | None = None):
+        """engine: 0 default, 1 vector (SGPR centres), 2 matrix cores (MFMA distance + exact fallback)."""
+        check(lib.ecc_kmeans_run_f32_engine(self.ctx, xy.ptr, n, C.byref(cfg), engine, centroids.ptr,
+                                            _ptr(labels), _ptr(iters), self.stream), "ecc_kmeans_run_f32_engine")
 
     def kmeans_assign_f32(self, xy: DeviceArray, n: int, centroids: DeviceArray, k: int,
                           thr: float, labels: DeviceArray):

@@ -162,6 +162,21 @@ int ecc_kmeans_run_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_
                         uint8_t *labels, int32_t *iters_out, ecc_stream_t stream);
 int ecc_kmeans_run_f32(ecc_ctx *ctx, const float *xy, int64_t n_points, const ecc_kmeans_cfg *cfg,
                        float *centroids, uint8_t *labels, int32_t *iters_out, ecc_stream_t stream);
+/* ecc_kmeans_run_xy16 with the sensor frame known (1 <= frame_w, frame_h <= 2048): the per-pixel
+ * counts cover [0, frame_w) x [0, frame_h) with no bounding-box pass; points outside the frame
+ * are still assigned (listed and added point by point).  Same results as ecc_kmeans_run_xy16. */
+int ecc_kmeans_run_xy16_frame(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                              const int32_t *seg_counts, int32_t frame_w, int32_t frame_h,
+                              const ecc_kmeans_cfg *cfg, float *centroids, uint8_t *labels,
+                              int32_t *iters_out, ecc_stream_t stream);
+/* The same with an explicit assignment engine for k <= 32 (BASELINE config C3): 0 = default
+ * (the vector engine), 1 = vector (centres in scalar registers, exact fp32 d^2 per centre),
+ * 2 = matrix cores (d^2 - |p|^2 from v_mfma_f32_4x4x1f32, exact fallback near ties, the
+ * winner's exact d^2 against the threshold).  Both return the reference's labels; sums are fp64
+ * (exact for integer-valued coordinates).  xy must be 8-byte aligned. */
+int ecc_kmeans_run_f32_engine(ecc_ctx *ctx, const float *xy, int64_t n_points, const ecc_kmeans_cfg *cfg,
+                              int32_t engine, float *centroids, uint8_t *labels, int32_t *iters_out,
+                              ecc_stream_t stream);
 /* Split form of one Lloyd iteration, for multi-GPU: each rank accumulates its shard's exact
  * integer partial sums into acc (DEVICE uint64[3k]: count, sum x, sum y per centre; added to,
  * so zero it first), the ranks all-reduce acc (SUM), then every rank applies the identical

@@ -202,6 +202,43 @@ def test_kmeans_f32_matches_oracle(ecc, orc, gpu):
     assert (d_lab.numpy() != o_lab).mean() < 1e-4
 
 
+@pytest.mark.parametrize("engine", [1, 2])
+@pytest.mark.parametrize("k,data", [(16, "float"), (5, "int"), (32, "int"), (16, "ties")])
+def test_kmeans_f32_engines_match_oracle(ecc, orc, gpu, engine, k, data):
+    """Both assignment engines (vector / matrix cores): labels identical to the oracle's
+    assign_to_centers rule; centroids bit-exact for integer-valued points (fp64 sums are exact),
+    within 1e-4 otherwise.  'ties': points on a small integer grid with coinciding centres, so the
+    matrix engine's exact fallback decides most points."""
+    rng = np.random.default_rng(k * 7 + engine)
+    if data == "float":
+        pts = np.concatenate([rng.normal(m, 9.0, (40000, 2)) for m in rng.uniform(0, 340, (8, 2))])
+    elif data == "int":
+        pts = np.floor(rng.uniform(0, 346, (300001, 2)))
+    else:
+        pts = rng.integers(0, 12, (100000, 2)).astype(np.float64)
+    pts = pts.astype(np.float32).ravel()
+    if data == "ties":
+        c0 = np.array([[3, 3], [3, 3], [8, 8], [3, 8], [8, 3]] * 4, np.float32)[:k].ravel()
+    else:
+        c0 = _init_centroids(k, seed=k)
+    iters = 5
+    o_c, o_lab, o_it = orc.kmeans_run_f32(pts, c0, iters)
+    d_c = dev(ecc, c0)
+    d_lab = ecc.DeviceArray(len(pts) // 2, np.uint8)
+    d_it = ecc.DeviceArray(1, np.int32)
+    gpu.kmeans_f32_engine(dev(ecc, pts), len(pts) // 2, d_c, ecc.kmeans_cfg(k=k, max_iters=iters, tol=-1.0), engine,
+                          d_lab, d_it)
+    gpu.sync()
+    g_c = d_c.numpy()
+    assert d_it.numpy()[0] == o_it
+    if data == "float":
+        assert np.allclose(g_c, o_c, atol=1e-4, rtol=0)
+        assert (d_lab.numpy() != o_lab).mean() < 1e-4
+    else:
+        assert np.array_equal(g_c.view(np.uint32), o_c.view(np.uint32)), (g_c, o_c)
+        assert (d_lab.numpy() == o_lab).all()
+
+
 def test_kmeans_assign_ties_and_threshold(ecc, orc, gpu):
     """assign_to_centers semantics: first minimum wins, strict < threshold 50, 255 = none."""
     c = np.array([10, 10, 20, 10, 10, 10, 100, 100], np.float32)  # centres 0 and 2 coincide
@@ -738,6 +775,54 @@ def test_eps_duplicates_and_kdtree_kat(ecc, gpu):
                 q = np.array([q[0] + shift, 0.0])
             i = int(np.where((pts == q).all(1))[0][0])
             assert list(nbr[off[i]:off[i + 1]]) == expected, (name, q)
+
+
+# ------------------------------------------------------------------------------ BASELINE config C3
+@pytest.fixture(scope="module")
+def c3_points(ecc, orc):
+    """C3: k-means k=16 on 50 M points = the representatives of a 10 M-event 346x260 batch (C2)
+    tiled to 50 M, as packed u16 and as interleaved float; plus the oracle's 3-pass k-means."""
+    xy, _, _ = ecc.gen_events(10_000_000, seed=12, width=346, height=260)
+    rx, _, u, _ = orc.downsample_hash(xy)
+    dense = np.concatenate([rx[w * 8192: w * 8192 + u[w]] for w in range(len(u))])
+    n = 50_000_000
+    pts = np.resize(dense, n)
+    c0 = np.stack([np.linspace(20, 326, 16), np.linspace(20, 240, 16)[::-1]], 1).astype(np.float32).ravel()
+    o_c, o_lab, o_it = orc.kmeans_run_xy16(pts, c0, 3)
+    return pts, c0, o_c, o_lab, o_it
+
+
+@pytest.mark.parametrize("frame", [None, (346, 260), (300, 200)])
+def test_kmeans_c3_xy16_50m(ecc, gpu, c3_points, frame):
+    """Bounding-box form, the sensor frame, and a frame smaller than the points' extent (the
+    points outside it are assigned one by one): all equal the oracle."""
+    pts, c0, o_c, o_lab, o_it = c3_points
+    n = len(pts)
+    d_c, d_lab, d_it = dev(ecc, c0), ecc.DeviceArray(n, np.uint8), ecc.DeviceArray(1, np.int32)
+    cfg = ecc.kmeans_cfg(k=16, max_iters=3, tol=-1.0)
+    if frame is None:
+        gpu.kmeans_xy16(dev(ecc, pts), 1, n, None, d_c, cfg, d_lab, d_it)
+    else:
+        gpu.kmeans_xy16_frame(dev(ecc, pts), 1, n, None, frame[0], frame[1], d_c, cfg, d_lab, d_it)
+    gpu.sync()
+    assert d_it.numpy()[0] == o_it
+    assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
+    assert (d_lab.numpy() == o_lab).all()
+
+
+@pytest.mark.parametrize("engine", [1, 2])
+def test_kmeans_c3_f32_50m(ecc, gpu, c3_points, engine):
+    pts, c0, o_c, o_lab, o_it = c3_points
+    n = len(pts)
+    x, y = ecc.unpack_xy(pts)
+    f = np.empty(2 * n, np.float32)
+    f[0::2], f[1::2] = x, y
+    d_c, d_lab, d_it = dev(ecc, c0), ecc.DeviceArray(n, np.uint8), ecc.DeviceArray(1, np.int32)
+    gpu.kmeans_f32_engine(dev(ecc, f), n, d_c, ecc.kmeans_cfg(k=16, max_iters=3, tol=-1.0), engine, d_lab, d_it)
+    gpu.sync()
+    assert d_it.numpy()[0] == o_it
+    assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
+    assert (d_lab.numpy() == o_lab).all()
 
 
 # ------------------------------------------------------------------------------ multi-GPU building blocks
