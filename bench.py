@@ -593,6 +593,32 @@ def bench_eps(ecc, ctx, args, rep_xy, uniq, n_win, n_reps):
         "neighbour_entries": nbr_cap - 16, "clusters": int(nc.sum()), "status": st,
         "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
     }
+    # the same DBSCAN fused (ecc_dbscan_grid: no lists, one launch); its clusters must equal the
+    # chain's (labels, cluster counts, duplicate memberships as a set)
+    lab_chain, nd_chain = d_lab.numpy().copy(), int(d_nd.numpy()[0])
+    dups_chain = d_dups.numpy()[:2 * min(nd_chain, dup_cap)].reshape(-1, 2)
+    g_lab = ecc.DeviceArray(tot, np.int32)
+    g_nc = ecc.DeviceArray(n_win, np.int32)
+    g_nd = ecc.DeviceArray(1, np.int64)
+    grid_ms, kern = timed_kernels(ctx, lambda: ctx.dbscan_grid(rep_xy, n_win, WINDOW, uniq, 20.0, 20, 100, 25000,
+                                                               g_lab, g_nc, d_dups, dup_cap, g_nd), reps)
+    st_g = ctx.dbscan_status()
+    nd_g = int(g_nd.numpy()[0])
+    dups_g = d_dups.numpy()[:2 * min(nd_g, dup_cap)].reshape(-1, 2)
+    same = (np.array_equal(g_lab.numpy()[valid], lab_chain[valid]) and np.array_equal(g_nc.numpy(), nc)
+            and nd_g == nd_chain and set(map(tuple, dups_g.tolist())) == set(map(tuple, dups_chain.tolist())))
+    gk = kern.get("dbscan_grid_kernel", float("nan"))
+    res["dbscan_grid_eps20_minpts20"] = {
+        "reps": n_reps, "windows": n_win, "ms_per_call": round(grid_ms, 4),
+        "us_per_window": round(grid_ms * 1e3 / n_win, 3), "mreps_s": round(n_reps / (grid_ms * 1e-3) / 1e6, 1),
+        "clusters": int(g_nc.numpy().sum()), "dup_memberships": nd_g, "status": st_g,
+        "equals_chain": bool(same),
+        "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
+        "roofline": {"kernel": "dbscan_grid_kernel", "bound": "hbm",
+                     "achieved": round(n_reps * 8 / (gk * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(n_reps * 8 / (gk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "algorithmic_bytes": "4 B/rep in + 4 B/rep label out"},
+    }
     return res
 
 

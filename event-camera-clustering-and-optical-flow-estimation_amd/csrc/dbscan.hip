@@ -21,7 +21,14 @@
 // roots, and sizes / first members / the output order (size desc, first index asc, creation
 // asc) from LDS atomics and an O(C^2) rank over the <= 4096 components.  Neighbour lists are
 // read from HBM (ecc_eps_lists: int64 offsets + int32 segment-local indices).
-#include "ecc_internal.hpp"
+//
+// ecc_dbscan_grid is the same closed form with no lists at all: the segment's points are binned
+// into an LDS cell grid (eps_grid.hpp, cell > eps) and every phase that walks a neighbour list
+// walks the 3x3 cells instead (exact integer eps test), so the whole DBSCAN of a segment reads
+// its 4-B points once and writes its labels once (+ the duplicate memberships).
+#include "eps_grid.hpp"
+
+#include <cmath>
 
 namespace {
 
@@ -246,6 +253,320 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
     }
 }
 
+
+// The segment's eps test (g.narrow is uniform per segment: a scalar select, no divergence).
+__device__ __forceinline__ bool eps_in(const ecc::epsg::CellGrid &g, uint32_t v, uint32_t w, int e_int, uint32_t r2i) {
+    uint32_t d2;
+    return g.narrow ? ecc::epsg::in_eps<true>(v, w, e_int, r2i, &d2) : ecc::epsg::in_eps<false>(v, w, e_int, r2i, &d2);
+}
+
+#ifndef ECC_DBSCAN_PROFILE
+#define ECC_DBSCAN_PROFILE 0
+#endif
+#if ECC_DBSCAN_PROFILE
+// profiling builds (make DBSCAN_PROFILE=1): dbscan_grid_kernel's summed per-segment phase ticks
+__device__ unsigned long long g_db_prof[8];
+#define DB_MARK(k)                                                        \
+    do {                                                                  \
+        if (tid == 0) {                                                   \
+            const unsigned long long now_ = wall_clock64();               \
+            atomicAdd(&g_db_prof[k], now_ - db_t_);                       \
+            db_t_ = now_;                                                 \
+        }                                                                 \
+    } while (0)
+#else
+#define DB_MARK(k) do { } while (0)
+#endif
+
+// ---- fused grid DBSCAN (no neighbour lists) ----------------------------------------------------
+// Dynamic LDS: cend[kCells + 1] | spt[stride] | sidx[stride] | parent[stride]; ~90 KB at stride
+// 8192, plus the 48 KB component tables.
+constexpr int kGridMaxPts = 8192;
+constexpr int kGridPer = kGridMaxPts / kThreads;  // queries per lane
+
+__global__ void __launch_bounds__(kThreads)
+dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stride, const int32_t *__restrict__ seg_counts,
+                   int e_int, uint32_t r2i, int min_pts, int min_size, int max_size, int32_t *__restrict__ labels,
+                   int32_t *__restrict__ n_clusters, int64_t *__restrict__ dups, int64_t dup_cap,
+                   unsigned long long *n_dups, int32_t *err) {
+    extern __shared__ uint32_t lds_d[];
+    uint32_t *cend = lds_d;
+    uint32_t *spt = cend + ecc::epsg::kCells + 1;
+    uint16_t *sidx = reinterpret_cast<uint16_t *>(spt + stride);
+    int *parent = reinterpret_cast<int *>(sidx + ((stride + 1) & ~1ll));
+    __shared__ int c_size[kMaxComp], c_front[kMaxComp], c_rank[kMaxComp];
+    __shared__ int wsum[kThreads / 64];
+    __shared__ int red[64];
+    __shared__ int s_kept;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int64_t s = blockIdx.x; s < n_segs; s += gridDim.x) {
+        int m = seg_counts ? seg_counts[s] : (int)stride;
+        m = m < 0 ? 0 : (m > (int)stride ? (int)stride : m);
+        const int64_t base = s * stride;
+#if ECC_DBSCAN_PROFILE
+        unsigned long long db_t_ = wall_clock64();
+#endif
+        const ecc::epsg::CellGrid g = ecc::epsg::bin_cells(xy, base, m, e_int, r2i, cend, spt, sidx, red, false, true);
+        // 1. core flags: |N_eps| >= min_pts (self included)
+        for (int q = tid; q < m; q += kThreads) {
+            const uint32_t v = spt[q];
+            int cnt = 0;
+            ecc::epsg::for_candidates(g, cend, spt, v, [&](int a, uint32_t w, bool ok) {
+                cnt += (eps_in(g, v, w, e_int, r2i) & ok) ? 1 : 0;
+            });
+            const int i = sidx[q];
+            parent[i] = cnt >= min_pts ? i : -1;
+        }
+        __syncthreads();
+        DB_MARK(0);  // bin + counts
+        // 2. core connectivity by cells.  A cell pair at offset (dxc, dyc) is a CLIQUE when its
+        //    farthest two points are within eps: ((|dxc|+1)cs-1)^2 + ((|dyc|+1)cs-1)^2 <= eps^2
+        //    (at eps 20 the fine cells of 7 px: the cell itself and its 8 neighbours).  Then all
+        //    core points of the pair are one component: every core point hangs under its cell's
+        //    smallest core index (rep; a valid forest, parents < children) and clique neighbours'
+        //    reps are united.  Every other cell pair the eps pattern reaches is tested point by
+        //    point only while the two cells' components still differ, and one close core pair
+        //    unites them (cells that are not cliques themselves — coarse grids — test every pair).  The component tables are free until phase 4: c_size holds the reps.
+        int *rep = c_size;
+        const int n_cells = g.gx * g.gy;
+        const int cs1 = g.cs - 1;
+        auto clique = [&](int dxc, int dyc) {
+            const int64_t ax = (int64_t)(abs(dxc) + 1) * g.cs - 1, ay = (int64_t)(abs(dyc) + 1) * g.cs - 1;
+            return ax * ax + ay * ay <= (int64_t)r2i;
+        };
+        const bool self_clique = 2 * (int64_t)cs1 * cs1 <= (int64_t)r2i;
+        for (int c = tid; c < n_cells; c += kThreads) {
+            const int lo = c == 0 ? 0 : (int)cend[c - 1], hi = (int)cend[c];
+            int r = 0x7fffffff;
+            for (int p = lo; p < hi; ++p) {
+                const int k = sidx[p];
+                r = (parent[k] != -1 && k < r) ? k : r;
+            }
+            rep[c] = r;
+            if (self_clique && r != 0x7fffffff)
+                for (int p = lo; p < hi; ++p) {
+                    const int k = sidx[p];
+                    if (parent[k] != -1 && k != r) parent[k] = r;
+                }
+        }
+        __syncthreads();
+        // (clique unions first, so that the point-pair tests below mostly find the two cells'
+        //  components already merged)
+        for (int c = tid; c < n_cells; c += kThreads) {
+            const int ra = rep[c];
+            if (ra == 0x7fffffff || !self_clique) continue;
+            const int cx = c % g.gx, cy = c / g.gx;
+#pragma unroll 1
+            for (int r = 0; r <= 2 * ecc::epsg::kMaxR; ++r) {
+                const int dyc = r - ecc::epsg::kMaxR, kx = g.kx[r], ry = cy + dyc;
+                if (kx < 0 || dyc < 0 || ry >= g.gy) continue;
+                for (int dxc = -kx; dxc <= kx; ++dxc) {
+                    const int rx = cx + dxc;
+                    if ((dyc == 0 && dxc <= 0) || rx < 0 || rx >= g.gx || !clique(dxc, dyc)) continue;
+                    const int rb = rep[ry * g.gx + rx];
+                    if (rb != 0x7fffffff) uf_union(parent, ra, rb);
+                }
+            }
+        }
+        __syncthreads();
+        for (int c = tid; c < n_cells; c += kThreads) {
+            const int ra = rep[c];
+            if (ra == 0x7fffffff) continue;
+            const int cx = c % g.gx, cy = c / g.gx;
+            const int alo = c == 0 ? 0 : (int)cend[c - 1], ahi = (int)cend[c];
+            // point-pair test of cells [alo, ahi) x [blo, bhi) (same: only pairs p < p')
+            auto pair_test = [&](int blo, int bhi, bool same) {
+                for (int p = alo; p < ahi; ++p) {
+                    const int i = sidx[p];
+                    if (parent[i] == -1) continue;
+                    const uint32_t v = spt[p];
+                    for (int p2 = same ? p + 1 : blo; p2 < bhi; ++p2) {
+                        const int j = sidx[p2];
+                        if (parent[j] == -1 || !eps_in(g, v, spt[p2], e_int, r2i)) continue;
+                        uf_union(parent, i, j);
+                        if (self_clique) return;  // both cells are cliques: their components are one now
+                    }
+                }
+            };
+            if (!self_clique) pair_test(alo, ahi, true);
+#pragma unroll 1
+            for (int r = 0; r <= 2 * ecc::epsg::kMaxR; ++r) {
+                const int dyc = r - ecc::epsg::kMaxR, kx = g.kx[r], ry = cy + dyc;
+                if (kx < 0 || dyc < 0 || ry >= g.gy) continue;
+                for (int dxc = -kx; dxc <= kx; ++dxc) {
+                    const int rx = cx + dxc;
+                    if ((dyc == 0 && dxc <= 0) || rx < 0 || rx >= g.gx) continue;  // each pair once
+                    const int cb = ry * g.gx + rx, rb = rep[cb];
+                    if (rb == 0x7fffffff) continue;
+                    if (self_clique && clique(dxc, dyc)) continue;  // united above
+                    if (!self_clique || uf_find(parent, ra) != uf_find(parent, rb)) {
+                        pair_test(cb == 0 ? 0 : (int)cend[cb - 1], (int)cend[cb], false);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        DB_MARK(1);  // unions
+        // 3. compress; roots -> component ids in ascending root order (block scan over j)
+        int roots[kGridPer], nr = 0;
+        const int j0 = tid * kGridPer;
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u) {
+            const int j = j0 + u;
+            roots[u] = 0;
+            if (j < m && parent[j] != -1) {
+                const int r = uf_find(parent, j);
+                roots[u] = r == j;
+                nr += roots[u];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u) {
+            const int j = j0 + u;
+            if (j < m && parent[j] != -1 && !roots[u]) parent[j] = uf_root(parent, j);
+        }
+        int x = nr;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(x, d);
+            if (lane >= d) x += o;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        int pre = 0, nc = 0;
+        for (int w = 0; w < kThreads / 64; ++w) {
+            if (w < wave) pre += wsum[w];
+            nc += wsum[w];
+        }
+        int cid = pre + x - nr;
+        if (nc <= kMaxComp) {
+#pragma unroll
+            for (int u = 0; u < kGridPer; ++u)
+                if (roots[u]) parent[j0 + u] = -(cid++) - 2;
+        }
+        __syncthreads();
+        if (nc > kMaxComp) {  // too many components for the LDS tables
+            if (tid == 0) {
+                atomicOr(err, 2);
+                n_clusters[s] = 0;
+            }
+            for (int j = tid; j < m; j += kThreads) labels[base + j] = -1;
+            __syncthreads();
+            continue;
+        }
+        for (int c = tid; c < nc; c += kThreads) {
+            c_size[c] = 0;
+            c_front[c] = 0x7fffffff;
+        }
+        __syncthreads();
+        DB_MARK(2);  // compress + ids
+        // 4. memberships -> sizes and first members.  A non-core point's first claim (the
+        //    first-created cluster with a core neighbour) and whether a LATER cluster's seed is
+        //    its neighbour come from one walk over its cells; the claim stays in registers for
+        //    the labels, the (rare) further memberships are walked again in phase 6.
+        int claim[kGridPer];
+        uint32_t more = 0u;  // bit u: query u has further memberships
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u) {
+            const int q = u * kThreads + tid;
+            claim[u] = -1;
+            if (q >= m) continue;
+            const int i = sidx[q];
+            const int ci = comp_of(parent, i);
+            if (ci >= 0) {
+                claim[u] = ci;
+                atomicAdd(&c_size[ci], 1);
+                atomicMin(&c_front[ci], i);
+                continue;
+            }
+            const uint32_t v = spt[q];
+            int first = 0x7fffffff, n_seed = 0, seed_c = -1;
+            ecc::epsg::for_candidates(g, cend, spt, v, [&](int a, uint32_t w, bool ok) {
+                if (!(eps_in(g, v, w, e_int, r2i) & ok)) return;
+                const int pv = parent[sidx[a]];
+                if (pv == -1) return;
+                const int c = pv <= -2 ? -pv - 2 : -parent[pv] - 2;
+                first = c < first ? c : first;
+                n_seed += pv <= -2 ? 1 : 0;
+                seed_c = pv <= -2 ? c : seed_c;
+            });
+            if (first == 0x7fffffff) continue;  // noise
+            claim[u] = first;
+            atomicAdd(&c_size[first], 1);
+            atomicMin(&c_front[first], i);
+            if (n_seed == 0 || (n_seed == 1 && seed_c == first)) continue;
+            more |= 1u << u;
+            ecc::epsg::for_candidates(g, cend, spt, v, [&](int a, uint32_t w, bool ok) {  // later clusters seeded by a neighbour
+                if (!(eps_in(g, v, w, e_int, r2i) & ok)) return;
+                const int pv = parent[sidx[a]];
+                if (pv <= -2 && -pv - 2 != first) {
+                    atomicAdd(&c_size[-pv - 2], 1);
+                    atomicMin(&c_front[-pv - 2], i);
+                }
+            });
+        }
+        __syncthreads();
+        DB_MARK(3);  // memberships
+        // 5. output order: kept clusters by (size desc, front asc, creation asc)
+        if (tid == 0) s_kept = 0;
+        __syncthreads();
+        for (int c = tid; c < nc; c += kThreads) {
+            const int sz = c_size[c], fr = c_front[c];
+            int r = -1;
+            if (sz >= min_size && sz <= max_size) {
+                r = 0;
+                for (int o = 0; o < nc; ++o) {
+                    const int so = c_size[o];
+                    if (so < min_size || so > max_size) continue;
+                    r += so > sz || (so == sz && (c_front[o] < fr || (c_front[o] == fr && o < c)));
+                }
+                atomicAdd(&s_kept, 1);
+            }
+            c_rank[c] = r;
+        }
+        __syncthreads();
+        if (tid == 0) n_clusters[s] = s_kept;
+        DB_MARK(4);  // ranks
+        // 6. labels (the first claim, staged over parent[] by segment index for a coalesced
+        //    write) and the further memberships
+        int lab[kGridPer], lidx[kGridPer];
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u) {
+            const int q = u * kThreads + tid;
+            lidx[u] = q < m ? (int)sidx[q] : -1;
+            lab[u] = claim[u] >= 0 ? c_rank[claim[u]] : -1;
+            if (!((more >> u) & 1u)) continue;
+            const int i = lidx[u], first = claim[u];
+            const uint32_t v = spt[q];
+            ecc::epsg::for_candidates(g, cend, spt, v, [&](int a, uint32_t w, bool ok) {
+                if (!(eps_in(g, v, w, e_int, r2i) & ok)) return;
+                const int pv = parent[sidx[a]];
+                if (pv <= -2 && -pv - 2 != first && c_rank[-pv - 2] >= 0) {
+                    const unsigned long long at = atomicAdd(n_dups, 1ull);
+                    if ((int64_t)at < dup_cap) {
+                        dups[2 * at] = base + i;
+                        dups[2 * at + 1] = c_rank[-pv - 2];
+                    } else {
+                        atomicOr(err, 2);
+                    }
+                }
+            });
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u)
+            if (lidx[u] >= 0) parent[lidx[u]] = lab[u];
+        __syncthreads();
+        for (int j = tid; j < m; j += kThreads) labels[base + j] = parent[j];
+        __syncthreads();
+        DB_MARK(5);  // labels + dups
+#if ECC_DBSCAN_PROFILE
+        if (tid == 0) atomicAdd(&g_db_prof[7], 1ull);
+#endif
+    }
+}
+
 }  // namespace
 
 ECC_API int ecc_dbscan_extract(ecc_ctx *ctx, int64_t n_segs, int64_t seg_stride, const int32_t *seg_counts,
@@ -272,6 +593,36 @@ ECC_API int ecc_dbscan_extract(ecc_ctx *ctx, int64_t n_segs, int64_t seg_stride,
     return ECC_OK;
 }
 
+ECC_API int ecc_dbscan_grid(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                            const int32_t *seg_counts, double eps, int32_t min_pts, int32_t min_cluster_size,
+                            int32_t max_cluster_size, int32_t *labels, int32_t *n_clusters, int64_t *dups,
+                            int64_t dup_cap, int64_t *n_dups, ecc_stream_t stream) {
+    if (!ctx || n_segs < 0 || seg_stride < 1 || seg_stride > kGridMaxPts || min_pts < 1 || dup_cap < 0 ||
+        !(eps >= 0.0) || eps > 32767.0)
+        return ECC_ERR_INVALID;
+    if (n_segs > 0 && (!xy || !labels || !n_clusters || !n_dups || (dup_cap > 0 && !dups))) return ECC_ERR_INVALID;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    int32_t *err = ctx->flags + kFlagWord;
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(err, 0, 4, s), "memset(dbscan err)");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(n_dups, 0, 8, s), "memset(n_dups)");
+    if (n_segs == 0) return ECC_OK;
+    // d^2 <= eps^2 (fp64) <=> d^2 <= floor(eps^2) for integer d^2; |dx|, |dy| <= floor(eps)
+    const int r2i = (int)std::floor(eps * eps), e_int = (int)std::floor(eps);
+    const size_t lds = (size_t)(ecc::epsg::kCells + 1 + seg_stride) * 4 + (size_t)((seg_stride + 1) & ~1ll) * 2 +
+                       (size_t)seg_stride * 4;
+    ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(dbscan_grid_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                  "dbscan_grid lds");
+    const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 2048);
+    ECC_TIMED(ctx, s, "dbscan_grid_kernel");
+    hipLaunchKernelGGL(dbscan_grid_kernel, dim3(grid), dim3(kThreads), lds, s, xy, n_segs, seg_stride, seg_counts,
+                       e_int, (uint32_t)r2i, min_pts, min_cluster_size, max_cluster_size, labels, n_clusters, dups,
+                       dup_cap, reinterpret_cast<unsigned long long *>(n_dups), err);
+    ECC_CHECK_LAUNCH(ctx, "dbscan_grid");
+    return ECC_OK;
+}
+
 ECC_API int ecc_dbscan_status(ecc_ctx *ctx, ecc_stream_t stream) {
     if (!ctx) return ECC_ERR_INVALID;
     int32_t f = 0;
@@ -280,3 +631,17 @@ ECC_API int ecc_dbscan_status(ecc_ctx *ctx, ecc_stream_t stream) {
     ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
     return (f & 2) ? ECC_ERR_CAPACITY : ECC_OK;
 }
+
+#if ECC_DBSCAN_PROFILE
+// Profiling builds only: dbscan_grid_kernel's summed phase ticks since the last call (reset after
+// reading); out[7] = segments timed; ticks_per_us from the device.
+ECC_API int ecc_dbscan_profile(unsigned long long *out8, double *ticks_per_us) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_db_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return ECC_ERR_HIP;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_db_prof), z, sizeof(z));
+    int khz = 0;
+    hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
+    *ticks_per_us = khz / 1000.0;
+    return ECC_OK;
+}
+#endif

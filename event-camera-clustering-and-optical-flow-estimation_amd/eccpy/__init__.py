@@ -175,6 +175,7 @@ _sigs = {
     "ecc_evt_status": (C.c_int, [P, P]),
     "ecc_evt_encode": (i64, [i32, P, P, P, i64, P, i64]),
     "ecc_dbscan_extract": (C.c_int, [P, i64, i64, P, P, P, i64, i32, i32, i32, P, P, P, i64, P, P]),
+    "ecc_dbscan_grid": (C.c_int, [P, P, i64, i64, P, C.c_double, i32, i32, i32, P, P, P, i64, P, P]),
     "ecc_dbscan_status": (C.c_int, [P, P]),
     "ecc_device_sync": (C.c_int, []),
     "ecc_reslice_n_us": (C.c_int, [P, P, i64, i64, P, i64, P, P]),
@@ -403,6 +404,13 @@ class Context:
                                      nbr.nbytes // 4, min_pts,
                                      min_size, max_size, labels.ptr, n_clusters.ptr, _ptr(dups), dup_cap,
                                      n_dups.ptr, self.stream), "ecc_dbscan_extract")
+
+    def dbscan_grid(self, xy: DeviceArray, n_segs: int, stride: int, counts_in, eps: float, min_pts: int,
+                    min_size: int, max_size: int, labels: DeviceArray, n_clusters: DeviceArray,
+                    dups: DeviceArray | None, dup_cap: int, n_dups: DeviceArray):
+        check(lib.ecc_dbscan_grid(self.ctx, xy.ptr, n_segs, stride, _ptr(counts_in), eps, min_pts, min_size,
+                                  max_size, labels.ptr, n_clusters.ptr, _ptr(dups), dup_cap, n_dups.ptr,
+                                  self.stream), "ecc_dbscan_grid")
 
     def dbscan_status(self) -> int:
         return lib.ecc_dbscan_status(self.ctx, self.stream)

@@ -484,9 +484,10 @@ std::vector<std::vector<std::size_t>> get_cluster_indices(const std::vector<reac
 
 // ------------------------------------------------------------------------------ DBSCAN
 void DBSCANSimpleCluster::extract(std::vector<PointIndices> &cluster_indices) {  // DBSCAN_simple.h:27-90
-    // radiusSearch for every point (ecc_eps_counts / ecc_eps_lists) and the seed-queue expansion
-    // (ecc_dbscan_extract: union-find closed form) both run on the GPU; the host only turns
-    // labels + duplicate memberships into PointIndices.
+    // radiusSearch for every point and the seed-queue expansion (union-find closed form) both run
+    // on the GPU — fused over an LDS cell grid (ecc_dbscan_grid) up to 8192 points, else through
+    // ecc_eps_counts / ecc_eps_lists / ecc_dbscan_extract; the host only turns labels + duplicate
+    // memberships into PointIndices.
     cluster_indices.clear();
     const int64_t n = (int64_t)cloud_.size();
     if (n == 0) return;
@@ -507,25 +508,34 @@ void DBSCANSimpleCluster::extract(std::vector<PointIndices> &cluster_indices) { 
     std::vector<uint32_t> xy(n);  // translation keeps every distance
     for (int64_t i = 0; i < n; ++i) xy[i] = pack_xy((int)cloud_[i].x - mnx, (int)cloud_[i].y - mny);
     ecc_stream_t s = ctx_.stream();
-    DeviceBuffer d_xy(n * 4), d_cnt(n * 4), d_off((n + 1) * 8), d_lab(n * 4), d_nc(4), d_nd(8);
+    DeviceBuffer d_xy(n * 4), d_lab(n * 4), d_nc(4), d_nd(8);
     d_xy.upload(xy.data(), n * 4, s);
-    check(ecc_eps_counts(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, 1, d_cnt.as<int32_t>(), nullptr, s),
-          "ecc_eps_counts");
-    std::vector<int32_t> cnt(n);
-    d_cnt.download(cnt.data(), n * 4, s);
-    ctx_.sync();
-    int64_t total = 0;
-    for (int32_t c : cnt) total += c;
-    DeviceBuffer d_nbr(std::max<int64_t>(total, 1) * 4);
-    check(ecc_eps_lists(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, d_cnt.as<int32_t>(),
-                        d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, s),
-          "ecc_eps_lists");
     const int64_t dup_cap = std::max<int64_t>(n, 1024);
     DeviceBuffer d_dups(dup_cap * 16);
-    check(ecc_dbscan_extract(ctx_.get(), 1, n, nullptr, d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, minPts_,
-                             min_pts_per_cluster_, max_pts_per_cluster_, d_lab.as<int32_t>(), d_nc.as<int32_t>(),
-                             d_dups.as<int64_t>(), dup_cap, d_nd.as<int64_t>(), s),
-          "ecc_dbscan_extract");
+    if (n <= 8192) {  // one fused launch over an LDS cell grid, no neighbour lists
+        check(ecc_dbscan_grid(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, minPts_, min_pts_per_cluster_,
+                              max_pts_per_cluster_, d_lab.as<int32_t>(), d_nc.as<int32_t>(), d_dups.as<int64_t>(),
+                              dup_cap, d_nd.as<int64_t>(), s),
+              "ecc_dbscan_grid");
+    } else {  // counts -> ascending lists -> extraction
+        DeviceBuffer d_cnt(n * 4), d_off((n + 1) * 8);
+        check(ecc_eps_counts(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, 1, d_cnt.as<int32_t>(), nullptr, s),
+              "ecc_eps_counts");
+        std::vector<int32_t> cnt(n);
+        d_cnt.download(cnt.data(), n * 4, s);
+        ctx_.sync();
+        int64_t total = 0;
+        for (int32_t c : cnt) total += c;
+        DeviceBuffer d_nbr(std::max<int64_t>(total, 1) * 4);
+        check(ecc_eps_lists(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, d_cnt.as<int32_t>(),
+                            d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, s),
+              "ecc_eps_lists");
+        check(ecc_dbscan_extract(ctx_.get(), 1, n, nullptr, d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, minPts_,
+                                 min_pts_per_cluster_, max_pts_per_cluster_, d_lab.as<int32_t>(), d_nc.as<int32_t>(),
+                                 d_dups.as<int64_t>(), dup_cap, d_nd.as<int64_t>(), s),
+              "ecc_dbscan_extract");
+        ctx_.sync();  // the lists must outlive the extraction
+    }
     check(ecc_dbscan_status(ctx_.get(), s), "ecc_dbscan_extract");
     int32_t nc = 0;
     int64_t nd = 0;

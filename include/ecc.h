@@ -404,6 +404,15 @@ int ecc_dbscan_extract(ecc_ctx *ctx, int64_t n_segs, int64_t seg_stride, const i
                        int32_t min_cluster_size, int32_t max_cluster_size, int32_t *labels,
                        int32_t *n_clusters, int64_t *dups, int64_t dup_cap, int64_t *n_dups,
                        ecc_stream_t stream);
+/* ecc_dbscan_grid: the same extraction (same outputs, same status) straight from the points,
+ * with no neighbour lists: the segment is binned into an LDS cell grid and every phase walks the
+ * 3x3 cells around a point (exact integer eps test, as ecc_eps_counts).  This is the whole of
+ * DBSCANSimpleCluster::extract (:27-90) including its radiusSearch (:118-142) in one launch.
+ * seg_stride <= 8192 (one downsample window). */
+int ecc_dbscan_grid(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_stride,
+                    const int32_t *seg_counts, double eps, int32_t min_pts, int32_t min_cluster_size,
+                    int32_t max_cluster_size, int32_t *labels, int32_t *n_clusters, int64_t *dups,
+                    int64_t dup_cap, int64_t *n_dups, ecc_stream_t stream);
 int ecc_dbscan_status(ecc_ctx *ctx, ecc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------

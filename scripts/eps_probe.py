@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""eps-neighbourhood / grid-DBSCAN kernels on the bench workload (the representatives of the
+20 M-event 346x260 stream, 2442 windows of 8192): a few calls each, for rocprofv3 counter passes.
+Usage: eps_probe.py [counts|dbscan|lists|all]"""
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "event-camera-clustering-and-optical-flow-estimation_amd"))
+import eccpy as ecc  # noqa: E402
+
+what = sys.argv[1] if len(sys.argv) > 1 else "all"
+n, W, H, WIN = 2442 * 8192, 346, 260, 8192
+ctx = ecc.Context(0)
+xy, _, _ = ecc.gen_events(n, seed=1, width=W, height=H)
+d_xy = ecc.DeviceArray.from_numpy(xy, ctx.stream)
+rep_xy, rep_idx, uniq, rep, nw = ctx.downsample_hash(d_xy, n)
+tot = nw * WIN
+cnt = ecc.DeviceArray(tot, np.int32)
+core = ecc.DeviceArray(tot, np.float64)
+for _ in range(3):
+    if what in ("counts", "all"):
+        ctx.eps_counts(rep_xy, nw, WIN, uniq, 20.0, 20, cnt, None)
+        ctx.eps_counts(rep_xy, nw, WIN, uniq, 10.0, 2, cnt, core)
+    if what in ("dbscan", "all"):
+        lab = ecc.DeviceArray(tot, np.int32)
+        nc = ecc.DeviceArray(nw, np.int32)
+        nd = ecc.DeviceArray(1, np.int64)
+        ctx.dbscan_grid(rep_xy, nw, WIN, uniq, 20.0, 20, 100, 25000, lab, nc, None, 0, nd)
+ctx.sync()
+print("ok", nw, int(uniq.numpy().sum()))
+
+if what == "dbscan" and hasattr(ecc.lib, "ecc_dbscan_profile"):
+    import ctypes as C
+    o, tpu = (C.c_ulonglong * 8)(), C.c_double()
+    ecc.lib.ecc_dbscan_profile(o, C.byref(tpu))
+    ctx.dbscan_grid(rep_xy, nw, WIN, uniq, 20.0, 20, 100, 25000, lab, nc, None, 0, nd)
+    ctx.sync()
+    ecc.lib.ecc_dbscan_profile(o, C.byref(tpu))
+    segs = max(o[7], 1)
+    names = ["bin+counts", "unions", "compress+ids", "memberships", "ranks", "labels+dups"]
+    print(f"{segs} segments; per segment (us): " + ", ".join(f"{nm} {o[k] / tpu.value / segs:.2f}" for k, nm in enumerate(names)))

@@ -879,10 +879,19 @@ def test_sae_handoff_equals_single_stream(ecc, orc, gpu):
 
 
 # ------------------------------------------------------------------------------ DBSCAN extraction (§8f rank 3)
-def _dbscan_gpu(ecc, gpu, xy, n_segs, stride, counts, eps, min_pts, min_size, max_size):
+def _dbscan_gpu(ecc, gpu, xy, n_segs, stride, counts, eps, min_pts, min_size, max_size, fused=False):
     d_xy = dev(ecc, xy)
     d_u = None if counts is None else dev(ecc, counts)
     n = n_segs * stride
+    if fused:  # ecc_dbscan_grid: no neighbour lists
+        d_lab = ecc.DeviceArray(n, np.int32)
+        d_nc = ecc.DeviceArray(n_segs, np.int32)
+        dup_cap = 1 << 20
+        d_dups = ecc.DeviceArray(2 * dup_cap, np.int64)
+        d_nd = ecc.DeviceArray(1, np.int64)
+        gpu.dbscan_grid(d_xy, n_segs, stride, d_u, eps, min_pts, min_size, max_size, d_lab, d_nc, d_dups,
+                        dup_cap, d_nd)
+        return _dbscan_collect(ecc, gpu, n_segs, stride, counts, d_lab, d_nc, d_dups, d_nd)
     d_cnt = ecc.DeviceArray(n, np.int32)
     gpu.eps_counts(d_xy, n_segs, stride, d_u, eps, 1, d_cnt, None)
     d_off = ecc.DeviceArray(n + 1, np.int64)
@@ -904,6 +913,10 @@ def _dbscan_gpu(ecc, gpu, xy, n_segs, stride, counts, eps, min_pts, min_size, ma
     d_nd = ecc.DeviceArray(1, np.int64)
     gpu.dbscan_extract(n_segs, stride, d_u, d_off, d_nbr, min_pts, min_size, max_size, d_lab, d_nc, d_dups,
                        dup_cap, d_nd)
+    return _dbscan_collect(ecc, gpu, n_segs, stride, counts, d_lab, d_nc, d_dups, d_nd)
+
+
+def _dbscan_collect(ecc, gpu, n_segs, stride, counts, d_lab, d_nc, d_dups, d_nd):
     st = gpu.dbscan_status()
     assert st == 0, gpu.last_error()
     lab, nc, nd = d_lab.numpy(), d_nc.numpy(), int(d_nd.numpy()[0])
@@ -921,16 +934,17 @@ def _dbscan_gpu(ecc, gpu, xy, n_segs, stride, counts, eps, min_pts, min_size, ma
     return out
 
 
+@pytest.mark.parametrize("fused", [False, True], ids=["lists", "grid"])
 @pytest.mark.parametrize("eps,min_pts,min_size,max_size", [
     (20.0, 20, 100, 25000),   # pcl_cluster.cpp:113-120 driver parameters
     (3.0, 4, 1, 1 << 30),
     (1.5, 3, 2, 50),
 ])
-def test_dbscan_extract_matches_reference_semantics(ecc, orc, gpu, eps, min_pts, min_size, max_size):
+def test_dbscan_extract_matches_reference_semantics(ecc, orc, gpu, eps, min_pts, min_size, max_size, fused):
     xy, _, _ = ecc.gen_events(40_000, seed=61)
     rep_xy, _, u, _ = orc.downsample_hash(xy)
     nw = min(len(u), 4)
-    got = _dbscan_gpu(ecc, gpu, rep_xy[:nw * 8192], nw, 8192, u[:nw], eps, min_pts, min_size, max_size)
+    got = _dbscan_gpu(ecc, gpu, rep_xy[:nw * 8192], nw, 8192, u[:nw], eps, min_pts, min_size, max_size, fused)
     for w in range(nw):
         pts = rep_xy[w * 8192: w * 8192 + u[w]]
         ref = orc.dbscan_lists(np.stack([pts & 0xFFFF, pts >> 16], 1), eps, min_pts, min_size, max_size)
@@ -939,13 +953,14 @@ def test_dbscan_extract_matches_reference_semantics(ecc, orc, gpu, eps, min_pts,
             assert np.array_equal(a, b)
 
 
-def test_dbscan_extract_border_duplicates(ecc, orc, gpu):
+@pytest.mark.parametrize("fused", [False, True], ids=["lists", "grid"])
+def test_dbscan_extract_border_duplicates(ecc, orc, gpu, fused):
     """Many tiny random segments (dense in seeds, borders and duplicate memberships)."""
     rng = np.random.default_rng(7)
     n_segs, stride = 300, 64
     counts = rng.integers(1, stride + 1, n_segs).astype(np.int32)
     xy = ecc.pack_xy(rng.integers(0, 14, n_segs * stride), rng.integers(0, 14, n_segs * stride))
-    got = _dbscan_gpu(ecc, gpu, xy, n_segs, stride, counts, 2.0, 4, 1, 1 << 30)
+    got = _dbscan_gpu(ecc, gpu, xy, n_segs, stride, counts, 2.0, 4, 1, 1 << 30, fused)
     n_dup = 0
     for s in range(n_segs):
         pts = xy[s * stride: s * stride + counts[s]]
