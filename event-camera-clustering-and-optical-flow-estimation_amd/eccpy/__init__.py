@@ -129,6 +129,7 @@ _sigs = {
     "ecc_graph_launch": (C.c_int, [P, P]),
     "ecc_graph_destroy": (C.c_int, [P]),
     "ecc_hash_cfg_default": (None, [C.POINTER(HashCfg)]),
+    "ecc_dedup_exact": (C.c_int, [P, P, i64, i32, P, P, P, P]),
     "ecc_downsample_hash": (C.c_int, [P, P, i64, C.POINTER(HashCfg), P, P, P, P, P]),
     "ecc_kmeans_cfg_default": (None, [C.POINTER(KmeansCfg)]),
     "ecc_kmeans_run_xy16": (C.c_int, [P, P, i64, i64, P, C.POINTER(KmeansCfg), P, P, P, P]),
@@ -319,6 +320,16 @@ class Context:
                                       _ptr(rep_idx), uniq.ptr, rep.ptr, self.stream),
               "ecc_downsample_hash")
         return rep_xy, rep_idx, uniq, rep, nw
+
+    def dedup_exact(self, xy: DeviceArray, n: int, window: int = 8192):
+        """analyzeCoordinates per window: (uniq_idx, uniq_cnt, n_unique, n_windows)."""
+        nw = (n + window - 1) // window
+        idx = DeviceArray(max(nw * window, 1), np.uint32)
+        cnt = DeviceArray(max(nw * window, 1), np.int32)
+        u = DeviceArray(max(nw, 1), np.int32)
+        check(lib.ecc_dedup_exact(self.ctx, xy.ptr, n, window, idx.ptr, cnt.ptr, u.ptr, self.stream),
+              "ecc_dedup_exact")
+        return idx, cnt, u, nw
 
     # ---- 2. k-means
     def kmeans_xy16(self, xy: DeviceArray, n_segs: int, stride: int, counts: DeviceArray | None,

@@ -315,6 +315,38 @@ DownsampleResult HashDownsampler::process(const std::vector<std::pair<int, int>>
     return r;
 }
 
+int analyzeCoordinates(Context &ctx, const int *data, int n_ints, std::vector<CoordinateInfo> *coords) {
+    const int n = n_ints / 2;  // the reference walks i = 0, 2, ... < ARRAY_SIZE (:74)
+    if (n_ints < 0 || n > 8192) throw Error(ECC_ERR_INVALID, "analyzeCoordinates: more than 8192 pairs");
+    if (coords) coords->clear();
+    if (n == 0) return 0;
+    std::vector<uint32_t> xy(n);
+    for (int i = 0; i < n; ++i) {
+        const int x = data[2 * i], y = data[2 * i + 1];
+        if (x < 0 || y < 0 || x > 65535 || y > 65535)
+            throw Error(ECC_ERR_INVALID, "analyzeCoordinates: coordinate outside 0..65535");
+        xy[i] = pack_xy(x, y);
+    }
+    ecc_stream_t s = ctx.stream();
+    DeviceBuffer d_xy, d_idx((size_t)n * 4), d_cnt((size_t)n * 4), d_u(4);
+    d_xy.upload(xy.data(), (size_t)n * 4, s);
+    check(ecc_dedup_exact(ctx.get(), d_xy.as<uint32_t>(), n, n, d_idx.as<uint32_t>(), d_cnt.as<int32_t>(),
+                          d_u.as<int32_t>(), s),
+          "ecc_dedup_exact");
+    int32_t u = 0;
+    d_u.download(&u, 4, s);
+    if (coords) {
+        std::vector<uint32_t> idx(n);
+        std::vector<int32_t> cnt(n);
+        d_idx.download(idx.data(), (size_t)n * 4, s);
+        d_cnt.download(cnt.data(), (size_t)n * 4, s);
+        ctx.sync();
+        for (int k = 0; k < u; ++k) coords->push_back(CoordinateInfo{data[2 * idx[k]], data[2 * idx[k] + 1], cnt[k]});
+    }
+    ctx.sync();
+    return u;
+}
+
 KMeans::KMeans(Context &ctx, int k, int max_iters, float threshold, float tol) : ctx_(ctx) {
     cfg_ = ecc_kmeans_cfg{k, max_iters, threshold, tol};
 }

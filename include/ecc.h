@@ -132,6 +132,18 @@ int ecc_downsample_hash(ecc_ctx *ctx, const uint32_t *xy, int64_t n, const ecc_h
                         uint32_t *rep_xy, uint32_t *rep_idx, int32_t *win_unique,
                         int32_t *win_repeated, ecc_stream_t stream);
 
+/* Exact (x, y) deduplication per window.
+ * Reference: analyzeCoordinates / findCoordinate FCT/metavision_time_surface_periodic.cpp:56-120
+ *   (linear search over the unique list: first-occurrence order, a count per coordinate; it
+ *   prints the unique count).  Windows of `window` events (<= 8192 pairs: ARRAY_SIZE 16384 ints),
+ *   the last one partial.  Outputs, per window w (base = w * window):
+ *   n_unique[w] = the number of distinct (x, y) in the window (the reference's uniqueCount);
+ *   uniq_idx[base + k] = global index of the k-th distinct coordinate's first event (ascending);
+ *   uniq_cnt[base + k] = how many events of the window carry it (the reference's count).
+ *   Any output may be NULL. */
+int ecc_dedup_exact(ecc_ctx *ctx, const uint32_t *xy, int64_t n, int32_t window, uint32_t *uniq_idx,
+                    int32_t *uniq_cnt, int32_t *n_unique, ecc_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * 2. k-means (2-D, k <= 64)
  * Reference: __kernel assign_to_centers / assign_data_cluster / reduction_scalar

@@ -239,6 +239,15 @@ class HashDownsampler {  // process_coordinates + slice path (SMP/…opencl_stor
     ecc_hash_cfg cfg_;
 };
 
+// Exact dedup of one window.  FCT/metavision_time_surface_periodic.cpp:
+// CoordinateInfo :47-52, analyzeCoordinates :68-120 over the reference's int data[] laid out
+// x0, y0, x1, y1, ... (ARRAY_SIZE = 16384 ints).  Returns uniqueCount; `coords` (optional) gets the
+// distinct coordinates in first-occurrence order with their counts.  GPU: ecc_dedup_exact.
+struct CoordinateInfo {
+    int x, y, count;
+};
+int analyzeCoordinates(Context &ctx, const int *data, int n_ints = 16384, std::vector<CoordinateInfo> *coords = nullptr);
+
 class KMeans {  // assign_to_centers + host loop, "fixed" mode (Appendix A Q7-Q10)
   public:
     KMeans(Context &ctx, int k, int max_iters = 20, float threshold = 50.f, float tol = 1e-3f);

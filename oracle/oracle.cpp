@@ -75,6 +75,37 @@ ORC_API int orc_downsample_hash(const uint32_t *xy, int64_t n, int window, int x
 }
 
 // ------------------------------------------------------------------------------------------
+// a4: analyzeCoordinates / findCoordinate, FCT/metavision_time_surface_periodic.cpp:56-120 — per
+// window of `window` pairs, a linear search of the unique list (:56-66) appending new
+// coordinates with count 1 or bumping an existing count (:75-95); uniqueCount (:98).
+// ------------------------------------------------------------------------------------------
+ORC_API int orc_dedup_exact(const uint32_t *xy, int64_t n, int window, uint32_t *uniq_idx, int32_t *uniq_cnt,
+                            int32_t *n_unique) {
+    if (window <= 0 || n < 0) return -1;
+    struct CoordinateInfo { int x, y, count; int64_t first; };
+    std::vector<CoordinateInfo> coords;
+    const int64_t n_win = (n + window - 1) / window;
+    for (int64_t w = 0; w < n_win; ++w) {
+        coords.clear();
+        const int64_t lo = w * window, hi = std::min<int64_t>(n, lo + window);
+        for (int64_t i = lo; i < hi; ++i) {
+            const int x = (int)(xy[i] & 0xffffu), y = (int)(xy[i] >> 16);
+            int found = -1;
+            for (int k = 0; k < (int)coords.size(); k++)  // findCoordinate :56-66
+                if (coords[k].x == x && coords[k].y == y) { found = k; break; }
+            if (found != -1) coords[found].count++;
+            else coords.push_back({x, y, 1, i});
+        }
+        for (size_t k = 0; k < coords.size(); ++k) {
+            if (uniq_idx) uniq_idx[lo + k] = (uint32_t)coords[k].first;
+            if (uniq_cnt) uniq_cnt[lo + k] = coords[k].count;
+        }
+        if (n_unique) n_unique[w] = (int32_t)coords.size();
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------------
 // a5: assign_to_centers, KM/assign_to_centers.cl:1-34.  length((cx-x, cy-y, 0)) < threshold,
 // first minimum wins (strict <), indMin = 255 when nothing is closer than the threshold.
 // Labels here are centre indices (the kernel stores the even float offset 2c, :26).
@@ -157,6 +188,42 @@ static float tree_sum_1024(const float *v) {
     for (int s = 512; s > 0; s >>= 1)
         for (int l = 0; l < s; ++l) buf[l] += buf[l + s];
     return buf[0];
+}
+
+// One pass of the loop above from a given bin buffer (output[8*4096], in/out: the previous
+// pass's readback with its stale tails, Q8): the bins' first cluster_index[c] slots are this
+// pass's points (index order), the rest keeps the input; sums, update.  Returns 1 when the
+// reference would restart (error_max > 10).
+ORC_API int orc_kmeans_refcompat_pass(const float *xy, int64_t n, float *c16, float *output, int32_t *bin_counts_out,
+                                      float *partial_sums_out) {
+    if (n > 2048 * 8) return -1;
+    int cluster_index[8] = {0};
+    for (int64_t g = 0; g < n; ++g) {
+        const uint8_t a = assign_one(xy[2 * g], xy[2 * g + 1], c16, 8, 50.f);
+        const unsigned cl = (a == 255) ? 127u : (unsigned)a;
+        if (cl < 8) {
+            const int idx = cluster_index[cl]++;
+            if (idx < 2048) {
+                output[cl * 4096 + idx] = xy[2 * g];
+                output[cl * 4096 + 2048 + idx] = xy[2 * g + 1];
+            }
+        }
+    }
+    float ss[32];
+    for (int gidx = 0; gidx < 32; ++gidx) ss[gidx] = tree_sum_1024(&output[gidx * 1024]);
+    float nc[16];
+    for (int j = 0; j < 16; j += 2) {
+        nc[j] = (ss[j] + ss[j + 1]) / (float)cluster_index[j / 2];
+        nc[j + 1] = (ss[j + 2] + ss[j + 3]) / (float)cluster_index[j / 2];
+    }
+    float error_max = 0.f;
+    for (int j = 0; j < 16; ++j) {
+        const float a = (float)std::abs((int)(nc[j] - c16[j]));
+        if (a > error_max) { error_max = a; c16[j] = nc[j]; }
+    }
+    if (bin_counts_out) std::memcpy(bin_counts_out, cluster_index, sizeof(cluster_index));
+    if (partial_sums_out) std::memcpy(partial_sums_out, ss, sizeof(ss));
+    return error_max > 10.f ? 1 : 0;
 }
 
 ORC_API int orc_kmeans_refcompat(const float *xy, int64_t n, float *c16, int max_passes,

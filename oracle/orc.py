@@ -28,10 +28,12 @@ P = C.c_void_p
 i64, i32, f32, f64 = C.c_int64, C.c_int32, C.c_float, C.c_double
 _sigs = {
     "orc_downsample_hash": (C.c_int, [P, i64, i32, i32, i32, i32, i32, i32, P, P, P, P]),
+    "orc_dedup_exact": (C.c_int, [P, i64, i32, P, P, P]),
     "orc_kmeans_assign_f32": (C.c_int, [P, i64, P, i32, f32, P]),
     "orc_kmeans_run_f32": (C.c_int, [P, i64, P, i32, i32, f32, f32, P, P]),
     "orc_kmeans_run_xy16": (C.c_int, [P, i64, P, i32, i32, f32, f32, P, P]),
     "orc_kmeans_refcompat": (C.c_int, [P, i64, P, i32, P, P]),
+    "orc_kmeans_refcompat_pass": (C.c_int, [P, i64, P, P, P, P]),
     "orc_arc_test": (C.c_int, [P, i32, i32, i32]),
     "orc_fast_detect": (C.c_int, [P, P, i64, i32, i32, i32, i32, i32, i32, P, P]),
     "orc_filter_corners": (C.c_int, [P, i32, i32, i32, i32, P, i32]),
@@ -78,6 +80,18 @@ def downsample_hash(xy, window=8192, x_max=1280, y_max=720, mult_x=1619, mult_y=
                                  _p(rep_idx), _p(u), _p(r))
     assert rc == 0
     return rep_xy, rep_idx, u, r
+
+
+def dedup_exact(xy, window=8192):
+    """analyzeCoordinates per window: (uniq_idx, uniq_cnt, n_unique), padded per window."""
+    xy = np.ascontiguousarray(xy, np.uint32)
+    n = len(xy)
+    nw = (n + window - 1) // window
+    idx = np.zeros(nw * window, np.uint32)
+    cnt = np.zeros(nw * window, np.int32)
+    u = np.zeros(nw, np.int32)
+    assert lib.orc_dedup_exact(_p(xy), n, window, _p(idx), _p(cnt), _p(u)) == 0
+    return idx, cnt, u
 
 
 def kmeans_assign_f32(xy2, centroids, thr=50.0):

@@ -62,6 +62,23 @@ def test_downsample_matches_oracle(ecc, orc, gpu, n, window, seed, wh):
         assert (gi[sl] == o_idx[sl]).all(), f"window {w} representative indices differ"
 
 
+@pytest.mark.parametrize("n,window,wh,seed", [(8192 * 5 + 77, 8192, (346, 260), 3), (50_000, 8192, (1280, 720), 4),
+                                              (20_000, 1000, (40, 30), 5), (1, 8192, (346, 260), 6)])
+def test_dedup_exact_matches_oracle(ecc, orc, gpu, n, window, wh, seed):
+    """analyzeCoordinates (a4): unique counts, first-occurrence order and per-coordinate counts;
+    (40, 30) packs each window with many repeats of few coordinates."""
+    xy, _, _ = ecc.gen_events(n, seed=seed, width=wh[0], height=wh[1])
+    g_idx, g_cnt, g_u, nw = gpu.dedup_exact(dev(ecc, xy), n, window)
+    gpu.sync()
+    o_idx, o_cnt, o_u = orc.dedup_exact(xy, window)
+    assert (g_u.numpy()[:nw] == o_u).all()
+    gi, gc = g_idx.numpy(), g_cnt.numpy()
+    for w in range(nw):
+        sl = slice(w * window, w * window + o_u[w])
+        assert (gi[sl] == o_idx[sl]).all() and (gc[sl] == o_cnt[sl]).all()
+        assert gc[sl].sum() == min(window, n - w * window)
+
+
 @pytest.mark.parametrize("wh", [(1280, 720), (346, 260)])
 def test_downsample_full_size_properties(ecc, gpu, wh):
     """10 M events (BASELINE config C2, both sensors) — size-independent properties: every

@@ -239,3 +239,18 @@ def test_aeclustering_oracle_merge(orc):
     assert list(cpw) == [1]
     assert rows.shape[0] == 1 and rows[0, 2] == 3
     assert tuple(rows[0, 3:5]) == (50.0, 10.0)  # centroid = mean of the three points
+
+
+def test_dedup_exact_oracle_equals_numpy(orc):
+    """The literal analyzeCoordinates restatement (linear search, first-occurrence order)
+    against an independent numpy formulation (np.unique on packed keys)."""
+    import eccpy as ecc
+    xy, _, _ = ecc.gen_events(30_000, seed=9, width=60, height=40)
+    idx, cnt, u = orc.dedup_exact(xy, 8192)
+    for w in range(len(u)):
+        win = xy[w * 8192:(w + 1) * 8192]
+        keys, first, counts = np.unique(win, return_index=True, return_counts=True)
+        order = np.argsort(first)
+        assert u[w] == len(keys)
+        assert (idx[w * 8192: w * 8192 + u[w]] == first[order] + w * 8192).all()
+        assert (cnt[w * 8192: w * 8192 + u[w]] == counts[order]).all()

@@ -91,3 +91,41 @@ def test_reference_assign_to_centers_pins_oracle(ecc, orc, tmp_path):
     o = orc.kmeans_assign_f32(pts.ravel(), cen).astype(np.int32)
     mism = np.nonzero(ref_lab != o)[0]
     assert len(mism) == 0, (len(mism), pts[mism[:5]], ref_lab[mism[:5]], o[mism[:5]])
+
+
+def test_reference_kmeans_loop_pins_refcompat_oracle(orc, tmp_path):
+    """The reference's three k-means kernels (assign_to_centers, assign_data_cluster,
+    reduction_scalar) run on the GPU box's OpenCL device in the pass loop of
+    KM/assign_to_centers2.c:184-548 (demo data, stale bins carried over, the y_offset index and
+    int-abs update quirks Q7-Q9).  Each pass is replayed by orc_kmeans_refcompat_pass from the
+    reference's own state before it (centroids, and the bin buffer read back in the previous
+    pass: its stale tails depend on that pass's atomic order, Q8, so the oracle cannot predict
+    them — it is given them): bin counts, the partial sums (per bin half: a bin above 1024 points
+    splits between two 1024-float chunks in atomic order) and the updated centroids must be
+    bit-identical in every pass (integer-valued floats < 2^24: every summation order is exact),
+    and the restart decision must agree, so the oracle replays the whole run — whose length
+    itself varies from run to run with the stale tails (scripts/kmeans_ref_debug.py prints it)."""
+    _need_ref()
+    out = tmp_path / "km.bin"
+    _run(["kmeans_loop", REF / "assign_to_centers.gfx950.co", 50, out], tmp_path)
+    raw = np.frombuffer(out.read_bytes(), np.int32)
+    passes = int(raw[0])
+    rec = raw[1:1 + 72 * passes].reshape(passes, 72)
+    bufs = raw[1 + 72 * passes:].view(np.float32).reshape(passes, 8 * 4096)
+    assert passes >= 2
+    data = (np.arange(4096) % 100).astype(np.float32)
+    c = np.array([1, 1, 10, 10, 20, 20, 30, 30, 50, 50, 60, 60, 70, 70, 80, 80], np.float32)
+    buf = np.zeros(8 * 4096, np.float32)
+    for k in range(passes):
+        cnt = np.zeros(8, np.int32)
+        ss = np.zeros(32, np.float32)
+        again = orc.lib.orc_kmeans_refcompat_pass(data.ctypes.data, 2048, c.ctypes.data, buf.ctypes.data,
+                                                  cnt.ctypes.data, ss.ctypes.data)
+        assert np.array_equal(rec[k, :8], cnt), (k, rec[k, :8], cnt)
+        # the sums enter the update only in (even, odd) chunk pairs = the x and y halves of a bin;
+        # how a bin above 1024 points splits between its two chunks is the atomic order (Q8)
+        r_ss = rec[k, 8:40].view(np.float32)
+        assert np.array_equal(r_ss[0::2] + r_ss[1::2], ss[0::2] + ss[1::2]), (k, r_ss, ss)
+        assert np.array_equal(rec[k, 56:72], c.view(np.int32)), (k, rec[k, 56:72].view(np.float32), c)
+        assert again == (1 if k + 1 < passes else 0) or k + 1 == 50
+        buf = bufs[k].copy()  # the reference's readback (its stale tails) for the next pass
