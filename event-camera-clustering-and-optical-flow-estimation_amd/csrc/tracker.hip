@@ -261,6 +261,217 @@ __device__ __forceinline__ void store_track(DevTrack *dst, const DevTrack &t, bo
     if (!cand) { dst->vx = t.vx; dst->vy = t.vy; dst->group_id = t.group_id; }
 }
 
+// P4 of one slice (wave 0 of the caller's workgroup; wave-synchronous: a wave's LDS operations
+// execute in issue order, so only compiler reordering is fenced): greedy grouping in seed order
+// over the G candidates staged in LDS (:321-398), then the velocity blend with the group
+// average (:388-397) written to the candidates' tracks.  Only the average velocities feed the
+// next slice; centroids, radii and the label lists (the getCornerGroups() view) are formed when
+// `last` (the launch's last slice), since every slice overwrites them.
+struct GroupLds {
+    const int *ck_x, *ck_y, *ck_label;
+    const int16_t *ck_tidx;
+    const float *ck_vx, *ck_vy;
+    int *ck_gid;
+    uint8_t *ck_proc;
+    float2 *gav;
+    uint64_t *gmem;
+    int *goff;
+    float4 *stage;
+    unsigned *rad;
+};
+
+__device__ __forceinline__ void group_slice(const GroupLds L, int G, bool last, const TrackerParams p, int max_tracks,
+                                         DevTrack *Bf, DevGroup *__restrict__ groups, int *__restrict__ group_labels,
+                                         int *n_groups_out, int *n_glabels_out) {
+    const int lane = threadIdx.x & 63;
+    int n_groups = 0, n_glabels = 0;
+    if (G <= 64) {
+        // one candidate per lane, in registers: seed search and membership are ballots
+        const bool valid = lane < G;
+        const int mx = valid ? L.ck_x[lane] : 0, my = valid ? L.ck_y[lane] : 0;
+        const float mvx = valid ? L.ck_vx[lane] : 0.f, mvy = valid ? L.ck_vy[lane] : 0.f;
+        const int mtidx = valid ? L.ck_tidx[lane] : 0;
+        int mgid = valid ? L.ck_gid[lane] : -1;
+        bool proc = !valid;
+        int next = 0;
+        // phase A: seeds in order, each group's members (ballot) and label range
+        for (;;) {
+            const uint64_t open_ = __ballot(!proc && lane >= next);
+            if (!open_) break;
+            const int sl = __ffsll((unsigned long long)open_) - 1;
+            next = sl + 1;
+            const F2 pi{(float)__builtin_amdgcn_readlane(mx, sl), (float)__builtin_amdgcn_readlane(my, sl)};
+            const bool mem = !proc && dist2(pi, F2{(float)mx, (float)my}) <= p.s_group;
+            const uint64_t m = __ballot(mem);
+            if (!m) continue;
+            if (mem) {
+                proc = true;
+                mgid = n_groups;
+                const int r = __popcll(m & lanes_below());
+                if (last && n_glabels + r < max_tracks) group_labels[n_glabels + r] = L.ck_label[lane];
+            }
+            if (lane == 0) {
+                L.gmem[n_groups] = m;
+                L.goff[n_groups] = n_glabels;
+            }
+            n_glabels += __popcll(m);
+            n_groups++;
+        }
+        wave_sync();
+        // phase B: one lane per group (<= 64 groups): ordered fp32 sums over its members
+        // (candidate order), four members' loads issued ahead of their adds
+        if (lane < n_groups) {
+            const uint64_t m = L.gmem[lane];
+            const int cnt = __popcll(m);
+            F2 sp{0.f, 0.f}, sv{0.f, 0.f};
+            uint64_t mm = m;
+            while (mm) {
+                int k[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    ok[u] = mm != 0;
+                    k[u] = ok[u] ? __ffsll((unsigned long long)mm) - 1 : 0;
+                    mm &= mm - 1;
+                }
+                float vx[4], vy[4], px[4], py[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    vx[u] = L.ck_vx[k[u]];
+                    vy[u] = L.ck_vy[k[u]];
+                    px[u] = last ? (float)L.ck_x[k[u]] : 0.f;
+                    py[u] = last ? (float)L.ck_y[k[u]] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (!ok[u]) continue;
+                    sv = add(sv, F2{vx[u], vy[u]});
+                    if (last) sp = add(sp, F2{px[u], py[u]});
+                }
+            }
+            const float inv = __fdiv_rn(1.0f, (float)cnt);
+            const F2 av = mul(sv, inv);
+            if (last) {
+                const F2 cen = mul(sp, inv);
+                float smax = 0.f;  // max over members of sqrt_rn(s) == sqrt_rn(max s) (monotone)
+                for (uint64_t m2 = m; m2; m2 &= m2 - 1) {
+                    const int k = __ffsll((unsigned long long)m2) - 1;
+                    smax = fmaxf(smax, dist2(F2{(float)L.ck_x[k], (float)L.ck_y[k]}, cen));
+                }
+                if (lane < max_tracks)
+                    groups[lane] = DevGroup{lane, cnt, L.goff[lane], av.x, av.y, cen.x, cen.y, ecc::sqrt_rn(smax)};
+            }
+            L.gav[lane] = make_float2(av.x, av.y);
+        }
+        wave_sync();
+        // velocity blend with the group average (:388-397); candidates' last fields.  With
+        // group_radius >= 0 every candidate joins a group this slice; otherwise none forms.
+        if (valid) {
+            float vx = mvx, vy = mvy;
+            if (mgid >= 0 && mgid < n_groups) {
+                const float2 g = L.gav[mgid];
+                vx = __fadd_rn(__fmul_rn(vx, 0.7f), __fmul_rn(g.x, 0.3f));
+                vy = __fadd_rn(__fmul_rn(vy, 0.7f), __fmul_rn(g.y, 0.3f));
+            }
+            DevTrack *dst = Bf + mtidx;
+            dst->vx = vx;
+            dst->vy = vy;
+            dst->group_id = mgid;
+        }
+    } else {
+        for (int k = lane; k < G; k += 64) L.ck_proc[k] = 0;
+        wave_sync();
+        int next = 0;
+        for (;;) {
+            int seed = -1;
+            for (int b0 = next; b0 < G; b0 += 64) {
+                const int k = b0 + lane;
+                const uint64_t m = __ballot(k < G && !L.ck_proc[k]);
+                if (m) {
+                    seed = b0 + __ffsll((unsigned long long)m) - 1;
+                    break;
+                }
+            }
+            if (seed < 0) break;
+            next = seed + 1;
+            const F2 pi{(float)L.ck_x[seed], (float)L.ck_y[seed]};
+            const int gid = n_groups;
+            int cnt = 0;
+            uint64_t mine = 0;  // bit c: this lane is a member in chunk c
+            F2 sp{0.f, 0.f}, sv{0.f, 0.f};
+            for (int b0 = 0, c = 0; b0 < G; b0 += 64, ++c) {
+                const int k = b0 + lane;
+                bool mem = false;
+                if (k < G && !L.ck_proc[k]) mem = dist(pi, F2{(float)L.ck_x[k], (float)L.ck_y[k]}) <= p.group_radius;
+                const uint64_t m = __ballot(mem);
+                if (!m) continue;
+                const int r = __popcll(m & lanes_below());
+                if (mem) {
+                    mine |= 1ull << c;
+                    L.ck_proc[k] = 1;
+                    L.ck_gid[k] = gid;
+                    if (last && n_glabels + cnt + r < max_tracks) group_labels[n_glabels + cnt + r] = L.ck_label[k];
+                    L.stage[r] = make_float4((float)L.ck_x[k], (float)L.ck_y[k], L.ck_vx[k], L.ck_vy[k]);
+                }
+                wave_sync();
+                // ordered fp32 sums over the members (k ascending), evaluated by every lane
+                const int nm = __popcll(m);
+                int q = 0;
+                for (; q + 4 <= nm; q += 4) {
+                    const float4 v0 = L.stage[q], v1 = L.stage[q + 1], v2 = L.stage[q + 2], v3 = L.stage[q + 3];
+                    sp = add(add(add(add(sp, F2{v0.x, v0.y}), F2{v1.x, v1.y}), F2{v2.x, v2.y}), F2{v3.x, v3.y});
+                    sv = add(add(add(add(sv, F2{v0.z, v0.w}), F2{v1.z, v1.w}), F2{v2.z, v2.w}), F2{v3.z, v3.w});
+                }
+                for (; q < nm; ++q) {
+                    const float4 v = L.stage[q];
+                    sp = add(sp, F2{v.x, v.y});
+                    sv = add(sv, F2{v.z, v.w});
+                }
+                cnt += nm;
+                wave_sync();
+            }
+            if (cnt > 0) {
+                const F2 av = mul(sv, __fdiv_rn(1.0f, (float)cnt));
+                if (last) {
+                    const F2 cen = mul(sp, __fdiv_rn(1.0f, (float)cnt));
+                    // radius = max distance of the group's members to the centroid (fp32 >= 0
+                    // orders like its bit pattern)
+                    if (lane == 0) *L.rad = 0u;
+                    wave_sync();
+                    for (uint64_t mm = mine; mm; mm &= mm - 1) {
+                        const int k = (__ffsll((unsigned long long)mm) - 1) * 64 + lane;
+                        atomicMax(L.rad, __float_as_uint(dist(F2{(float)L.ck_x[k], (float)L.ck_y[k]}, cen)));
+                    }
+                    wave_sync();
+                    const float mr = __uint_as_float(*L.rad);
+                    if (lane == 0 && gid < max_tracks)
+                        groups[gid] = DevGroup{gid, cnt, n_glabels, av.x, av.y, cen.x, cen.y, mr};
+                }
+                if (lane == 0) L.gav[gid] = make_float2(av.x, av.y);
+                n_glabels += cnt;
+                n_groups++;
+            }
+            wave_sync();
+        }
+        // velocity blend with the group average (:388-397); candidates' last fields
+        for (int k = lane; k < G; k += 64) {
+            const int gid = L.ck_gid[k];
+            float vx = L.ck_vx[k], vy = L.ck_vy[k];
+            if (gid >= 0 && gid < n_groups) {
+                const float2 g = L.gav[gid];
+                vx = __fadd_rn(__fmul_rn(vx, 0.7f), __fmul_rn(g.x, 0.3f));
+                vy = __fadd_rn(__fmul_rn(vy, 0.7f), __fmul_rn(g.y, 0.3f));
+            }
+            DevTrack *dst = Bf + L.ck_tidx[k];
+            dst->vx = vx;
+            dst->vy = vy;
+            dst->group_id = gid;
+        }
+    }
+    *n_groups_out = n_groups;
+    *n_glabels_out = n_glabels;
+}
+
 // One workgroup processes the slices in order (the algorithm is sequential over slices); inside
 // a slice every phase is parallel over tracks / detections / candidates except the greedy
 // grouping (wave 0).
@@ -686,174 +897,11 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
         cur ^= 1;
         __syncthreads();
         TRK_MARK(3);
-        // P4: greedy grouping in seed order over the candidates, then the velocity blend (wave 0).
-        // Wave-synchronous: a wave's LDS operations execute in issue order, so only compiler
-        // reordering has to be fenced (wave_sync).
-        if (wave == 0 && G <= 64) {
-            // one candidate per lane, in registers: seed search and membership are ballots,
-            // the ordered sums walk the member lanes with readlane
-            const bool valid = lane < G;
-            const int mx = valid ? ck_x[lane] : 0, my = valid ? ck_y[lane] : 0;
-            const float mvx = valid ? ck_vx[lane] : 0.f, mvy = valid ? ck_vy[lane] : 0.f;
-            const int mlab = valid ? ck_label[lane] : 0, mtidx = valid ? ck_tidx[lane] : 0;
-            int mgid = valid ? ck_gid[lane] : -1;
-            bool proc = !valid;
-            n_groups = 0;
-            n_glabels = 0;
-            int next = 0;
-            // phase A: seeds in order, each group's members (ballot) and label range
-            for (;;) {
-                const uint64_t open_ = __ballot(!proc && lane >= next);
-                if (!open_) break;
-                const int sl = __ffsll((unsigned long long)open_) - 1;
-                next = sl + 1;
-                const F2 pi{(float)__builtin_amdgcn_readlane(mx, sl), (float)__builtin_amdgcn_readlane(my, sl)};
-                const bool mem = !proc && dist2(pi, F2{(float)mx, (float)my}) <= p.s_group;
-                const uint64_t m = __ballot(mem);
-                if (!m) continue;
-                if (mem) {
-                    proc = true;
-                    mgid = n_groups;
-                    const int r = __popcll(m & lanes_below());
-                    if (n_glabels + r < max_tracks) group_labels[n_glabels + r] = mlab;
-                }
-                if (lane == 0) {
-                    s_gmem[n_groups] = m;
-                    s_goff[n_groups] = n_glabels;
-                }
-                n_glabels += __popcll(m);
-                n_groups++;
-            }
-            wave_sync();
-            // phase B: one lane per group (<= 64 groups): ordered fp32 sums over its members
-            // (candidate order), centroid, average velocity, radius
-            if (lane < n_groups) {
-                const uint64_t m = s_gmem[lane];
-                const int cnt = __popcll(m);
-                F2 sp{0.f, 0.f}, sv{0.f, 0.f};
-                for (uint64_t mm = m; mm; mm &= mm - 1) {
-                    const int k = __ffsll((unsigned long long)mm) - 1;
-                    sp = add(sp, F2{(float)ck_x[k], (float)ck_y[k]});
-                    sv = add(sv, F2{ck_vx[k], ck_vy[k]});
-                }
-                const F2 cen = mul(sp, __fdiv_rn(1.0f, (float)cnt));
-                const F2 av = mul(sv, __fdiv_rn(1.0f, (float)cnt));
-                float smax = 0.f;  // max over members of sqrt_rn(s) == sqrt_rn(max s) (monotone)
-                for (uint64_t mm = m; mm; mm &= mm - 1) {
-                    const int k = __ffsll((unsigned long long)mm) - 1;
-                    smax = fmaxf(smax, dist2(F2{(float)ck_x[k], (float)ck_y[k]}, cen));
-                }
-                if (lane < max_tracks)
-                    groups[lane] = DevGroup{lane, cnt, s_goff[lane], av.x, av.y, cen.x, cen.y, ecc::sqrt_rn(smax)};
-                gav[lane] = make_float2(av.x, av.y);
-            }
-            wave_sync();
-            const float gax = (mgid >= 0 && mgid < n_groups) ? gav[mgid].x : 0.f;
-            const float gay = (mgid >= 0 && mgid < n_groups) ? gav[mgid].y : 0.f;
-            // velocity blend with the group average (:388-397); candidates' last fields.  With
-            // group_radius >= 0 every candidate joins a group this slice; otherwise none forms.
-            if (valid) {
-                float vx = mvx, vy = mvy;
-                if (mgid >= 0 && mgid < n_groups) {
-                    vx = __fadd_rn(__fmul_rn(vx, 0.7f), __fmul_rn(gax, 0.3f));
-                    vy = __fadd_rn(__fmul_rn(vy, 0.7f), __fmul_rn(gay, 0.3f));
-                }
-                DevTrack *dst = Bf + mtidx;
-                dst->vx = vx;
-                dst->vy = vy;
-                dst->group_id = mgid;
-            }
-        } else if (wave == 0) {
-            for (int k = lane; k < G; k += 64) ck_proc[k] = 0;
-            wave_sync();
-            n_groups = 0;
-            n_glabels = 0;
-            int next = 0;
-            for (;;) {
-                int seed = -1;
-                for (int b0 = next; b0 < G; b0 += 64) {
-                    const int k = b0 + lane;
-                    const uint64_t m = __ballot(k < G && !ck_proc[k]);
-                    if (m) {
-                        seed = b0 + __ffsll((unsigned long long)m) - 1;
-                        break;
-                    }
-                }
-                if (seed < 0) break;
-                next = seed + 1;
-                const F2 pi{(float)ck_x[seed], (float)ck_y[seed]};
-                const int gid = n_groups;
-                int cnt = 0;
-                uint64_t mine = 0;  // bit c: this lane is a member in chunk c
-                F2 sp{0.f, 0.f}, sv{0.f, 0.f};
-                for (int b0 = 0, c = 0; b0 < G; b0 += 64, ++c) {
-                    const int k = b0 + lane;
-                    bool mem = false;
-                    if (k < G && !ck_proc[k]) mem = dist(pi, F2{(float)ck_x[k], (float)ck_y[k]}) <= p.group_radius;
-                    const uint64_t m = __ballot(mem);
-                    if (!m) continue;
-                    const int r = __popcll(m & lanes_below());
-                    if (mem) {
-                        mine |= 1ull << c;
-                        ck_proc[k] = 1;
-                        ck_gid[k] = gid;
-                        if (n_glabels + cnt + r < max_tracks) group_labels[n_glabels + cnt + r] = ck_label[k];
-                        stage[r] = make_float4((float)ck_x[k], (float)ck_y[k], ck_vx[k], ck_vy[k]);
-                    }
-                    wave_sync();
-                    // ordered fp32 sums over the members (k ascending), evaluated by every lane
-                    const int nm = __popcll(m);
-                    int q = 0;
-                    for (; q + 4 <= nm; q += 4) {
-                        const float4 v0 = stage[q], v1 = stage[q + 1], v2 = stage[q + 2], v3 = stage[q + 3];
-                        sp = add(add(add(add(sp, F2{v0.x, v0.y}), F2{v1.x, v1.y}), F2{v2.x, v2.y}), F2{v3.x, v3.y});
-                        sv = add(add(add(add(sv, F2{v0.z, v0.w}), F2{v1.z, v1.w}), F2{v2.z, v2.w}), F2{v3.z, v3.w});
-                    }
-                    for (; q < nm; ++q) {
-                        const float4 v = stage[q];
-                        sp = add(sp, F2{v.x, v.y});
-                        sv = add(sv, F2{v.z, v.w});
-                    }
-                    cnt += nm;
-                    wave_sync();
-                }
-                if (cnt > 0) {
-                    const F2 cen = mul(sp, __fdiv_rn(1.0f, (float)cnt));
-                    const F2 av = mul(sv, __fdiv_rn(1.0f, (float)cnt));
-                    // radius = max distance of the group's members to the centroid (fp32 >= 0
-                    // orders like its bit pattern)
-                    if (lane == 0) s_rad = 0u;
-                    wave_sync();
-                    for (uint64_t mm = mine; mm; mm &= mm - 1) {
-                        const int k = (__ffsll((unsigned long long)mm) - 1) * 64 + lane;
-                        atomicMax(&s_rad, __float_as_uint(dist(F2{(float)ck_x[k], (float)ck_y[k]}, cen)));
-                    }
-                    wave_sync();
-                    const float mr = __uint_as_float(s_rad);
-                    if (lane == 0) {
-                        if (gid < max_tracks) groups[gid] = DevGroup{gid, cnt, n_glabels, av.x, av.y, cen.x, cen.y, mr};
-                        gav[gid] = make_float2(av.x, av.y);
-                    }
-                    n_glabels += cnt;
-                    n_groups++;
-                }
-                wave_sync();
-            }
-            // velocity blend with the group average (:388-397); candidates' last fields
-            for (int k = lane; k < G; k += 64) {
-                const int gid = ck_gid[k];
-                float vx = ck_vx[k], vy = ck_vy[k];
-                if (gid >= 0 && gid < n_groups) {
-                    const float2 g = gav[gid];
-                    vx = __fadd_rn(__fmul_rn(vx, 0.7f), __fmul_rn(g.x, 0.3f));
-                    vy = __fadd_rn(__fmul_rn(vy, 0.7f), __fmul_rn(g.y, 0.3f));
-                }
-                DevTrack *dst = Bf + ck_tidx[k];
-                dst->vx = vx;
-                dst->vy = vy;
-                dst->group_id = gid;
-            }
-        }
+        // P4: greedy grouping in seed order over the candidates, then the velocity blend (wave 0)
+        if (wave == 0)
+            group_slice(GroupLds{ck_x, ck_y, ck_label, ck_tidx, ck_vx, ck_vy, ck_gid, ck_proc, gav,
+                                 s_gmem, s_goff, stage, &s_rad},
+                        G, s == n_slices - 1, p, max_tracks, Bf, groups, group_labels, &n_groups, &n_glabels);
         __syncthreads();
         TRK_MARK(4);
     }
@@ -874,6 +922,7 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
         ctr->err = err;
     }
 }
+
 
 }  // namespace
 

@@ -49,3 +49,18 @@ for rep in range(3):
         line += f" core_MHz={o[10] / (o[11] / tpu.value):.0f}"
     print(line, "tracks", len(tr.tracks()), flush=True)
     tr.close()
+
+cnt = d_cnt.numpy()
+print(f"detections per slice: mean {cnt.mean():.1f} median {np.median(cnt):.0f} p90 {np.percentile(cnt, 90):.0f} "
+      f"max {cnt.max()} (> 64: {(cnt > 64).mean() * 100:.0f} % of slices)")
+if os.environ.get("TRK_TRACKS"):  # tracks alive per slice (oracle tracker, slow)
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import orc
+    otr = orc.OracleTracker(ecc.tracker_cfg())
+    out = d_out.numpy()
+    nt = []
+    for s_ in range(ns):
+        otr.update(out[s_ * cap: s_ * cap + cnt[s_]])
+        nt.append(len(otr.tracks(ecc.Track)))
+    nt = np.array(nt)
+    print(f"tracks per slice: mean {nt.mean():.1f} p90 {np.percentile(nt, 90):.0f} max {nt.max()}")
