@@ -387,6 +387,7 @@ def main():
     eps_res = None
     if not args.no_eps and rank == 0:
         eps_res = bench_eps(ecc, ctx, args, rep_xy, uniq, n_win, n_reps)
+        eps_res["optics_published_workloads"] = bench_optics_published(ecc, ctx)
 
     # ---- BASELINE C3: k-means k=16 on 50 M points (the step's representatives tiled) -------------
     c3_res = None
@@ -619,6 +620,46 @@ def bench_eps(ecc, ctx, args, rep_xy, uniq, n_win, n_reps):
                      "frac": round(n_reps * 8 / (gk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "algorithmic_bytes": "4 B/rep in + 4 B/rep label out"},
     }
+    return res
+
+
+# The only published timings of the reference: the vendored OPTICS library's benchmark
+# (OPT/test/Benchmark/benchmark.cpp:62-226 -> Benchmark.ods): uniform random
+# doubles in the unit hypercube, compute_reachability_dists with auto-epsilon, mean of 2 laps,
+# on an Intel Xeon E3-1225 V2 (one thread).
+PUBLISHED_OPTICS = (
+    ("d2_100k_minpts10", 2, 100_000, 10, 231.0, "Benchmark.ods TestMatrix (min_pts 10, auto-eps)"),
+    ("d2_500k_minpts10", 2, 500_000, 10, 1511.0, "Benchmark.ods TestMatrix (min_pts 10, auto-eps)"),
+    ("d3_100k_minpts10", 3, 100_000, 10, 376.0, "Benchmark.ods Tabelle1 row 9 (d=3, custom kd-tree, 1 thread)"),
+)
+
+
+def bench_optics_published(ecc, ctx):
+    """OPTICS on the published benchmark's workloads through the drop-in entry (ecc_optics_f64:
+    GPU eps-balls, host seed-set expansion): wall ms per call (mean of 2 laps after a warm-up,
+    host points in, host ordering out) and the GPU kernels' share."""
+    res = {}
+    for name, dim, n, min_pts, pub_ms, src in PUBLISHED_OPTICS:
+        pts = np.random.default_rng(1).random((n, dim))
+        ctx.optics_f64(pts, min_pts)  # warm-up (workspace growth)
+        laps = []
+        for _ in range(2):
+            t0 = time.perf_counter()
+            order, reach = ctx.optics_f64(pts, min_pts)
+            laps.append((time.perf_counter() - t0) * 1e3)
+        ctx.set_timing(True)
+        ctx.timing_reset()
+        ctx.optics_f64(pts, min_pts)
+        st = ctx.timing_report()
+        ctx.set_timing(False)
+        gpu_ms = sum(v["total_ms"] for v in st.values())
+        ms = sum(laps) / len(laps)
+        res[name] = {"points": n, "dim": dim, "min_pts": min_pts, "ms_per_call": round(ms, 2),
+                     "gpu_kernels_ms": round(gpu_ms, 3), "host_expansion_and_copies_ms": round(ms - gpu_ms, 2),
+                     "published_ms": pub_ms, "published_source": src,
+                     "speedup_vs_published": round(pub_ms / ms, 2),
+                     "undefined_reach": int((reach < 0).sum()),
+                     "kernels_ms": {k: round(v["total_ms"], 3) for k, v in sorted(st.items())}}
     return res
 
 

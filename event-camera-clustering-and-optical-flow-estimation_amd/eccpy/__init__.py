@@ -175,6 +175,10 @@ _sigs = {
     "ecc_evt_decode": (C.c_int, [P, i32, P, i64, P, P, P, i64, P, P, P]),
     "ecc_evt_status": (C.c_int, [P, P]),
     "ecc_evt_encode": (i64, [i32, P, P, P, i64, P, i64]),
+    "ecc_radius_counts_f64": (C.c_int, [P, P, i64, i32, C.c_double, i32, P, P, P]),
+    "ecc_radius_lists_f64": (C.c_int, [P, P, i64, i32, C.c_double, P, P, P, P, i64, P]),
+    "ecc_radius_status": (C.c_int, [P, P]),
+    "ecc_optics_f64": (C.c_int, [P, P, i64, i32, i32, C.c_double, P, P, P]),
     "ecc_dbscan_extract": (C.c_int, [P, i64, i64, P, P, P, i64, i32, i32, i32, P, P, P, i64, P, P]),
     "ecc_dbscan_grid": (C.c_int, [P, P, i64, i64, P, C.c_double, i32, i32, i32, P, P, P, i64, P, P]),
     "ecc_dbscan_status": (C.c_int, [P, P]),
@@ -422,6 +426,30 @@ class Context:
         check(lib.ecc_dbscan_grid(self.ctx, xy.ptr, n_segs, stride, _ptr(counts_in), eps, min_pts, min_size,
                                   max_size, labels.ptr, n_clusters.ptr, _ptr(dups), dup_cap, n_dups.ptr,
                                   self.stream), "ecc_dbscan_grid")
+
+    def radius_counts_f64(self, pts: DeviceArray, n: int, dim: int, eps: float, min_pts: int,
+                          counts: DeviceArray, core: DeviceArray | None = None):
+        check(lib.ecc_radius_counts_f64(self.ctx, pts.ptr, n, dim, eps, min_pts, counts.ptr, _ptr(core),
+                                        self.stream), "ecc_radius_counts_f64")
+
+    def radius_lists_f64(self, pts: DeviceArray, n: int, dim: int, eps: float, counts: DeviceArray,
+                         offsets: DeviceArray, nbr: DeviceArray | None, nbr_cap: int,
+                         nbr_dist: DeviceArray | None = None):
+        check(lib.ecc_radius_lists_f64(self.ctx, pts.ptr, n, dim, eps, counts.ptr, offsets.ptr, _ptr(nbr),
+                                       _ptr(nbr_dist), nbr_cap, self.stream), "ecc_radius_lists_f64")
+
+    def radius_status(self) -> int:
+        return lib.ecc_radius_status(self.ctx, self.stream)
+
+    def optics_f64(self, pts_host, min_pts: int, eps: float = -1.0):
+        """OPTICS ordering of host points (n x dim, dim 1-3): (order int64[n], reach double[n])."""
+        pts = np.ascontiguousarray(pts_host, np.float64)
+        n, dim = pts.shape
+        order = np.zeros(n, np.int64)
+        reach = np.zeros(n, np.float64)
+        check(lib.ecc_optics_f64(self.ctx, pts.ctypes.data, n, dim, min_pts, eps, order.ctypes.data,
+                                 reach.ctypes.data, self.stream), "ecc_optics_f64")
+        return order, reach
 
     def dbscan_status(self) -> int:
         return lib.ecc_dbscan_status(self.ctx, self.stream)

@@ -3,6 +3,9 @@
 // sequentially by nature (OPTICS seed-set ordering, DBSCAN cluster expansion) on GPU-computed
 // neighbourhoods, plus argument marshalling.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -427,79 +430,163 @@ bool operator==(const reachability_dist &l, const reachability_dist &r) {
     return (l.reach_dist <= r.reach_dist && l.reach_dist >= r.reach_dist) && (l.point_index == r.point_index);
 }
 
-std::vector<reachability_dist> compute_reachability_dists(Context &ctx,
-                                                          const std::vector<std::array<int, 2>> &points,
-                                                          std::size_t min_pts, double epsilon) {
-    if (points.empty()) return {};
+namespace {
+
+// GPU eps-balls (ecc_radius_*_f64: counts, core distances, lists) + the ordered expansion on the
+// host (optics.hpp:525-555, sequential by nature) for n points of D doubles (host, row-major).
+// The seed set (a std::set ordered by (reach, index), :67-69, erase + re-insert on a decrease)
+// is a binary heap with lazy deletion: reachabilities only decrease, so a superseded entry is
+// larger than the live one and is skipped when popped — the live entries pop in the same
+// (reach, index) order as from the set.
+std::vector<reachability_dist> optics_f64(ecc_ctx *ctx, ecc_stream_t s, const double *pts, int64_t n, int D,
+                                          std::size_t min_pts, double epsilon) {
+    if (n == 0) return {};
     if (min_pts < 1 || min_pts > 64) throw Error(ECC_ERR_INVALID, "compute_reachability_dists: min_pts must be 1..64");
-    if (epsilon <= 0.0) epsilon = epsilon_estimation(points, min_pts);  // optics.hpp:428-430
-    std::vector<int64_t> off;
-    std::vector<int32_t> nbr;
-    std::vector<double> core;
-    eps_neighbour_lists(ctx, points, epsilon, off, nbr, (int)min_pts, &core);  // GPU (:496-503, :286-299)
-    const size_t n = points.size();
-    auto dist = [&](size_t a, size_t b) {
-        const double dx = (double)points[a][0] - points[b][0], dy = (double)points[a][1] - points[b][1];
-        return std::sqrt(dx * dx + dy * dy);
+    if (D < 1 || D > 3) throw Error(ECC_ERR_INVALID, "compute_reachability_dists: dimension must be 1..3");
+    if (n >= INT32_MAX) throw Error(ECC_ERR_INVALID, "compute_reachability_dists: too many points");
+    static const bool timing = std::getenv("ECC_OPTICS_TIMING") != nullptr;  // phase split to stderr
+    auto t_last = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "optics_f64 %-10s %8.2f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
     };
-    std::vector<bool> processed(n, false);
-    std::vector<double> reach(n, -1.0);
-    std::vector<size_t> ordered;
-    ordered.reserve(n);
-    auto update = [&](size_t p, double cd, std::set<reachability_dist> &seeds) {  // :315-337
+    DeviceBuffer d_pts, d_cnt((size_t)n * 4), d_core((size_t)n * 8), d_off((size_t)(n + 1) * 8);
+    d_pts.upload(pts, (size_t)n * D * 8, s);
+    check(ecc_radius_counts_f64(ctx, d_pts.as<double>(), n, D, epsilon, (int32_t)min_pts, d_cnt.as<int32_t>(),
+                                d_core.as<double>(), s),
+          "ecc_radius_counts_f64");
+    check(ecc_radius_lists_f64(ctx, d_pts.as<double>(), n, D, epsilon, d_cnt.as<int32_t>(), d_off.as<int64_t>(), nullptr,
+                               nullptr, 0, s),
+          "ecc_radius_lists_f64 (size)");
+    int64_t total = 0;
+    check(ecc_memcpy_d2h(&total, d_off.as<int64_t>() + n, 8, s), "read list size");
+    check(ecc_stream_sync(s), "sync");
+    mark("counts");
+    DeviceBuffer d_nbr((size_t)std::max<int64_t>(total, 1) * 4), d_nd((size_t)std::max<int64_t>(total, 1) * 8);
+    check(ecc_radius_lists_f64(ctx, d_pts.as<double>(), n, D, epsilon, d_cnt.as<int32_t>(), d_off.as<int64_t>(),
+                               d_nbr.as<int32_t>(), d_nd.as<double>(), total, s),
+          "ecc_radius_lists_f64");
+    std::vector<int64_t> off((size_t)n + 1);
+    std::vector<int32_t> nbr((size_t)total);
+    std::vector<double> nd((size_t)total);
+    std::vector<double> core((size_t)n);
+    d_off.download(off.data(), off.size() * 8, s);
+    d_nbr.download(nbr.data(), nbr.size() * 4, s);
+    d_nd.download(nd.data(), nd.size() * 8, s);
+    d_core.download(core.data(), core.size() * 8, s);
+    check(ecc_stream_sync(s), "sync");
+    check(ecc_radius_status(ctx, s), "ecc_radius_lists_f64 capacity");
+    mark("lists+copy");
+    struct Seed {
+        double r;
+        int64_t idx;
+    };
+    auto after = [](const Seed &a, const Seed &b) {  // heap order: the smallest (reach, index) on top
+        return (a.r <= b.r && a.r >= b.r) ? (a.idx > b.idx) : (a.r > b.r);
+    };
+    std::vector<Seed> heap;
+    std::vector<char> processed((size_t)n, 0);
+    std::vector<double> reach((size_t)n, -1.0);
+    std::vector<int64_t> ordered;
+    ordered.reserve((size_t)n);
+    auto update = [&](int64_t p, double cd) {  // :315-337
         for (int64_t k = off[p]; k < off[p + 1]; ++k) {
-            const size_t o = (size_t)nbr[k];
+            const int64_t o = nbr[k];
             if (processed[o]) continue;
-            const double nr = std::max(cd, dist(p, o));
-            if (reach[o] < 0.0) {
+            const double nr = std::max(cd, nd[k]);  // geom::dist(point, points[o]), from the GPU
+            if (reach[o] < 0.0 || nr < reach[o]) {
                 reach[o] = nr;
-                seeds.insert(reachability_dist(o, nr));
-            } else if (nr < reach[o]) {
-                seeds.erase(reachability_dist(o, reach[o]));
-                reach[o] = nr;
-                seeds.insert(reachability_dist(o, nr));
+                heap.push_back(Seed{nr, o});
+                std::push_heap(heap.begin(), heap.end(), after);
             }
         }
     };
-    for (size_t p = 0; p < n; ++p) {  // :525-555
+    for (int64_t p = 0; p < n; ++p) {  // :525-555
         if (processed[p]) continue;
-        processed[p] = true;
+        processed[p] = 1;
         ordered.push_back(p);
-        std::set<reachability_dist> seeds;
         if (core[p] < 0.0) continue;
-        update(p, core[p], seeds);
-        while (!seeds.empty()) {
-            const reachability_dist s = *seeds.begin();
-            seeds.erase(seeds.begin());
-            processed[s.point_index] = true;
-            ordered.push_back(s.point_index);
-            if (core[s.point_index] < 0.0) continue;
-            update(s.point_index, core[s.point_index], seeds);
+        update(p, core[p]);
+        while (!heap.empty()) {
+            std::pop_heap(heap.begin(), heap.end(), after);
+            const Seed sd = heap.back();
+            heap.pop_back();
+            if (processed[sd.idx] || !(sd.r <= reach[sd.idx] && sd.r >= reach[sd.idx])) continue;  // superseded
+            processed[sd.idx] = 1;
+            ordered.push_back(sd.idx);
+            if (core[sd.idx] < 0.0) continue;
+            update(sd.idx, core[sd.idx]);
         }
     }
+    mark("expansion");
     std::vector<reachability_dist> result;
-    result.reserve(n);
-    for (size_t idx : ordered) result.emplace_back(idx, reach[idx]);
+    result.reserve((size_t)n);
+    for (int64_t idx : ordered) result.emplace_back((std::size_t)idx, reach[idx]);
     return result;
 }
 
-std::vector<reachability_dist> compute_reachability_dists(const std::vector<std::array<int, 2>> &points,
-                                                          std::size_t min_pts, double epsilon) {
-    return compute_reachability_dists(Context::default_context(), points, min_pts, epsilon);
+template <typename T, std::size_t D>
+std::vector<reachability_dist> optics_points(Context &ctx, const std::vector<std::array<T, D>> &points,
+                                             std::size_t min_pts, double epsilon) {
+    if (points.empty()) return {};
+    if (epsilon <= 0.0) epsilon = epsilon_estimation(points, min_pts);  // optics.hpp:428-430
+    // square_distance takes d = p1[i] - p2[i] in the coordinate type, then d * d in double
+    // (kdTree.hpp:186-187): exact in double for int and double coordinates alike
+    std::vector<double> flat(points.size() * D);
+    for (std::size_t i = 0; i < points.size(); ++i)
+        for (std::size_t d = 0; d < D; ++d) flat[i * D + d] = static_cast<double>(points[i][d]);
+    return optics_f64(ctx.get(), ctx.stream(), flat.data(), (int64_t)points.size(), (int)D, min_pts, epsilon);
 }
 
+}  // namespace
+
+std::vector<reachability_dist> optics_f64_export(ecc_ctx *ctx, ecc_stream_t s, const double *pts, int64_t n, int D,
+                                                 std::size_t min_pts, double epsilon) {
+    return optics_f64(ctx, s, pts, n, D, min_pts, epsilon);
+}
+
+std::vector<reachability_dist> compute_reachability_dists(Context &ctx, const std::vector<std::array<int, 2>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return optics_points(ctx, points, min_pts, epsilon);
+}
+std::vector<reachability_dist> compute_reachability_dists(Context &ctx, const std::vector<std::array<int, 3>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return optics_points(ctx, points, min_pts, epsilon);
+}
+std::vector<reachability_dist> compute_reachability_dists(Context &ctx, const std::vector<std::array<double, 1>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return optics_points(ctx, points, min_pts, epsilon);
+}
+std::vector<reachability_dist> compute_reachability_dists(Context &ctx, const std::vector<std::array<double, 2>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return optics_points(ctx, points, min_pts, epsilon);
+}
+std::vector<reachability_dist> compute_reachability_dists(Context &ctx, const std::vector<std::array<double, 3>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return optics_points(ctx, points, min_pts, epsilon);
+}
+std::vector<reachability_dist> compute_reachability_dists(const std::vector<std::array<int, 2>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return optics_points(Context::default_context(), points, min_pts, epsilon);
+}
+std::vector<reachability_dist> compute_reachability_dists(const std::vector<std::array<int, 3>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return optics_points(Context::default_context(), points, min_pts, epsilon);
+}
+std::vector<reachability_dist> compute_reachability_dists(const std::vector<std::array<double, 1>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return optics_points(Context::default_context(), points, min_pts, epsilon);
+}
 std::vector<reachability_dist> compute_reachability_dists(const std::vector<std::array<double, 2>> &points,
                                                           std::size_t min_pts, double epsilon) {
-    std::vector<std::array<int, 2>> ip(points.size());
-    for (size_t i = 0; i < points.size(); ++i)
-        for (int d = 0; d < 2; ++d) {
-            const double v = points[i][d];
-            if (v != std::floor(v) || std::fabs(v) > 1e9)
-                throw Error(ECC_ERR_INVALID, "compute_reachability_dists: GPU path needs integer-valued coordinates");
-            ip[i][d] = (int)v;
-        }
-    if (epsilon <= 0.0) epsilon = epsilon_estimation(points, min_pts);
-    return compute_reachability_dists(Context::default_context(), ip, min_pts, epsilon);
+    return optics_points(Context::default_context(), points, min_pts, epsilon);
+}
+std::vector<reachability_dist> compute_reachability_dists(const std::vector<std::array<double, 3>> &points,
+                                                          std::size_t min_pts, double epsilon) {
+    return optics_points(Context::default_context(), points, min_pts, epsilon);
 }
 
 std::vector<std::vector<std::size_t>> get_cluster_indices(const std::vector<reachability_dist> &rd,
@@ -589,3 +676,43 @@ void DBSCANSimpleCluster::extract(std::vector<PointIndices> &cluster_indices) { 
 }
 
 }  // namespace ecc
+
+// C ABI of the OPTICS entry (optics::compute_reachability_dists, OPT/include/optics/optics.hpp:
+// 413-565) for bindings: HOST points in, HOST ordering out.
+extern "C" __attribute__((visibility("default"))) int ecc_optics_f64(ecc_ctx *ctx, const double *pts, int64_t n,
+                                                                    int32_t dim, int32_t min_pts, double eps,
+                                                                    int64_t *order, double *reach, ecc_stream_t stream) {
+    if (!ctx || n < 0 || (n > 0 && (!pts || !order || !reach)) || dim < 1 || dim > 3) return ECC_ERR_INVALID;
+    try {
+        if (n == 0) return ECC_OK;
+        if (eps <= 0.0) {  // optics.hpp:369-387 (bounding box max from points[1], Q20)
+            if (n <= 1) {
+                eps = 0.0;
+            } else {
+                double mn[3], mx[3];
+                for (int d = 0; d < dim; ++d) { mn[d] = pts[d]; mx[d] = pts[dim + d]; }
+                for (int64_t i = 0; i < n; ++i)
+                    for (int d = 0; d < dim; ++d) {
+                        if (pts[i * dim + d] < mn[d]) mn[d] = pts[i * dim + d];
+                        if (pts[i * dim + d] > mx[d]) mx[d] = pts[i * dim + d];
+                    }
+                double vol = 1;
+                for (int d = 0; d < dim; ++d) vol *= std::abs(mx[d] - mn[d]);
+                const double dd = (double)dim;
+                const double space = (vol / (double)n) * (double)min_pts;
+                const double ball = std::sqrt(std::pow(M_PI, dd)) / std::tgamma(dd / 2.0 + 1.0);
+                eps = std::pow(space / ball, 1.0 / dd);
+            }
+        }
+        const auto r = ecc::optics::optics_f64_export(ctx, stream, pts, n, dim, (std::size_t)min_pts, eps);
+        for (int64_t i = 0; i < n; ++i) {
+            order[i] = (int64_t)r[i].point_index;
+            reach[i] = r[i].reach_dist;
+        }
+        return ECC_OK;
+    } catch (const ecc::Error &e) {
+        return e.status();
+    } catch (...) {
+        return ECC_ERR_NOMEM;
+    }
+}

@@ -391,6 +391,33 @@ int ecc_eps_lists(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_
 int ecc_eps_total(ecc_ctx *ctx, const int64_t *offsets, int64_t n, int64_t *total,
                   ecc_stream_t stream);
 
+/* Radius neighbourhoods of ONE fp64 point set of any size in 1-3 dimensions (the OPTICS
+ * library's radius search, §8a rows a11-a12, beyond the int 2-D windows above).
+ * Reference: kdt::KDTree::radius_search OPT/include/optics/kdTree.hpp:407-422 (keep i iff
+ *   square_distance(points[i], p) <= radius*radius, square_distance = sum of d*d in double with
+ *   d = p1[i] - p2[i], :180-192; self included); optics::compute_core_dist optics.hpp:286-299.
+ * pts: DEVICE double[n*dim] row-major.  counts[i] = |ball(i)|; core_dist[i] = sqrt of the
+ * (min_pts-1)-th smallest squared distance in the ball, or -1 below min_pts (NULL to skip).
+ * ecc_radius_lists_f64: offsets[n+1] = exclusive scan of counts (computed here); with nbr ==
+ * NULL only the offsets (offsets[n] = entries needed); else nbr[offsets[i]..offsets[i+1]) = the
+ * ball's indices in grid order (the OPTICS expansion does not depend on it) and, when nbr_dist
+ * is not NULL, their distances sqrt(square_distance) (geom::dist, optics.hpp:326);
+ * ecc_radius_status reports ECC_ERR_CAPACITY if nbr_cap was too small.  Deterministic counts
+ * and core distances. */
+int ecc_radius_counts_f64(ecc_ctx *ctx, const double *pts, int64_t n, int32_t dim, double eps,
+                          int32_t min_pts, int32_t *counts, double *core_dist, ecc_stream_t stream);
+int ecc_radius_lists_f64(ecc_ctx *ctx, const double *pts, int64_t n, int32_t dim, double eps,
+                         const int32_t *counts, int64_t *offsets, int32_t *nbr, double *nbr_dist,
+                         int64_t nbr_cap, ecc_stream_t stream);
+int ecc_radius_status(ecc_ctx *ctx, ecc_stream_t stream);
+
+/* OPTICS ordering (optics::compute_reachability_dists, optics.hpp:413-565): HOST pts[n*dim]
+ * (dim 1-3) in; the GPU radius search above, then the ordered seed-set expansion on the host.
+ * eps <= 0: epsilon_estimation (:369-387).  order[i] = point index of the i-th ordered point,
+ * reach[i] = its reachability (-1 undefined).  Synchronises `stream`. */
+int ecc_optics_f64(ecc_ctx *ctx, const double *pts, int64_t n, int32_t dim, int32_t min_pts, double eps,
+                   int64_t *order, double *reach, ecc_stream_t stream);
+
 /* DBSCAN cluster extraction over the eps-lists.
  * Reference: DBSCANSimpleCluster::extract PCC/DBSCAN_simple.h:27-90 (seed-queue expansion in
  *   point order, clusters kept when min_cluster_size <= size <= max_cluster_size, each

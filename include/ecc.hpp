@@ -375,17 +375,34 @@ struct reachability_dist {  // optics.hpp:57-65
 bool operator<(const reachability_dist &lhs, const reachability_dist &rhs);   // :67-69
 bool operator==(const reachability_dist &lhs, const reachability_dist &rhs);  // :70-72
 
-// eps-neighbourhoods and core distances on the GPU (integer-valued 2-D points, <= 16384 per
-// call), ordered seed-set expansion on the host (sequential by nature, :525-555).
-// epsilon <= 0: estimated with epsilon_estimation (:428-430).  Throws ecc::Error
-// (ECC_ERR_INVALID) for non-integer coordinates or spans beyond 65535.
+// eps-balls, core distances and neighbour lists on the GPU for any number of points in 1-3
+// dimensions (ecc_radius_*_f64: one global cell grid, fp64 distances in the reference's
+// operation order), the ordered seed-set expansion on the host (sequential by nature,
+// :525-555).  The reference's template N (points.size() must equal it, :422-425) is the runtime
+// size.  epsilon <= 0: estimated with epsilon_estimation (:428-430).
 std::vector<reachability_dist> compute_reachability_dists(
     const std::vector<std::array<int, 2>> &points, std::size_t min_pts, double epsilon = -1.0);
 std::vector<reachability_dist> compute_reachability_dists(
+    const std::vector<std::array<int, 3>> &points, std::size_t min_pts, double epsilon = -1.0);
+std::vector<reachability_dist> compute_reachability_dists(
+    const std::vector<std::array<double, 1>> &points, std::size_t min_pts, double epsilon = -1.0);
+std::vector<reachability_dist> compute_reachability_dists(
     const std::vector<std::array<double, 2>> &points, std::size_t min_pts, double epsilon = -1.0);
 std::vector<reachability_dist> compute_reachability_dists(
-    Context &ctx, const std::vector<std::array<int, 2>> &points, std::size_t min_pts,
-    double epsilon = -1.0);
+    const std::vector<std::array<double, 3>> &points, std::size_t min_pts, double epsilon = -1.0);
+std::vector<reachability_dist> compute_reachability_dists(
+    Context &ctx, const std::vector<std::array<int, 2>> &points, std::size_t min_pts, double epsilon = -1.0);
+std::vector<reachability_dist> compute_reachability_dists(
+    Context &ctx, const std::vector<std::array<int, 3>> &points, std::size_t min_pts, double epsilon = -1.0);
+std::vector<reachability_dist> compute_reachability_dists(
+    Context &ctx, const std::vector<std::array<double, 1>> &points, std::size_t min_pts, double epsilon = -1.0);
+std::vector<reachability_dist> compute_reachability_dists(
+    Context &ctx, const std::vector<std::array<double, 2>> &points, std::size_t min_pts, double epsilon = -1.0);
+std::vector<reachability_dist> compute_reachability_dists(
+    Context &ctx, const std::vector<std::array<double, 3>> &points, std::size_t min_pts, double epsilon = -1.0);
+// the same over a raw host array of n D-dim points (the ecc_optics_f64 C ABI)
+std::vector<reachability_dist> optics_f64_export(ecc_ctx *ctx, ecc_stream_t s, const double *pts, int64_t n, int D,
+                                                 std::size_t min_pts, double epsilon);
 
 template <typename T, std::size_t dimension>
 double epsilon_estimation(const std::vector<std::array<T, dimension>> &points, std::size_t min_pts);

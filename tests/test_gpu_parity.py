@@ -1113,3 +1113,90 @@ def test_kmeans_count_images_sum_over_shards(ecc, orc, gpu):
     cnt = ecc.DeviceArray(W * H, np.uint32)
     ecc.check(lib.ecc_kmeans_counts_xy16(gpu.ctx, dev(ecc, bad).ptr, 1, 1, None, W, H, cnt.ptr, gpu.stream))
     assert lib.ecc_kmeans_counts_status(gpu.ctx, gpu.stream) == ecc.ERR_INVALID
+
+
+# ------------------------------------------------------------------------------ fp64 radius / OPTICS
+def _brute_ball(pts, i, eps2):
+    """square_distance (kdTree.hpp:180-192) in the same operation order, vectorised."""
+    s = np.zeros(len(pts))
+    for d in range(pts.shape[1]):
+        dd = pts[:, d] - pts[i, d]
+        s = s + dd * dd
+    return s <= eps2, s
+
+
+@pytest.mark.parametrize("dim,n,eps,min_pts,kind", [
+    (2, 3000, 0.02, 10, "uniform"), (3, 3000, 0.06, 10, "uniform"), (1, 2000, 0.001, 4, "uniform"),
+    (2, 3000, 1.5, 20, "blobs"), (3, 2500, 2.0, 64, "blobs"), (2, 1500, 0.0, 1, "dups"),
+])
+def test_radius_f64_matches_brute_force(ecc, gpu, dim, n, eps, min_pts, kind):
+    rng = np.random.default_rng(dim * 100 + n)
+    if kind == "uniform":
+        pts = rng.random((n, dim))
+    elif kind == "blobs":
+        pts = rng.normal(0, 3, (n, dim)) + rng.integers(0, 4, (n, 1)) * 25.0
+    else:  # many exact duplicates (eps 0: the ball is the set of equal points)
+        pts = rng.integers(0, 30, (n, dim)).astype(np.float64)
+    d_pts = dev(ecc, pts)
+    cnt = ecc.DeviceArray(n, np.int32)
+    core = ecc.DeviceArray(n, np.float64)
+    gpu.radius_counts_f64(d_pts, n, dim, eps, min_pts, cnt, core)
+    off = ecc.DeviceArray(n + 1, np.int64)
+    gpu.radius_lists_f64(d_pts, n, dim, eps, cnt, off, None, 0)
+    gpu.sync()
+    total = int(off.numpy()[n])
+    nbr = ecc.DeviceArray(max(total, 1), np.int32)
+    nd = ecc.DeviceArray(max(total, 1), np.float64)
+    gpu.radius_lists_f64(d_pts, n, dim, eps, cnt, off, nbr, total, nd)
+    gpu.sync()
+    assert gpu.radius_status() == 0
+    g_cnt, g_core, g_off, g_nbr, g_nd = cnt.numpy(), core.numpy(), off.numpy(), nbr.numpy(), nd.numpy()
+    eps2 = eps * eps
+    for i in range(n):
+        ball, s = _brute_ball(pts, i, eps2)
+        idx = np.nonzero(ball)[0]
+        assert g_cnt[i] == len(idx), i
+        lst = g_nbr[g_off[i]:g_off[i + 1]]
+        assert sorted(lst.tolist()) == idx.tolist(), i
+        assert np.array_equal(g_nd[g_off[i]:g_off[i + 1]], np.sqrt(s[lst])), i
+        want = np.sqrt(np.sort(s[idx])[min_pts - 1]) if len(idx) >= min_pts else -1.0
+        assert g_core[i] == want, (i, g_core[i], want)
+
+
+def test_radius_f64_large_sampled(ecc, gpu):
+    """500 000 uniform points (the published benchmark's size): counts of 2000 sampled points
+    against brute force over all points; the list total equals the sum of the counts."""
+    n, dim, eps = 500_000, 2, 0.0025
+    rng = np.random.default_rng(5)
+    pts = rng.random((n, dim))
+    d_pts = dev(ecc, pts)
+    cnt = ecc.DeviceArray(n, np.int32)
+    gpu.radius_counts_f64(d_pts, n, dim, eps, 1, cnt, None)
+    off = ecc.DeviceArray(n + 1, np.int64)
+    gpu.radius_lists_f64(d_pts, n, dim, eps, cnt, off, None, 0)
+    gpu.sync()
+    g_cnt = cnt.numpy()
+    assert int(off.numpy()[n]) == int(g_cnt.sum())
+    for i in rng.choice(n, 2000, replace=False):
+        ball, _ = _brute_ball(pts, i, eps * eps)
+        assert g_cnt[i] == int(ball.sum()), i
+
+
+@pytest.mark.parametrize("dim,n,min_pts,eps,kind", [
+    (2, 2000, 10, -1.0, "uniform"), (3, 2000, 10, -1.0, "uniform"), (2, 1500, 5, 1.0, "blobs"),
+    (1, 1000, 3, -1.0, "uniform"), (2, 1200, 2, 10.0, "pixels"),
+])
+def test_optics_f64_matches_oracle(ecc, orc, gpu, dim, n, min_pts, eps, kind):
+    """The C ABI OPTICS (GPU eps-balls + host heap expansion) against the oracle's literal
+    std::set expansion over brute-force balls: identical ordering and reachabilities."""
+    rng = np.random.default_rng(n + dim)
+    if kind == "uniform":
+        pts = rng.random((n, dim))
+    elif kind == "blobs":
+        pts = rng.normal(0, 2, (n, dim)) + rng.integers(0, 5, (n, 1)) * 15.0
+    else:  # integer pixels with duplicates (the event drivers' case, cluster_event_data.cpp)
+        pts = rng.integers(0, 120, (n, dim)).astype(np.float64)
+    g_order, g_reach = gpu.optics_f64(pts, min_pts, eps)
+    o_order, o_reach = orc.optics(pts, min_pts, eps)
+    assert np.array_equal(g_order, o_order)
+    assert np.array_equal(g_reach.view(np.uint64), o_reach.view(np.uint64))
