@@ -726,6 +726,26 @@ def cpu_leg(ecc, args, W, H, K, I, xy, t, n, c0, ctx, g):
             "sample": f"the step's full batch: {n} events, same pipeline (oracle/oracle.cpp, 1 thread, "
                       f"downsample + k-means + SAE/arc + NMS); {dt:.2f} s; host {model}, nproc={os.cpu_count()}"}
 
+    # all-cores variant (oracle/cpu_omp.cpp): same pipeline, the parallel stages over every host
+    # thread (OMP_NUM_THREADS); its outputs must equal the 1-thread oracle's
+    nt = orc.omp_threads()
+    t0 = time.perf_counter()
+    p_rx, _, p_u, p_r = orc.omp_downsample_hash(xy)
+    p_dense = np.concatenate([p_rx[w * WINDOW: w * WINDOW + p_u[w]] for w in range(len(p_u))])
+    p_c, p_lab, _ = orc.omp_kmeans_run_xy16(p_dense, c0, I)
+    p_flags, p_sae = orc.omp_fast_detect(xy, t, W, H)
+    p_out, p_cnt, _ = orc.omp_corner_nms(xy, p_flags, W, H, cap=g["cap"])
+    dt_omp = time.perf_counter() - t0
+    omp_same = bool(np.array_equal(p_u, o_u) and np.array_equal(p_r, o_r) and np.array_equal(p_dense, dense)
+                    and np.array_equal(p_c.view(np.uint32), o_c.view(np.uint32)) and np.array_equal(p_lab, o_lab)
+                    and np.array_equal(p_flags, o_flags) and np.array_equal(p_sae, o_sae)
+                    and np.array_equal(p_cnt, o_cnt) and nms_mismatches(p_out, p_cnt, o_out, o_cnt, g["cap"])[0] == 0)
+    base["all_cores"] = {
+        "value": round(n / dt_omp / 1e6, 3), "unit": "Mevents/s", "cores": nt, "kind": "port",
+        "equals_single_thread": omp_same,
+        "sample": f"same {n} events and pipeline, oracle/cpu_omp.cpp (OpenMP, {nt} threads: windows, k-means "
+                  f"assignment, per-slice arc tests, per-slice NMS in parallel; SAE update sequential); {dt_omp:.2f} s"}
+
     par = {"events": n}
     u, r = g["uniq"].numpy(), g["rep"].numpy()
     par["downsample_windows_mismatch"] = int(np.count_nonzero(u != o_u) + np.count_nonzero(r != o_r))

@@ -321,3 +321,78 @@ def aec_run(rep_xy, win_unique, stride=8192, sz_buffer=800, radius=40.0, kappa=0
         if k <= cap:
             return rows[:k].copy(), cpw[:nw].copy()
         cap = int(k)
+
+
+# ------------------------------------------------------------------------------------------
+# All-cores CPU baseline (oracle/cpu_omp.cpp, OpenMP): the same restatement with its parallel
+# stages spread over the host's threads (OMP_NUM_THREADS).  Same outputs as the functions above.
+# ------------------------------------------------------------------------------------------
+OMP_LIB_PATH = ORACLE_DIR / "libcpu_omp.so"
+_omp = None
+
+
+def omp_lib():
+    global _omp
+    if _omp is None:
+        if not OMP_LIB_PATH.exists():
+            build()
+        _omp = C.CDLL(str(OMP_LIB_PATH))
+        for _n, (_r, _a) in {
+            "omp_threads": (C.c_int, []),
+            "omp_downsample_hash": _sigs["orc_downsample_hash"],
+            "omp_kmeans_run_xy16": _sigs["orc_kmeans_run_xy16"],
+            "omp_fast_detect": _sigs["orc_fast_detect"],
+            "omp_corner_nms": _sigs["orc_corner_nms"],
+        }.items():
+            f = getattr(_omp, _n)
+            f.restype = _r
+            f.argtypes = _a
+    return _omp
+
+
+def omp_threads():
+    return omp_lib().omp_threads()
+
+
+def omp_downsample_hash(xy, window=8192, x_max=1280, y_max=720, mult_x=1619, mult_y=31, nb=8192):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    n = len(xy)
+    nw = (n + window - 1) // window
+    rep_xy = np.zeros(nw * window, np.uint32)
+    rep_idx = np.zeros(nw * window, np.uint32)
+    u = np.zeros(nw, np.int32)
+    r = np.zeros(nw, np.int32)
+    rc = omp_lib().omp_downsample_hash(_p(xy), n, window, x_max, y_max, mult_x, mult_y, nb, _p(rep_xy),
+                                       _p(rep_idx), _p(u), _p(r))
+    assert rc == 0
+    return rep_xy, rep_idx, u, r
+
+
+def omp_kmeans_run_xy16(xy, centroids, max_iters, thr=50.0, tol=-1.0):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    c = np.array(centroids, np.float32).copy()
+    lab = np.zeros(len(xy), np.uint8)
+    it = np.zeros(1, np.int32)
+    omp_lib().omp_kmeans_run_xy16(_p(xy), len(xy), _p(c), c.size // 2, max_iters, thr, tol, _p(lab), _p(it))
+    return c, lab, int(it[0])
+
+
+def omp_fast_detect(xy, t, W, H, slice_events=16384, margin=4, border_mode=0, first_detect=1):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    t = np.ascontiguousarray(t, np.int64)
+    sae = np.zeros(W * H, np.int64)
+    flags = np.zeros(len(xy), np.uint8)
+    rc = omp_lib().omp_fast_detect(_p(xy), _p(t), len(xy), W, H, slice_events, margin, border_mode,
+                                   first_detect, _p(sae), _p(flags))
+    assert rc == 0
+    return flags, sae
+
+
+def omp_corner_nms(xy, flags, W, H, slice_events=16384, box=15, cap=4096):
+    xy = np.ascontiguousarray(xy, np.uint32)
+    flags = np.ascontiguousarray(flags, np.uint8)
+    ns = (len(xy) + slice_events - 1) // slice_events
+    out = np.zeros(ns * cap, CORNER_DTYPE)
+    counts = np.zeros(ns, np.int32)
+    rc = omp_lib().omp_corner_nms(_p(xy), _p(flags), len(xy), slice_events, W, H, box, cap, _p(out), _p(counts))
+    return out, counts, rc

@@ -254,3 +254,28 @@ def test_dedup_exact_oracle_equals_numpy(orc):
         assert u[w] == len(keys)
         assert (idx[w * 8192: w * 8192 + u[w]] == first[order] + w * 8192).all()
         assert (cnt[w * 8192: w * 8192 + u[w]] == counts[order]).all()
+
+
+# ---------------------------------------------------------------- all-cores baseline (oracle/cpu_omp.cpp)
+def test_omp_baseline_equals_single_thread_oracle(orc, ecc):
+    """The OpenMP CPU baseline bench.py times beside the 1-thread one returns exactly the 1-thread
+    oracle's outputs: downsample windows, k-means centroids + labels, corner flags + SAE, NMS."""
+    W, H = 346, 260
+    xy, t, _ = ecc.gen_events(300_000, seed=11, width=W, height=H)
+    a, b = orc.downsample_hash(xy), orc.omp_downsample_hash(xy)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    rx, _, u, _ = a
+    dense = np.concatenate([rx[w * 8192: w * 8192 + u[w]] for w in range(len(u))])
+    c0 = np.array([40, 40, 100, 60, 180, 90, 250, 130, 300, 200, 60, 220, 150, 180, 320, 40], np.float32)
+    oc, ol, oi = orc.kmeans_run_xy16(dense, c0, 10)
+    pc, pl, pi = orc.omp_kmeans_run_xy16(dense, c0, 10)
+    assert oi == pi and np.array_equal(oc.view(np.uint32), pc.view(np.uint32)) and np.array_equal(ol, pl)
+    of, osae = orc.fast_detect(xy, t, W, H)
+    pf, psae = orc.omp_fast_detect(xy, t, W, H)
+    assert of.sum() > 0 and np.array_equal(of, pf) and np.array_equal(osae, psae)
+    oo, ocnt, orc_rc = orc.corner_nms(xy, of, W, H)
+    po, pcnt, p_rc = orc.omp_corner_nms(xy, of, W, H)
+    assert orc_rc == p_rc and np.array_equal(ocnt, pcnt)
+    for s in range(len(ocnt)):
+        assert np.array_equal(oo[s * 4096: s * 4096 + ocnt[s]], po[s * 4096: s * 4096 + pcnt[s]])
