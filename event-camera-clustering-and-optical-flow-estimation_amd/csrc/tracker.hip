@@ -59,7 +59,9 @@ struct DevGroup {
 };
 
 struct TrackerCounters {
-    int32_t n_tracks, next_label, cur, n_groups, n_group_labels, err, pad0, pad1;
+    int32_t n_tracks, next_label, cur, n_groups, n_group_labels, err;
+    int32_t resume;  // first slice of the launch left to tracker_kernel (tracker_fast_kernel stopped there)
+    int32_t pad1;
 };
 
 struct TrackerParams {
@@ -280,8 +282,11 @@ struct GroupLds {
     unsigned *rad;
 };
 
+// `put(new_index, vx, vy, group_id)` stores a candidate's blended velocity and group id: into the
+// next global track list (tracker_kernel) or into the LDS-resident list (tracker_fast_kernel).
+template <class Put>
 __device__ __forceinline__ void group_slice(const GroupLds L, int G, bool last, const TrackerParams p, int max_tracks,
-                                         DevTrack *Bf, DevGroup *__restrict__ groups, int *__restrict__ group_labels,
+                                         Put &&put, DevGroup *__restrict__ groups, int *__restrict__ group_labels,
                                          int *n_groups_out, int *n_glabels_out) {
     const int lane = threadIdx.x & 63;
     int n_groups = 0, n_glabels = 0;
@@ -373,10 +378,7 @@ __device__ __forceinline__ void group_slice(const GroupLds L, int G, bool last, 
                 vx = __fadd_rn(__fmul_rn(vx, 0.7f), __fmul_rn(g.x, 0.3f));
                 vy = __fadd_rn(__fmul_rn(vy, 0.7f), __fmul_rn(g.y, 0.3f));
             }
-            DevTrack *dst = Bf + mtidx;
-            dst->vx = vx;
-            dst->vy = vy;
-            dst->group_id = mgid;
+            put(mtidx, vx, vy, mgid);
         }
     } else {
         for (int k = lane; k < G; k += 64) L.ck_proc[k] = 0;
@@ -462,10 +464,7 @@ __device__ __forceinline__ void group_slice(const GroupLds L, int G, bool last, 
                 vx = __fadd_rn(__fmul_rn(vx, 0.7f), __fmul_rn(g.x, 0.3f));
                 vy = __fadd_rn(__fmul_rn(vy, 0.7f), __fmul_rn(g.y, 0.3f));
             }
-            DevTrack *dst = Bf + L.ck_tidx[k];
-            dst->vx = vx;
-            dst->vy = vy;
-            dst->group_id = gid;
+            put((int)L.ck_tidx[k], vx, vy, gid);
         }
     }
     *n_groups_out = n_groups;
@@ -535,13 +534,15 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
     // grid matching for sane radii; otherwise every scan walks all detections
     const bool grid_ok = p.max_distance >= 0.0f && p.max_distance < 1.0e5f;
     const int cell = grid_ok ? (int)ceilf(reach) + 1 : 1;
+    const int s0 = ctr->resume;  // slices before it were processed by tracker_fast_kernel
+    if (s0 >= n_slices) return;
     int T = ctr->n_tracks, next_label = ctr->next_label, cur = ctr->cur, err = ctr->err;
     int n_groups = 0, n_glabels = 0;
 #if ECC_TRACKER_PROFILE
     unsigned long long prof[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, last_ = wall_clock64();
     const unsigned long long c0_ = clock64(), w0_ = last_;
 #endif
-    for (int s = 0; s < n_slices; ++s) {
+    for (int s = s0; s < n_slices; ++s) {
         DevTrack *A = cur ? buf1 : buf0;   // active tracks
         DevTrack *Bf = cur ? buf0 : buf1;  // next active list
         int C = counts[s];
@@ -901,7 +902,14 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
         if (wave == 0)
             group_slice(GroupLds{ck_x, ck_y, ck_label, ck_tidx, ck_vx, ck_vy, ck_gid, ck_proc, gav,
                                  s_gmem, s_goff, stage, &s_rad},
-                        G, s == n_slices - 1, p, max_tracks, Bf, groups, group_labels, &n_groups, &n_glabels);
+                        G, s == n_slices - 1, p, max_tracks,
+                        [Bf](int k, float vx, float vy, int gid) {
+                            DevTrack *dst = Bf + k;
+                            dst->vx = vx;
+                            dst->vy = vy;
+                            dst->group_id = gid;
+                        },
+                        groups, group_labels, &n_groups, &n_glabels);
         __syncthreads();
         TRK_MARK(4);
     }
@@ -923,6 +931,562 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
     }
 }
 
+
+// ---- tracker_fast_kernel: the slice loop with every track in a register file --------------------
+// The common regime (tens of tracks and detections per slice) is bound by latency, not work: the
+// 512-lane kernel above spends most of a slice on global round trips (its track list lives in
+// HBM between phases) and on workgroup barriers.  Here one 256-lane workgroup (one wave per
+// SIMD) keeps track i in the registers of thread i for the whole launch; a slice moves the list
+// through LDS only to apply the stable erase, detections are prefetched one slice ahead, and the
+// matching rounds read the in-range detections each track found in its first scan from
+// registers.  The arithmetic, the matching rule and the grouping are tracker_kernel's (same
+// helpers, same operation order), so the state is bit-identical.  A slice with T + C > 256
+// (tracks + detections) hands the rest of the launch to tracker_kernel: the list is written to
+// the current buffer and ctr->resume = that slice.
+constexpr int kFT = 256;    // threads = the largest T + C of a slice handled here
+constexpr int kFList = 8;   // in-range detections a track keeps in registers (more: it rescans)
+constexpr int kFTagTop = (1 << 23) - 1;  // round tags: ((kFTagTop - round) << 8) | track
+static_assert(kFT <= 256, "track index packs into 8 bits of the matching tag");
+
+struct FastList {  // the track list, structure of arrays (conflict-free LDS)
+    int x[kFT], y[kFT], label[kFT], frame_count[kFT], is_matched[kFT], fsld[kFT], hist_len[kFT];
+    int hx[kH][kFT], hy[kH][kFT];
+    float vx[kFT], vy[kFT], dcx[kFT], dcy[kFT], dtx[kFT], dty[kFT];
+    int group_id[kFT];
+    float ux[kH][kFT], uy[kH][kFT];  // direction cache (FastTrack)
+    uint32_t um[kFT];
+};
+
+// A track plus its direction cache: u[i] = the normalised step h[i-1] - h[i] of its history and
+// bit i of um = that step is non-zero (calc_direction's `magnitude > 0`, :250).  A step's unit
+// vector depends only on its integer difference, so after push_hist the old u[i-1] is the new
+// u[i] bit for bit and only u[1] is computed; calc_direction then sums the cached terms in its
+// own order (one sqrt + one divide per slice instead of one per history step).
+struct FastTrack {
+    DevTrack t;
+    float ux[kH], uy[kH];
+    uint32_t um;
+};
+
+__device__ __forceinline__ void unit_step(const DevTrack &t, int i, float &ux, float &uy, bool &nz) {  // :244-252
+    F2 d{(float)(t.hx[i - 1] - t.hx[i]), (float)(t.hy[i - 1] - t.hy[i])};
+    const float mag = norm(d);
+    nz = mag > 0.f;
+    d = mul(d, __fdiv_rn(1.0f, mag));
+    ux = d.x;
+    uy = d.y;
+}
+
+__device__ __forceinline__ void cache_all(FastTrack &f) {
+    f.um = 0u;
+    f.ux[0] = f.uy[0] = 0.f;
+#pragma unroll
+    for (int i = 1; i < kH; ++i) {
+        bool nz;
+        unit_step(f.t, i, f.ux[i], f.uy[i], nz);
+        f.um |= nz ? (1u << i) : 0u;
+    }
+}
+
+// push_hist + the cache shift + the new step u[1]
+__device__ __forceinline__ void push_hist_cached(FastTrack &f, int history) {
+    push_hist(f.t, history);
+#pragma unroll
+    for (int i = kH - 1; i > 1; --i) { f.ux[i] = f.ux[i - 1]; f.uy[i] = f.uy[i - 1]; }
+    bool nz;
+    unit_step(f.t, 1, f.ux[1], f.uy[1], nz);
+    f.um = ((f.um << 1) & ~3u) | (nz ? 2u : 0u);
+}
+
+__device__ __forceinline__ F2 calc_direction_cached(const FastTrack &f, const TrackerParams &p) {  // :233-271
+    if (f.t.hist_len < 2) return F2{0.f, 0.f};
+    F2 w{0.f, 0.f};
+    float total = 0.f;
+#pragma unroll
+    for (int i = 1; i < kH; ++i) {
+        if (i < f.t.hist_len && ((f.um >> i) & 1u)) {
+            const float wt = p.pow_tab[i - 1];
+            w = add(w, mul(F2{f.ux[i], f.uy[i]}, wt));
+            total = __fadd_rn(total, wt);
+        }
+    }
+    if (total > 0.f) {
+        w = mul(w, __fdiv_rn(1.0f, total));
+        const float mag = norm(w);
+        if (mag > 0.f) w = mul(w, __fdiv_rn(1.0f, mag));
+    }
+    return w;
+}
+
+__device__ __forceinline__ void fast_put(FastList &L, int k, const FastTrack &f) {
+    const DevTrack &t = f.t;
+#pragma unroll
+    for (int h = 0; h < kH; ++h) { L.ux[h][k] = f.ux[h]; L.uy[h][k] = f.uy[h]; }
+    L.um[k] = f.um;
+    L.x[k] = t.x; L.y[k] = t.y; L.label[k] = t.label; L.frame_count[k] = t.frame_count;
+    L.is_matched[k] = t.is_matched; L.fsld[k] = t.fsld; L.hist_len[k] = t.hist_len;
+#pragma unroll
+    for (int h = 0; h < kH; ++h) { L.hx[h][k] = t.hx[h]; L.hy[h][k] = t.hy[h]; }
+    L.vx[k] = t.vx; L.vy[k] = t.vy; L.dcx[k] = t.dcx; L.dcy[k] = t.dcy; L.dtx[k] = t.dtx; L.dty[k] = t.dty;
+    L.group_id[k] = t.group_id;
+}
+
+__device__ __forceinline__ FastTrack fast_get(const FastList &L, int k) {
+    FastTrack f;
+#pragma unroll
+    for (int h = 0; h < kH; ++h) { f.ux[h] = L.ux[h][k]; f.uy[h] = L.uy[h][k]; }
+    f.um = L.um[k];
+    DevTrack &t = f.t;
+    t.x = L.x[k]; t.y = L.y[k]; t.label = L.label[k]; t.frame_count = L.frame_count[k];
+    t.is_matched = L.is_matched[k]; t.fsld = L.fsld[k]; t.hist_len = L.hist_len[k];
+#pragma unroll
+    for (int h = 0; h < kH; ++h) { t.hx[h] = L.hx[h][k]; t.hy[h] = L.hy[h][k]; }
+    t.vx = L.vx[k]; t.vy = L.vy[k]; t.dcx = L.dcx[k]; t.dcy = L.dcy[k]; t.dtx = L.dtx[k]; t.dty = L.dty[k];
+    t.group_id = L.group_id[k];
+    return f;
+}
+
+__global__ void __launch_bounds__(kFT)
+tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restrict__ groups,
+                    int *__restrict__ group_labels, TrackerCounters *__restrict__ ctr, TrackerParams p,
+                    const ecc_corner *__restrict__ corners, const int64_t *__restrict__ starts,
+                    const int32_t *__restrict__ counts, int n_slices, int cap) {
+    __shared__ FastList L;                     // next track list (P3), velocities blended in P4
+    FastList *const Lp = &L;
+    __shared__ int2 f_det[kFT];
+    __shared__ float2 f_detf[kFT + 32];         // as floats (+32: a scan chunk never reads past it)
+    __shared__ int16_t f_li[kFList][kFT];       // a round-0 lane's in-range detections
+    __shared__ float f_ld[kFList][kFT];         // and their distances
+    __shared__ int16_t f_mi[kFList][kFT];       // a track's in-range detections (merged over its lanes)
+    __shared__ float f_md[kFList][kFT];
+    __shared__ int8_t f_mn[kFT];                // their number (-1: more than kFList, rescan)
+    __shared__ int16_t f_best[kFT];             // round 0's choice of track i
+    __shared__ float2 f_pp[kFT];                // predictions
+    __shared__ int8_t f_st[kFT];                // P1 states
+    __shared__ int16_t f_tail[64];              // matching tail: the unresolved tracks, in order
+    __shared__ int16_t f_res[kFT];              //   and their results
+    __shared__ int f_want[kFT + 1];             // [kFT]: sink of the tail's masked-off atomics
+    __shared__ uint8_t f_claim[kFT + 1];        // [kFT]: always claimed
+    __shared__ int f_ws[3 * (kFT / 64)];
+    __shared__ int ck_x[kFT], ck_y[kFT], ck_label[kFT], ck_gid[kFT];
+    __shared__ int16_t ck_tidx[kFT];
+    __shared__ float ck_vx[kFT], ck_vy[kFT];
+    __shared__ uint8_t ck_proc[kFT];
+    __shared__ float2 gav[kFT];
+    __shared__ uint64_t gmem[64];
+    __shared__ int goff[64];
+    __shared__ float4 gstage[64];
+    __shared__ unsigned grad;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int T = ctr->n_tracks, next_label = ctr->next_label, err = ctr->err;
+    DevTrack *A = ctr->cur ? buf1 : buf0;
+    int n_groups = 0, n_glabels = 0;
+    if (T > kFT) {  // uniform: the whole launch is tracker_kernel's
+        if (tid == 0) ctr->resume = 0;
+        return;
+    }
+    FastTrack me;
+    if (tid < T) {
+        me.t = A[tid];
+        cache_all(me);
+    }
+    if (tid == 0) f_claim[kFT] = 1;
+    const int cload = min(cap, kFT);  // detections a slice handled here can have
+    auto first_of = [&](int s) -> int64_t { return starts ? starts[s] : (int64_t)s * cap; };
+    // detection prefetch: slice s's corner in (dnx, dny) of thread d; counts/starts of s + 1
+    int dnx = 0, dny = 0;
+    int c_cur = counts[0];
+    {
+        const int64_t f0 = first_of(0);
+        if (tid < min(max(c_cur, 0), cload)) { dnx = corners[f0 + tid].x; dny = corners[f0 + tid].y; }
+    }
+    int c_nxt = n_slices > 1 ? counts[1] : 0;
+    int64_t f_nxt = n_slices > 1 ? first_of(1) : 0;
+    const bool keep_new = !(0 > p.frames_to_skip || 1 > p.max_frames);
+    int stop = n_slices;
+#if ECC_TRACKER_PROFILE
+    unsigned long long prof[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, last_ = wall_clock64();
+    const unsigned long long c0_ = clock64(), w0_ = last_;
+#endif
+    for (int s = 0; s < n_slices; ++s) {
+        int C = c_cur;
+        const bool over_cap = C > cap;
+        if (over_cap) C = cap;
+        if (C < 0) C = 0;
+        if (T + C > kFT) { stop = s; break; }  // uniform
+        if (over_cap) err = ECC_ERR_CAPACITY;   // beyond max_detections: dropped, reported
+        // P0: detections, claims, matching tags; prefetch of the next slice
+        if (tid < C) {
+            f_det[tid] = make_int2(dnx, dny);
+            f_detf[tid] = make_float2((float)dnx, (float)dny);
+            f_want[tid] = 0x7fffffff;
+            f_claim[tid] = 0;
+        }
+        int pnx = 0, pny = 0, c_nn = 0;
+        int64_t f_nn = 0;
+        if (s + 1 < n_slices && tid < min(max(c_nxt, 0), cload)) { pnx = corners[f_nxt + tid].x; pny = corners[f_nxt + tid].y; }
+        if (s + 2 < n_slices) { c_nn = counts[s + 2]; f_nn = first_of(s + 2); }
+        // P1: prediction (:451) of track tid; -2 skipped (or no track), -3 unresolved, -1 missed,
+        // >= 0 matched
+        int st = -2;
+        F2 pp{0.f, 0.f};
+        if (tid < T) {
+            pp = predict(me.t, p);
+            st = me.t.fsld > p.frames_to_skip ? -2 : (C == 0 ? -1 : -3);
+            f_pp[tid] = make_float2(pp.x, pp.y);
+            f_st[tid] = (int8_t)st;
+        }
+        __syncthreads();
+        TRK_MARK(7);
+        // P2 round 0 with L lanes per track: sub-lane tj scans the 32-detection chunks tj,
+        // tj + L, ... as an unrolled in-range bit mask, then the mask's set bits four at a time
+        // (their loads batched).  A track's choice, the first minimum of dist in detection
+        // order, is the minimum of (dist, index) over its lanes; its in-range detections are
+        // merged into one list (order irrelevant) for the later rounds.
+        {
+            const int lsh = T <= 64 ? 2 : (T <= 128 ? 1 : 0);  // uniform: L = 1 << lsh
+            const int L = 1 << lsh;
+            const int ti = tid >> lsh, tj = tid & (L - 1);
+            const bool act = ti < T && f_st[ti] == -3;
+            const float2 pq = ti < T ? f_pp[ti] : make_float2(0.f, 0.f);
+            const F2 tp{pq.x, pq.y};
+            const int tag0 = (kFTagTop << 8) | ti;
+            int l_n = 0;
+            bool l_ovf = false;
+            int bi = -1;
+            float bd = 0.f;
+            if (act) {
+                for (int c0 = tj * 32; c0 < C; c0 += L * 32) {
+                    const int nc = C - c0;
+                    uint32_t m = 0u;
+#pragma unroll
+                    for (int k = 0; k < 32; ++k) {
+                        const float2 q = f_detf[c0 + k];
+                        m |= (k < nc && dist2(tp, F2{q.x, q.y}) < p.s_match) ? (1u << k) : 0u;
+                    }
+                    while (m) {  // dist < max_distance; dist = sqrt_rn(s2) as dist() rounds it
+                        int d4[4];
+                        bool v4[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            v4[u] = m != 0u;
+                            d4[u] = v4[u] ? c0 + __ffs(m) - 1 : 0;
+                            m &= m - 1u;
+                        }
+                        float dd4[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const float2 q = f_detf[d4[u]];
+                            dd4[u] = ecc::sqrt_rn(dist2(tp, F2{q.x, q.y}));
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (!v4[u]) continue;
+                            const int d = d4[u];
+                            atomicMin(&f_want[d], tag0);
+                            if (bi < 0 || dd4[u] < bd || (dd4[u] == bd && d < bi)) { bd = dd4[u]; bi = d; }
+                            if (l_n < kFList) {
+                                f_li[l_n][tid] = (int16_t)d;
+                                f_ld[l_n][tid] = dd4[u];
+                                ++l_n;
+                            } else {
+                                l_ovf = true;
+                            }
+                        }
+                    }
+                }
+            }
+            // the track's lanes: minimum, list sizes -> merged list offsets
+            int cnt = l_ovf ? kFList + 1 : l_n, incl = cnt;
+            for (int o = 1; o < L; o <<= 1) {
+                const float od = __shfl_xor(bd, o);
+                const int oi = __shfl_xor(bi, o);
+                if (oi >= 0 && (bi < 0 || od < bd || (od == bd && oi < bi))) { bd = od; bi = oi; }
+                const int v = __shfl_up(incl, o, L);
+                if (tj >= o) incl += v;
+            }
+            const int total = __shfl(incl, (lane & ~(L - 1)) + L - 1);
+            if (act && total <= kFList) {
+                const int off = incl - cnt;
+                for (int k = 0; k < l_n; ++k) {
+                    f_mi[off + k][ti] = f_li[k][tid];
+                    f_md[off + k][ti] = f_ld[k][tid];
+                }
+            }
+            if (act && tj == 0) {
+                f_mn[ti] = (int8_t)(total <= kFList ? total : -1);
+                f_best[ti] = (int16_t)bi;
+            }
+        }
+        __syncthreads();
+        if (st == -3) {  // round 0 resolves (owner thread)
+            const int b0 = f_best[tid];
+            if (b0 < 0) {
+                st = -1;
+            } else if (f_want[b0] == ((kFTagTop << 8) | tid)) {
+                st = b0;
+                f_claim[b0] = 1;
+            }
+        }
+        TRK_MARK(8);
+        const int my_n = st == -3 ? f_mn[tid] : 0;  // -1: more than kFList in range (rescan)
+        {
+            // Tail: with <= 64 unresolved tracks and no list overflow, one wave finishes the
+            // rounds with no workgroup barrier (a wave's LDS instructions execute in order);
+            // each round reads the claims of a track's whole list at once (branch-free: a
+            // past-the-list slot reads the always-claimed slot kFT).
+            const bool unres = st == -3;
+            const uint64_t mu = __ballot(unres), mo = __ballot(unres && my_n < 0);
+            if (lane == 0) {
+                f_ws[wave] = __popcll(mu);
+                f_ws[4 + wave] = __popcll(mo);
+            }
+            __syncthreads();
+            int u = __popcll(mu & lanes_below()), n_unres = 0, n_ovf = 0;
+#pragma unroll
+            for (int w = 0; w < kFT / 64; ++w) {
+                u += w < wave ? f_ws[w] : 0;
+                n_unres += f_ws[w];
+                n_ovf += f_ws[4 + w];
+            }
+            if (n_unres > 0 && n_unres <= 64 && n_ovf == 0) {
+                if (unres) f_tail[u] = (int16_t)tid;
+                __syncthreads();
+                if (wave == 0) {
+                    const bool act = lane < n_unres;
+                    const int ti = act ? f_tail[lane] : 0;
+                    const int ln = act ? f_mn[ti] : 0;
+                    int li[kFList];
+                    float ld[kFList];
+#pragma unroll
+                    for (int k = 0; k < kFList; ++k) {
+                        li[k] = k < ln ? f_mi[k][ti] : kFT;
+                        ld[k] = f_md[k][ti];
+                    }
+                    int res = act ? -3 : -2;
+                    for (int r = 1; __ballot(res == -3); ++r) {
+                        const int tg = ((kFTagTop - r) << 8) | ti;
+                        uint8_t cl[kFList];
+#pragma unroll
+                        for (int k = 0; k < kFList; ++k) cl[k] = f_claim[li[k]];
+                        int bi = -1;
+                        float bd = 0.f;
+#pragma unroll
+                        for (int k = 0; k < kFList; ++k) {
+                            if (res != -3 || cl[k]) continue;
+                            atomicMin(&f_want[li[k]], tg);
+                            if (bi < 0 || ld[k] < bd) { bd = ld[k]; bi = li[k]; }
+                        }
+                        if (res == -3 && bi < 0) res = -1;
+                        wave_sync();
+                        if (res == -3 && f_want[bi] == tg) {
+                            res = bi;
+                            f_claim[bi] = 1;
+                        }
+                        wave_sync();
+#if ECC_TRACKER_PROFILE
+                        prof[9] += 1;
+#endif
+                    }
+                    if (act) f_res[ti] = (int16_t)res;
+                }
+                __syncthreads();
+                if (unres) st = f_res[tid];
+            }
+        }
+        // P2 rounds 1.. across the workgroup (many unresolved tracks, or a list overflow)
+        int round = 1;
+        for (; __syncthreads_or(st == -3); ++round) {
+            const int tag = ((kFTagTop - round) << 8) | tid;
+            int best = -1;
+            if (st == -3) {
+                float bd = 0.f;
+                if (my_n >= 0) {
+#pragma unroll
+                    for (int k = 0; k < kFList; ++k) {
+                        if (k >= my_n) break;
+                        const int d = f_mi[k][tid];
+                        if (f_claim[d]) continue;
+                        const float dd = f_md[k][tid];
+                        atomicMin(&f_want[d], tag);
+                        if (best < 0 || dd < bd || (dd == bd && d < best)) { bd = dd; best = d; }
+                    }
+                } else {
+                    for (int d = 0; d < C; ++d) {
+                        if (f_claim[d]) continue;
+                        const float2 q = f_detf[d];
+                        const float s2 = dist2(pp, F2{q.x, q.y});
+                        if (!(s2 < p.s_match)) continue;
+                        const float dd = ecc::sqrt_rn(s2);
+                        atomicMin(&f_want[d], tag);
+                        if (best < 0 || dd < bd) { bd = dd; best = d; }
+                    }
+                }
+                if (best < 0) st = -1;
+            }
+            __syncthreads();
+            if (st == -3 && f_want[best] == tag) {
+                st = best;
+                f_claim[best] = 1;
+            }
+        }
+        TRK_MARK(1);
+#if ECC_TRACKER_PROFILE
+        prof[6] += round;
+#endif
+        // P3: update (:471-497); kept tracks at their rank, then new tracks for the unmatched
+        // detections in detection order (:501-514); candidates (fsld == 0) listed for P4
+        FastTrack ft = me;
+        DevTrack &t = ft.t;
+        bool keep = false, cand = false;
+        if (tid < T) {
+            t.is_matched = 0;
+            const bool matched = st >= 0;
+            if (matched || st == -1) {
+                if (matched) {  // :471-485
+                    const int2 q = f_det[st];
+                    t.x = q.x;
+                    t.y = q.y;
+                    t.is_matched = 1;
+                    t.fsld = 0;
+                    t.frame_count++;
+                } else {  // missed (:488-497): move to the prediction of P1 (same state)
+                    t.x = (int)pp.x;  // Q16 truncation
+                    t.y = (int)pp.y;
+                    t.fsld++;
+                }
+                push_hist_cached(ft, p.history);
+                if (matched) {
+                    const F2 nd = calc_direction_cached(ft, p);
+                    t.dtx = nd.x;  // DirectionVector::update
+                    t.dty = nd.y;
+                    t.dcx = __fadd_rn(__fmul_rn(t.dcx, p.damping), __fmul_rn(t.dtx, __fsub_rn(1.0f, p.damping)));
+                    t.dcy = __fadd_rn(__fmul_rn(t.dcy, p.damping), __fmul_rn(t.dty, __fsub_rn(1.0f, p.damping)));
+                }
+                const F2 v = estimate_velocity(t, p);
+                t.vx = v.x;
+                t.vy = v.y;
+            }
+            keep = !(t.fsld > p.frames_to_skip || t.frame_count > p.max_frames);
+            cand = keep && t.fsld == 0;
+        }
+        TRK_MARK(2);
+        const bool un = tid < C && !f_claim[tid];
+        const uint64_t mk = __ballot(keep), mc = __ballot(cand), mu = __ballot(un);
+        if (lane == 0) {
+            f_ws[wave] = __popcll(mk);
+            f_ws[4 + wave] = __popcll(mc);
+            f_ws[8 + wave] = __popcll(mu);
+        }
+        __syncthreads();
+        int rk = __popcll(mk & lanes_below()), rc = __popcll(mc & lanes_below()), ru = __popcll(mu & lanes_below());
+        int T2 = 0, G0 = 0, n_unm = 0;
+#pragma unroll
+        for (int w = 0; w < kFT / 64; ++w) {
+            const int a = f_ws[w], b = f_ws[4 + w], c = f_ws[8 + w];
+            rk += w < wave ? a : 0;
+            rc += w < wave ? b : 0;
+            ru += w < wave ? c : 0;
+            T2 += a;
+            G0 += b;
+            n_unm += c;
+        }
+        if (keep) fast_put(L, rk, ft);
+        if (cand) {
+            ck_x[rc] = t.x;
+            ck_y[rc] = t.y;
+            ck_vx[rc] = t.vx;
+            ck_vy[rc] = t.vy;
+            ck_label[rc] = t.label;
+            ck_tidx[rc] = (int16_t)rk;
+            ck_gid[rc] = t.group_id;
+        }
+        const int room = max_tracks - T;  // counted before the erase, like append-then-erase
+        if (un) {
+            if (ru < room) {
+                if (keep_new) {
+                    FastTrack nf;
+                    DevTrack &nt = nf.t;
+                    nt.x = dnx;
+                    nt.y = dny;
+                    nt.label = next_label + ru;
+                    nt.frame_count = 1;
+                    nt.is_matched = 0;
+                    nt.fsld = 0;
+                    nt.hist_len = 0;
+#pragma unroll
+                    for (int h = 0; h < kH; ++h) { nt.hx[h] = 0; nt.hy[h] = 0; }
+                    push_hist(nt, p.history);
+                    nt.vx = nt.vy = 0.f;
+                    nt.dcx = nt.dcy = nt.dtx = nt.dty = 0.f;
+                    nt.group_id = -1;  // Q17
+                    // hist_len 1: no step is read before push_hist_cached computes it (the
+                    // entry a push shifts in always sits at index hist_len, past the sum)
+#pragma unroll
+                    for (int h = 0; h < kH; ++h) { nf.ux[h] = 0.f; nf.uy[h] = 0.f; }
+                    nf.um = 0u;
+                    fast_put(L, T2 + ru, nf);
+                    const int k = G0 + ru;
+                    ck_x[k] = nt.x;
+                    ck_y[k] = nt.y;
+                    ck_vx[k] = 0.f;
+                    ck_vy[k] = 0.f;
+                    ck_label[k] = nt.label;
+                    ck_tidx[k] = (int16_t)(T2 + ru);
+                    ck_gid[k] = -1;
+                }
+            } else {
+                err = ECC_ERR_CAPACITY;
+            }
+        }
+        next_label += n_unm;
+        const int added = (keep_new && room > 0) ? min(n_unm, room) : 0;
+        const int G = G0 + added;
+        __syncthreads();
+        TRK_MARK(3);
+        // P4: greedy grouping in seed order, group-velocity blend into the LDS list (wave 0)
+        if (wave == 0)
+            group_slice(GroupLds{ck_x, ck_y, ck_label, ck_tidx, ck_vx, ck_vy, ck_gid, ck_proc, gav, gmem, goff,
+                                 gstage, &grad},
+                        G, s == n_slices - 1, p, max_tracks,
+                        [Lp](int k, float vx, float vy, int gid) {
+                            Lp->vx[k] = vx;
+                            Lp->vy[k] = vy;
+                            Lp->group_id[k] = gid;
+                        },
+                        groups, group_labels, &n_groups, &n_glabels);
+        __syncthreads();
+        TRK_MARK(4);
+        T = T2 + added;
+        if (tid < T) me = fast_get(L, tid);
+        TRK_MARK(5);
+        dnx = pnx;
+        dny = pny;
+        c_cur = c_nxt;
+        c_nxt = c_nn;
+        f_nxt = f_nn;
+    }
+#if ECC_TRACKER_PROFILE
+    prof[10] = clock64() - c0_;
+    prof[11] = wall_clock64() - w0_;
+    if (tid == 0 && stop > 0)
+        for (int k = 0; k < 12; ++k) g_trk_prof[k] = prof[k];
+#endif
+    if (tid < T) A[tid] = me.t;
+    const bool any_err = __syncthreads_or(err != 0);
+    if (tid == 0) {
+        if (any_err && err == 0) err = ECC_ERR_CAPACITY;
+        ctr->n_tracks = T;
+        ctr->next_label = next_label;
+        ctr->err = err;
+        ctr->resume = stop;
+        if (stop == n_slices) {
+            ctr->n_groups = n_groups;
+            ctr->n_group_labels = n_glabels;
+        }
+    }
+}
 
 }  // namespace
 
@@ -1021,12 +1585,19 @@ static int tracker_launch(ecc_tracker *tr, const ecc_corner *corners, const int6
                           int32_t n_slices, int32_t cap, ecc_stream_t stream) {
     ecc_ctx *ctx = tr->ctx;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    const int cap_eff = cap < tr->max_det ? cap : tr->max_det;
     {
+        ECC_TIMED(ctx, ecc::as_stream(stream), "tracker_fast_kernel");
+        hipLaunchKernelGGL(tracker_fast_kernel, dim3(1), dim3(kFT), 0, ecc::as_stream(stream),
+                           tr->buf[0], tr->buf[1], tr->max_tracks, tr->groups, tr->group_labels,
+                           tr->ctr, tr->params, corners, starts, counts, n_slices, cap_eff);
+    }
+    ECC_CHECK_LAUNCH(ctx, "tracker_fast_kernel");
+    {  // the slices from ctr->resume on (none when the fast kernel finished the launch)
         ECC_TIMED(ctx, ecc::as_stream(stream), "tracker_kernel");
         hipLaunchKernelGGL(tracker_kernel, dim3(1), dim3(kNT), 0, ecc::as_stream(stream),
                            tr->buf[0], tr->buf[1], tr->max_tracks, tr->groups, tr->group_labels,
-                           tr->ctr, tr->params, corners, starts, counts, n_slices,
-                           cap < tr->max_det ? cap : tr->max_det);
+                           tr->ctr, tr->params, corners, starts, counts, n_slices, cap_eff);
     }
     ECC_CHECK_LAUNCH(ctx, "tracker_kernel");
     return ECC_OK;

@@ -10,8 +10,9 @@ import csv, glob, sys, collections
 acc = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/*/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if "tracker_kernel" in r["Kernel_Name"]:
-            acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, v in sorted(acc.items()):
-    print(f"{k:24s} mean {sum(v)/len(v):14.1f}  n={len(v)}")
+        if "tracker" in r["Kernel_Name"]:
+            kn = "fast" if "tracker_fast_kernel" in r["Kernel_Name"] else "general"
+            acc[(kn, r["Counter_Name"])].append(float(r["Counter_Value"]))
+for (kn, k), v in sorted(acc.items()):
+    print(f"{kn:8s} {k:24s} mean {sum(v)/len(v):14.1f}  n={len(v)}")
 PY

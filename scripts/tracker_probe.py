@@ -33,7 +33,7 @@ ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
 ctx.corner_nms(d_xy, flags, n, 16384, W, H, 15, cap, d_out, d_cnt)
 ctx.sync()
 prof = getattr(ecc.lib, "ecc_tracker_profile", None)
-names = {0: "P0P1+grid", 7: "P0P1", 8: "P2scan0", 1: "P2scanN+tail", 5: "P2resolve", 2: "P3upd", 3: "P3new", 4: "P4group"}
+names = {0: "P0P1+grid", 7: "P0P1", 8: "P2scan0", 1: "P2scanN+tail", 5: "P2resolve|reload", 2: "P3upd", 3: "P3new", 4: "P4group"}
 for rep in range(3):
     tr = ecc.Tracker(ctx)
     ctx.sync()

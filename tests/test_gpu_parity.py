@@ -698,6 +698,34 @@ def test_corner_pack_and_tracker_lists_match_strided(ecc, orc, gpu):
     assert g1.status() == 0 and g2.status() == 0
 
 
+def test_tracker_fast_path_handover_matches_oracle(ecc, orc, gpu):
+    """tracker_fast_kernel (T + C <= 256 per slice, state in registers) hands a launch over to
+    tracker_kernel at the first slice above that bound; the next launch starts on the fast path
+    again once the list is small.  Sparse -> dense -> sparse slices, three launches, vs the oracle."""
+    sparse = _dense_detections(61, 30, 40, 6, 10.0)
+    dense = _dense_detections(62, 6, 700, 60, 8.0)
+    dets = sparse[:12] + dense + sparse[12:]
+    cfg = ecc.tracker_cfg(max_frames=4, frames_to_skip=2)  # short-lived tracks: T falls again
+    cap = max(len(d) for d in dets)
+    ns = len(dets)
+    flat = np.zeros(ns * cap, ecc.CORNER_DTYPE)
+    cnt = np.zeros(ns, np.int32)
+    for s, d in enumerate(dets):
+        flat[s * cap: s * cap + len(d)] = d
+        cnt[s] = len(d)
+    otr = orc.OracleTracker(cfg)
+    gtr = ecc.Tracker(gpu, cfg)
+    bounds = [0, 15, 26, ns]  # launch 1 hands over at slice 12; launch 2 starts above 256
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        for d in dets[a:b]:
+            otr.update(d)
+        gtr.update(dev(ecc, flat[a * cap: b * cap]), dev(ecc, cnt[a:b]), b - a, cap)
+        gpu.sync()
+        assert gtr.status() == 0
+        n_tr, _ = _compare_trackers(ecc, gtr, otr)
+        assert n_tr > 0
+
+
 def test_tracker_capacity_flag(ecc, gpu):
     """More new tracks than max_tracks: the overflow is dropped and reported."""
     dets = _dense_detections(55, 4, 300, 40, 30.0)
