@@ -20,6 +20,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #ifndef ECC_TRACKER_PROFILE
@@ -30,7 +31,7 @@ namespace {
 
 #if ECC_TRACKER_PROFILE
 // wall-clock ticks per phase (thread 0, after the phase's barrier) + matching rounds
-__device__ unsigned long long g_trk_prof[12];
+__device__ unsigned long long g_trk_prof[16];
 #define TRK_MARK(k)                                                  \
     do {                                                             \
         const unsigned long long now_ = wall_clock64();              \
@@ -287,8 +288,14 @@ struct GroupLds {
 template <class Put>
 __device__ __forceinline__ void group_slice(const GroupLds L, int G, bool last, const TrackerParams p, int max_tracks,
                                          Put &&put, DevGroup *__restrict__ groups, int *__restrict__ group_labels,
-                                         int *n_groups_out, int *n_glabels_out) {
+                                         int *n_groups_out, int *n_glabels_out, unsigned long long *gprof = nullptr) {
     const int lane = threadIdx.x & 63;
+#if ECC_TRACKER_PROFILE
+    unsigned long long g_last = wall_clock64();
+#define GRP_MARK(k) do { if (gprof) { const unsigned long long n_ = wall_clock64(); gprof[k] += n_ - g_last; g_last = n_; } } while (0)
+#else
+#define GRP_MARK(k) do { } while (0)
+#endif
     int n_groups = 0, n_glabels = 0;
     if (G <= 64) {
         // one candidate per lane, in registers: seed search and membership are ballots
@@ -314,6 +321,8 @@ __device__ __forceinline__ void group_slice(const GroupLds L, int G, bool last, 
                 mgid = n_groups;
                 const int r = __popcll(m & lanes_below());
                 if (last && n_glabels + r < max_tracks) group_labels[n_glabels + r] = L.ck_label[lane];
+                // members in label order = candidate order: staged contiguously for phase B
+                L.stage[n_glabels + r] = make_float4((float)mx, (float)my, mvx, mvy);
             }
             if (lane == 0) {
                 L.gmem[n_groups] = m;
@@ -323,35 +332,22 @@ __device__ __forceinline__ void group_slice(const GroupLds L, int G, bool last, 
             n_groups++;
         }
         wave_sync();
+        GRP_MARK(0);
         // phase B: one lane per group (<= 64 groups): ordered fp32 sums over its members
-        // (candidate order), four members' loads issued ahead of their adds
+        // (candidate order), streamed from their contiguous staging, eight loads ahead
         if (lane < n_groups) {
             const uint64_t m = L.gmem[lane];
-            const int cnt = __popcll(m);
+            const int cnt = __popcll(m), off = L.goff[lane];
             F2 sp{0.f, 0.f}, sv{0.f, 0.f};
-            uint64_t mm = m;
-            while (mm) {
-                int k[4];
-                bool ok[4];
+            for (int q = 0; q < cnt; q += 8) {
+                float4 v[8];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    ok[u] = mm != 0;
-                    k[u] = ok[u] ? __ffsll((unsigned long long)mm) - 1 : 0;
-                    mm &= mm - 1;
-                }
-                float vx[4], vy[4], px[4], py[4];
+                for (int u = 0; u < 8; ++u) v[u] = L.stage[off + min(q + u, cnt - 1)];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    vx[u] = L.ck_vx[k[u]];
-                    vy[u] = L.ck_vy[k[u]];
-                    px[u] = last ? (float)L.ck_x[k[u]] : 0.f;
-                    py[u] = last ? (float)L.ck_y[k[u]] : 0.f;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (!ok[u]) continue;
-                    sv = add(sv, F2{vx[u], vy[u]});
-                    if (last) sp = add(sp, F2{px[u], py[u]});
+                for (int u = 0; u < 8; ++u) {
+                    if (q + u >= cnt) break;
+                    sv = add(sv, F2{v[u].z, v[u].w});
+                    if (last) sp = add(sp, F2{v[u].x, v[u].y});
                 }
             }
             const float inv = __fdiv_rn(1.0f, (float)cnt);
@@ -369,6 +365,7 @@ __device__ __forceinline__ void group_slice(const GroupLds L, int G, bool last, 
             L.gav[lane] = make_float2(av.x, av.y);
         }
         wave_sync();
+        GRP_MARK(1);
         // velocity blend with the group average (:388-397); candidates' last fields.  With
         // group_radius >= 0 every candidate joins a group this slice; otherwise none forms.
         if (valid) {
@@ -380,6 +377,7 @@ __device__ __forceinline__ void group_slice(const GroupLds L, int G, bool last, 
             }
             put(mtidx, vx, vy, mgid);
         }
+        GRP_MARK(2);
     } else {
         for (int k = lane; k < G; k += 64) L.ck_proc[k] = 0;
         wave_sync();
@@ -909,7 +907,11 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
                             dst->vy = vy;
                             dst->group_id = gid;
                         },
-                        groups, group_labels, &n_groups, &n_glabels);
+                        groups, group_labels, &n_groups, &n_glabels
+#if ECC_TRACKER_PROFILE
+                        , prof + 12
+#endif
+                        );
         __syncthreads();
         TRK_MARK(4);
     }
@@ -943,7 +945,9 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
 // helpers, same operation order), so the state is bit-identical.  A slice with T + C > 256
 // (tracks + detections) hands the rest of the launch to tracker_kernel: the list is written to
 // the current buffer and ctr->resume = that slice.
-constexpr int kFT = 256;    // threads = the largest T + C of a slice handled here
+constexpr int kFT = 256;    // the largest T + C of a slice handled here (LDS arrays)
+constexpr int kFThreads = 512;  // 8 waves: the round-0 scan runs 2-4 lanes per track
+constexpr int kFW = kFThreads / 64;
 constexpr int kFList = 8;   // in-range detections a track keeps in registers (more: it rescans)
 constexpr int kFTagTop = (1 << 23) - 1;  // round tags: ((kFTagTop - round) << 8) | track
 static_assert(kFT <= 256, "track index packs into 8 bits of the matching tag");
@@ -1046,7 +1050,7 @@ __device__ __forceinline__ FastTrack fast_get(const FastList &L, int k) {
     return f;
 }
 
-__global__ void __launch_bounds__(kFT)
+__global__ void __launch_bounds__(kFThreads)
 tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restrict__ groups,
                     int *__restrict__ group_labels, TrackerCounters *__restrict__ ctr, TrackerParams p,
                     const ecc_corner *__restrict__ corners, const int64_t *__restrict__ starts,
@@ -1055,8 +1059,8 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
     FastList *const Lp = &L;
     __shared__ int2 f_det[kFT];
     __shared__ float2 f_detf[kFT + 32];         // as floats (+32: a scan chunk never reads past it)
-    __shared__ int16_t f_li[kFList][kFT];       // a round-0 lane's in-range detections
-    __shared__ float f_ld[kFList][kFT];         // and their distances
+    __shared__ int16_t f_li[kFList][kFThreads];  // a round-0 lane's in-range detections
+    __shared__ float f_ld[kFList][kFThreads];    // and their distances
     __shared__ int16_t f_mi[kFList][kFT];       // a track's in-range detections (merged over its lanes)
     __shared__ float f_md[kFList][kFT];
     __shared__ int8_t f_mn[kFT];                // their number (-1: more than kFList, rescan)
@@ -1067,7 +1071,7 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
     __shared__ int16_t f_res[kFT];              //   and their results
     __shared__ int f_want[kFT + 1];             // [kFT]: sink of the tail's masked-off atomics
     __shared__ uint8_t f_claim[kFT + 1];        // [kFT]: always claimed
-    __shared__ int f_ws[3 * (kFT / 64)];
+    __shared__ int f_ws[3 * kFW];
     __shared__ int ck_x[kFT], ck_y[kFT], ck_label[kFT], ck_gid[kFT];
     __shared__ int16_t ck_tidx[kFT];
     __shared__ float ck_vx[kFT], ck_vy[kFT];
@@ -1106,7 +1110,7 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
     const bool keep_new = !(0 > p.frames_to_skip || 1 > p.max_frames);
     int stop = n_slices;
 #if ECC_TRACKER_PROFILE
-    unsigned long long prof[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, last_ = wall_clock64();
+    unsigned long long prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, last_ = wall_clock64();
     const unsigned long long c0_ = clock64(), w0_ = last_;
 #endif
     for (int s = 0; s < n_slices; ++s) {
@@ -1145,7 +1149,7 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
         // order, is the minimum of (dist, index) over its lanes; its in-range detections are
         // merged into one list (order irrelevant) for the later rounds.
         {
-            const int lsh = T <= 64 ? 2 : (T <= 128 ? 1 : 0);  // uniform: L = 1 << lsh
+            const int lsh = T <= 128 ? 2 : 1;  // uniform: L = 1 << lsh, T * L <= kFThreads
             const int L = 1 << lsh;
             const int ti = tid >> lsh, tj = tid & (L - 1);
             const bool act = ti < T && f_st[ti] == -3;
@@ -1156,12 +1160,13 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
             bool l_ovf = false;
             int bi = -1;
             float bd = 0.f;
-            if (act) {
-                for (int c0 = tj * 32; c0 < C; c0 += L * 32) {
+            auto scan = [&](auto width) {
+                constexpr int CW = decltype(width)::value;  // detections per chunk
+                for (int c0 = tj * CW; c0 < C; c0 += L * CW) {
                     const int nc = C - c0;
                     uint32_t m = 0u;
 #pragma unroll
-                    for (int k = 0; k < 32; ++k) {
+                    for (int k = 0; k < CW; ++k) {
                         const float2 q = f_detf[c0 + k];
                         m |= (k < nc && dist2(tp, F2{q.x, q.y}) < p.s_match) ? (1u << k) : 0u;
                     }
@@ -1196,6 +1201,12 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
                         }
                     }
                 }
+            };
+            if (act) {
+                if (C <= 16 * L)
+                    scan(std::integral_constant<int, 16>{});
+                else
+                    scan(std::integral_constant<int, 32>{});
             }
             // the track's lanes: minimum, list sizes -> merged list offsets
             int cnt = l_ovf ? kFList + 1 : l_n, incl = cnt;
@@ -1240,15 +1251,15 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
             const uint64_t mu = __ballot(unres), mo = __ballot(unres && my_n < 0);
             if (lane == 0) {
                 f_ws[wave] = __popcll(mu);
-                f_ws[4 + wave] = __popcll(mo);
+                f_ws[kFW + wave] = __popcll(mo);
             }
             __syncthreads();
             int u = __popcll(mu & lanes_below()), n_unres = 0, n_ovf = 0;
 #pragma unroll
-            for (int w = 0; w < kFT / 64; ++w) {
+            for (int w = 0; w < kFW; ++w) {
                 u += w < wave ? f_ws[w] : 0;
                 n_unres += f_ws[w];
-                n_ovf += f_ws[4 + w];
+                n_ovf += f_ws[kFW + w];
             }
             if (n_unres > 0 && n_unres <= 64 && n_ovf == 0) {
                 if (unres) f_tail[u] = (int16_t)tid;
@@ -1376,15 +1387,15 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
         const uint64_t mk = __ballot(keep), mc = __ballot(cand), mu = __ballot(un);
         if (lane == 0) {
             f_ws[wave] = __popcll(mk);
-            f_ws[4 + wave] = __popcll(mc);
-            f_ws[8 + wave] = __popcll(mu);
+            f_ws[kFW + wave] = __popcll(mc);
+            f_ws[2 * kFW + wave] = __popcll(mu);
         }
         __syncthreads();
         int rk = __popcll(mk & lanes_below()), rc = __popcll(mc & lanes_below()), ru = __popcll(mu & lanes_below());
         int T2 = 0, G0 = 0, n_unm = 0;
 #pragma unroll
-        for (int w = 0; w < kFT / 64; ++w) {
-            const int a = f_ws[w], b = f_ws[4 + w], c = f_ws[8 + w];
+        for (int w = 0; w < kFW; ++w) {
+            const int a = f_ws[w], b = f_ws[kFW + w], c = f_ws[2 * kFW + w];
             rk += w < wave ? a : 0;
             rc += w < wave ? b : 0;
             ru += w < wave ? c : 0;
@@ -1455,7 +1466,11 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
                             Lp->vy[k] = vy;
                             Lp->group_id[k] = gid;
                         },
-                        groups, group_labels, &n_groups, &n_glabels);
+                        groups, group_labels, &n_groups, &n_glabels
+#if ECC_TRACKER_PROFILE
+                        , prof + 12
+#endif
+                        );
         __syncthreads();
         TRK_MARK(4);
         T = T2 + added;
@@ -1471,7 +1486,7 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
     prof[10] = clock64() - c0_;
     prof[11] = wall_clock64() - w0_;
     if (tid == 0 && stop > 0)
-        for (int k = 0; k < 12; ++k) g_trk_prof[k] = prof[k];
+        for (int k = 0; k < 16; ++k) g_trk_prof[k] = prof[k];
 #endif
     if (tid < T) A[tid] = me.t;
     const bool any_err = __syncthreads_or(err != 0);
@@ -1588,7 +1603,7 @@ static int tracker_launch(ecc_tracker *tr, const ecc_corner *corners, const int6
     const int cap_eff = cap < tr->max_det ? cap : tr->max_det;
     {
         ECC_TIMED(ctx, ecc::as_stream(stream), "tracker_fast_kernel");
-        hipLaunchKernelGGL(tracker_fast_kernel, dim3(1), dim3(kFT), 0, ecc::as_stream(stream),
+        hipLaunchKernelGGL(tracker_fast_kernel, dim3(1), dim3(kFThreads), 0, ecc::as_stream(stream),
                            tr->buf[0], tr->buf[1], tr->max_tracks, tr->groups, tr->group_labels,
                            tr->ctr, tr->params, corners, starts, counts, n_slices, cap_eff);
     }
@@ -1623,7 +1638,7 @@ ECC_API int ecc_tracker_update_lists(ecc_tracker *tr, const ecc_corner *corners,
 // Profiling builds only (make TRACKER_PROFILE=1): wall-clock ticks of the last update's phases
 // (P0+P1, P2, P3 update, P3 append, P4) and the matching rounds; ticks_per_us from the device.
 ECC_API int ecc_tracker_profile(unsigned long long *out8, double *ticks_per_us) {
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_trk_prof), 12 * sizeof(unsigned long long)) != hipSuccess) return ECC_ERR_HIP;
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_trk_prof), 16 * sizeof(unsigned long long)) != hipSuccess) return ECC_ERR_HIP;
     int khz = 0;
     hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
     *ticks_per_us = khz / 1000.0;

@@ -42,11 +42,12 @@ for rep in range(3):
     ctx.sync()
     line = f"rep {rep}: {(time.perf_counter() - t0) * 1e6 / ns:.2f} us/slice"
     if prof:
-        o, tpu = (C.c_ulonglong * 12)(), C.c_double()
+        o, tpu = (C.c_ulonglong * 16)(), C.c_double()
         prof(o, C.byref(tpu))
         line += "  " + " ".join(f"{k}={o[i] / tpu.value / ns:.2f}" for i, k in names.items())
         line += f" block_rounds/slice={o[6] / ns:.2f} tail_rounds/slice={o[9] / ns:.2f}"
         line += f" core_MHz={o[10] / (o[11] / tpu.value):.0f}"
+        line += " grpA/B/blend=" + "/".join(f"{o[12 + k] / tpu.value / ns:.2f}" for k in range(3))
     print(line, "tracks", len(tr.tracks()), flush=True)
     tr.close()
 
