@@ -102,6 +102,16 @@ __device__ __forceinline__ bool group_narrow(const int64_t *__restrict__ t, cons
     return (uint64_t)(t[(end < g.n ? end : g.n) - 1] - *t_first) < 0xffffffffull;
 }
 
+// Groups spanning < 2^24 - 1 ticks (the common case: 524288 events in under 16.7 s) are sorted
+// into ONE 4-byte key per event, (t - t(first event of the group)) << 8 | pixel in tile: the
+// slice an event belongs to is the slice segment it is read from.  Other groups keep the event
+// index in the key and the relative timestamp in t32.
+__device__ __forceinline__ bool group_fmt4(const int64_t *__restrict__ t, const CornerGeom &g, int64_t grp) {
+    const int64_t first = grp * kGroup * (int64_t)g.S;
+    const int64_t end = (grp + 1) * kGroup * (int64_t)g.S;
+    return (uint64_t)(t[(end < g.n ? end : g.n) - 1] - t[first]) < 0xFFFFFFull;
+}
+
 // floor(el / S) for el < 2^24 (float estimate, then exact correction).
 __device__ __forceinline__ int slice_in_group(uint32_t el, const CornerGeom &g) {
     uint32_t q = (uint32_t)((float)el * g.inv_S);
@@ -158,6 +168,7 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
     const int64_t grp_first = grp * kGroup * (int64_t)g.S;
     int64_t t_first;
     const bool narrow = group_narrow(t, g, grp, &t_first);  // uniform
+    const bool fmt4 = group_fmt4(t, g, grp);                // uniform
     const int nb = g.n_tiles + 1;
     for (int b = tid; b < nb; b += kSortThreads) hist[b] = 0;
     __syncthreads();
@@ -210,11 +221,11 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
         for (int u = 0; u < kSortEPT; ++u) {
             if (br[u] == 0xffffffffu) continue;
             const int i = u * kSortThreads + tid;
-            stage[hist[br[u] >> 16] + (br[u] & 0xffffu)] = tile_key(v[u], (uint32_t)(lo + i - grp_first));
+            stage[hist[br[u] >> 16] + (br[u] & 0xffffu)] = tile_key(v[u], fmt4 ? tv[u] : (uint32_t)(lo + i - grp_first));
         }
         __syncthreads();
         for (int i = tid; i < len; i += kSortThreads) so.key[lo + i] = stage[i];
-        if (!narrow) return;
+        if (fmt4 || !narrow) return;
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u)
@@ -229,8 +240,12 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
         if (i >= len) continue;
         const uint32_t vv = xy[lo + i];
         const int64_t pos = lo + atomicAdd(&hist[tile_of(vv, g)], 1);
-        so.key[pos] = tile_key(vv, (uint32_t)(lo + i - grp_first));
-        if (narrow) so.t32[pos] = (uint32_t)(t[lo + i] - t_first);
+        if (fmt4) {
+            so.key[pos] = tile_key(vv, (uint32_t)(t[lo + i] - t_first));
+        } else {
+            so.key[pos] = tile_key(vv, (uint32_t)(lo + i - grp_first));
+            if (narrow) so.t32[pos] = (uint32_t)(t[lo + i] - t_first);
+        }
     }
 }
 
@@ -272,8 +287,8 @@ __device__ __forceinline__ void tile_segs(const CornerGeom &g, const Sorted &so,
     }
 }
 
-__device__ __forceinline__ int64_t seg_at(const TileSegs &T, int i) {
-    int r = 0;
+__device__ __forceinline__ int64_t seg_at(const TileSegs &T, int i, int &r) {
+    r = 0;
 #pragma unroll
     for (int step = kGroup / 2; step > 0; step >>= 1)
         if (T.pref[r + step] <= i) r += step;
@@ -358,22 +373,42 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
     }
     tile_segs(g, so, grp, tile, segs);
     const GroupRef gr = group_ref(t, g, grp);
+    const bool fmt4 = group_fmt4(t, g, grp);  // uniform; the same test as slice_sort's
     __syncthreads();
     const int total = segs.pref[kGroup];
-    for (int i0 = 0; i0 < total; i0 += kBuildUnroll * kThreads) {
-        uint32_t k[kBuildUnroll], tv[kBuildUnroll];
+    if (fmt4) {  // 4-byte keys: slice = the segment, value = relative t + dlt
+        for (int i0 = 0; i0 < total; i0 += kBuildUnroll * kThreads) {
+            uint32_t k[kBuildUnroll];
+            int r[kBuildUnroll];
 #pragma unroll
-        for (int u = 0; u < kBuildUnroll; ++u) {
-            const int i = i0 + u * kThreads + tid;
-            const int64_t gi = (i < total) ? seg_at(segs, i) : 0;
-            k[u] = (i < total) ? so.key[gi] : 0xffffffffu;
-            tv[u] = (i < total && gr.narrow) ? so.t32[gi] : 0u;
+            for (int u = 0; u < kBuildUnroll; ++u) {
+                const int i = i0 + u * kThreads + tid;
+                const int64_t gi = (i < total) ? seg_at(segs, i, r[u]) : 0;
+                k[u] = (i < total) ? so.key[gi] : 0xffffffffu;
+            }
+#pragma unroll
+            for (int u = 0; u < kBuildUnroll; ++u) {
+                if (k[u] == 0xffffffffu) continue;
+                atomicMax(&tab[r[u]][k[u] & 255u], (k[u] >> 8) + gr.dlt);
+            }
         }
+    } else {
+        for (int i0 = 0; i0 < total; i0 += kBuildUnroll * kThreads) {
+            uint32_t k[kBuildUnroll], tv[kBuildUnroll];
 #pragma unroll
-        for (int u = 0; u < kBuildUnroll; ++u) {
-            if (k[u] == 0xffffffffu) continue;
-            const uint32_t el = k[u] >> 8;
-            atomicMax(&tab[slice_in_group(el, g)][k[u] & 255u], gr.narrow ? tv[u] + gr.dlt : el + 1u);
+            for (int u = 0; u < kBuildUnroll; ++u) {
+                const int i = i0 + u * kThreads + tid;
+                int r_unused;
+                const int64_t gi = (i < total) ? seg_at(segs, i, r_unused) : 0;
+                k[u] = (i < total) ? so.key[gi] : 0xffffffffu;
+                tv[u] = (i < total && gr.narrow) ? so.t32[gi] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kBuildUnroll; ++u) {
+                if (k[u] == 0xffffffffu) continue;
+                const uint32_t el = k[u] >> 8;
+                atomicMax(&tab[slice_in_group(el, g)][k[u] & 255u], gr.narrow ? tv[u] + gr.dlt : el + 1u);
+            }
         }
     }
     __syncthreads();

@@ -286,6 +286,9 @@ def _fast_gpu(ecc, gpu, xy, t, W, H, border_mode=0, first_detect=1, sae0=None, s
     (1000, 0),        # ns ticks: a group spans > 2^27 ticks (arc staging takes the int64 clamp path)
     (1, 1 << 33),     # a 2^33-tick gap inside a group: t32 does not fit (build gathers t by index)
     (997, 1 << 40),   # both, plus odd spacing
+    (300, 0),         # a group spans 2^24..2^27 ticks: keys carry the event index, t in t32
+    (1, 1 << 25),     # 4-byte-key groups before the jump, an index-key group across it
+    (97, 0),          # coarse ticks, every group below 2^24: 4-byte keys throughout
 ])
 def test_fast_detect_wide_time_ranges(ecc, orc, gpu, scale, jump):
     W, H = 346, 260
