@@ -126,8 +126,12 @@ __device__ __forceinline__ int slice_in_group(uint32_t el, const CornerGeom &g) 
 // time-order check (Metavision stream order: t non-decreasing) and, for Q11, the slice's first
 // border event.  Slices of <= 16384 events stay in registers (one read); longer ones take a
 // counting pass and a placing pass.
+// Two 1024-lane workgroups per CU (64 VGPRs: only each event's final key and tile/rank stay in
+// registers), so one workgroup's loads overlap the other's LDS phases (one workgroup per CU left
+// the CU idle outside its load phase).
 constexpr int kSortThreads = 1024;
 constexpr int kSortEPT = 16;
+constexpr int kSortFence = 4;  // events whose loads may be in flight together
 constexpr int kSortChunk = kSortThreads * kSortEPT;
 
 // Block-wide exclusive scan in place of a[0, n) (kSortThreads threads, each a contiguous run).
@@ -154,7 +158,7 @@ __device__ __forceinline__ void block_excl_scan_inplace(int32_t *a, int n, int32
     }
 }
 
-__global__ void __launch_bounds__(kSortThreads)
+__global__ void __launch_bounds__(kSortThreads, 8)  // 8 waves/SIMD: two workgroups per CU
 slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g, Sorted so,
                   int32_t *__restrict__ first_border, int32_t *__restrict__ err) {
     extern __shared__ int32_t hist[];  // [nb]: counts, then offsets, then (long slices) cursors;
@@ -175,27 +179,33 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
     bool bad = false;
     int fb = 0x7fffffff;
     const bool single = len <= kSortChunk;
-    uint32_t v[kSortEPT], tv[kSortEPT];
-    uint32_t br[kSortEPT];  // tile << 16 | rank within the tile (single slices: rank < 2^14)
+    // per event only its final key and tile << 16 | rank stay in registers (single slices:
+    // rank < 2^14); the key is formed at load time
+    uint32_t kv[kSortEPT], br[kSortEPT];
+    const uint32_t *__restrict__ xs = xy + lo;
+    const int64_t *__restrict__ ts = t + lo;
     for (int c0 = 0; c0 < len; c0 += kSortChunk) {  // one iteration for single slices
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u) {
+            // a compiler fence every kSortFence events keeps later loads from being hoisted above
+            // earlier uses (all 16 events' loads in flight would spill)
+            if (u > 0 && u % kSortFence == 0) asm volatile("" ::: "memory");
             const int i = c0 + u * kSortThreads + tid;
-            const int64_t e = lo + i;
             const bool ok = i < len;
-            v[u] = ok ? xy[e] : 0u;
-            const int64_t tc = ok ? t[e] : INT64_MAX;
-            int64_t tp = __shfl_up(tc, 1);  // the previous event is the previous lane's ...
-            if (lane == 0) tp = (ok && e > 0) ? t[e - 1] : INT64_MIN;  // ... except at a wave's start
+            const int ic = ok ? i : len - 1;  // clamped: unconditional loads off uniform bases
+            const uint32_t v = xs[ic];
+            const int64_t tc = ts[ic];
+            // the previous event's t: a coalesced load of the neighbouring element (cache hit)
+            const int64_t tp = (ic > 0 || lo > 0) ? ts[ic - 1] : INT64_MIN;
             bad |= ok && tp > tc;
-            tv[u] = (uint32_t)(tc - t_first);
-            br[u] = ok ? (uint32_t)tile_of(v[u], g) << 16 : 0xffffffffu;
+            kv[u] = tile_key(v, fmt4 ? (uint32_t)(tc - t_first) : (uint32_t)(lo + i - grp_first));
+            br[u] = ok ? (uint32_t)tile_of(v, g) << 16 : 0xffffffffu;
+            if (ok && is_border(ecc::xy_x(v), ecc::xy_y(v), g)) fb = min(fb, i);
         }
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u) {
             if (br[u] == 0xffffffffu) continue;
             br[u] |= (uint32_t)atomicAdd(&hist[br[u] >> 16], 1) & 0xffffu;
-            if (is_border(ecc::xy_x(v[u]), ecc::xy_y(v[u]), g)) fb = min(fb, c0 + u * kSortThreads + tid);
         }
     }
     if (__any(bad) && lane == 0) *err = 1;
@@ -218,18 +228,15 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
         uint32_t *stage = reinterpret_cast<uint32_t *>(hist + nb);
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < kSortEPT; ++u) {
-            if (br[u] == 0xffffffffu) continue;
-            const int i = u * kSortThreads + tid;
-            stage[hist[br[u] >> 16] + (br[u] & 0xffffu)] = tile_key(v[u], fmt4 ? tv[u] : (uint32_t)(lo + i - grp_first));
-        }
+        for (int u = 0; u < kSortEPT; ++u)
+            if (br[u] != 0xffffffffu) stage[hist[br[u] >> 16] + (br[u] & 0xffffu)] = kv[u];
         __syncthreads();
         for (int i = tid; i < len; i += kSortThreads) so.key[lo + i] = stage[i];
         if (fmt4 || !narrow) return;
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < kSortEPT; ++u)
-            if (br[u] != 0xffffffffu) stage[hist[br[u] >> 16] + (br[u] & 0xffffu)] = tv[u];
+        for (int u = 0; u < kSortEPT; ++u)  // rare (groups spanning >= 2^24 ticks): t read again
+            if (br[u] != 0xffffffffu) stage[hist[br[u] >> 16] + (br[u] & 0xffffu)] = (uint32_t)(t[lo + u * kSortThreads + tid] - t_first);
         __syncthreads();
         for (int i = tid; i < len; i += kSortThreads) so.t32[lo + i] = stage[i];
         return;
