@@ -1194,6 +1194,7 @@ arc_dense_kernel(const int64_t *__restrict__ t, CornerGeom g, const int64_t *__r
 // first-detect rule (Q15) and, in ref_compat mode (Q11), "before the slice's first border event";
 // corner pairs are never border pixels.
 constexpr int kFlagThreads = 512;
+constexpr int kFlagQuads = 8;  // 4-event quads a lane loads up front (16384-event slices)
 constexpr int kSegWords = (kTilePix + 31) / 32 + 1;  // 7: a 196-bit segment at any bit offset
 
 // kStaged: bit lp of tile in the LDS segments; otherwise (sensors whose segments exceed the
@@ -1222,6 +1223,16 @@ flags_event_kernel(const uint32_t *__restrict__ xy, CornerGeom g, const uint32_t
     // events [0, live_end) of the slice can be corners
     const int live_end = s < g.first_detect ? 0 : (g.border_mode == 1 ? min(len, max(first_border[s], 0)) : len);
     const uint32_t *rg = res + (s / kGroup) * g.n_tiles * kPairWords;
+    const bool vec = (lo & 3) == 0;  // 4-event quads: 16-B loads, 4-B flag stores
+    const int n4 = vec ? len / 4 : 0;
+    // a lane's quads (<= kFlagQuads of them for slices up to 16384 events) are loaded before the
+    // staging, so the two latencies overlap
+    uint4 pre[kFlagQuads];
+#pragma unroll
+    for (int u = 0; u < kFlagQuads; ++u) {
+        const int q = u * kFlagThreads + (int)threadIdx.x;
+        pre[u] = (q < n4 && 4 * q < live_end) ? *reinterpret_cast<const uint4 *>(xy + lo + 4 * q) : make_uint4(0u, 0u, 0u, 0u);
+    }
     if (kStaged && live_end > 0) {
         const int b0 = j * kTilePix, w0 = b0 >> 5, sh = b0 & 31;
         for (int k = threadIdx.x; k < g.n_tiles * kSegWords; k += kFlagThreads) {
@@ -1233,9 +1244,19 @@ flags_event_kernel(const uint32_t *__restrict__ xy, CornerGeom g, const uint32_t
         }
     }
     __syncthreads();
-    const bool vec = (lo & 3) == 0;  // 4-event quads: 16-B loads, 4-B flag stores
-    const int n4 = vec ? len / 4 : 0;
-    for (int q = threadIdx.x; q < n4; q += kFlagThreads) {
+    auto quad_flags = [&](int i, const uint4 v) {
+        return corner_bit<kStaged>(v.x, g, sb, rg, j) | (i + 1 < live_end ? corner_bit<kStaged>(v.y, g, sb, rg, j) << 8 : 0u) |
+               (i + 2 < live_end ? corner_bit<kStaged>(v.z, g, sb, rg, j) << 16 : 0u) |
+               (i + 3 < live_end ? corner_bit<kStaged>(v.w, g, sb, rg, j) << 24 : 0u);
+    };
+#pragma unroll
+    for (int u = 0; u < kFlagQuads; ++u) {
+        const int q = u * kFlagThreads + (int)threadIdx.x;
+        if (q >= n4) break;
+        const int i = 4 * q;
+        *reinterpret_cast<uint32_t *>(flags + lo + i) = i < live_end ? quad_flags(i, pre[u]) : 0u;
+    }
+    for (int q = kFlagQuads * kFlagThreads + threadIdx.x; q < n4; q += kFlagThreads) {  // slices > 16384 events
         const int i = 4 * q;
         uint32_t f = 0u;
         if (i < live_end) {
