@@ -908,9 +908,6 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
                             dst->group_id = gid;
                         },
                         groups, group_labels, &n_groups, &n_glabels
-#if ECC_TRACKER_PROFILE
-                        , prof + 12
-#endif
                         );
         __syncthreads();
         TRK_MARK(4);
