@@ -217,7 +217,7 @@ __device__ __forceinline__ float uniform_f32(float v) {
 // Replicated accumulators: the per-WG flush goes to replica blockIdx % n_copies, which spreads
 // the same-address global atomics; the update kernel sums the replicas.
 constexpr int kAccStride = 3 * kMaxK;
-constexpr int kAccCopies = 8;
+constexpr int kAccCopies = 4;
 
 // One Lloyd pass (kAccumulate) or the final labelling.  Accumulation: every point adds
 // (1 << 52) | (x << 26) | y to its cluster's u64 slot of its WAVE in LDS with one no-return
@@ -631,7 +631,7 @@ kmeans_extent_kernel(const uint32_t *__restrict__ xy, Segs segs, uint32_t *__res
 // workgroups of chunk 0 also list the points outside the kImgSide^2 image.
 constexpr int kHistThreads = 1024;
 constexpr int kHistChunk = 32768;  // pixels per LDS chunk (128 KiB)
-constexpr int kHistParts = 128;
+constexpr int kHistParts = 64;
 constexpr int64_t kHistBudget = 16 << 20;  // partial-count entries (64 MiB): parts used = budget / cells
 
 __host__ __device__ inline int parts_used(int parts, int64_t cells) {

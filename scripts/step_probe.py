@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Two-stream step decomposition on the bench workload (20 M events, 346x260): wall time per step
+of the corner chain alone, of the downsample -> k-means chain alone, and of the corner chain with
+the downsample only / the whole k-means chain on the second stream.  Shows how much of the
+k-means chain the corner chain (the critical path) absorbs.  Usage: step_probe.py [steps]"""
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "event-camera-clustering-and-optical-flow-estimation_amd"))
+import eccpy as ecc  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+W, H, SLICE, WINDOW, K, I = 346, 260, 16384, 8192, 16, 10
+n = 1221 * SLICE
+ctx = ecc.Context(0)
+lib = ecc.lib
+xy, t, _ = ecc.gen_events(n, seed=1, width=W, height=H)
+d_xy, d_t = ecc.DeviceArray.from_numpy(xy, ctx.stream), ecc.DeviceArray.from_numpy(t, ctx.stream)
+n_win = (n + WINDOW - 1) // WINDOW
+rep_xy = ecc.DeviceArray(n_win * WINDOW, np.uint32)
+uniq = ecc.DeviceArray(n_win, np.int32)
+rep = ecc.DeviceArray(n_win * WINDOW, np.int32)
+labels = ecc.DeviceArray(n_win * WINDOW, np.uint8)
+hcfg = ecc.hash_cfg(window=WINDOW)
+c0 = np.stack([np.linspace(20, W - 20, K), np.linspace(20, H - 20, K)], 1).astype(np.float32).ravel()
+d_c0, d_c = ecc.DeviceArray.from_numpy(c0), ecc.DeviceArray(2 * K, np.float32)
+kcfg = ecc.kmeans_cfg(k=K, max_iters=I, tol=-1.0)
+ccfg = ecc.corner_cfg(width=W, height=H)
+sae = ecc.DeviceArray(W * H, np.int64)
+flags = ecc.DeviceArray(n, np.uint8)
+cap = 4096
+ns = n // SLICE
+nms_out, nms_cnt = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE), ecc.DeviceArray(ns, np.int32)
+s2 = ecc.C.c_void_p()
+ecc.check(lib.ecc_stream_create(ecc.C.byref(s2)))
+ev_fork, ev_join = ecc.C.c_void_p(), ecc.C.c_void_p()
+ecc.check(lib.ecc_event_create(ecc.C.byref(ev_fork)))
+ecc.check(lib.ecc_event_create(ecc.C.byref(ev_join)))
+
+
+def ds(ks):
+    ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg),
+                                      rep_xy.ptr, None, uniq.ptr, rep.ptr, ks), "downsample")
+
+
+def km(ks):
+    ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, ks))
+    ecc.check(lib.ecc_kmeans_run_xy16_frame(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, W, H, ecc.C.byref(kcfg),
+                                            d_c.ptr, labels.ptr, None, ks), "kmeans")
+
+
+def corner():
+    ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
+    ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
+    ctx.corner_nms(d_xy, flags, n, SLICE, W, H, 15, cap, nms_out, nms_cnt)
+
+
+def two(side):
+    ks = s2.value
+    ecc.check(lib.ecc_event_record(ev_fork, ctx.stream))
+    ecc.check(lib.ecc_stream_wait_event(ks, ev_fork))
+    side(ks)
+    ecc.check(lib.ecc_event_record(ev_join, ks))
+    corner()
+    ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_join))
+
+
+variants = {
+    "corner chain alone": corner,
+    "downsample+kmeans alone": lambda: (ds(ctx.stream), km(ctx.stream)),
+    "corner | downsample": lambda: two(ds),
+    "corner | downsample+kmeans (bench step)": lambda: two(lambda ks: (ds(ks), km(ks))),
+}
+ds(ctx.stream)  # representatives for the k-means-only variants
+for name, fn in variants.items():
+    for _ in range(3):
+        fn()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    ctx.sync()
+    print(f"{name:42s} {(time.perf_counter() - t0) * 1e3 / steps:.3f} ms/step", flush=True)
