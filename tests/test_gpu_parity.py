@@ -636,6 +636,11 @@ def _dense_detections(seed, n_slices, per_slice, n_centres, spread, W=346, H=260
     (54, 900, 80, 6.0, {"max_distance": 12.5, "damping": 0.5, "smoothing": 0.6}),
     (56, 500, 40, 10.0, {"max_distance": 1.0e6}),                   # radius too large for the grid
     (57, 450, 30, 15.0, {"max_distance": 45.0, "group_radius": -1.0}),  # no group ever forms
+    # short-lived tracks keep T + C <= 256 (tracker_fast_kernel) while every track has far more
+    # than 8 detections in range (its list overflows: the rounds rescan) ...
+    (58, 120, 2, 4.0, {"max_frames": 2, "frames_to_skip": 1}),
+    # ... or more than 64 tracks stay unresolved after round 0 (workgroup-wide rounds), C > 64
+    (59, 110, 40, 2.0, {"max_frames": 2, "frames_to_skip": 1, "max_distance": 12.0}),
 ])
 def test_tracker_dense_conflicts_match_oracle(ecc, orc, gpu, seed, per_slice, n_centres, spread, cfg_over):
     cfg = ecc.tracker_cfg(**cfg_over)
