@@ -1284,7 +1284,7 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
                         for (int k = 0; k < kFList; ++k) {
                             if (res != -3 || cl[k]) continue;
                             atomicMin(&f_want[li[k]], tg);
-                            if (bi < 0 || ld[k] < bd) { bd = ld[k]; bi = li[k]; }
+                            if (bi < 0 || ld[k] < bd || (ld[k] == bd && li[k] < bi)) { bd = ld[k]; bi = li[k]; }
                         }
                         if (res == -3 && bi < 0) res = -1;
                         wave_sync();

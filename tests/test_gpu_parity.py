@@ -641,6 +641,10 @@ def _dense_detections(seed, n_slices, per_slice, n_centres, spread, W=346, H=260
     (58, 120, 2, 4.0, {"max_frames": 2, "frames_to_skip": 1}),
     # ... or more than 64 tracks stay unresolved after round 0 (workgroup-wide rounds), C > 64
     (59, 110, 40, 2.0, {"max_frames": 2, "frames_to_skip": 1, "max_distance": 12.0}),
+    # C > 128 with few tracks: a track's merged candidate list is not in detection order, and
+    # integer detections around a prediction tie in distance (first minimum = smallest index)
+    (60, 200, 3, 6.0, {"max_frames": 2, "frames_to_skip": 1}),
+    (61, 220, 2, 3.0, {"max_frames": 1, "frames_to_skip": 1, "max_distance": 8.0}),
 ])
 def test_tracker_dense_conflicts_match_oracle(ecc, orc, gpu, seed, per_slice, n_centres, spread, cfg_over):
     cfg = ecc.tracker_cfg(**cfg_over)
