@@ -738,20 +738,21 @@ def test_tracker_fast_path_handover_matches_oracle(ecc, orc, gpu):
         assert n_tr > 0
 
 
-def test_tracker_capacity_flag(ecc, gpu):
+@pytest.mark.parametrize("per_slice,max_tracks", [(300, 64), (40, 16)])  # general / fast kernel
+def test_tracker_capacity_flag(ecc, gpu, per_slice, max_tracks):
     """More new tracks than max_tracks: the overflow is dropped and reported."""
-    dets = _dense_detections(55, 4, 300, 40, 30.0)
+    dets = _dense_detections(55, 4, per_slice, 40, 30.0)
     cap = max(len(d) for d in dets)
     flat = np.zeros(4 * cap, ecc.CORNER_DTYPE)
     cnt = np.zeros(4, np.int32)
     for s, d in enumerate(dets):
         flat[s * cap: s * cap + len(d)] = d
         cnt[s] = len(d)
-    gtr = ecc.Tracker(gpu, max_tracks=64)
+    gtr = ecc.Tracker(gpu, max_tracks=max_tracks)
     gtr.update(dev(ecc, flat), dev(ecc, cnt), 4, cap)
     gpu.sync()
     assert gtr.status() == ecc.ERR_CAPACITY
-    assert len(gtr.tracks()) <= 64
+    assert len(gtr.tracks()) <= max_tracks
 
 
 # ------------------------------------------------------------------------------ eps-neighbourhoods
