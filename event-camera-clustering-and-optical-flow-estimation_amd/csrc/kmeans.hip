@@ -363,6 +363,166 @@ kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__re
     }
 }
 
+// Final labels from the label image: one workgroup per segment, 16 points per lane, so a
+// segment of up to 4096 points is ONE trip — its four 16-B loads, sixteen image gathers and four
+// packed stores each in flight together (kmeans_fast_kernel's two-batch trips took two dependent
+// load -> gather -> store rounds per bench segment of ~3150 points).  The loads are issued
+// before the segment count arrives: a lane reads within the segment's stride (always readable),
+// and only the stores are masked by the count.  Labels equal kmeans_fast_kernel<K, false, true>'s.
+constexpr int kLabPer = 16;
+template <int K>
+__global__ void __launch_bounds__(kThreads)
+kmeans_img_labels_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__restrict__ cent, int k,
+                         float thr, const uint8_t *__restrict__ img, const uint32_t *__restrict__ img_wh,
+                         uint8_t *__restrict__ labels) {
+    __shared__ float s_cx[K], s_cy[K];
+    const int tid = threadIdx.x;
+    if (tid < K) {
+        s_cx[tid] = tid < k ? cent[2 * tid] : 1e30f;
+        s_cy[tid] = tid < k ? cent[2 * tid + 1] : 1e30f;
+    }
+    __syncthreads();
+    const uint32_t img_w = img_wh[0], img_h = img_wh[1];
+    const bool vec_ok = (segs.stride & 3) == 0;
+    for (int64_t s = blockIdx.x; s < segs.n_segs; s += gridDim.x) {
+        const int64_t base = s * segs.stride;
+        // readable extent: the whole stride (the next segment starts after it), except in the
+        // last segment, whose buffer may end at its count
+        const int64_t cnt = segs.count(s);
+        const int64_t lim = s + 1 < segs.n_segs ? segs.stride : cnt;
+        for (int64_t j0 = 0; j0 < cnt; j0 += kLabPer * kThreads) {
+            uint32_t v[kLabPer], lab[kLabPer];
+#pragma unroll
+            for (int u = 0; u < kLabPer / 4; ++u) {
+                const int64_t j = j0 + u * 4 * kThreads + 4 * tid;
+                if (vec_ok && j + 3 < lim) {
+                    const uint4 q = *reinterpret_cast<const uint4 *>(xy + base + j);
+                    v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[4 * u + e] = (j + e < lim) ? xy[base + j + e] : 0u;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kLabPer / 4; ++u) {
+                const int64_t j = j0 + u * 4 * kThreads + 4 * tid;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t w = v[4 * u + e];
+                    const uint32_t x = (uint32_t)ecc::xy_x(w), y = (uint32_t)ecc::xy_y(w);
+                    uint32_t l = 255u;
+                    if (j + e < cnt) {
+                        if (__builtin_expect(x < img_w && y < img_h, 1)) l = img[y * kImgSide + x];
+                        else l = assign_lds<K>((float)x, (float)y, s_cx, s_cy, thr);
+                    }
+                    lab[4 * u + e] = l;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kLabPer / 4; ++u) {
+                const int64_t j = j0 + u * 4 * kThreads + 4 * tid;
+                if (j + 3 < cnt && ((base + j) & 3) == 0) {
+                    const uint32_t pk = lab[4 * u] | (lab[4 * u + 1] << 8) | (lab[4 * u + 2] << 16) |
+                                        (lab[4 * u + 3] << 24);
+                    *reinterpret_cast<uint32_t *>(labels + base + j) = pk;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (j + e < cnt) labels[base + j + e] = (uint8_t)lab[4 * u + e];
+                }
+            }
+        }
+    }
+}
+
+// The same labels with the label image staged in LDS (frames up to kLabLdsBytes, e.g. the
+// 90 KB of 346x260): the image gathers of kmeans_img_labels_kernel hit a different cache line per
+// lane, so its 7.7 M gathers were bound by the texture units' one-line-per-cycle tag lookups, not
+// by HBM.  One 1024-lane workgroup per CU copies the image once from L2, then takes four segments
+// per trip (256 lanes x 16 points each), loads issued before the counts arrive as above.
+constexpr int kLabLdsThreads = 1024;
+constexpr int kLabLdsBytes = 96 * 1024;
+template <int K>
+__global__ void __launch_bounds__(kLabLdsThreads)
+kmeans_lds_labels_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__restrict__ cent, int k,
+                         float thr, const uint8_t *__restrict__ img, const uint32_t *__restrict__ img_wh,
+                         uint8_t *__restrict__ labels) {
+    extern __shared__ uint8_t s_img[];  // [img_h][img_w], compact
+    __shared__ float s_cx[K], s_cy[K];
+    const int tid = threadIdx.x, sub = tid >> 8, t = tid & 255;
+    if (tid < K) {
+        s_cx[tid] = tid < k ? cent[2 * tid] : 1e30f;
+        s_cy[tid] = tid < k ? cent[2 * tid + 1] : 1e30f;
+    }
+    const uint32_t img_w = img_wh[0], img_h = img_wh[1];
+    // rows copied as words (row pitch img_w rounded up to 4), eight loads in flight per lane
+    const uint32_t wq = (img_w + 3) >> 2, pitch = 4 * wq, n_words = wq * img_h;
+    for (uint32_t i0 = 0; i0 < n_words; i0 += 8 * kLabLdsThreads) {
+        uint32_t wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t i = i0 + u * kLabLdsThreads + tid, r = i / wq;
+            wv[u] = i < n_words ? *reinterpret_cast<const uint32_t *>(img + r * kImgSide + 4 * (i - r * wq)) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t i = i0 + u * kLabLdsThreads + tid;
+            if (i < n_words) reinterpret_cast<uint32_t *>(s_img)[i] = wv[u];
+        }
+    }
+    __syncthreads();
+    const bool vec_ok = (segs.stride & 3) == 0;
+    for (int64_t s0 = 4 * (int64_t)blockIdx.x; s0 < segs.n_segs; s0 += 4 * (int64_t)gridDim.x) {
+        const int64_t s = s0 + sub;
+        if (s >= segs.n_segs) continue;  // no barrier below
+        const int64_t base = s * segs.stride;
+        const int64_t cnt = segs.count(s);
+        const int64_t lim = s + 1 < segs.n_segs ? segs.stride : cnt;
+        for (int64_t j0 = 0; j0 < cnt; j0 += kLabPer * 256) {
+            uint32_t v[kLabPer], lab[kLabPer];
+#pragma unroll
+            for (int u = 0; u < kLabPer / 4; ++u) {
+                const int64_t j = j0 + u * 4 * 256 + 4 * t;
+                if (vec_ok && j + 3 < lim) {
+                    const uint4 q = *reinterpret_cast<const uint4 *>(xy + base + j);
+                    v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[4 * u + e] = (j + e < lim) ? xy[base + j + e] : 0u;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kLabPer / 4; ++u) {
+                const int64_t j = j0 + u * 4 * 256 + 4 * t;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t w = v[4 * u + e];
+                    const uint32_t x = (uint32_t)ecc::xy_x(w), y = (uint32_t)ecc::xy_y(w);
+                    uint32_t l = 255u;
+                    if (j + e < cnt) {
+                        if (__builtin_expect(x < img_w && y < img_h, 1)) l = s_img[y * pitch + x];
+                        else l = assign_lds<K>((float)x, (float)y, s_cx, s_cy, thr);
+                    }
+                    lab[4 * u + e] = l;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kLabPer / 4; ++u) {
+                const int64_t j = j0 + u * 4 * 256 + 4 * t;
+                if (j + 3 < cnt && ((base + j) & 3) == 0) {
+                    const uint32_t pk = lab[4 * u] | (lab[4 * u + 1] << 8) | (lab[4 * u + 2] << 16) |
+                                        (lab[4 * u + 3] << 24);
+                    *reinterpret_cast<uint32_t *>(labels + base + j) = pk;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (j + e < cnt) labels[base + j + e] = (uint8_t)lab[4 * u + e];
+                }
+            }
+        }
+    }
+}
+
 // float-input variant (reference data layout: interleaved float x,y): fp64 LDS + global
 // atomics (order-dependent only at the 1e-16 relative level).
 template <bool kAccumulate>
@@ -631,7 +791,6 @@ kmeans_extent_kernel(const uint32_t *__restrict__ xy, Segs segs, uint32_t *__res
 // workgroups of chunk 0 also list the points outside the kImgSide^2 image.
 constexpr int kHistThreads = 1024;
 constexpr int kHistChunk = 32768;  // pixels per LDS chunk (128 KiB)
-constexpr int kHistParts = 64;
 constexpr int64_t kHistBudget = 16 << 20;  // partial-count entries (64 MiB): parts used = budget / cells
 
 __host__ __device__ inline int parts_used(int parts, int64_t cells) {
@@ -639,6 +798,7 @@ __host__ __device__ inline int parts_used(int parts, int64_t cells) {
     return (int)(p < 1 ? 1 : (p < parts ? p : parts));
 }
 constexpr int kHistUnroll = 4;
+constexpr int kHistSegs = 4;
 constexpr int kPixGrid = 256;  // pixel-pass workgroups (64 measured slower: the per-pixel assignment dominates)
 
 __device__ __forceinline__ void reduce_extent(const uint32_t *__restrict__ ext, int n_ext, uint32_t *s_red,
@@ -663,19 +823,27 @@ __device__ __forceinline__ void reduce_extent(const uint32_t *__restrict__ ext, 
 // 1-D grid, XCD-aware: workgroup b runs on XCD b % 8; the kCountSlots chunk workgroups of one
 // part (point range) share b % 8 and are dispatched back to back, so the second and third reads of
 // the part's points hit that XCD's L2 instead of HBM.
+// The slot count is the frame's chunk count when the caller gives the frame (3 at 346x260, so
+// no workgroup of a fourth slot idles), else 4; parts fill the 256 CUs: 8 * (32 / slots).
 constexpr int kCountSlots = 4;
 
-__host__ __device__ inline int count_grid(int parts) { return 8 * ((parts + 7) / 8) * kCountSlots; }
+__host__ __device__ inline int count_grid(int parts, int slots) { return 8 * ((parts + 7) / 8) * slots; }
+
+inline void count_layout(int64_t n_segs, int64_t cells, int &parts, int &slots) {
+    const int64_t ch = (cells + kHistChunk - 1) / kHistChunk;
+    slots = cells > 0 ? (int)(ch < 1 ? 1 : (ch < kCountSlots ? ch : kCountSlots)) : kCountSlots;
+    parts = (int)std::min<int64_t>(8 * (32 / slots), std::max<int64_t>(n_segs, 1));
+}
 
 __global__ void __launch_bounds__(kHistThreads)
 kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *__restrict__ ext, int n_ext,
-                    int parts, uint32_t *__restrict__ partial, uint32_t *__restrict__ wh,
+                    int parts, int slots, uint32_t *__restrict__ partial, uint32_t *__restrict__ wh,
                     uint32_t *__restrict__ outside, uint32_t *__restrict__ n_outside, uint32_t fixed_w,
                     uint32_t fixed_h, int32_t *__restrict__ err) {
     extern __shared__ uint32_t hist[];  // [kHistChunk]
     __shared__ uint32_t s_red[2 * kHistThreads / 64];
     const int xcd = (int)(blockIdx.x % 8), i8 = (int)(blockIdx.x / 8);
-    const int m = (i8 / kCountSlots) * 8 + xcd, slot = i8 % kCountSlots, tid = threadIdx.x;
+    const int m = (i8 / slots) * 8 + xcd, slot = i8 % slots, tid = threadIdx.x;
     // frame: fixed_w > 0 = the caller's frame; points outside it are an error (err != null: the
     // multi-GPU count images) or go to the outside list; otherwise the bounding box of the points
     // inside the kImgSide^2 image
@@ -692,32 +860,45 @@ kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *
     if (m >= parts) return;
     const int64_t s0 = segs.n_segs * m / parts, s1 = segs.n_segs * (m + 1) / parts;
     const int64_t n_chunks = (cells + kHistChunk - 1) / kHistChunk;
-    for (int64_t c = slot; c < (n_chunks > 0 ? n_chunks : 1); c += kCountSlots) {
+    for (int64_t c = slot; c < (n_chunks > 0 ? n_chunks : 1); c += slots) {
         const int64_t lo = c * kHistChunk;
         const int n_loc = (int)((cells - lo) < kHistChunk ? (cells - lo) : kHistChunk);
         for (int i = tid; i < kHistChunk; i += kHistThreads) hist[i] = 0u;
         __syncthreads();
-        for (int64_t sg = s0; sg < s1; ++sg) {
-            const int64_t cnt = segs.count(sg), base = sg * segs.stride;
-            for (int64_t j0 = 0; j0 < cnt; j0 += kHistUnroll * kHistThreads) {
-                uint32_t v[kHistUnroll];
+        // kHistSegs segments per trip, kHistUnroll x 1024 points of each: 16 independent loads per
+        // lane in flight (a bench segment holds ~3150 points, so one segment per trip left the
+        // trips latency-bound: 30 dependent trips per part)
+        for (int64_t sg = s0; sg < s1; sg += kHistSegs) {
+            int64_t cnt[kHistSegs], base[kHistSegs], cmax = 0;
 #pragma unroll
-                for (int u = 0; u < kHistUnroll; ++u) {
-                    const int64_t j = j0 + u * kHistThreads + tid;
-                    v[u] = j < cnt ? xy[base + j] : 0xffffffffu;
-                }
+            for (int i = 0; i < kHistSegs; ++i) {
+                cnt[i] = sg + i < s1 ? segs.count(sg + i) : 0;
+                base[i] = (sg + i) * segs.stride;
+                cmax = cnt[i] > cmax ? cnt[i] : cmax;
+            }
+            for (int64_t j0 = 0; j0 < cmax; j0 += kHistUnroll * kHistThreads) {
+                uint32_t v[kHistSegs][kHistUnroll];
 #pragma unroll
-                for (int u = 0; u < kHistUnroll; ++u) {
-                    if (j0 + u * kHistThreads + tid >= cnt) continue;
-                    const uint32_t x = v[u] & 0xffffu, y = v[u] >> 16;
-                    if (x < lim_x && y < lim_y) {
-                        const int64_t idx = (int64_t)y * w + x - lo;
-                        if (idx >= 0 && idx < n_loc) atomicAdd(&hist[idx], 1u);
-                    } else if (c == 0) {
-                        if (err) *err = 1;
-                        else outside[atomicAdd(n_outside, 1u)] = v[u];
+                for (int i = 0; i < kHistSegs; ++i)
+#pragma unroll
+                    for (int u = 0; u < kHistUnroll; ++u) {
+                        const int64_t j = j0 + u * kHistThreads + tid;
+                        v[i][u] = j < cnt[i] ? xy[base[i] + j] : 0xffffffffu;
                     }
-                }
+#pragma unroll
+                for (int i = 0; i < kHistSegs; ++i)
+#pragma unroll
+                    for (int u = 0; u < kHistUnroll; ++u) {
+                        if (j0 + u * kHistThreads + tid >= cnt[i]) continue;
+                        const uint32_t x = v[i][u] & 0xffffu, y = v[i][u] >> 16;
+                        if (x < lim_x && y < lim_y) {
+                            const int64_t idx = (int64_t)y * w + x - lo;
+                            if (idx >= 0 && idx < n_loc) atomicAdd(&hist[idx], 1u);
+                        } else if (c == 0) {
+                            if (err) *err = 1;
+                            else outside[atomicAdd(n_outside, 1u)] = v[i][u];
+                        }
+                    }
             }
         }
         __syncthreads();
@@ -988,7 +1169,8 @@ static int kmeans_run_xy16_impl(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
     const size_t off_img = ecc::align_up(off_ext + (size_t)grid * 8, 256);
     const size_t off_cnt = ecc::align_up(off_img + (size_t)kImgSide * kImgSide, 256);
     const size_t off_part = off_cnt + (size_t)kImgSide * kImgSide * 4;
-    const int parts = (int)std::min<int64_t>(kHistParts, std::max<int64_t>(segs.n_segs, 1));
+    int parts, slots;
+    count_layout(segs.n_segs, (int64_t)frame_w * frame_h, parts, slots);
     const size_t off_out = off_part + (size_t)kHistBudget * 4;
     const int64_t n_pts_max = segs.n_segs * segs.stride;
     rc = ecc::ws_reserve(ctx, off_out + 256 + (size_t)n_pts_max * 4);
@@ -1053,8 +1235,8 @@ static int kmeans_run_xy16_impl(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
                               "kmeans_count LDS");
                 lds_ok = true;
             }
-            hipLaunchKernelGGL(kmeans_count_kernel, dim3(count_grid(parts)), dim3(kHistThreads), kHistChunk * 4, s,
-                               xy, segs, ext, grid, parts, partial, wh, outside, n_out, (uint32_t)frame_w,
+            hipLaunchKernelGGL(kmeans_count_kernel, dim3(count_grid(parts, slots)), dim3(kHistThreads), kHistChunk * 4,
+                               s, xy, segs, ext, grid, parts, slots, partial, wh, outside, n_out, (uint32_t)frame_w,
                                (uint32_t)frame_h, (int32_t *)nullptr);
         }
         {
@@ -1090,8 +1272,33 @@ static int kmeans_run_xy16_impl(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
         ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 iteration");
         if (labels) {
             ECC_TIMED(ctx, s, "kmeans_xy16_labels");
-            launch_fast<false>(cfg->k, dim3(grid_pts), s, xy, segs, centroids, cfg->threshold, nullptr, 1, st,
-                               labels, img, wh);
+            const int64_t frame_px = (int64_t)frame_w * frame_h;
+            const int64_t frame_lds = (int64_t)ecc::align_up((size_t)frame_w, 4) * frame_h;
+            if (frame_px > 0 && frame_lds <= kLabLdsBytes) {  // the frame's label image fits in LDS
+                const int lds = (int)frame_lds;
+                const dim3 g((unsigned)std::min<int64_t>((segs.n_segs + 3) / 4, 256));
+                static bool lab_lds_ok = false;
+                if (!lab_lds_ok) {
+                    ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&kmeans_lds_labels_kernel<16>),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLabLdsBytes),
+                                  "kmeans labels LDS");
+                    ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&kmeans_lds_labels_kernel<32>),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLabLdsBytes),
+                                  "kmeans labels LDS");
+                    lab_lds_ok = true;
+                }
+                if (cfg->k <= 16)
+                    hipLaunchKernelGGL(kmeans_lds_labels_kernel<16>, g, dim3(kLabLdsThreads), lds, s, xy, segs,
+                                       centroids, cfg->k, cfg->threshold, img, wh, labels);
+                else
+                    hipLaunchKernelGGL(kmeans_lds_labels_kernel<32>, g, dim3(kLabLdsThreads), lds, s, xy, segs,
+                                       centroids, cfg->k, cfg->threshold, img, wh, labels);
+            } else if (cfg->k <= 16)
+                hipLaunchKernelGGL(kmeans_img_labels_kernel<16>, dim3(grid_pts), dim3(kThreads), 0, s, xy, segs,
+                                   centroids, cfg->k, cfg->threshold, img, wh, labels);
+            else
+                hipLaunchKernelGGL(kmeans_img_labels_kernel<32>, dim3(grid_pts), dim3(kThreads), 0, s, xy, segs,
+                                   centroids, cfg->k, cfg->threshold, img, wh, labels);
             ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 labels");
         }
     }
@@ -1301,7 +1508,8 @@ ECC_API int ecc_kmeans_counts_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_s
         return ECC_OK;
     }
     if (!xy) return ECC_ERR_INVALID;
-    const int parts = (int)std::min<int64_t>(kHistParts, segs.n_segs);
+    int parts, slots;
+    count_layout(segs.n_segs, cells, parts, slots);
     const size_t off_part = 256;
     int rc = ecc::ws_reserve(ctx, off_part + (size_t)kHistBudget * 4);
     if (rc) return rc;
@@ -1317,8 +1525,8 @@ ECC_API int ecc_kmeans_counts_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_s
     }
     {
         ECC_TIMED(ctx, s, "kmeans_count_kernel");
-        hipLaunchKernelGGL(kmeans_count_kernel, dim3(count_grid(parts)), dim3(kHistThreads), kHistChunk * 4, s, xy, segs,
-                           (const uint32_t *)nullptr, 0, parts, partial, wh, (uint32_t *)nullptr, (uint32_t *)nullptr,
+        hipLaunchKernelGGL(kmeans_count_kernel, dim3(count_grid(parts, slots)), dim3(kHistThreads), kHistChunk * 4, s,
+                           xy, segs, (const uint32_t *)nullptr, 0, parts, slots, partial, wh, (uint32_t *)nullptr, (uint32_t *)nullptr,
                            (uint32_t)frame_w, (uint32_t)frame_h, ctx->flags + kKmFlagWord);
     }
     {
