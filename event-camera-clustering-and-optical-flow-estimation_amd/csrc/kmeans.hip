@@ -1052,16 +1052,16 @@ kmeans_step_kernel(StepArgs a, const uint32_t *__restrict__ ext, int n_ext, uint
     const uint32_t w = s_wh[0][0], h = s_wh[1][0];
     const int64_t cells = (int64_t)w * h;
     if constexpr (!kPix) {
-        for (int64_t c = (int64_t)blockIdx.x * kThreads + tid; c < cells; c += (int64_t)gridDim.x * kThreads) {
-            const uint32_t x = (uint32_t)(c % w), y = (uint32_t)(c / w);
+        for (uint32_t c = blockIdx.x * kThreads + tid; c < (uint32_t)cells; c += gridDim.x * kThreads) {
+            const uint32_t y = c / w, x = c - y * w;  // cells <= kImgSide^2: 32-bit index
             img[(int64_t)y * kImgSide + x] = (uint8_t)assign_fast<K>((float)x, (float)y, cx, cy, a.thr);
         }
     } else {
         __shared__ unsigned long long w_acc[3][K];
         for (int i = tid; i < 3 * K; i += kThreads) (&w_acc[0][0])[i] = 0ull;
         __syncthreads();
-        for (int64_t c = (int64_t)blockIdx.x * kThreads + tid; c < cells; c += (int64_t)gridDim.x * kThreads) {
-            const uint32_t x = (uint32_t)(c % w), y = (uint32_t)(c / w);
+        for (uint32_t c = blockIdx.x * kThreads + tid; c < (uint32_t)cells; c += gridDim.x * kThreads) {
+            const uint32_t y = c / w, x = c - y * w;  // cells <= kImgSide^2: 32-bit index
             const uint32_t n = px.cnt[c];
             if (!n) continue;
             const uint32_t l = assign_fast<K>((float)x, (float)y, cx, cy, a.thr);
