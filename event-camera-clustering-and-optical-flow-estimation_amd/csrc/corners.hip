@@ -55,6 +55,7 @@ constexpr int kMaxSlice = 1 << 19;       // group-local event index must fit 24 
 
 struct CornerGeom {
     int W, H, S, margin, border_mode, first_detect;
+    int any_order;         // timestamps in any order: every group wide (index values, exact tests)
     int tiles_x, n_tiles;  // bin n_tiles of each group holds the events outside the sensor
     float inv_S;
     int64_t n, n_slices;
@@ -99,6 +100,7 @@ __device__ __forceinline__ bool group_narrow(const int64_t *__restrict__ t, cons
     const int64_t first = grp * kGroup * (int64_t)g.S;
     const int64_t end = (grp + 1) * kGroup * (int64_t)g.S;
     *t_first = t[first];
+    if (g.any_order) return false;
     return (uint64_t)(t[(end < g.n ? end : g.n) - 1] - *t_first) < 0xffffffffull;
 }
 
@@ -109,6 +111,7 @@ __device__ __forceinline__ bool group_narrow(const int64_t *__restrict__ t, cons
 __device__ __forceinline__ bool group_fmt4(const int64_t *__restrict__ t, const CornerGeom &g, int64_t grp) {
     const int64_t first = grp * kGroup * (int64_t)g.S;
     const int64_t end = (grp + 1) * kGroup * (int64_t)g.S;
+    if (g.any_order) return false;
     return (uint64_t)(t[(end < g.n ? end : g.n) - 1] - t[first]) < 0xFFFFFFull;
 }
 
@@ -208,7 +211,7 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
             br[u] |= (uint32_t)atomicAdd(&hist[br[u] >> 16], 1) & 0xffffu;
         }
     }
-    if (__any(bad) && lane == 0) *err = 1;
+    if (__any(bad) && lane == 0 && !g.any_order) *err = 1;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) fb = min(fb, __shfl_xor(fb, o));
     if (lane == 0) wsum[tid >> 6] = fb;
@@ -320,7 +323,8 @@ __device__ __forceinline__ GroupRef group_ref(const int64_t *__restrict__ t, con
     const int64_t end = (grp + 1) * kGroup * (int64_t)g.S;
     r.t_first = t[r.first];
     r.Lt = t[(end < g.n ? end : g.n) - 1] - (int64_t)kVMax;
-    r.narrow = (r.Lt + (int64_t)kVMax) - r.t_first < (int64_t)kVMax;
+    // any order: the span of the first and last timestamps says nothing about the others
+    r.narrow = !g.any_order && (r.Lt + (int64_t)kVMax) - r.t_first < (int64_t)kVMax;
     r.dlt = r.narrow ? (uint32_t)(r.t_first - r.Lt) : 0u;
     return r;
 }
@@ -1406,6 +1410,7 @@ ECC_API void ecc_corner_cfg_default(ecc_corner_cfg *cfg) {
     cfg->margin = 4;              // cs = max_scale * 4, :948-951
     cfg->border_mode = 0;         // fixed; 1 = ref_compat `break` (Q11)
     cfg->first_detect_slice = 1;  // time_surface_flag (Q15)
+    cfg->any_order = 0;           // Metavision stream order (checked)
 }
 
 // phase bit 1: sort + pair entries (+ the shard-local last-t image when local_last != null);
@@ -1424,6 +1429,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     if (cfg->slice_events < 1 || cfg->slice_events > kMaxSlice ||
         (cfg->border_mode != 0 && cfg->border_mode != 1))
         return ECC_ERR_INVALID;
+    if (cfg->any_order != 0 && (cfg->any_order != 1 || phases != 3)) return ECC_ERR_INVALID;
     CornerGeom g{};
     g.W = cfg->width;
     g.H = cfg->height;
@@ -1432,6 +1438,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     g.margin = cfg->margin;
     g.border_mode = cfg->border_mode;
     g.first_detect = cfg->first_detect_slice;
+    g.any_order = cfg->any_order;
     g.tiles_x = (g.W + kTile - 1) / kTile;
     g.n_tiles = g.tiles_x * ((g.H + kTile - 1) / kTile);
     if (g.n_tiles > kMaxTiles) return ECC_ERR_INVALID;  // > 8191 16x16 tiles (~2.1 Mpixel)

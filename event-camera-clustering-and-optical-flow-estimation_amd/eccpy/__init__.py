@@ -52,7 +52,7 @@ class KmeansCfg(C.Structure):
 class CornerCfg(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("slice_events", C.c_int32),
                 ("margin", C.c_int32), ("border_mode", C.c_int32),
-                ("first_detect_slice", C.c_int32)]
+                ("first_detect_slice", C.c_int32), ("any_order", C.c_int32)]
 
 
 class RawInfo(C.Structure):

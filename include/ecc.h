@@ -244,6 +244,10 @@ typedef struct ecc_corner_cfg {
     int32_t margin;             /* 4 */
     int32_t border_mode;        /* 0 fixed (continue), 1 ref_compat (break) */
     int32_t first_detect_slice; /* 1 */
+    int32_t any_order;          /* 0: timestamps non-decreasing (checked: ECC_ERR_UNSORTED_TIME);
+                                 * 1: any order - the SAE keeps the LAST writer in stream order
+                                 * (Q14) and every arc test takes the exact path; ecc_fast_detect
+                                 * only (the multi-GPU hand-off combines shards by max time) */
 } ecc_corner_cfg;
 
 void ecc_corner_cfg_default(ecc_corner_cfg *cfg);

@@ -366,6 +366,60 @@ def test_fast_detect_rejects_decreasing_time(ecc, gpu):
     assert gpu.fast_detect_status() == ecc.ERR_UNSORTED_TIME
 
 
+def _any_order_times(kind, n, seed):
+    """Timestamps that are NOT non-decreasing: the oracle (the reference's loop) keeps the last
+    writer in stream order at every pixel, whatever the times are."""
+    rng = np.random.default_rng(seed)
+    t = np.cumsum(rng.integers(0, 40, n)).astype(np.int64)
+    if kind == "jitter":      # a sensor's slightly out-of-order packets
+        t = t + rng.integers(-300, 300, n)
+    elif kind == "shuffled":  # every slice's times permuted (ties and reversals everywhere)
+        for lo in range(0, n, 16384):
+            seg = t[lo:lo + 16384]
+            t[lo:lo + 16384] = rng.permutation(seg)
+    elif kind == "reversed":  # decreasing stream, negative times, 2^40-tick steps between slices
+        t = -(t + (np.arange(n) // 16384).astype(np.int64) * (1 << 40))
+    elif kind == "coarse":    # few distinct values: equal times at many circle pixels
+        t = rng.integers(0, 8, n).astype(np.int64)
+    return t
+
+
+@pytest.mark.parametrize("kind,mode", [("sorted", 0), ("jitter", 0), ("shuffled", 1), ("reversed", 0),
+                                       ("coarse", 0)])
+def test_fast_detect_any_order_matches_oracle(ecc, orc, gpu, kind, mode):
+    """cfg.any_order = 1: timestamps in any order (Q14's last writer in stream order), every
+    group on the exact index-valued path; flags and the final SAE equal the oracle's."""
+    W, H = 346, 260
+    n = 16384 * 70 + 123  # three groups + a ragged tail
+    xy, t0, _ = ecc.gen_events(n, seed=43, width=W, height=H)
+    t = t0.astype(np.int64) if kind == "sorted" else _any_order_times(kind, n, 7)
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H, border_mode=mode)
+    cfg = ecc.corner_cfg(width=W, height=H, border_mode=mode, any_order=1)
+    sae = ecc.DeviceArray.zeros(W * H, np.int64)
+    flags = ecc.DeviceArray(n, np.uint8)
+    gpu.fast_detect(dev(ecc, xy), dev(ecc, t), n, cfg, sae, flags)
+    assert gpu.fast_detect_status() == 0
+    g_flags = flags.numpy()
+    assert o_flags.sum() > 0
+    assert (g_flags == o_flags).all(), f"{(g_flags != o_flags).sum()} corner labels differ"
+    assert (sae.numpy() == o_sae).all()
+
+
+def test_fast_detect_any_order_single_call_only(ecc, gpu):
+    """The multi-GPU hand-off combines shard images by max time, so any_order is refused there."""
+    xy, t, _ = ecc.gen_events(40000, seed=2)
+    cfg = ecc.corner_cfg(width=W_SMALL, height=H_SMALL, any_order=1)
+    local = ecc.DeviceArray(W_SMALL * H_SMALL, np.int64)
+    rc = ecc.lib.ecc_fast_detect_prepare(gpu.ctx, dev(ecc, xy).ptr, dev(ecc, t).ptr, len(xy), ecc.C.byref(cfg),
+                                         local.ptr, gpu.stream)
+    assert rc == ecc.ERR_INVALID
+    cfg.any_order = 2
+    sae = ecc.DeviceArray.zeros(W_SMALL * H_SMALL, np.int64)
+    flags = ecc.DeviceArray(len(xy), np.uint8)
+    with pytest.raises(ecc.EccError):
+        gpu.fast_detect(dev(ecc, xy), dev(ecc, t), len(xy), cfg, sae, flags)
+
+
 def test_arc_test_known_patterns(ecc, orc, gpu):
     """Hand-built SAE patterns around one event (checked by the literal reference loop in the
     oracle): a contiguous fresh arc on both circles is a corner; gaps / ties / too long are not."""
