@@ -960,7 +960,8 @@ template <int K, bool kPix>
 __global__ void __launch_bounds__(kThreads)
 kmeans_step_kernel(StepArgs a, const uint32_t *__restrict__ ext, int n_ext, uint8_t *__restrict__ img,
                    KmState *st, PixArgs px) {
-    const bool done_in = st->done != 0;
+    // tol < 0 never sets done (fixed pass count): no dependent read of the state before the update
+    const bool done_in = a.tol >= 0.f && st->done != 0;
     if (done_in && !a.final_pass) return;
     const int tid = threadIdx.x;
     __shared__ uint32_t s_wh[2][kThreads];
