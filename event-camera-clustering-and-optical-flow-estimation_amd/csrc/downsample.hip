@@ -5,7 +5,7 @@
 // race with atomic_inc: the first hit of a bucket appends (x,y) to unique_coords (racy winner
 // and order, Q2), the second hit bumps repeated_count.
 //
-// MI355X design: one workgroup (4 wave64) per 8192-event window, all windows of a batch in
+// MI355X design: one workgroup (8 wave64) per 8192-event window, all windows of a batch in
 // ONE launch.  The window's packed-xy events are loaded with 16-B loads straight into
 // registers (HBM-bound stream, 4 B/event), each bucket keeps the MINIMUM local event index via
 // ds_min_u32 (canonical deterministic representative), a second pass marks repeated buckets
@@ -16,10 +16,11 @@
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / 64;
-constexpr int kChunk = kThreads * 4;      // events per chunk: 4 consecutive per lane
-constexpr int kMaxChunks = 16;            // window <= 16384
+// 8 waves per window (16 events per lane at 8192): four workgroups per CU by waves (33 KB of LDS
+// each).  Measured per kernel on the bench stream: 256 lanes 50 us (five per CU by LDS, each
+// window's phases on 4 waves), 512 lanes 42 us, 1024 lanes 48 us (two per CU).
+constexpr int kThreads = 512;
+constexpr int kMaxWindow = 16384;
 constexpr int kBuckets = 8192;            // LDS table (32 KiB)
 constexpr uint32_t kEmpty = 0x7fffffffu;
 constexpr uint32_t kRepeatBit = 0x80000000u;
@@ -35,14 +36,15 @@ __device__ inline void load4(const uint32_t *__restrict__ xy, int64_t g, int64_t
     }
 }
 
-template <int MAXC>
-__global__ void __launch_bounds__(kThreads)
+template <int NT, int MAXC>
+__global__ void __launch_bounds__(NT)
 downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, int n_chunks,
                        int x_max, int y_max, int mult_x, int mult_y,
                        uint32_t *__restrict__ rep_xy, uint32_t *__restrict__ rep_idx,
                        int32_t *__restrict__ win_unique, int32_t *__restrict__ win_repeated) {
     __shared__ __attribute__((aligned(16))) uint32_t table[kBuckets];
-    __shared__ int wave_tot[kMaxChunks][kWaves];
+    constexpr int kWaves = NT / 64, kChunk = NT * 4;  // events per chunk: 4 consecutive per lane
+    __shared__ int wave_tot[MAXC][kWaves];
     __shared__ int red[2][kWaves];
 
     const int tid = threadIdx.x;
@@ -56,7 +58,7 @@ downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, i
     {
         uint4 *t4 = reinterpret_cast<uint4 *>(table);
         const uint4 e = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
-        for (int i = tid; i < kBuckets / 4; i += kThreads) t4[i] = e;
+        for (int i = tid; i < kBuckets / 4; i += NT) t4[i] = e;
     }
 
     // 2. load the window into registers: lane owns events wbase + c*1024 + 4*tid + k
@@ -129,7 +131,7 @@ downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, i
     {
         int u = 0, rp = 0;
         const uint4 *t4 = reinterpret_cast<const uint4 *>(table);
-        for (int i = tid; i < kBuckets / 4; i += kThreads) {
+        for (int i = tid; i < kBuckets / 4; i += NT) {
             const uint4 q = t4[i];
             u += (q.x != kEmpty) + (q.y != kEmpty) + (q.z != kEmpty) + (q.w != kEmpty);
             rp += (q.x >> 31) + (q.y >> 31) + (q.z >> 31) + (q.w >> 31);
@@ -190,7 +192,7 @@ ECC_API int ecc_downsample_hash(ecc_ctx *ctx, const uint32_t *xy, int64_t n,
                                 const ecc_hash_cfg *cfg, uint32_t *rep_xy, uint32_t *rep_idx,
                                 int32_t *win_unique, int32_t *win_repeated, ecc_stream_t stream) {
     if (!ctx || !cfg || n < 0 || (n > 0 && !xy)) return ECC_ERR_INVALID;
-    if (cfg->window < 1 || cfg->window > kMaxChunks * kChunk) return ECC_ERR_INVALID;
+    if (cfg->window < 1 || cfg->window > kMaxWindow) return ECC_ERR_INVALID;
     if (cfg->n_buckets != kBuckets) return ECC_ERR_INVALID;
     if (cfg->x_max < 0 || cfg->y_max < 0 || cfg->mult_x < 0 || cfg->mult_y < 0) return ECC_ERR_INVALID;
     // (x*mult_x + y*mult_y) must not overflow int32 for u16 coordinates
@@ -198,9 +200,9 @@ ECC_API int ecc_downsample_hash(ecc_ctx *ctx, const uint32_t *xy, int64_t n,
     if (n == 0) return ECC_OK;
     const int64_t n_win = (n + cfg->window - 1) / cfg->window;
     if (n_win > INT32_MAX) return ECC_ERR_INVALID;
-    const int n_chunks = (cfg->window + kChunk - 1) / kChunk;
+    const int n_chunks = (cfg->window + 4 * kThreads - 1) / (4 * kThreads);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    auto kern = n_chunks <= 8 ? downsample_hash_kernel<8> : downsample_hash_kernel<kMaxChunks>;
+    auto kern = n_chunks <= 4 ? downsample_hash_kernel<kThreads, 4> : downsample_hash_kernel<kThreads, 8>;
     {
         ECC_TIMED(ctx, ecc::as_stream(stream), "downsample_hash_kernel");
         hipLaunchKernelGGL(kern, dim3((unsigned)n_win), dim3(kThreads), 0, ecc::as_stream(stream), xy,
