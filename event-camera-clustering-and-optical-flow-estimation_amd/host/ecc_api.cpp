@@ -257,13 +257,14 @@ std::vector<int64_t> reslice_n_us(Context &ctx, const int64_t *d_t, int64_t n, i
 }
 
 TimeSurfaceCornerDetector::TimeSurfaceCornerDetector(Context &ctx, int width, int height,
-                                                     int slice_events, int border_mode)
+                                                     int slice_events, int border_mode, bool any_order)
     : ctx_(ctx) {
     ecc_corner_cfg_default(&cfg_);
     cfg_.width = width;
     cfg_.height = height;
     cfg_.slice_events = slice_events;
     cfg_.border_mode = border_mode;
+    cfg_.any_order = any_order ? 1 : 0;
     sae_.reserve((size_t)width * height * 8);
     check(ecc_memset_async(sae_.data(), 0, (size_t)width * height * 8, ctx.stream()), "memset(sae)");
 }

@@ -176,8 +176,9 @@ class CornerTracker {  // :201-537, device-resident state
 // Batch SAE + arc-test corner detector (the aggregate lambda, :884-1070), stream-continuable.
 class TimeSurfaceCornerDetector {
   public:
+    // any_order: timestamps need not be non-decreasing (ecc_corner_cfg.any_order; exact path)
     TimeSurfaceCornerDetector(Context &ctx, int width, int height, int slice_events = 16384,
-                              int border_mode = 0);
+                              int border_mode = 0, bool any_order = false);
     // xy/t on the device; flags (device, n bytes) receive 1 for corner events.  The SAE carries
     // over between calls; the first call skips the first slice (time_surface_flag, :926).
     void detect(const uint32_t *d_xy, const int64_t *d_t, int64_t n, uint8_t *d_flags);
