@@ -922,6 +922,35 @@ def test_kmeans_c3_xy16_50m(ecc, gpu, c3_points, frame):
     assert (d_lab.numpy() == o_lab).all()
 
 
+@pytest.mark.parametrize("wh,frame,k", [
+    ((346, 260), (346, 260), 16),  # label image staged in LDS (90 KB)
+    ((346, 260), (346, 260), 24),  # the same with the K = 32 kernels
+    ((480, 360), (480, 360), 16),  # 173 KB frame: labels gathered from the global image
+    ((346, 260), (300, 200), 20),  # points outside the frame: assigned one by one
+])
+def test_kmeans_frame_segments_match_oracle(ecc, orc, gpu, wh, frame, k):
+    """The bench's layout: downsample windows of 8192 slots with per-window counts (ragged last
+    window, whose buffer ends at its count), through the frame path's count kernel and both
+    label kernels; centroids and every label equal the oracle's over the dense points."""
+    W, H = wh
+    n = 8192 * 300 + 1111
+    xy, _, _ = ecc.gen_events(n, seed=29, width=W, height=H)
+    rx, _, u, _ = orc.downsample_hash(xy)
+    nw = len(u)
+    dense = np.concatenate([rx[w * 8192: w * 8192 + u[w]] for w in range(nw)])
+    buf = rx[: (nw - 1) * 8192 + u[-1]].copy()  # no slack after the last window's points
+    c0 = np.stack([np.linspace(10, W - 10, k), np.linspace(10, H - 10, k)[::-1]], 1).astype(np.float32).ravel()
+    o_c, o_lab, o_it = orc.kmeans_run_xy16(dense, c0, 4)
+    d_c, d_lab = dev(ecc, c0), ecc.DeviceArray(nw * 8192, np.uint8)
+    cfg = ecc.kmeans_cfg(k=k, max_iters=4, tol=-1.0)
+    gpu.kmeans_xy16_frame(dev(ecc, buf), nw, 8192, dev(ecc, u.astype(np.int32)), frame[0], frame[1], d_c, cfg, d_lab)
+    gpu.sync()
+    assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
+    g_lab = d_lab.numpy()
+    g_dense = np.concatenate([g_lab[w * 8192: w * 8192 + u[w]] for w in range(nw)])
+    assert (g_dense == o_lab).all()
+
+
 @pytest.mark.parametrize("engine", [1, 2])
 def test_kmeans_c3_f32_50m(ecc, gpu, c3_points, engine):
     pts, c0, o_c, o_lab, o_it = c3_points
