@@ -131,25 +131,45 @@ def main():
         t_local = torch.zeros(W * H, dtype=torch.int64, device=f"cuda:{local}")
         t_all = torch.zeros(world * W * H, dtype=torch.int64, device=f"cuda:{local}")
 
-    def step_sharded(nb=0):
+    if dist:
+        t_b = torch.cuda.Stream(device=f"cuda:{local}")  # the k-means chain's stream
+        ev_f, ev_j = torch.cuda.Event(), torch.cuda.Event()
+
+    def step_sharded(nb=0, serial=args.serial):
         """Shard-local downsample/detection/NMS; global k-means from ONE all-reduce of the
         shards' per-pixel count images; exact SAE hand-off (all-gather of the shards' own last-t
-        images, computed by the detection's prepare phase)."""
+        images, computed by the detection's prepare phase).  As on one GPU, the downsample ->
+        k-means chain runs on a second stream beside the detection chain (--serial: one stream);
+        its all-reduce is issued from that stream, before the all-gather on every rank."""
         S = ctx.stream
+        main = torch.cuda.current_stream()
+        if not serial:
+            ev_f.record(main)
+            t_b.wait_event(ev_f)
+        B = S if serial else t_b.cuda_stream
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
-                                          uniq.ptr, rep.ptr, S), "downsample")
-        ecc.check(lib.ecc_kmeans_counts_xy16(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, W, H, t_counts.data_ptr(), S))
+                                          uniq.ptr, rep.ptr, B), "downsample")
+        ecc.check(lib.ecc_kmeans_counts_xy16(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, W, H, t_counts.data_ptr(), B))
+        # prepare is enqueued before the collectives: a blocking backend (gloo) waits on the host
         ecc.check(lib.ecc_fast_detect_prepare(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), t_local.data_ptr(), S))
-        dist.all_reduce(t_counts)
+        if serial:
+            dist.all_reduce(t_counts)
+        else:
+            with torch.cuda.stream(t_b):
+                dist.all_reduce(t_counts)
         dist.all_gather_into_tensor(t_all, t_local)
-        ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, S))
-        ecc.check(lib.ecc_kmeans_run_counts(ctx.ctx, t_counts.data_ptr(), W, H, ecc.C.byref(kcfg), d_c.ptr, None, S))
+        ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, B))
+        ecc.check(lib.ecc_kmeans_run_counts(ctx.ctx, t_counts.data_ptr(), W, H, ecc.C.byref(kcfg), d_c.ptr, None, B))
         ecc.check(lib.ecc_kmeans_labels_xy16(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, d_c.ptr, K,
-                                             kcfg.threshold, labels.ptr, S))
+                                             kcfg.threshold, labels.ptr, B))
+        if not serial:
+            ev_j.record(t_b)
         ecc.check(lib.ecc_sae_max_combine(ctx.ctx, t_all.data_ptr(), rank, W * H, sae.ptr, S))
         ecc.check(lib.ecc_fast_detect_finish(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), sae.ptr,
                                              flags.ptr, S), "fast_detect_finish")
         ctx.corner_nms(d_xy, flags, n, SLICE, W, H, 15, cap, nms_out[nb], nms_cnt[nb])
+        if not serial:
+            main.wait_event(ev_j)
 
     # single GPU: downsample -> k-means and the corner chain read the same resident batch and are
     # independent, so they run on two streams (fork/join with events) and overlap
@@ -161,7 +181,8 @@ def main():
 
     def step(serial=args.serial, nb=0):
         if dist:
-            return step_sharded(nb)
+            # gloo collectives block the host, so its rehearsals keep one stream (measured faster)
+            return step_sharded(nb, serial or args.dist_backend != "nccl")
         ks = ctx.stream if serial else s2.value  # the k-means chain's stream
         ecc.check(lib.ecc_event_record(ev_fork, ctx.stream))
         ecc.check(lib.ecc_stream_wait_event(ks, ev_fork))
