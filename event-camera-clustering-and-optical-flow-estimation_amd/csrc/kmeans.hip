@@ -227,33 +227,20 @@ constexpr int kAccCopies = 4;
 // atomic per (WG, cluster, field) at the end, spread over n_copies accumulator replicas.
 // (Fusing the update into the last-arriving workgroup was measured slower: the device-scope
 // release every workgroup needs before arriving costs more than the separate 1-wave launch.)
-template <int K, bool kAccumulate, bool kImg>
+template <int K, bool kAccumulate>
 __global__ void __launch_bounds__(kThreads)
 kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__restrict__ cent, int k, float thr,
-                   unsigned long long *acc, int n_copies, const KmState *st, uint8_t *__restrict__ labels,
-                   const uint8_t *__restrict__ img, const uint32_t *__restrict__ img_wh) {
+                   unsigned long long *acc, int n_copies, const KmState *st, uint8_t *__restrict__ labels) {
     if (kAccumulate && st->done) return;
-    // the label image covers [0, img_w) x [0, img_h) (the counted frame; <= kImgSide^2)
-    const uint32_t img_w = kImg ? img_wh[0] : 0u, img_h = kImg ? img_wh[1] : 0u;
     __shared__ unsigned long long slot[kWaves][K];
     __shared__ unsigned long long w_acc[3][K];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    // Label-image passes keep the centroids in LDS (only points outside the image read them), so
-    // the kernel holds no 2K centre registers; otherwise they live in scalar registers.
-    __shared__ float s_cx[kImg ? K : 1], s_cy[kImg ? K : 1];
-    float cx[kImg ? 1 : K], cy[kImg ? 1 : K];
-    if constexpr (kImg) {
-        if (tid < K) {
-            s_cx[tid] = tid < k ? cent[2 * tid] : 1e30f;
-            s_cy[tid] = tid < k ? cent[2 * tid + 1] : 1e30f;
-        }
-        if (!kAccumulate) __syncthreads();
-    } else {
+    // the centroids live in scalar registers
+    float cx[K], cy[K];
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
-            cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
-        }
+    for (int i = 0; i < K; ++i) {
+        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
+        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
     }
     if (kAccumulate) {
         for (int i = tid; i < 3 * K; i += kThreads) (&w_acc[0][0])[i] = 0ull;
@@ -299,12 +286,7 @@ kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__re
                     const uint32_t x = (uint32_t)ecc::xy_x(w), y = (uint32_t)ecc::xy_y(w);
                     uint32_t l;
                     if (j + e >= cnt) l = 255u;
-                    else if constexpr (kImg) {
-                        if (__builtin_expect(x < img_w && y < img_h, 1)) l = img[y * kImgSide + x];
-                        else l = assign_lds<K>((float)x, (float)y, s_cx, s_cy, thr);
-                    } else {
-                        l = assign_fast<K>((float)x, (float)y, cx, cy, thr);
-                    }
+                    else l = assign_fast<K>((float)x, (float)y, cx, cy, thr);
                     lab[4 * u + e] = l;
                 }
             }
@@ -368,7 +350,7 @@ kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__re
 // packed stores each in flight together (kmeans_fast_kernel's two-batch trips took two dependent
 // load -> gather -> store rounds per bench segment of ~3150 points).  The loads are issued
 // before the segment count arrives: a lane reads within the segment's stride (always readable),
-// and only the stores are masked by the count.  Labels equal kmeans_fast_kernel<K, false, true>'s.
+// and only the stores are masked by the count.  Labels equal assign_fast's on the same points.
 constexpr int kLabPer = 16;
 template <int K>
 __global__ void __launch_bounds__(kThreads)
@@ -1098,23 +1080,14 @@ void launch_step(dim3 grid, hipStream_t s, const StepArgs &a, const uint32_t *ex
 // Launch helpers for the fast path (k <= kFastMaxK); false when k needs the generic kernel.
 template <bool kAccumulate>
 bool launch_fast(int k, dim3 grid, hipStream_t s, const uint32_t *xy, const Segs &segs, const float *cent,
-                 float thr, unsigned long long *acc, int n_copies, const KmState *st, uint8_t *labels,
-                 const uint8_t *img = nullptr, const uint32_t *img_wh = nullptr) {
+                 float thr, unsigned long long *acc, int n_copies, const KmState *st, uint8_t *labels) {
     if (k > kFastMaxK) return false;
-    if (img) {
-        if (k <= 16)
-            hipLaunchKernelGGL((kmeans_fast_kernel<16, kAccumulate, true>), grid, dim3(kThreads), 0, s, xy, segs,
-                               cent, k, thr, acc, n_copies, st, labels, img, img_wh);
-        else
-            hipLaunchKernelGGL((kmeans_fast_kernel<32, kAccumulate, true>), grid, dim3(kThreads), 0, s, xy, segs,
-                               cent, k, thr, acc, n_copies, st, labels, img, img_wh);
-    } else if (k <= 16) {
-        hipLaunchKernelGGL((kmeans_fast_kernel<16, kAccumulate, false>), grid, dim3(kThreads), 0, s, xy, segs,
-                           cent, k, thr, acc, n_copies, st, labels, img, img_wh);
-    } else {
-        hipLaunchKernelGGL((kmeans_fast_kernel<32, kAccumulate, false>), grid, dim3(kThreads), 0, s, xy, segs,
-                           cent, k, thr, acc, n_copies, st, labels, img, img_wh);
-    }
+    if (k <= 16)
+        hipLaunchKernelGGL((kmeans_fast_kernel<16, kAccumulate>), grid, dim3(kThreads), 0, s, xy, segs, cent, k, thr,
+                           acc, n_copies, st, labels);
+    else
+        hipLaunchKernelGGL((kmeans_fast_kernel<32, kAccumulate>), grid, dim3(kThreads), 0, s, xy, segs, cent, k, thr,
+                           acc, n_copies, st, labels);
     return true;
 }
 

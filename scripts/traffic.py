@@ -20,6 +20,8 @@ def short(name: str) -> str:
     # map to the names libecc's timing report (and bench.py) use
     if base in ("kmeans_xy16_kernel", "kmeans_fast_kernel"):
         return "kmeans_xy16_labels" if re.search(r"<(\d+, )?false[,>]", name) else "kmeans_xy16_kernel"
+    if base in ("kmeans_lds_labels_kernel", "kmeans_img_labels_kernel"):
+        return "kmeans_xy16_labels"
     if base in ("nms_grid_kernel", "nms_greedy_kernel"):
         return "nms_kernel"
     if base == "kmeans_step_kernel" and re.search(r"<\d+, true>", name):
