@@ -77,6 +77,13 @@ def parse():
                          "shard's outputs, the global centroids and (rank 0) the merged tracker (rehearsal sizes)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on device 0 (with --dist-backend gloo)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the sharded step even at world size 1: a 1-rank process group of --dist-backend "
+                         "(nccl = RCCL), so the C5 code path — collectives, SAE combine, corner pack/gather, "
+                         "track merge — executes on a single GPU")
+    ap.add_argument("--overlap", action="store_true",
+                    help="keep the two-stream sharded schedule under gloo too (correctness rehearsals; gloo "
+                         "collectives block the host, so it is not a timing configuration)")
     a = ap.parse_args()
     if a.events is None:
         a.events = {"c4": 1221, "c5": 3052}[a.preset] * SLICE
@@ -92,9 +99,14 @@ def main():
         local = 0
     dist = None
     torch = None
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch
         import torch.distributed as tdist
+        if world == 1:  # a 1-rank group needs its own rendezvous
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 2000))
         torch.cuda.set_device(local)
         tdist.init_process_group(args.dist_backend)
         dist = tdist
@@ -181,8 +193,9 @@ def main():
 
     def step(serial=args.serial, nb=0):
         if dist:
-            # gloo collectives block the host, so its rehearsals keep one stream (measured faster)
-            return step_sharded(nb, serial or args.dist_backend != "nccl")
+            # gloo collectives block the host, so its timing runs keep one stream (measured faster);
+            # --overlap keeps the two-stream schedule for correctness rehearsals
+            return step_sharded(nb, serial or (args.dist_backend != "nccl" and not args.overlap))
         ks = ctx.stream if serial else s2.value  # the k-means chain's stream
         ecc.check(lib.ecc_event_record(ev_fork, ctx.stream))
         ecc.check(lib.ecc_stream_wait_event(ks, ev_fork))
