@@ -61,3 +61,15 @@ inline int opt_int(int argc, char **argv, const char *name, int def) {
         if (!std::strcmp(argv[i], name)) return std::atoi(argv[i + 1]);
     return def;
 }
+
+inline double opt_double(int argc, char **argv, const char *name, double def) {
+    for (int i = 1; i + 1 < argc; ++i)
+        if (!std::strcmp(argv[i], name)) return std::atof(argv[i + 1]);
+    return def;
+}
+
+inline bool has_flag(int argc, char **argv, const char *name) {
+    for (int i = 1; i < argc; ++i)
+        if (!std::strcmp(argv[i], name)) return true;
+    return false;
+}

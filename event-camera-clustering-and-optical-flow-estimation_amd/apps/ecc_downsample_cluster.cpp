@@ -10,11 +10,6 @@
 
 #include "app_common.hpp"
 
-static double opt_double(int argc, char **argv, const char *name, double def) {
-    for (int i = 1; i + 1 < argc; ++i)
-        if (!std::strcmp(argv[i], name)) return std::atof(argv[i + 1]);
-    return def;
-}
 static const char *opt_str(int argc, char **argv, const char *name) {
     for (int i = 1; i + 1 < argc; ++i)
         if (!std::strcmp(argv[i], name)) return argv[i + 1];

@@ -1699,3 +1699,50 @@ ECC_API int ecc_tracker_get_groups(ecc_tracker *tr, ecc_group *out, int32_t cap,
         ECC_CHECK_HIP(tr->ctx, hipMemcpy(labels, tr->group_labels, sizeof(int) * nl, hipMemcpyDeviceToHost), "read labels");
     return (c.n_groups > cap || c.n_group_labels > labels_cap) ? ECC_ERR_CAPACITY : ECC_OK;
 }
+
+// Checkpoint / hand-over (SURVEY §5, §8e "track state handed rank->rank"): the reference's
+// CornerTracker is a value (FCT/…group_track.cpp:163-199: the track list plus next_label); this
+// replaces the device tracker's list by a host copy, e.g. one ecc_tracker_get_tracks returned.
+// The groups are derived state (updateCornerGroups rebuilds them on every update, :321-398) and
+// read as empty until the next update.
+ECC_API int ecc_tracker_set_tracks(ecc_tracker *tr, const ecc_track *tracks, int32_t n, int32_t next_label,
+                                   ecc_stream_t stream) {
+    if (!tr || n < 0 || (n > 0 && !tracks)) return ECC_ERR_INVALID;
+    if (n > tr->max_tracks) return ECC_ERR_CAPACITY;
+    for (int i = 0; i < n; ++i)
+        if (tracks[i].hist_len < 0 || tracks[i].hist_len > kH) return ECC_ERR_INVALID;
+    hipStream_t s = ecc::as_stream(stream);
+    ECC_CHECK_HIP(tr->ctx, hipSetDevice(tr->ctx->device), "hipSetDevice");
+    std::vector<DevTrack> h((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        const ecc_track &t = tracks[i];
+        DevTrack &o = h[i];
+        std::memset(&o, 0, sizeof(o));
+        o.x = t.x; o.y = t.y; o.label = t.label; o.frame_count = t.frame_count;
+        o.is_matched = t.is_matched; o.fsld = t.frames_since_last_detection;
+        o.hist_len = t.hist_len;
+        for (int k = 0; k < t.hist_len; ++k) { o.hx[k] = t.hist_x[k]; o.hy[k] = t.hist_y[k]; }
+        o.vx = t.vx; o.vy = t.vy;
+        o.dcx = t.dir_cur_x; o.dcy = t.dir_cur_y; o.dtx = t.dir_tgt_x; o.dty = t.dir_tgt_y;
+        o.group_id = t.group_id;
+    }
+    TrackerCounters c{};
+    c.n_tracks = n;
+    c.next_label = next_label;
+    // the copies are staged in pageable memory: synchronous with respect to the host
+    ECC_CHECK_HIP(tr->ctx, hipStreamSynchronize(s), "sync");
+    if (n > 0)
+        ECC_CHECK_HIP(tr->ctx, hipMemcpy(tr->buf[0], h.data(), sizeof(DevTrack) * (size_t)n, hipMemcpyHostToDevice),
+                      "write tracks");
+    ECC_CHECK_HIP(tr->ctx, hipMemcpy(tr->ctr, &c, sizeof(c), hipMemcpyHostToDevice), "write ctr");
+    return ECC_OK;
+}
+
+ECC_API int ecc_tracker_next_label(ecc_tracker *tr, int32_t *next_label, ecc_stream_t stream) {
+    if (!tr || !next_label) return ECC_ERR_INVALID;
+    TrackerCounters c{};
+    ECC_CHECK_HIP(tr->ctx, hipMemcpyAsync(&c, tr->ctr, sizeof(c), hipMemcpyDeviceToHost, ecc::as_stream(stream)), "read ctr");
+    ECC_CHECK_HIP(tr->ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
+    *next_label = c.next_label;
+    return ECC_OK;
+}

@@ -162,6 +162,8 @@ _sigs = {
     "ecc_tracker_get_tracks": (C.c_int, [P, P, i32, C.POINTER(i32), P]),
     "ecc_tracker_get_groups": (C.c_int, [P, P, i32, C.POINTER(i32), P, i32, P]),
     "ecc_tracker_status": (C.c_int, [P, P]),
+    "ecc_tracker_set_tracks": (C.c_int, [P, P, i32, i32, P]),
+    "ecc_tracker_next_label": (C.c_int, [P, C.POINTER(i32), P]),
     "ecc_eps_counts": (C.c_int, [P, P, i64, i64, P, C.c_double, i32, P, P, P]),
     "ecc_eps_lists": (C.c_int, [P, P, i64, i64, P, C.c_double, P, P, P, i64, P]),
     "ecc_eps_total": (C.c_int, [P, P, i64, C.POINTER(i64), P]),
@@ -178,6 +180,12 @@ _sigs = {
     "ecc_radius_counts_f64": (C.c_int, [P, P, i64, i32, C.c_double, i32, P, P, P]),
     "ecc_radius_lists_f64": (C.c_int, [P, P, i64, i32, C.c_double, P, P, P, P, i64, P]),
     "ecc_radius_status": (C.c_int, [P, P]),
+    "ecc_radius_counts_f32": (C.c_int, [P, P, i64, i32, C.c_double, i32, P, P, P]),
+    "ecc_radius_lists_f32": (C.c_int, [P, P, i64, i32, C.c_double, P, P, P, P, i64, P]),
+    "ecc_lists_sort_ascending": (C.c_int, [P, i64, P, i64, P, P, P]),
+    "ecc_dbscan_cloud_f32": (C.c_int, [P, P, i64, i32, C.c_double, i32, i32, i32, P, P, P, i64, P, P]),
+    "ecc_dbscan_cloud_f64": (C.c_int, [P, P, i64, i32, C.c_double, i32, i32, i32, P, P, P, i64, P, P]),
+    "ecc_dbscan_cloud_status": (C.c_int, [P, P]),
     "ecc_optics_f64": (C.c_int, [P, P, i64, i32, i32, C.c_double, P, P, P]),
     "ecc_dbscan_extract": (C.c_int, [P, i64, i64, P, P, P, i64, i32, i32, i32, P, P, P, i64, P, P]),
     "ecc_dbscan_grid": (C.c_int, [P, P, i64, i64, P, C.c_double, i32, i32, i32, P, P, P, i64, P, P]),
@@ -441,6 +449,33 @@ class Context:
     def radius_status(self) -> int:
         return lib.ecc_radius_status(self.ctx, self.stream)
 
+    def radius_counts_f32(self, pts: DeviceArray, n: int, dim: int, eps: float, min_pts: int,
+                          counts: DeviceArray, core: DeviceArray | None = None):
+        check(lib.ecc_radius_counts_f32(self.ctx, pts.ptr, n, dim, eps, min_pts, counts.ptr, _ptr(core),
+                                        self.stream), "ecc_radius_counts_f32")
+
+    def radius_lists_f32(self, pts: DeviceArray, n: int, dim: int, eps: float, counts: DeviceArray,
+                         offsets: DeviceArray, nbr: DeviceArray | None, nbr_cap: int,
+                         nbr_dist: DeviceArray | None = None):
+        check(lib.ecc_radius_lists_f32(self.ctx, pts.ptr, n, dim, eps, counts.ptr, offsets.ptr, _ptr(nbr),
+                                       _ptr(nbr_dist), nbr_cap, self.stream), "ecc_radius_lists_f32")
+
+    def lists_sort_ascending(self, n: int, offsets: DeviceArray, total: int, nbr: DeviceArray,
+                             nbr_dist: DeviceArray | None = None):
+        check(lib.ecc_lists_sort_ascending(self.ctx, n, offsets.ptr, total, nbr.ptr, _ptr(nbr_dist), self.stream),
+              "ecc_lists_sort_ascending")
+
+    def dbscan_cloud(self, pts: DeviceArray, n: int, dim: int, eps: float, min_pts: int, min_size: int,
+                     max_size: int, labels: DeviceArray, n_clusters: DeviceArray, dups: DeviceArray | None,
+                     dup_cap: int, n_dups: DeviceArray):
+        """DBSCAN of one cloud (device float32 or float64 [n*dim], picked by pts.dtype)."""
+        fn = lib.ecc_dbscan_cloud_f32 if pts.dtype == np.float32 else lib.ecc_dbscan_cloud_f64
+        check(fn(self.ctx, pts.ptr, n, dim, eps, min_pts, min_size, max_size, labels.ptr, n_clusters.ptr,
+                 _ptr(dups), dup_cap, n_dups.ptr, self.stream), "ecc_dbscan_cloud")
+
+    def dbscan_cloud_status(self) -> int:
+        return lib.ecc_dbscan_cloud_status(self.ctx, self.stream)
+
     def optics_f64(self, pts_host, min_pts: int, eps: float = -1.0):
         """OPTICS ordering of host points (n x dim, dim 1-3): (order int64[n], reach double[n])."""
         pts = np.ascontiguousarray(pts_host, np.float64)
@@ -513,6 +548,17 @@ class Tracker:
         if rc not in (OK, ERR_CAPACITY):
             check(rc, "ecc_tracker_get_groups")
         return [buf[i] for i in range(min(n.value, cap))], labels
+
+    def next_label(self) -> int:
+        v = i32(0)
+        check(lib.ecc_tracker_next_label(self.tr, C.byref(v), self.ctx.stream), "ecc_tracker_next_label")
+        return v.value
+
+    def set_tracks(self, tracks, next_label: int):
+        """Replace the state by a track list (e.g. another tracker's tracks()) and next label."""
+        arr = (Track * max(len(tracks), 1))(*tracks)
+        check(lib.ecc_tracker_set_tracks(self.tr, arr, len(tracks), next_label, self.ctx.stream),
+              "ecc_tracker_set_tracks")
 
     def close(self):
         if self.tr:

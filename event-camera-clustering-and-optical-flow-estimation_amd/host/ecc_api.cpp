@@ -339,15 +339,15 @@ int analyzeCoordinates(Context &ctx, const int *data, int n_ints, std::vector<Co
           "ecc_dedup_exact");
     int32_t u = 0;
     d_u.download(&u, 4, s);
+    std::vector<uint32_t> idx(coords ? n : 0);
+    std::vector<int32_t> cnt(coords ? n : 0);
     if (coords) {
-        std::vector<uint32_t> idx(n);
-        std::vector<int32_t> cnt(n);
         d_idx.download(idx.data(), (size_t)n * 4, s);
         d_cnt.download(cnt.data(), (size_t)n * 4, s);
-        ctx.sync();
-        for (int k = 0; k < u; ++k) coords->push_back(CoordinateInfo{data[2 * idx[k]], data[2 * idx[k] + 1], cnt[k]});
     }
-    ctx.sync();
+    ctx.sync();  // one sync for the count and the lists
+    if (coords)
+        for (int k = 0; k < u; ++k) coords->push_back(CoordinateInfo{data[2 * idx[k]], data[2 * idx[k] + 1], cnt[k]});
     return u;
 }
 
@@ -379,40 +379,59 @@ void eps_neighbour_lists(Context &ctx, const std::vector<std::array<int, 2>> &po
     offsets.assign(n + 1, 0);
     nbr.clear();
     if (n == 0) return;
-    if (n > 16384) throw Error(ECC_ERR_INVALID, "eps_neighbour_lists: more than 16384 points");
+    ecc_stream_t s = ctx.stream();
     int mnx = points[0][0], mny = points[0][1], mxx = mnx, mxy = mny;
     for (const auto &p : points) {
         mnx = std::min(mnx, p[0]); mny = std::min(mny, p[1]);
         mxx = std::max(mxx, p[0]); mxy = std::max(mxy, p[1]);
     }
-    if ((int64_t)mxx - mnx > 65535 || (int64_t)mxy - mny > 65535)
-        throw Error(ECC_ERR_INVALID, "eps_neighbour_lists: coordinate span exceeds 65535");
-    std::vector<uint32_t> xy(n);  // translation keeps every distance
-    for (int64_t i = 0; i < n; ++i) xy[i] = pack_xy(points[i][0] - mnx, points[i][1] - mny);
-    DeviceBuffer d_xy, d_cnt(n * 4), d_core(core_dist ? n * 8 : 8), d_off((n + 1) * 8);
-    d_xy.upload(xy.data(), n * 4, ctx.stream());
-    check(ecc_eps_counts(ctx.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps, std::max(1, min_pts),
-                         d_cnt.as<int32_t>(), core_dist ? d_core.as<double>() : nullptr, ctx.stream()),
-          "ecc_eps_counts");
+    const bool windowed = n <= 16384 && (int64_t)mxx - mnx <= 65535 && (int64_t)mxy - mny <= 65535 &&
+                          (!core_dist || min_pts <= 64);
+    DeviceBuffer d_cnt(n * 4), d_core(core_dist ? n * 8 : 8), d_off((n + 1) * 8), d_pts;
+    if (windowed) {  // one segment of packed u16 pixels (translation keeps every distance)
+        std::vector<uint32_t> xy(n);
+        for (int64_t i = 0; i < n; ++i) xy[i] = pack_xy(points[i][0] - mnx, points[i][1] - mny);
+        d_pts.upload(xy.data(), n * 4, s);
+        check(ecc_eps_counts(ctx.get(), d_pts.as<uint32_t>(), 1, n, nullptr, eps, std::max(1, min_pts),
+                             d_cnt.as<int32_t>(), core_dist ? d_core.as<double>() : nullptr, s),
+              "ecc_eps_counts");
+    } else {  // any size / span / min_pts: the global grid over the points as doubles (exact for int)
+        std::vector<double> f(2 * n);
+        for (int64_t i = 0; i < n; ++i) { f[2 * i] = points[i][0]; f[2 * i + 1] = points[i][1]; }
+        d_pts.upload(f.data(), f.size() * 8, s);
+        check(ecc_radius_counts_f64(ctx.get(), d_pts.as<double>(), n, 2, eps, std::max(1, min_pts), d_cnt.as<int32_t>(),
+                                    core_dist ? d_core.as<double>() : nullptr, s),
+              "ecc_radius_counts_f64");
+    }
     // list size from the counts (one small readback, as the reference reads sizes back)
     std::vector<int32_t> cnt(n);
-    d_cnt.download(cnt.data(), n * 4, ctx.stream());
+    d_cnt.download(cnt.data(), n * 4, s);
     int64_t total = 0;
     for (int32_t c : cnt) total += c;
     DeviceBuffer d_nbr(std::max<int64_t>(total, 1) * 4);
-    check(ecc_eps_lists(ctx.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps, d_cnt.as<int32_t>(),
-                        d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, ctx.stream()),
-          "ecc_eps_lists");
-    int64_t tot2 = 0;
-    check(ecc_eps_total(ctx.get(), d_off.as<int64_t>(), n, &tot2, ctx.stream()), "ecc_eps_lists capacity");
+    if (windowed) {
+        check(ecc_eps_lists(ctx.get(), d_pts.as<uint32_t>(), 1, n, nullptr, eps, d_cnt.as<int32_t>(),
+                            d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, s),
+              "ecc_eps_lists");
+        int64_t tot2 = 0;
+        check(ecc_eps_total(ctx.get(), d_off.as<int64_t>(), n, &tot2, s), "ecc_eps_lists capacity");
+    } else {
+        check(ecc_radius_lists_f64(ctx.get(), d_pts.as<double>(), n, 2, eps, d_cnt.as<int32_t>(), d_off.as<int64_t>(),
+                                   d_nbr.as<int32_t>(), nullptr, total, s),
+              "ecc_radius_lists_f64");
+        check(ecc_lists_sort_ascending(ctx.get(), n, d_off.as<int64_t>(), total, d_nbr.as<int32_t>(), nullptr, s),
+              "ecc_lists_sort_ascending");
+        check(ecc_radius_status(ctx.get(), s), "ecc_radius_lists_f64");
+    }
     offsets.resize(n + 1);
     nbr.resize(total);
-    d_off.download(offsets.data(), (n + 1) * 8, ctx.stream());
-    d_nbr.download(nbr.data(), total * 4, ctx.stream());
+    d_off.download(offsets.data(), (n + 1) * 8, s);
+    d_nbr.download(nbr.data(), total * 4, s);
     if (core_dist) {
         core_dist->resize(n);
-        d_core.download(core_dist->data(), n * 8, ctx.stream());
+        d_core.download(core_dist->data(), n * 8, s);
     }
+    ctx.sync();
 }
 
 // ------------------------------------------------------------------------------ OPTICS
@@ -442,7 +461,7 @@ namespace {
 std::vector<reachability_dist> optics_f64(ecc_ctx *ctx, ecc_stream_t s, const double *pts, int64_t n, int D,
                                           std::size_t min_pts, double epsilon) {
     if (n == 0) return {};
-    if (min_pts < 1 || min_pts > 64) throw Error(ECC_ERR_INVALID, "compute_reachability_dists: min_pts must be 1..64");
+    if (min_pts < 1) throw Error(ECC_ERR_INVALID, "compute_reachability_dists: min_pts must be >= 1");
     if (D < 1 || D > 3) throw Error(ECC_ERR_INVALID, "compute_reachability_dists: dimension must be 1..3");
     if (n >= INT32_MAX) throw Error(ECC_ERR_INVALID, "compute_reachability_dists: too many points");
     static const bool timing = std::getenv("ECC_OPTICS_TIMING") != nullptr;  // phase split to stderr
@@ -604,64 +623,37 @@ std::vector<std::vector<std::size_t>> get_cluster_indices(const std::vector<reac
 
 // ------------------------------------------------------------------------------ DBSCAN
 void DBSCANSimpleCluster::extract(std::vector<PointIndices> &cluster_indices) {  // DBSCAN_simple.h:27-90
-    // radiusSearch for every point and the seed-queue expansion (union-find closed form) both run
-    // on the GPU — fused over an LDS cell grid (ecc_dbscan_grid) up to 8192 points, else through
-    // ecc_eps_counts / ecc_eps_lists / ecc_dbscan_extract; the host only turns labels + duplicate
-    // memberships into PointIndices.
+    // The reference's own input (float x, y, z; any size): radiusSearch (:118-142) and the
+    // seed-queue expansion (union-find closed form) both run on the GPU over one global cell grid
+    // (ecc_dbscan_cloud_f32); the host only turns labels + duplicate memberships into PointIndices.
     cluster_indices.clear();
     const int64_t n = (int64_t)cloud_.size();
     if (n == 0) return;
-    if (n > 16384) throw Error(ECC_ERR_INVALID, "DBSCAN: more than 16384 points per cloud");
-    int mnx = 0, mny = 0, mxx = 0, mxy = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const PointXYZ &p = cloud_[i];
-        if (p.x != std::floor(p.x) || p.y != std::floor(p.y) || p.z != cloud_[0].z)
-            throw Error(ECC_ERR_INVALID, "DBSCAN: GPU path needs integer-valued 2-D points (constant z)");
-        const int x = (int)p.x, y = (int)p.y;
-        if (i == 0 || x < mnx) mnx = x;
-        if (i == 0 || y < mny) mny = y;
-        if (i == 0 || x > mxx) mxx = x;
-        if (i == 0 || y > mxy) mxy = y;
-    }
-    if ((int64_t)mxx - mnx > 65535 || (int64_t)mxy - mny > 65535)
-        throw Error(ECC_ERR_INVALID, "DBSCAN: coordinate span exceeds 65535");
-    std::vector<uint32_t> xy(n);  // translation keeps every distance
-    for (int64_t i = 0; i < n; ++i) xy[i] = pack_xy((int)cloud_[i].x - mnx, (int)cloud_[i].y - mny);
+    static_assert(sizeof(PointXYZ) == 12, "PointXYZ must be three packed floats");
     ecc_stream_t s = ctx_.stream();
-    DeviceBuffer d_xy(n * 4), d_lab(n * 4), d_nc(4), d_nd(8);
-    d_xy.upload(xy.data(), n * 4, s);
-    const int64_t dup_cap = std::max<int64_t>(n, 1024);
-    DeviceBuffer d_dups(dup_cap * 16);
-    if (n <= 8192) {  // one fused launch over an LDS cell grid, no neighbour lists
-        check(ecc_dbscan_grid(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, minPts_, min_pts_per_cluster_,
-                              max_pts_per_cluster_, d_lab.as<int32_t>(), d_nc.as<int32_t>(), d_dups.as<int64_t>(),
-                              dup_cap, d_nd.as<int64_t>(), s),
-              "ecc_dbscan_grid");
-    } else {  // counts -> ascending lists -> extraction
-        DeviceBuffer d_cnt(n * 4), d_off((n + 1) * 8);
-        check(ecc_eps_counts(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, 1, d_cnt.as<int32_t>(), nullptr, s),
-              "ecc_eps_counts");
-        std::vector<int32_t> cnt(n);
-        d_cnt.download(cnt.data(), n * 4, s);
+    DeviceBuffer d_pts, d_lab(n * 4), d_nc(4), d_nd(8);
+    d_pts.upload(cloud_.data(), (size_t)n * 12, s);
+    int64_t dup_cap = std::max<int64_t>(n, 1024), nd = 0;
+    DeviceBuffer d_dups;
+    for (;;) {
+        d_dups.reserve((size_t)dup_cap * 16);
+        check(ecc_dbscan_cloud_f32(ctx_.get(), reinterpret_cast<const float *>(d_pts.data()), n, 3, searchTolerance(), minPts_,
+                                   min_pts_per_cluster_, max_pts_per_cluster_, d_lab.as<int32_t>(), d_nc.as<int32_t>(),
+                                   d_dups.as<int64_t>(), dup_cap, d_nd.as<int64_t>(), s),
+              "ecc_dbscan_cloud_f32");
+        const int st = ecc_dbscan_cloud_status(ctx_.get(), s);
+        d_nd.download(&nd, 8, s);
         ctx_.sync();
-        int64_t total = 0;
-        for (int32_t c : cnt) total += c;
-        DeviceBuffer d_nbr(std::max<int64_t>(total, 1) * 4);
-        check(ecc_eps_lists(ctx_.get(), d_xy.as<uint32_t>(), 1, n, nullptr, eps_, d_cnt.as<int32_t>(),
-                            d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, s),
-              "ecc_eps_lists");
-        check(ecc_dbscan_extract(ctx_.get(), 1, n, nullptr, d_off.as<int64_t>(), d_nbr.as<int32_t>(), total, minPts_,
-                                 min_pts_per_cluster_, max_pts_per_cluster_, d_lab.as<int32_t>(), d_nc.as<int32_t>(),
-                                 d_dups.as<int64_t>(), dup_cap, d_nd.as<int64_t>(), s),
-              "ecc_dbscan_extract");
-        ctx_.sync();  // the lists must outlive the extraction
+        if (st == ECC_ERR_CAPACITY && nd > dup_cap) {  // more duplicate memberships than room: grow, rerun
+            dup_cap = nd;
+            continue;
+        }
+        check(st, "ecc_dbscan_cloud_f32");
+        break;
     }
-    check(ecc_dbscan_status(ctx_.get(), s), "ecc_dbscan_extract");
     int32_t nc = 0;
-    int64_t nd = 0;
     std::vector<int32_t> lab(n);
     d_nc.download(&nc, 4, s);
-    d_nd.download(&nd, 8, s);
     d_lab.download(lab.data(), n * 4, s);
     std::vector<int64_t> dups((size_t)nd * 2);
     if (nd) d_dups.download(dups.data(), (size_t)nd * 16, s);
@@ -671,7 +663,7 @@ void DBSCANSimpleCluster::extract(std::vector<PointIndices> &cluster_indices) { 
         if (lab[i] >= 0) members[lab[i]].push_back((int)i);
     for (int64_t k = 0; k < nd; ++k) members[dups[2 * k + 1]].push_back((int)dups[2 * k]);
     for (auto &m : members) {
-        std::sort(m.begin(), m.end());
+        std::sort(m.begin(), m.end());  // :82
         cluster_indices.push_back(PointIndices{m});
     }
 }

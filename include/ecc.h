@@ -366,6 +366,15 @@ int ecc_tracker_get_groups(ecc_tracker *tr, ecc_group *out, int32_t cap, int32_t
                            int32_t *labels, int32_t labels_cap, ecc_stream_t stream);
 /* 0 = OK, otherwise an ecc_status (capacity overflow inside the device loop). */
 int ecc_tracker_status(ecc_tracker *tr, ecc_stream_t stream);
+/* Checkpoint / restore and rank->rank hand-over of the tracker state (the reference's
+ * CornerTracker is a copyable value, FCT/…group_track.cpp:163-199): the next label a new track
+ * gets, and a replacement track list (HOST tracks, e.g. from ecc_tracker_get_tracks) with that
+ * next label.  After set_tracks, updates continue exactly as the tracker the state came from;
+ * the groups read as empty until the next update rebuilds them (:321-398).  Synchronous.
+ * n > max_tracks: ECC_ERR_CAPACITY. */
+int ecc_tracker_next_label(ecc_tracker *tr, int32_t *next_label, ecc_stream_t stream);
+int ecc_tracker_set_tracks(ecc_tracker *tr, const ecc_track *tracks, int32_t n, int32_t next_label,
+                           ecc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * 6. eps-neighbourhoods for DBSCAN / OPTICS over 2-D integer points (pixels)
@@ -395,7 +404,7 @@ int ecc_eps_lists(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t seg_
 int ecc_eps_total(ecc_ctx *ctx, const int64_t *offsets, int64_t n, int64_t *total,
                   ecc_stream_t stream);
 
-/* Radius neighbourhoods of ONE fp64 point set of any size in 1-3 dimensions (the OPTICS
+/* Radius neighbourhoods of ONE fp64 (or fp32) point set of any size in 1-3 dimensions (the OPTICS
  * library's radius search, §8a rows a11-a12, beyond the int 2-D windows above).
  * Reference: kdt::KDTree::radius_search OPT/include/optics/kdTree.hpp:407-422 (keep i iff
  *   square_distance(points[i], p) <= radius*radius, square_distance = sum of d*d in double with
@@ -413,7 +422,24 @@ int ecc_radius_counts_f64(ecc_ctx *ctx, const double *pts, int64_t n, int32_t di
 int ecc_radius_lists_f64(ecc_ctx *ctx, const double *pts, int64_t n, int32_t dim, double eps,
                          const int32_t *counts, int64_t *offsets, int32_t *nbr, double *nbr_dist,
                          int64_t nbr_cap, ecc_stream_t stream);
+/* fp32 points (pcl::PointXYZ fields; DBSCAN_simple.h:132-135 / DBSCAN_precomp.h:31-34): the
+ * per-axis difference is taken in float, then widened: d^2 = dx*dx + dy*dy + dz*dz in double.
+ * Same outputs as the f64 forms; ecc_radius_lists_f32 is DBSCANPrecompCluster::precomp's
+ * adjacency (ecc_lists_sort_ascending gives its row order). */
+int ecc_radius_counts_f32(ecc_ctx *ctx, const float *pts, int64_t n, int32_t dim, double eps,
+                          int32_t min_pts, int32_t *counts, double *core_dist, ecc_stream_t stream);
+int ecc_radius_lists_f32(ecc_ctx *ctx, const float *pts, int64_t n, int32_t dim, double eps,
+                         const int32_t *counts, int64_t *offsets, int32_t *nbr, double *nbr_dist,
+                         int64_t nbr_cap, ecc_stream_t stream);
+/* min_pts has no upper bound (compute_core_dist has none): above 64 the core distance comes from
+ * a per-point radix select.  ECC_ERR_CAPACITY: nbr_cap too small; ECC_ERR_INVALID: a non-finite
+ * coordinate in the last call's points. */
 int ecc_radius_status(ecc_ctx *ctx, ecc_stream_t stream);
+/* Sorts every list nbr[offsets[i] .. offsets[i+1]) (i < n) ascending in place (nbr_dist, when not
+ * NULL, permuted alongside): the row order of DBSCAN_precomp.h:22-44's adjacency.  total =
+ * offsets[n] (host value). */
+int ecc_lists_sort_ascending(ecc_ctx *ctx, int64_t n, const int64_t *offsets, int64_t total,
+                             int32_t *nbr, double *nbr_dist, ecc_stream_t stream);
 
 /* OPTICS ordering (optics::compute_reachability_dists, optics.hpp:413-565): HOST pts[n*dim]
  * (dim 1-3) in; the GPU radius search above, then the ordered seed-set expansion on the host.
@@ -457,6 +483,27 @@ int ecc_dbscan_grid(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int64_t se
                     int32_t max_cluster_size, int32_t *labels, int32_t *n_clusters, int64_t *dups,
                     int64_t dup_cap, int64_t *n_dups, ecc_stream_t stream);
 int ecc_dbscan_status(ecc_ctx *ctx, ecc_stream_t stream);
+
+/* DBSCAN over ONE point cloud of any size in 1-3 dimensions: DBSCANSimpleCluster::extract
+ * (PCC/DBSCAN_simple.h:27-90) with its radiusSearch (:118-142) on the reference's own input type,
+ * a float pcl::PointXYZ cloud (ecc_dbscan_cloud_f32, dim 3 = x,y,z; the differences in float as
+ * ecc_radius_counts_f32) — or fp64 points (ecc_dbscan_cloud_f64).  The driver's parameters:
+ * eps 20, min_pts 20, sizes 100..25000 (PCC/pcl_cluster.cpp:112-123).  pts: DEVICE row-major
+ * [n*dim].  A negative eps acts as |eps| (radius_square = radius*radius, :127).  Outputs as
+ * ecc_dbscan_extract for a single segment: labels[n] (cluster index in output order or -1),
+ * *n_clusters (device int32), dups / *n_dups (device) further memberships.  No size cap and no
+ * component cap (global union-find, clusters ordered by a device radix sort).
+ * ecc_dbscan_cloud_status: ECC_ERR_CAPACITY if dups overflowed (*n_dups holds the number needed),
+ * ECC_ERR_INVALID if a coordinate was not finite. */
+int ecc_dbscan_cloud_f32(ecc_ctx *ctx, const float *pts, int64_t n, int32_t dim, double eps,
+                         int32_t min_pts, int32_t min_cluster_size, int32_t max_cluster_size,
+                         int32_t *labels, int32_t *n_clusters, int64_t *dups, int64_t dup_cap,
+                         int64_t *n_dups, ecc_stream_t stream);
+int ecc_dbscan_cloud_f64(ecc_ctx *ctx, const double *pts, int64_t n, int32_t dim, double eps,
+                         int32_t min_pts, int32_t min_cluster_size, int32_t max_cluster_size,
+                         int32_t *labels, int32_t *n_clusters, int64_t *dups, int64_t dup_cap,
+                         int64_t *n_dups, ecc_stream_t stream);
+int ecc_dbscan_cloud_status(ecc_ctx *ctx, ecc_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * 7. Host-side helpers (no GPU): synthetic event streams and event-file I/O.

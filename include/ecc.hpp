@@ -421,7 +421,7 @@ struct PointIndices {  // pcl::PointIndices
     std::vector<int> indices;
 };
 
-class DBSCANSimpleCluster {  // PCC/DBSCAN_simple.h:14-143 (GPU eps-lists, host extraction)
+class DBSCANSimpleCluster {  // PCC/DBSCAN_simple.h:14-143 (GPU radius search + extraction, any size)
   public:
     explicit DBSCANSimpleCluster(Context &ctx = Context::default_context()) : ctx_(ctx) {}
     virtual ~DBSCANSimpleCluster() = default;
@@ -430,10 +430,13 @@ class DBSCANSimpleCluster {  // PCC/DBSCAN_simple.h:14-143 (GPU eps-lists, host 
     void setMinClusterSize(int min_cluster_size) { min_pts_per_cluster_ = min_cluster_size; }
     void setMaxClusterSize(int max_cluster_size) { max_pts_per_cluster_ = max_cluster_size; }
     void setCorePointMinPts(int core_point_min_pts) { minPts_ = core_point_min_pts; }
-    // clusters sorted by size, descending (ties: smallest member index first)
+    // float x,y,z clouds of any size (ecc_dbscan_cloud_f32); clusters sorted by size,
+    // descending (ties: smallest member index first, then creation order)
     void extract(std::vector<PointIndices> &cluster_indices);
 
   protected:
+    // the tolerance the neighbourhoods are built with (radiusSearch(i, eps_, ...), :36, :61)
+    virtual double searchTolerance() const { return eps_; }
     Context &ctx_;
     std::vector<PointXYZ> cloud_;
     double eps_{0.0};
@@ -442,10 +445,24 @@ class DBSCANSimpleCluster {  // PCC/DBSCAN_simple.h:14-143 (GPU eps-lists, host 
     int max_pts_per_cluster_{std::numeric_limits<int>::max()};
 };
 
-// DBSCAN_precomp.h: same neighbourhoods, precomputed — on the GPU both are one eps-list pass.
-using DBSCANPrecompCluster = DBSCANSimpleCluster;
+// DBSCAN_precomp.h:7-55: the adjacency is precomputed in setInputCloud with the tolerance set AT
+// THAT TIME (precomp() reads eps_, :28) — a later setClusterTolerance does not change it.  The
+// neighbourhoods themselves are the same test as the simple variant's, so extraction is shared.
+class DBSCANPrecompCluster : public DBSCANSimpleCluster {
+  public:
+    using DBSCANSimpleCluster::DBSCANSimpleCluster;
+    void setInputCloud(const std::vector<PointXYZ> &cloud) override {
+        cloud_ = cloud;
+        precomp_eps_ = eps_;
+    }
 
-// Neighbour lists of 2-D integer points (x,y of the cloud) on the GPU: CSR, ascending indices.
+  protected:
+    double searchTolerance() const override { return precomp_eps_; }
+    double precomp_eps_{0.0};
+};
+
+// Neighbour lists of 2-D integer points (x,y of the cloud) on the GPU: CSR, ascending indices
+// (DBSCAN_precomp.h's adjacency row order); any number of points and any min_pts.
 void eps_neighbour_lists(Context &ctx, const std::vector<std::array<int, 2>> &points, double eps,
                          std::vector<int64_t> &offsets, std::vector<int32_t> &nbr,
                          int min_pts = 1, std::vector<double> *core_dist = nullptr);

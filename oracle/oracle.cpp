@@ -194,6 +194,15 @@ static float tree_sum_1024(const float *v) {
 // pass's readback with its stale tails, Q8): the bins' first cluster_index[c] slots are this
 // pass's points (index order), the rest keeps the input; sums, update.  Returns 1 when the
 // reference would restart (error_max > 10).
+// The reference's `abs(new - old)` on a float (assign_to_centers2.c:526-527) is C's int abs(int)
+// of the float converted to int.  An empty bin divides by zero (:509-512), and the conversion of
+// the resulting inf/NaN is undefined in C; on the reference's x86-64 target cvttss2si yields
+// INT_MIN and abs(INT_MIN) stays INT_MIN.  Restated without the UB (the sanitizer build checks).
+static float ref_int_abs(float d) {
+    if (!(d > -2147483648.f && d < 2147483648.f)) return -2147483648.f;
+    return (float)std::abs((int)d);
+}
+
 ORC_API int orc_kmeans_refcompat_pass(const float *xy, int64_t n, float *c16, float *output, int32_t *bin_counts_out,
                                       float *partial_sums_out) {
     if (n > 2048 * 8) return -1;
@@ -218,7 +227,7 @@ ORC_API int orc_kmeans_refcompat_pass(const float *xy, int64_t n, float *c16, fl
     }
     float error_max = 0.f;
     for (int j = 0; j < 16; ++j) {
-        const float a = (float)std::abs((int)(nc[j] - c16[j]));
+        const float a = ref_int_abs(nc[j] - c16[j]);
         if (a > error_max) { error_max = a; c16[j] = nc[j]; }
     }
     if (bin_counts_out) std::memcpy(bin_counts_out, cluster_index, sizeof(cluster_index));
@@ -254,7 +263,7 @@ ORC_API int orc_kmeans_refcompat(const float *xy, int64_t n, float *c16, int max
         float err[16], error_max = 0.f;
         for (int j = 0; j < 16; ++j) err[j] = nc[j] - c16[j];
         for (int j = 0; j < 16; ++j) {                   // :525-532 (Q9)
-            const float a = (float)std::abs((int)err[j]);
+            const float a = ref_int_abs(err[j]);
             if (a > error_max) { error_max = a; c16[j] = nc[j]; }
         }
         ++passes;
@@ -678,12 +687,18 @@ ORC_API int orc_eps_neighbours(const uint32_t *xy, int64_t n_segs, int64_t strid
     return off > nbr_cap && nbr ? -4 : 0;
 }
 
-// a9: DBSCANSimpleCluster::extract, PCC/DBSCAN_simple.h:27-90 over 3-D float points with the
-// brute-force radiusSearch (:118-142).  Output: label per point (cluster rank after the final
-// size-descending sort :89, ties by smallest member index — std::sort is not stable, see
-// DESIGN.md), -1 = not in a kept cluster.  Returns the number of kept clusters.
-ORC_API int orc_dbscan(const float *pts, int n, double eps, int min_pts, int min_size, int max_size,
-                       int32_t *labels) {
+// a9-a10: DBSCANSimpleCluster::extract, PCC/DBSCAN_simple.h:27-90, literally (seed queue, types,
+// noise flags), with the brute-force radiusSearch (:118-142) over a cloud of n points of `dim`
+// coordinates of type T.  pcl::PointXYZ's fields are float, so `double distance_x =
+// points[i].x - points[index].x` subtracts in FLOAT and widens the difference (:132-134);
+// distance_square = dx*dx + dy*dy + dz*dz in double (:135) <= radius*radius (:127).  The
+// index itself is pushed first with distance 0 (:124-125).  Output: the clusters in output order
+// (size descending :89, ties by smallest member — std::sort is unstable, Q23 — then creation),
+// each sorted + unique (:82-83), as CSR (offs[c]..offs[c+1]); labels[i] = the last output
+// cluster containing i, or -1.  Returns the number of clusters.
+template <typename T>
+static int dbscan_cloud(const T *pts, int n, int dim, double eps, int min_pts, int min_size, int max_size,
+                        int32_t *labels, int64_t *offs, int32_t *members, int64_t cap) {
     enum { UNP = 0, PROC = 1, DONE = 2 };
     const double r2 = eps * eps;
     auto radius = [&](int idx, std::vector<int> &out) {
@@ -691,10 +706,13 @@ ORC_API int orc_dbscan(const float *pts, int n, double eps, int min_pts, int min
         out.push_back(idx);
         for (int i = 0; i < n; i++) {
             if (i == idx) continue;
-            const double dx = (double)pts[3 * i] - pts[3 * idx];
-            const double dy = (double)pts[3 * i + 1] - pts[3 * idx + 1];
-            const double dz = (double)pts[3 * i + 2] - pts[3 * idx + 2];
-            if (dx * dx + dy * dy + dz * dz <= r2) out.push_back(i);
+            double d2 = 0.0;
+            for (int d = 0; d < dim; ++d) {
+                const T diff = pts[(int64_t)i * dim + d] - pts[(int64_t)idx * dim + d];  // in the point type
+                const double dd = (double)diff;
+                d2 = d == 0 ? dd * dd : d2 + dd * dd;
+            }
+            if (d2 <= r2) out.push_back(i);
         }
         return (int)out.size();
     };
@@ -720,7 +738,7 @@ ORC_API int orc_dbscan(const float *pts, int n, double eps, int min_pts, int min
             types[ci] = DONE;
             qi++;
         }
-        if ((int)q.size() >= min_size && (int)q.size() <= max_size) {
+        if ((int64_t)q.size() >= min_size && (int64_t)q.size() <= max_size) {
             std::sort(q.begin(), q.end());
             q.erase(std::unique(q.begin(), q.end()), q.end());
             clusters.push_back(q);
@@ -731,10 +749,73 @@ ORC_API int orc_dbscan(const float *pts, int n, double eps, int min_pts, int min
                          if (a.size() != b.size()) return a.size() > b.size();
                          return a.front() < b.front();
                      });
-    for (int i = 0; i < n; ++i) labels[i] = -1;
-    for (size_t c = 0; c < clusters.size(); ++c)
-        for (int idx : clusters[c]) labels[idx] = (int32_t)c;
+    if (labels) {  // a point in several clusters keeps the last one in output order
+        for (int i = 0; i < n; ++i) labels[i] = -1;
+        for (size_t c = 0; c < clusters.size(); ++c)
+            for (int idx : clusters[c]) labels[idx] = (int32_t)c;
+    }
+    if (offs) {
+        int64_t k = 0;
+        offs[0] = 0;
+        for (size_t c = 0; c < clusters.size(); ++c) {
+            for (int v : clusters[c]) { if (members && k < cap) members[k] = v; ++k; }
+            offs[c + 1] = k;
+        }
+    }
     return (int)clusters.size();
+}
+
+// 3-D float points (x, y, z per point); labels = the first output cluster holding the point
+ORC_API int orc_dbscan(const float *pts, int n, double eps, int min_pts, int min_size, int max_size,
+                       int32_t *labels) {
+    return dbscan_cloud<float>(pts, n, 3, eps, min_pts, min_size, max_size, labels, nullptr, nullptr, 0);
+}
+
+ORC_API int orc_dbscan_cloud_f32(const float *pts, int n, int dim, double eps, int min_pts, int min_size, int max_size,
+                                 int32_t *labels, int64_t *offs, int32_t *members, int64_t cap) {
+    return dbscan_cloud<float>(pts, n, dim, eps, min_pts, min_size, max_size, labels, offs, members, cap);
+}
+
+ORC_API int orc_dbscan_cloud_f64(const double *pts, int n, int dim, double eps, int min_pts, int min_size,
+                                 int max_size, int32_t *labels, int64_t *offs, int32_t *members, int64_t cap) {
+    return dbscan_cloud<double>(pts, n, dim, eps, min_pts, min_size, max_size, labels, offs, members, cap);
+}
+
+// a10 (DBSCAN_precomp.h:22-44 for float clouds): counts, core distances (optics.hpp:286-299 on
+// the same d^2) and adjacency rows in ascending index order, brute force over all pairs.
+ORC_API int orc_radius_f32(const float *pts, int n, int dim, double eps, int min_pts, int32_t *counts,
+                           double *core_dist, int64_t *offsets, int32_t *nbr, int64_t cap) {
+    const double r2 = eps * eps;
+    int64_t off = 0;
+    std::vector<double> d2s;
+    for (int i = 0; i < n; ++i) {
+        d2s.clear();
+        if (offsets) offsets[i] = off;
+        for (int j = 0; j < n; ++j) {
+            double d2 = 0.0;
+            for (int d = 0; d < dim; ++d) {
+                const float diff = pts[(int64_t)j * dim + d] - pts[(int64_t)i * dim + d];
+                const double dd = (double)diff;
+                d2 = d == 0 ? dd * dd : d2 + dd * dd;
+            }
+            if (d2 <= r2) {
+                d2s.push_back(d2);
+                if (nbr && off < cap) nbr[off] = j;
+                ++off;
+            }
+        }
+        if (counts) counts[i] = (int32_t)d2s.size();
+        if (core_dist) {
+            if ((int)d2s.size() < min_pts || min_pts < 1) {
+                core_dist[i] = -1.0;
+            } else {
+                std::nth_element(d2s.begin(), d2s.begin() + (min_pts - 1), d2s.end());
+                core_dist[i] = std::sqrt(d2s[min_pts - 1]);
+            }
+        }
+    }
+    if (offsets) offsets[n] = off;
+    return off > cap && nbr ? -4 : 0;
 }
 
 // a13: optics::compute_reachability_dists, OPT/include/optics/optics.hpp:413-565 with exact

@@ -56,6 +56,9 @@ _sigs = {
     "orc_evt3_encode": (i64, [P, P, P, i64, C.c_uint64, i32, i32, P, i64]),
     "orc_reslice_n_us": (i64, [P, i64, i64, P, i64]),
     "orc_dbscan_lists": (C.c_int, [P, i32, f64, i32, i32, i32, P, P, i64]),
+    "orc_dbscan_cloud_f32": (C.c_int, [P, i32, i32, f64, i32, i32, i32, P, P, P, i64]),
+    "orc_dbscan_cloud_f64": (C.c_int, [P, i32, i32, f64, i32, i32, i32, P, P, P, i64]),
+    "orc_radius_f32": (C.c_int, [P, i32, i32, f64, i32, P, P, P, P, i64]),
     "orc_aec_run": (i64, [P, P, i64, i64, i32, f64, i32, f64, i32, P, i64, P]),
 }
 for _n, (_r, _a) in _sigs.items():
@@ -211,6 +214,40 @@ def dbscan(pts3, eps, min_pts, min_size=1, max_size=2**31 - 1):
     lab = np.zeros(n, np.int32)
     k = lib.orc_dbscan(_p(pts3), n, eps, min_pts, min_size, max_size, _p(lab))
     return k, lab
+
+
+def dbscan_cloud(pts, eps, min_pts, min_size=1, max_size=2**31 - 1):
+    """DBSCAN_simple.h:27-142 literally over an (n, dim) float32 or float64 cloud: (labels, clusters)
+    with clusters a list of sorted index arrays in output order."""
+    pts = np.ascontiguousarray(pts)
+    assert pts.dtype in (np.float32, np.float64) and pts.ndim == 2
+    n, dim = pts.shape
+    fn = lib.orc_dbscan_cloud_f32 if pts.dtype == np.float32 else lib.orc_dbscan_cloud_f64
+    lab = np.zeros(n, np.int32)
+    cap = max(1, 2 * n)
+    while True:
+        offs = np.zeros(n + 2, np.int64)
+        mem = np.empty(cap, np.int32)
+        nc = fn(_p(pts), n, dim, eps, min_pts, min_size, max_size, _p(lab), _p(offs), _p(mem), cap)
+        if offs[nc] <= cap:
+            return lab, [mem[offs[c]:offs[c + 1]].copy() for c in range(nc)]
+        cap = int(offs[nc])
+
+
+def radius_f32(pts, eps, min_pts=1, want_lists=True):
+    """Brute-force eps-balls of an (n, dim) float32 cloud with float per-axis differences:
+    (counts, core distances, offsets, ascending neighbour lists)."""
+    pts = np.ascontiguousarray(pts, np.float32)
+    n, dim = pts.shape
+    counts = np.zeros(n, np.int32)
+    core = np.zeros(n, np.float64)
+    offs = np.zeros(n + 1, np.int64)
+    lib.orc_radius_f32(_p(pts), n, dim, eps, min_pts, _p(counts), _p(core), _p(offs), None, 0)
+    nbr = None
+    if want_lists:
+        nbr = np.zeros(max(int(offs[-1]), 1), np.int32)
+        lib.orc_radius_f32(_p(pts), n, dim, eps, min_pts, None, None, _p(offs), _p(nbr), len(nbr))
+    return counts, core, offs, nbr
 
 
 def epsilon_estimation(pts, min_pts):

@@ -1,7 +1,7 @@
 #!/bin/bash
-# GPU test session: the full -m gpu suite (one process), then smoke.
+# GPU test session: pytest over the given arguments (default: the whole -m gpu suite), one process.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
-timeout -k 10 1000 python -m pytest tests -m gpu -q -rf "$@" > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
-case $rc in 0|1) ;; *) exit $rc;; esac
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; echo "smoke rc=$?"; tail -3 gpurun_out/smoke.log
+LOG=gpurun_out/${LOG_NAME:-pytest_gpu}.log
+timeout -k 10 ${TMO:-900} python -u -m pytest -m gpu -x -v -rf --timeout 300 --timeout-method thread "${@:-tests}" > "$LOG" 2>&1; rc=$?
+echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR|passed|failed" "$LOG" | tail -40
+exit $rc

@@ -58,6 +58,7 @@ def test_rccl_one_rank_sharded_step_matches_oracle():
     assert par is not None and par["mismatches"] == 0, par
     tm = res["track_merge"]
     assert tm is not None and tm["ranks"] == 1 and tm["slices"] == 40 and tm["tracks_end"] > 0, tm
+    assert tm["pipelined"]["mevents_s"] > 0 and tm["pipelined"]["steps"] >= 3, tm
     assert res["n_gpus"] == 1
 
 
@@ -73,3 +74,4 @@ def test_gloo_two_ranks_overlapped_schedule_matches_oracle():
     assert par["events_total"] == 2 * 16384 * 24
     tm = res["track_merge"]
     assert tm is not None and tm["ranks"] == 2 and tm["slices"] == 48 and tm["tracks_end"] > 0, tm
+    assert tm["pipelined"]["mevents_s"] > 0, tm

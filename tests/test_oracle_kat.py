@@ -279,3 +279,34 @@ def test_omp_baseline_equals_single_thread_oracle(orc, ecc):
     assert orc_rc == p_rc and np.array_equal(ocnt, pcnt)
     for s in range(len(ocnt)):
         assert np.array_equal(oo[s * 4096: s * 4096 + ocnt[s]], po[s * 4096: s * 4096 + pcnt[s]])
+
+
+def test_dbscan_cloud_restatement_subtracts_in_float(orc):
+    """DBSCAN_simple.h:132-135: `double distance_x = points[i].x - points[index].x` with float
+    fields — the difference is rounded to float before widening.  A pair within eps only in float
+    arithmetic is one cluster; the same coordinates as doubles are two noise points."""
+    rng = np.random.default_rng(5)
+    for _ in range(200000):
+        a = np.float32(rng.uniform(-1, 1))
+        b = np.float32(a - np.float32(20.0) - np.float32(rng.uniform(-4e-6, 4e-6)))
+        fd = np.float64(np.float32(a - b))
+        dd = np.float64(a) - np.float64(b)
+        if fd * fd <= 400.0 < dd * dd:
+            break
+    else:
+        raise AssertionError("no float/double boundary pair found")
+    pts = np.array([[a, 0, 0], [b, 0, 0]], np.float32)
+    _, cl = orc.dbscan_cloud(pts, 20.0, 2)
+    assert len(cl) == 1 and list(cl[0]) == [0, 1]
+    _, cl64 = orc.dbscan_cloud(pts.astype(np.float64), 20.0, 2)
+    assert cl64 == []
+    cnt, _, _, _ = orc.radius_f32(pts, 20.0)
+    assert list(cnt) == [2, 2]
+
+
+def test_dbscan_cloud_restatement_matches_integer_window_restatement(orc):
+    rng = np.random.default_rng(4)
+    p2 = rng.integers(0, 30, (600, 2)).astype(np.int32)
+    ref = orc.dbscan_lists(p2, 2.0, 5, 3, 400)
+    _, got = orc.dbscan_cloud(p2.astype(np.float32), 2.0, 5, 3, 400)
+    assert len(got) == len(ref) and all(np.array_equal(a, b) for a, b in zip(got, ref))
