@@ -413,6 +413,48 @@ def main():
             merged_tracks = (tr.tracks(), tr.groups()[0])
             tr.close()
         dist.barrier()
+        # pipelined: the merged tracker of step b (rank 0, third stream) overlaps the sharded step
+        # b+1 on every rank; per step the shards' lists are packed and gathered (host-synchronising:
+        # the gather needs the list sizes).  Whole-job events / wall time of the loop.
+        s3, ev_g, ev_trk = ecc.P(), [ecc.P(), ecc.P()], [ecc.P(), ecc.P()]
+        ecc.check(lib.ecc_stream_create(ecc.C.byref(s3)), "stream")
+        for e in ev_g + ev_trk:
+            ecc.check(lib.ecc_event_create(ecc.C.byref(e)), "event")
+        trp = ecc.Tracker(ctx) if rank == 0 else None
+        held = [None, None]
+        kp = max(3, min(args.steps, 6))
+        dist.barrier()
+        ctx.sync()
+        tp0 = time.perf_counter()
+        for b in range(kp):
+            nb = b % 2
+            if b >= 2 and rank == 0:  # the gathered lists of step b-2 are released after their tracker
+                ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_trk[nb]))
+            step(nb=nb)
+            ctx.corner_pack(nms_out[nb], nms_cnt[nb], ns, cap, packed.data_ptr(), offs.data_ptr())
+            total_b = int(offs[-1].item())
+            ecc.check(lib.ecc_memcpy_d2d(cnt_t.data_ptr(), nms_cnt[nb].ptr, 4 * ns, ctx.stream))
+            held[nb] = edist.gather_corner_lists(comm, packed[:total_b], cnt_t)
+            if rank == 0:
+                pk_b, st_b, ct_b = held[nb]
+                ecc.check(lib.ecc_event_record(ev_g[nb], ctx.stream))
+                ecc.check(lib.ecc_stream_wait_event(s3.value, ev_g[nb]))
+                ecc.check(lib.ecc_tracker_update_lists(trp.tr, pk_b.data_ptr(), st_b.data_ptr(), ct_b.data_ptr(),
+                                                       int(st_b.numel()), s3.value), "tracker lists")
+                ecc.check(lib.ecc_event_record(ev_trk[nb], s3.value))
+        ecc.check(lib.ecc_stream_sync(s3.value))
+        ctx.sync()
+        dist.barrier()
+        tp = time.perf_counter() - tp0
+        if rank == 0:
+            if trp.status() != 0:
+                raise RuntimeError("pipelined merged tracker reported a status error")
+            track_merge["pipelined"] = {
+                "mevents_s": round(world * kp * n / tp / 1e6, 1), "ms_per_step": round(tp / kp * 1e3, 3),
+                "steps": kp, "how": "sharded step b+1 on every rank while rank 0's tracker consumes the gathered "
+                                    "lists of step b on a third stream; pack + gather per step"}
+            trp.close()
+        held = [None, None]
     dist_parity = None
     if dist and args.dist_parity:
         dist_parity = shard_parity(ecc, args, dist, torch, rank, world, local, W, H, I, c0,

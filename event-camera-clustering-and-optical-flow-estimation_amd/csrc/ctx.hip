@@ -139,6 +139,9 @@ ECC_API int ecc_ctx_create(ecc_ctx **out, int device) {
         delete ctx;
         return ECC_ERR_HIP;
     }
+    int n_cu = 0;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n_cu > 0)
+        ctx->n_cu = n_cu;
     *out = ctx;
     return ECC_OK;
 }

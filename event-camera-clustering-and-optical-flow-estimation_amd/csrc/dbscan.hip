@@ -83,6 +83,40 @@ __device__ __forceinline__ int comp_of(const int *parent, int j) {
     return v <= -2 ? -v - 2 : -parent[v] - 2;
 }
 
+// Walks the points j = wave, wave + kW, ... of a segment, one WAVE per point: lane L of the wave
+// prefetches the list range of the wave's next 64 points (no dependent offset load per point) and
+// body(j, e0, e1) is called wave-uniformly; its lanes read the list e0 + lane, e0 + lane + 64, ...
+// so every list read is one coalesced load per 64 entries (a lane walking its own list touched a
+// different line per lane and load: ~7 ms per C4 call).
+template <class F>
+__device__ __forceinline__ void for_points_by_wave(int m, int64_t base, const int64_t *__restrict__ offsets,
+                                                   F &&body) {
+    constexpr int kW = kThreads / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int t0 = 0; wave + kW * t0 < m; t0 += 64) {
+        const int jl = wave + kW * (t0 + lane);
+        const int64_t pe0 = jl < m ? offsets[base + jl] : 0, pe1 = jl < m ? offsets[base + jl + 1] : 0;
+        for (int tt = 0; tt < 64; ++tt) {
+            const int j = wave + kW * (t0 + tt);
+            if (j >= m) break;  // wave-uniform
+            body(j, (int64_t)__shfl(pe0, tt), (int64_t)__shfl(pe1, tt));
+        }
+    }
+}
+
+// Smallest component among the core neighbours of j's list, reduced over the wave (0x7fffffff: none).
+__device__ __forceinline__ int wave_first_comp(const int *parent, const int32_t *__restrict__ nbr, int64_t e0,
+                                               int64_t e1) {
+    int first = 0x7fffffff;
+    for (int64_t e = e0 + (threadIdx.x & 63); e < e1; e += 64) {
+        const int c = comp_of(parent, nbr[e]);
+        if (c >= 0 && c < first) first = c;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) first = min(first, __shfl_xor(first, o));
+    return first;
+}
+
 __global__ void __launch_bounds__(kThreads)
 dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict__ seg_counts,
                       const int64_t *__restrict__ offsets, const int32_t *__restrict__ nbr, int64_t nbr_len,
@@ -113,14 +147,13 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         }
         __syncthreads();
         // 2. union over core-core edges (each undirected edge once: q > j)
-        for (int j = tid; j < m; j += kThreads) {
-            if (parent[j] == -1) continue;
-            const int64_t e0 = offsets[base + j], e1 = offsets[base + j + 1];
-            for (int64_t e = e0; e < e1; ++e) {
+        for_points_by_wave(m, base, offsets, [&](int j, int64_t e0, int64_t e1) {
+            if (parent[j] == -1) return;  // non-core stays -1 during the unions: uniform
+            for (int64_t e = e0 + lane; e < e1; e += 64) {
                 const int q = nbr[e];
                 if (q > j && parent[q] != -1) uf_union(parent, j, q);
             }
-        }
+        });
         __syncthreads();
         // 3. compress; roots -> component ids in ascending root order (block scan over j)
         constexpr int kPer = kMaxPts / kThreads;  // 16 consecutive points per lane
@@ -176,31 +209,30 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
             c_front[c] = 0x7fffffff;
         }
         __syncthreads();
-        // 4. memberships -> sizes and first members
+        // 4. memberships -> sizes and first members (core points by lane, the others by wave)
         for (int j = tid; j < m; j += kThreads) {
             const int cj = comp_of(parent, j);
             if (cj >= 0) {
                 atomicAdd(&c_size[cj], 1);
                 atomicMin(&c_front[cj], j);
-                continue;
             }
-            const int64_t e0 = offsets[base + j], e1 = offsets[base + j + 1];
-            int first = 0x7fffffff;
-            for (int64_t e = e0; e < e1; ++e) {
-                const int c = comp_of(parent, nbr[e]);
-                if (c >= 0 && c < first) first = c;
+        }
+        for_points_by_wave(m, base, offsets, [&](int j, int64_t e0, int64_t e1) {
+            if (parent[j] != -1) return;  // core: counted above (uniform)
+            const int first = wave_first_comp(parent, nbr, e0, e1);
+            if (first == 0x7fffffff) return;  // noise
+            if (lane == 0) {
+                atomicAdd(&c_size[first], 1);
+                atomicMin(&c_front[first], j);
             }
-            if (first == 0x7fffffff) continue;  // noise
-            atomicAdd(&c_size[first], 1);
-            atomicMin(&c_front[first], j);
-            for (int64_t e = e0; e < e1; ++e) {  // later clusters seeded by a neighbour
+            for (int64_t e = e0 + lane; e < e1; e += 64) {  // later clusters seeded by a neighbour
                 const int v = parent[nbr[e]];
                 if (v <= -2 && -v - 2 != first) {
                     atomicAdd(&c_size[-v - 2], 1);
                     atomicMin(&c_front[-v - 2], j);
                 }
             }
-        }
+        });
         __syncthreads();
         // 5. output order: kept clusters by (size desc, front asc, creation asc)
         if (tid == 0) s_kept = 0;
@@ -221,22 +253,17 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         }
         __syncthreads();
         if (tid == 0) n_clusters[s] = s_kept;
-        // 6. labels (first claim) and further memberships
+        // 6. labels (first claim) and further memberships (core points by lane, the others by wave)
         for (int j = tid; j < m; j += kThreads) {
             const int cj = comp_of(parent, j);
-            if (cj >= 0) {
-                labels[base + j] = c_rank[cj];
-                continue;
-            }
-            const int64_t e0 = offsets[base + j], e1 = offsets[base + j + 1];
-            int first = 0x7fffffff;
-            for (int64_t e = e0; e < e1; ++e) {
-                const int c = comp_of(parent, nbr[e]);
-                if (c >= 0 && c < first) first = c;
-            }
-            labels[base + j] = first == 0x7fffffff ? -1 : c_rank[first];
-            if (first == 0x7fffffff) continue;
-            for (int64_t e = e0; e < e1; ++e) {
+            if (cj >= 0) labels[base + j] = c_rank[cj];
+        }
+        for_points_by_wave(m, base, offsets, [&](int j, int64_t e0, int64_t e1) {
+            if (parent[j] != -1) return;  // core: labelled above (uniform)
+            const int first = wave_first_comp(parent, nbr, e0, e1);
+            if (lane == 0) labels[base + j] = first == 0x7fffffff ? -1 : c_rank[first];
+            if (first == 0x7fffffff) return;
+            for (int64_t e = e0 + lane; e < e1; e += 64) {
                 const int v = parent[nbr[e]];
                 if (v <= -2 && -v - 2 != first && c_rank[-v - 2] >= 0) {
                     const unsigned long long at = atomicAdd(n_dups, 1ull);
@@ -248,7 +275,7 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
                     }
                 }
             }
-        }
+        });
         __syncthreads();
     }
 }

@@ -25,18 +25,24 @@ constexpr int kBuckets = 8192;            // LDS table (32 KiB)
 constexpr uint32_t kEmpty = 0x7fffffffu;
 constexpr uint32_t kRepeatBit = 0x80000000u;
 
-__device__ inline void load4(const uint32_t *__restrict__ xy, int64_t g, int64_t limit,
-                             uint32_t (&v)[4]) {
-    if (g + 3 < limit && (g & 3) == 0) {
-        const uint4 q = *reinterpret_cast<const uint4 *>(xy + g);
+// Four consecutive events per lane.  kQuads (window and n multiples of 4, xy 16-B aligned): one
+// 16-B load per lane, clamped to the last quad; otherwise four clamped 4-B loads.  Values past the
+// window are masked by the caller.  No load is conditional: a per-lane choice between a 16-B and
+// four 4-B loads into the same registers made the compiler wait for each chunk's load before
+// issuing the next (four HBM round trips per window instead of one).
+template <bool kQuads>
+__device__ inline void load4(const uint32_t *__restrict__ xy, int64_t g, int64_t n, uint32_t (&v)[4]) {
+    if constexpr (kQuads) {
+        const int64_t n4 = n >> 2, qi = g >> 2;
+        const uint4 q = reinterpret_cast<const uint4 *>(xy)[qi < n4 ? qi : n4 - 1];
         v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = (g + k < limit) ? xy[g + k] : 0u;
+        for (int k = 0; k < 4; ++k) v[k] = xy[g + k < n ? g + k : n - 1];
     }
 }
 
-template <int NT, int MAXC>
+template <int NT, int MAXC, bool kQuads>
 __global__ void __launch_bounds__(NT)
 downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, int n_chunks,
                        int x_max, int y_max, int mult_x, int mult_y,
@@ -66,8 +72,7 @@ downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, i
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
         if (c < n_chunks) {
-            const int64_t g = wbase + (int64_t)c * kChunk + 4 * tid;
-            load4(xy, g, wend, v[c]);
+            load4<kQuads>(xy, wbase + (int64_t)c * kChunk + 4 * tid, n, v[c]);
         }
     }
     __syncthreads();
@@ -202,7 +207,10 @@ ECC_API int ecc_downsample_hash(ecc_ctx *ctx, const uint32_t *xy, int64_t n,
     if (n_win > INT32_MAX) return ECC_ERR_INVALID;
     const int n_chunks = (cfg->window + 4 * kThreads - 1) / (4 * kThreads);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    auto kern = n_chunks <= 4 ? downsample_hash_kernel<kThreads, 4> : downsample_hash_kernel<kThreads, 8>;
+    // 16-B loads when every lane's quad is aligned (the instantiations keep one load form each)
+    const bool quads = (cfg->window & 3) == 0 && (n & 3) == 0 && (reinterpret_cast<uintptr_t>(xy) & 15) == 0;
+    auto kern = quads ? (n_chunks <= 4 ? downsample_hash_kernel<kThreads, 4, true> : downsample_hash_kernel<kThreads, 8, true>)
+                      : (n_chunks <= 4 ? downsample_hash_kernel<kThreads, 4, false> : downsample_hash_kernel<kThreads, 8, false>);
     {
         ECC_TIMED(ctx, ecc::as_stream(stream), "downsample_hash_kernel");
         hipLaunchKernelGGL(kern, dim3((unsigned)n_win), dim3(kThreads), 0, ecc::as_stream(stream), xy,

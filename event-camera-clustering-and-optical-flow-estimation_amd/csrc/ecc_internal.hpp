@@ -25,6 +25,7 @@ struct EccTimingPair {
 
 struct ecc_ctx {
     int device = 0;
+    int n_cu = 256;  // compute units of the device (persistent-grid sizing)
     // per-kernel timing (ecc_ctx_set_timing)
     bool timing = false;
     std::vector<EccTimingPair> pending;
@@ -87,6 +88,30 @@ void nms_state_release(const ecc_ctx *ctx);
 // Packed xy helpers (x | y << 16).
 __host__ __device__ inline int xy_x(uint32_t v) { return (int)(v & 0xffffu); }
 __host__ __device__ inline int xy_y(uint32_t v) { return (int)(v >> 16); }
+
+// Raw buffer view of [p, p + bytes) (stride 0, gfx9 resource word 3): loads at or past `bytes`
+// return 0 by the hardware range check, so a wave can issue all its loads over a ragged range
+// unconditionally (a load under a per-lane condition waits for every earlier one).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_view(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t buffer_load_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave with DPP moves (no LDS round trip): row_shr
+// 1/2/4/8 scans each row of 16 (bound_ctrl fills zeros at the row start), then row_bcast:15
+// adds row 0's total into row 1 and row 2's into row 3, and row_bcast:31 adds rows 0-1's
+// total into rows 2-3.  All 64 lanes must be active.
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+    return x;
+}
 
 // Correctly rounded fp32 square root.  On gfx950 `__fsqrt_rn` may lower to the bare
 // v_sqrt_f32 (<= 1 ulp), which breaks bit-exactness against IEEE sqrtf on the host.  This is

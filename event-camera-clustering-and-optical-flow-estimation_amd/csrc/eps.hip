@@ -13,9 +13,9 @@
 // count, and the (min_pts-1)-th smallest d^2 in a register insertion network (no
 // runtime-indexed arrays), so core distance = sqrt of an exact integer (fp64, correctly rounded -
 // bit-exact vs the oracle).  Results are staged in LDS by segment index and written out
-// coalesced (no 4/8-B scatter).  The list kernel emits each query's neighbours with a 9-way merge
-// of the cells' ascending runs, i.e. ascending segment-local indices (the order of
-// DBSCAN_precomp's adjacency lists), at offsets from a device exclusive scan of the counts.
+// coalesced (no 4/8-B scatter).  The list kernel builds each query's neighbour set as a bitmap
+// over the segment (one wave per query) and emits it in ascending segment-local index order (the
+// order of DBSCAN_precomp's adjacency lists), at offsets from a device exclusive scan of the counts.
 // Algorithmic bytes: 4 B/point in + 4 B/point (count) [+ 8 B core distance] out; lists: + 4 B
 // per neighbour out.
 #include "eps_grid.hpp"
@@ -108,9 +108,97 @@ eps_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32
     }
 }
 
-// Ascending neighbour lists.  Dynamic LDS: cend[kCells + 1] | spt[stride] | sidx[stride] with
-// every cell's run sorted by segment index; each query merges its (up to) 9 cell runs with the
-// run heads cached in registers, so one step = a 9-way min and one LDS read.
+// One query of eps_lists_kernel on the calling wave (all 64 lanes; v is wave-uniform): sets the
+// bitmap bits of its neighbours, then writes them ascending to nbr[out0, end) and clears the
+// bitmap words it used.  Branch-free row setup (all 14 cell-bound reads in flight together), two
+// candidates per lane per trip with their point and index read together, DPP prefix of the
+// per-lane counts: a handful of dependent LDS round trips per query.
+template <bool kN>
+__device__ __forceinline__ void emit_list(const CellGrid &g, const uint32_t *cend, const uint32_t *spt,
+                                          const uint16_t *sidx, unsigned long long *bits, uint32_t v, int e_int,
+                                          uint32_t r2i, int words, int wpl, int64_t out0, int64_t end,
+                                          int32_t *__restrict__ nbr, int64_t nbr_cap, int32_t *__restrict__ err) {
+    constexpr int kRows = 2 * ecc::epsg::kMaxR + 1;
+    const int lane = threadIdx.x & 63;
+    const int cx = ecc::epsg::cell_x(g, v), cy = ecc::epsg::cell_y(g, v);
+    // the rows' cell bounds: lane 2r reads row r's start bound, lane 2r + 1 its end (one LDS
+    // read per lane, all in flight together), then the wave takes them with readlane
+    int idx = 0;
+    {
+        const int r = lane >> 1, ry = cy + r - ecc::epsg::kMaxR, kx = lane < 2 * kRows ? g.kx[r] : -1;
+        if (kx >= 0 && ry >= 0 && ry < g.gy) {
+            const int cl = ry * g.gx + max(cx - kx, 0), ch = ry * g.gx + min(cx + kx, g.gx - 1);
+            idx = (lane & 1) ? ch : (cl > 0 ? cl - 1 : -1);
+        } else {
+            idx = -1;
+        }
+    }
+    const int bound = idx >= 0 ? (int)cend[idx] : 0;  // invalid rows and cell 0's start read as 0
+    int pre[kRows + 1], off[kRows];
+    pre[0] = 0;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int lo = __builtin_amdgcn_readlane(bound, 2 * r), hi = __builtin_amdgcn_readlane(bound, 2 * r + 1);
+        off[r] = lo - pre[r];
+        pre[r + 1] = pre[r] + (hi - lo);
+    }
+    const int total_c = pre[kRows];
+    auto pos_of = [&](int f) {
+        int a = f + off[0];
+#pragma unroll
+        for (int r = 1; r < kRows; ++r) a = f >= pre[r] ? f + off[r] : a;
+        return a;
+    };
+    for (int f = lane; f < total_c; f += 128) {
+        const int f2 = f + 64;
+        const int a0 = pos_of(f), a1 = pos_of(f2 < total_c ? f2 : f);
+        const uint32_t w0 = spt[a0], w1 = spt[a1];
+        const int j0 = sidx[a0], j1 = sidx[a1];
+        asm volatile("" ::"v"(j0), "v"(j1));  // both index reads issued with the point reads
+        uint32_t d2;
+        if (ecc::epsg::in_eps<kN>(v, w0, e_int, r2i, &d2))
+            __hip_atomic_fetch_or(&bits[j0 >> 6], 1ull << (j0 & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        if (f2 < total_c && ecc::epsg::in_eps<kN>(v, w1, e_int, r2i, &d2))
+            __hip_atomic_fetch_or(&bits[j1 >> 6], 1ull << (j1 & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    unsigned long long wv[4];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int w = lane * wpl + k;
+        const bool mine = k < wpl && w < words;
+        wv[k] = mine ? bits[w] : 0ull;
+        cnt += __popcll(wv[k]);
+        if (mine) bits[w] = 0ull;
+    }
+    const int inc = ecc::wave_incl_scan(cnt);
+    const int total = __shfl(inc, 63);
+    if (lane == 0 && out0 + total != end) *err = 1;  // counts disagree with the lists
+    int64_t out = out0 + (inc - cnt);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        unsigned long long x = wv[k];
+        const int jb = (lane * wpl + k) << 6;
+        while (x) {
+            const int j = jb + __builtin_ctzll(x);
+            x &= x - 1;
+            if (out < end && out < nbr_cap) nbr[out] = j;
+            else *err = 1;
+            ++out;
+        }
+    }
+}
+
+// Ascending neighbour lists, one WAVE per query, queries in segment-index order.  Dynamic LDS:
+// cend[kCells + 1] | spt[stride] | sidx[stride] (the fine grid) | a neighbour bitmap of
+// ceil(stride / 64) u64 words per wave.  The wave walks the query's candidate rows flattened
+// (lane f takes candidate f, f + 64, ...), sets bit j of every candidate j within eps (ds_or),
+// then each lane takes wpl consecutive bitmap words, and a wave prefix of their popcounts places
+// its indices: the list comes out ascending (DBSCAN_precomp's adjacency order) and one query's
+// list is written by one wave into its own contiguous range, so consecutive stores of a wave
+// land in the same lines (the lane-per-query merge wrote each lane's list one 4-B store at a
+// time into its own line: 3x write amplification at the memory side, 8 ms at C4).
 __global__ void __launch_bounds__(kNT)
 eps_lists_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32_t r2i,
                  const int64_t *__restrict__ offsets, int32_t *__restrict__ nbr, int64_t nbr_cap,
@@ -119,60 +207,35 @@ eps_lists_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32_
     uint32_t *cend = lds_l;
     uint32_t *spt = cend + kCells + 1;
     uint16_t *sidx = reinterpret_cast<uint16_t *>(spt + sv.stride);
+    const int n_words = (int)((sv.stride + 63) >> 6);
+    unsigned long long *bits_all =
+        reinterpret_cast<unsigned long long *>(lds_l + ((kCells + 1 + sv.stride + (sv.stride + 1) / 2 + 1) & ~1ll));
     __shared__ int red[64];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kW = kNT / 64;
+    unsigned long long *bits = bits_all + (int64_t)wave * n_words;
+    for (int w = lane; w < n_words; w += 64) bits[w] = 0ull;
     for (int64_t s = blockIdx.x; s < sv.n_segs; s += gridDim.x) {
         const int m = seg_points(sv, s);
         const int64_t base = s * sv.stride;
-        const CellGrid g = ecc::epsg::bin_cells(xy, base, m, e_int, r2i, cend, spt, sidx, red, true, false);
-        for (int q = tid; q < m; q += kNT) {
-            const uint32_t v = spt[q];
-            const int i = sidx[q];
-            const int cx = ecc::epsg::cell_x(g, v), cy = ecc::epsg::cell_y(g, v);
-            int lo[9], hi[9], head[9];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const int x = cx + (k % 3) - 1, y = cy + (k / 3) - 1;
-                const bool ok = x >= 0 && y >= 0 && x < g.gx && y < g.gy;
-                const int c = y * g.gx + x;
-                lo[k] = ok ? (c == 0 ? 0 : (int)cend[c - 1]) : 0;
-                hi[k] = ok ? (int)cend[c] : 0;
-                head[k] = lo[k] < hi[k] ? (int)sidx[lo[k]] : 0x7fffffff;
-            }
-            int64_t out = offsets[base + i];
-            const int64_t end = offsets[base + i + 1];
-            for (;;) {
-                int bk = 0, bi = head[0];
-#pragma unroll
-                for (int k = 1; k < 9; ++k) {
-                    const bool lt = head[k] < bi;
-                    bi = lt ? head[k] : bi;
-                    bk = lt ? k : bk;
-                }
-                if (bi == 0x7fffffff) break;
-                int pos = 0, h = 0;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    pos = (k == bk) ? lo[k] : pos;
-                    h = (k == bk) ? hi[k] : h;
-                }
-                uint32_t d2;
-                const bool in = g.narrow ? ecc::epsg::in_eps<true>(v, spt[pos], e_int, r2i, &d2)
-                                         : ecc::epsg::in_eps<false>(v, spt[pos], e_int, r2i, &d2);
-                const int nxt = pos + 1;
-                const int nh = nxt < h ? (int)sidx[nxt] : 0x7fffffff;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    lo[k] = (k == bk) ? nxt : lo[k];
-                    head[k] = (k == bk) ? nh : head[k];
-                }
-                if (in) {
-                    if (out < end && out < nbr_cap) nbr[out] = bi;
-                    else *err = 1;
-                    ++out;
+        const CellGrid g = ecc::epsg::bin_cells(xy, base, m, e_int, r2i, cend, spt, sidx, red, false, true);
+        const int words = (m + 63) >> 6, wpl = (words + 63) >> 6;  // bitmap words in use, per lane
+        ecc::epsg::with_narrow(g, [&](auto narrow) {
+            constexpr bool kN = decltype(narrow)::value;
+            // a wave's queries are q = wave + kW * t; lane L prefetches query t0 + L's point and
+            // list range for the next 64 (no dependent global load per query)
+            for (int t0 = 0; wave + kW * t0 < m; t0 += 64) {
+                const int ql = wave + kW * (t0 + lane);
+                const uint32_t pv = ql < m ? xy[base + ql] : 0u;
+                const int64_t po0 = ql < m ? offsets[base + ql] : 0, po1 = ql < m ? offsets[base + ql + 1] : 0;
+                for (int tt = 0; tt < 64; ++tt) {
+                    if (wave + kW * (t0 + tt) >= m) break;  // wave-uniform
+                    const uint32_t v = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)pv, tt));
+                    const int64_t out0 = __shfl(po0, tt), end = __shfl(po1, tt);
+                    emit_list<kN>(g, cend, spt, sidx, bits, v, e_int, r2i, words, wpl, out0, end, nbr, nbr_cap, err);
                 }
             }
-        }
+        });
         __syncthreads();
     }
 }
@@ -243,7 +306,8 @@ ECC_API int ecc_eps_lists(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int6
     ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + 2, 0, 4, s), "memset(eps err)");
     SegView sv{seg_counts, n_segs, seg_stride};
     const int r2i = (int)std::floor(eps * eps), e_int = (int)std::floor(eps);
-    const size_t lds = (size_t)(kCells + 1 + seg_stride) * 4 + (size_t)seg_stride * 2;
+    const size_t grid_words = (size_t)((kCells + 1 + seg_stride + (seg_stride + 1) / 2 + 1) & ~1ll);
+    const size_t lds = grid_words * 4 + (size_t)(kNT / 64) * ((seg_stride + 63) / 64) * 8;
     ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(eps_lists_kernel),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                   "eps_lists lds");

@@ -77,11 +77,14 @@ __device__ __forceinline__ CellGrid bin_cells(const uint32_t *__restrict__ xy, i
     constexpr int kHold = 16;
     uint32_t pv[kHold];
     int xmn = 0x7fffffff, ymn = 0x7fffffff, xmx = -1, ymx = -1;
+    // loads through a buffer view of the segment (0 past m), all unconditional (a load under a
+    // per-lane condition waited for every earlier one: 16 round trips per segment)
+    const __amdgpu_buffer_rsrc_t seg = buffer_view(xy + base, (uint32_t)m * 4u);
+#pragma unroll
+    for (int u = 0; u < kHold; ++u) pv[u] = buffer_load_u32(seg, (uint32_t)tid * 4u, (uint32_t)(u * kNT) * 4u);
 #pragma unroll
     for (int u = 0; u < kHold; ++u) {
-        const int i = u * kNT + tid;
-        pv[u] = i < m ? xy[base + i] : 0u;
-        if (i < m) {
+        if (u * kNT + tid < m) {
             xmn = min(xmn, xy_x(pv[u])); ymn = min(ymn, xy_y(pv[u]));
             xmx = max(xmx, xy_x(pv[u])); ymx = max(ymx, xy_y(pv[u]));
         }

@@ -22,6 +22,8 @@
 // Algorithmic bytes: 4 B/point/iteration (packed u16 xy) + 1 B/point for the final labels.
 #include "ecc_internal.hpp"
 
+#include <cmath>
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -174,6 +176,93 @@ __device__ __forceinline__ uint32_t assign_fast(float px, float py, const float 
         return best;
     }
     return ecc::sqrt_rn(m) < thr ? (uint32_t)ia : 255u;
+}
+
+// The f32 engine's screen on the packed fp32 ALU (v_pk_add/mul/fma_f32), two centres per op.
+// d2' = fma(dx, dx, dy*dy) (dx, dy exact as the reference's) is within 2 ulps of the reference's
+// d2 = dx*dx + dy*dy; keys (bits(d2') & ~31) | i order the centres by 32-ulp bucket, then index,
+// and one v_min + one v_med3 per centre keep the smallest two keys.  When the second-best key
+// lies two or more buckets above the best (>= 33 ulps, i.e. > 2^-19 relative, beyond both the
+// d2' error and assign_fast's 2^-20 square-root tie band), the best index is the reference's
+// unique choice: the first centre with the smallest sqrt_rn(d2).  Its exact d2 then meets the
+// threshold as d2 < thr2 (thr2 = the first float whose correctly rounded sqrt is >= thr, found
+// by bisection on the host: sqrt_rn is monotone).  Closer calls, inf and NaN take assign_fast.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// median of three: with a <= b the two smallest of {a, b, c} are min(a, c) and med3(a, b, c).
+// The min/max idiom is not matched to v_med3_u32 for register operands, hence the asm.
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// One point against the centres two at a time: the packed operands are a centre PAIR (two
+// consecutive scalar registers, no copies) and the point broadcast, so the screen costs
+// 2 packed + 3 scalar (v_and_or, v_min, v_med3) instructions per centre and point.
+template <int K>
+__device__ __forceinline__ void screen_point(float px, float py, const float (&cx)[K], const float (&cy)[K],
+                                             uint32_t &k1, uint32_t &k2) {
+    const f32x2 pxx = {px, px}, pyy = {py, py};
+    k1 = 0xffffffffu;
+    k2 = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < K; i += 2) {
+        const f32x2 dx = (f32x2){cx[i], cx[i + 1]} - pxx, dy = (f32x2){cy[i], cy[i + 1]} - pyy;
+        const f32x2 d2 = __builtin_elementwise_fma(dx, dx, dy * dy);
+        const uint32_t ka = (__float_as_uint(d2.x) & ~31u) | (uint32_t)i;
+        const uint32_t kb = (__float_as_uint(d2.y) & ~31u) | (uint32_t)(i + 1);
+        k2 = umed3(k1, k2, ka);
+        k1 = min(k1, ka);
+        k2 = umed3(k1, k2, kb);
+        k1 = min(k1, kb);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t finish_point(float px, float py, uint32_t k1, uint32_t k2,
+                                                 const float (&cx)[K], const float (&cy)[K],
+                                                 const float2 *__restrict__ s_c, float thr, float thr2) {
+    constexpr uint32_t kInfBucket = 0x7F800000u >> 5;
+    if (__builtin_expect((k1 >> 5) < kInfBucket && (k2 >> 5) > (k1 >> 5) + 1u, 1)) {
+        const float2 c = s_c[k1 & 31u];
+        const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
+        return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < thr2 ? (k1 & 31u) : 255u;
+    }
+    return assign_fast<K>(px, py, cx, cy, thr);
+}
+
+template <int K>
+__device__ __forceinline__ void assign_pair(float2 p0, float2 p1, const float (&cx)[K], const float (&cy)[K],
+                                            const float2 *__restrict__ s_c, float thr, float thr2, uint32_t &l0,
+                                            uint32_t &l1) {
+    // the two points' screens interleaved centre pair by centre pair: two independent min/med3
+    // chains per step (one point's chain alone leaves the VALU waiting on its own results)
+    uint32_t a1 = 0xffffffffu, a2 = 0xffffffffu, b1 = 0xffffffffu, b2 = 0xffffffffu;
+    {
+        const f32x2 pxa = {p0.x, p0.x}, pya = {p0.y, p0.y}, pxb = {p1.x, p1.x}, pyb = {p1.y, p1.y};
+#pragma unroll
+        for (int i = 0; i < K; i += 2) {
+            const f32x2 ccx = {cx[i], cx[i + 1]}, ccy = {cy[i], cy[i + 1]};
+            const f32x2 dxa = ccx - pxa, dya = ccy - pya, dxb = ccx - pxb, dyb = ccy - pyb;
+            const f32x2 da = __builtin_elementwise_fma(dxa, dxa, dya * dya);
+            const f32x2 db = __builtin_elementwise_fma(dxb, dxb, dyb * dyb);
+            const uint32_t ka0 = (__float_as_uint(da.x) & ~31u) | (uint32_t)i;
+            const uint32_t kb0 = (__float_as_uint(db.x) & ~31u) | (uint32_t)i;
+            const uint32_t ka1 = (__float_as_uint(da.y) & ~31u) | (uint32_t)(i + 1);
+            const uint32_t kb1 = (__float_as_uint(db.y) & ~31u) | (uint32_t)(i + 1);
+            a2 = umed3(a1, a2, ka0);
+            b2 = umed3(b1, b2, kb0);
+            a1 = min(a1, ka0);
+            b1 = min(b1, kb0);
+            a2 = umed3(a1, a2, ka1);
+            b2 = umed3(b1, b2, kb1);
+            a1 = min(a1, ka1);
+            b1 = min(b1, kb1);
+        }
+    }
+    l0 = finish_point<K>(p0.x, p0.y, a1, a2, cx, cy, s_c, thr, thr2);
+    l1 = finish_point<K>(p1.x, p1.y, b1, b2, cx, cy, s_c, thr, thr2);
 }
 
 // assign_fast's arithmetic, step for step, with the centres read from LDS inside a rolled loop
@@ -589,7 +678,7 @@ constexpr int kF32Unroll = 4;  // 64-point blocks per wave per trip (loads in fl
 template <int K, bool kMfma, bool kAccumulate>
 __global__ void __launch_bounds__(kThreads)
 kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__restrict__ cent, int k, float thr,
-                       double *__restrict__ acc, int n_copies, const KmState *__restrict__ st,
+                       float thr2, double *__restrict__ acc, int n_copies, const KmState *__restrict__ st,
                        uint8_t *__restrict__ labels) {
     if (kAccumulate && st->done) return;
     __shared__ uint32_t s_n[kWaves][K];
@@ -640,19 +729,27 @@ kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__
             q[u] = xy[p < n ? p : n - 1];
         }
 #pragma unroll
-        for (int u = 0; u < kF32Unroll; ++u) {
-            const int64_t blk = b0 + u * stride;
-            if (blk >= nblk) break;  // wave-uniform
-            const int64_t p = blk * 64 + lane;
-            uint32_t lab;
-            if constexpr (kMfma) lab = assign_mfma<K>(q[u].x, q[u].y, ax, ay, c2, em_c2, em_x, em_y, s_c, cx, cy, thr);
-            else lab = assign_fast<K>(q[u].x, q[u].y, cx, cy, thr);
-            if (p >= n) lab = 255u;
-            if (labels && p < n) labels[p] = (uint8_t)lab;
-            if (kAccumulate && lab < (uint32_t)K) {
-                atomicAdd(&s_n[wave][lab], 1u);
-                atomicAdd(&s_sx[wave][lab], (double)q[u].x);
-                atomicAdd(&s_sy[wave][lab], (double)q[u].y);
+        for (int u = 0; u < kF32Unroll; u += 2) {
+            if (b0 + u * stride >= nblk) break;  // wave-uniform
+            uint32_t lab[2];
+            if constexpr (kMfma) {
+                lab[0] = assign_mfma<K>(q[u].x, q[u].y, ax, ay, c2, em_c2, em_x, em_y, s_c, cx, cy, thr);
+                lab[1] = assign_mfma<K>(q[u + 1].x, q[u + 1].y, ax, ay, c2, em_c2, em_x, em_y, s_c, cx, cy, thr);
+            } else {
+                assign_pair<K>(q[u], q[u + 1], cx, cy, s_c, thr, thr2, lab[0], lab[1]);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int64_t blk = b0 + (u + h) * stride;
+                if (blk >= nblk) break;  // wave-uniform
+                const int64_t p = blk * 64 + lane;
+                const uint32_t l = p < n ? lab[h] : 255u;
+                if (labels && p < n) labels[p] = (uint8_t)l;
+                if (kAccumulate && l < (uint32_t)K) {
+                    atomicAdd(&s_n[wave][l], 1u);
+                    atomicAdd(&s_sx[wave][l], (double)q[u + h].x);
+                    atomicAdd(&s_sy[wave][l], (double)q[u + h].y);
+                }
             }
         }
     }
@@ -667,17 +764,143 @@ kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__
     }
 }
 
+// Vector engine, streaming form: a lane takes two consecutive points per 16-B load (the pair the
+// packed screen tests together), kPairUnroll such loads per trip, and the NEXT trip's loads are
+// issued before this trip's tests, so a wave keeps 2 x kPairUnroll x 16 B in flight across its
+// compute (the one-trip form waited on its loads every trip: bound by bytes in flight, ~2.2 TB/s).
+// The pair's two labels go out as one 2-byte store.  Needs 16-B aligned points (and labels 2-B
+// aligned); an odd last point is taken by lane 0 of workgroup 0.
+constexpr int kPairUnroll = 4;
+
+template <int K, bool kAccumulate>
+__global__ void __launch_bounds__(kThreads)
+kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *__restrict__ cent, int k, float thr,
+                       float thr2, double *__restrict__ acc, int n_copies, const KmState *__restrict__ st,
+                       uint8_t *__restrict__ labels) {
+    if (kAccumulate && st->done) return;
+    __shared__ uint32_t s_n[kWaves][K];
+    __shared__ double s_sx[kWaves][K], s_sy[kWaves][K];
+    __shared__ float2 s_c[K];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    float cx[K], cy[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
+        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+    }
+    if (tid < K) s_c[tid] = make_float2(tid < k ? cent[2 * tid] : 1e30f, tid < k ? cent[2 * tid + 1] : 1e30f);
+    if (kAccumulate && lane < K) {
+        s_n[wave][lane] = 0u;
+        s_sx[wave][lane] = 0.0;
+        s_sy[wave][lane] = 0.0;
+    }
+    __syncthreads();
+    auto account = [&](float2 q, uint32_t l) {
+        if (kAccumulate && l < (uint32_t)K) {
+            atomicAdd(&s_n[wave][l], 1u);
+            atomicAdd(&s_sx[wave][l], (double)q.x);
+            atomicAdd(&s_sy[wave][l], (double)q.y);
+        }
+    };
+    const int64_t npair = n / 2;
+    const int64_t nblk = (npair + 63) / 64;  // 64 pairs per wave block
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    const int64_t span = stride * kPairUnroll;
+    auto load = [&](int64_t b0, float4 (&q)[kPairUnroll]) {
+#pragma unroll
+        for (int u = 0; u < kPairUnroll; ++u) {  // clamped, unconditional
+            const int64_t pp = (b0 + u * stride) * 64 + lane;
+            q[u] = xy4[pp < npair ? pp : npair - 1];
+        }
+    };
+    auto test = [&](int64_t b0, const float4 (&q)[kPairUnroll]) {
+#pragma unroll
+        for (int u = 0; u < kPairUnroll; ++u) {
+            const int64_t blk = b0 + u * stride;
+            if (blk >= nblk) break;  // wave-uniform
+            const int64_t pp = blk * 64 + lane;
+            const float2 p0 = make_float2(q[u].x, q[u].y), p1 = make_float2(q[u].z, q[u].w);
+            uint32_t l0, l1;
+            assign_pair<K>(p0, p1, cx, cy, s_c, thr, thr2, l0, l1);
+            if (pp < npair) {
+                if (labels) reinterpret_cast<uint16_t *>(labels)[pp] = (uint16_t)(l0 | l1 << 8);
+                account(p0, l0);
+                account(p1, l1);
+            }
+        }
+    };
+    // Two buffers in ping-pong with unconditional (clamped) loads: no register copies between
+    // trips and no branch around the loads, so the wait before each trip's tests covers only
+    // that trip's own loads while the other buffer's are in flight.
+    float4 qa[kPairUnroll], qb[kPairUnroll];
+    int64_t b0 = (int64_t)blockIdx.x * kWaves + wave;
+    if (npair > 0 && b0 < nblk) {
+        load(b0, qa);
+        for (;;) {
+            load(b0 + span, qb);
+            test(b0, qa);
+            b0 += span;
+            if (b0 >= nblk) break;  // wave-uniform
+            load(b0 + span, qa);
+            test(b0, qb);
+            b0 += span;
+            if (b0 >= nblk) break;
+        }
+    }
+    if ((n & 1) && blockIdx.x == 0 && tid == 0) {  // the odd last point
+        const float2 q = reinterpret_cast<const float2 *>(xy4)[n - 1];
+        const uint32_t l = assign_fast<K>(q.x, q.y, cx, cy, thr);
+        if (labels) labels[n - 1] = (uint8_t)l;
+        account(q, l);
+    }
+    if (!kAccumulate) return;
+    __syncthreads();
+    if (tid < 3 * k) {
+        const int f = tid / k, c = tid - f * k;
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) v += f == 0 ? (double)s_n[w][c] : (f == 1 ? s_sx[w][c] : s_sy[w][c]);
+        if (v != 0.0) atomicAdd(&acc[(int)(blockIdx.x % n_copies) * kAccStride + 3 * c + f], v);
+    }
+}
+
+// Host: the smallest float s >= 0 with sqrtf(s) >= thr (sqrtf correctly rounded, like sqrt_rn;
+// monotone), so that sqrt_rn(d2) < thr <=> d2 < thr2.  Bisection over the bit patterns.
+inline float sqrt_threshold(float thr) {
+    if (!(thr > 0.f)) return 0.f;           // nothing is below (NaN threshold: nothing either)
+    if (std::isinf(thr)) return __builtin_inff();
+    uint32_t lo = 0u, hi = 0x7F800000u;      // sqrt(+0) < thr; sqrt(+inf) = inf >= thr
+    while (hi - lo > 1u) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        float f;
+        std::memcpy(&f, &mid, 4);
+        (std::sqrt(f) < thr ? lo : hi) = mid;
+    }
+    float r;
+    std::memcpy(&r, &hi, 4);
+    return r;
+}
+
 template <bool kAccumulate>
 bool launch_f32_fast(int k, int method, dim3 grid, hipStream_t s, const float *xy, int64_t n, const float *cent,
                      float thr, double *acc, int n_copies, const KmState *st, uint8_t *labels) {
+    const float thr2 = sqrt_threshold(thr);
     if (k > kFastMaxK) return false;
     const float2 *p = reinterpret_cast<const float2 *>(xy);
 #define ECC_F32_LAUNCH(KK, MF)                                                                               \
     hipLaunchKernelGGL((kmeans_f32_fast_kernel<KK, MF, kAccumulate>), grid, dim3(kThreads), 0, s, p, n, cent, k, \
-                       thr, acc, n_copies, st, labels)
+                       thr, thr2, acc, n_copies, st, labels)
     if (method == 2) {
         if (k <= 16) ECC_F32_LAUNCH(16, true);
         else ECC_F32_LAUNCH(32, true);
+    } else if ((reinterpret_cast<uintptr_t>(xy) & 15) == 0 && (reinterpret_cast<uintptr_t>(labels) & 1) == 0) {  // 16-B loads of point pairs
+        const float4 *p4 = reinterpret_cast<const float4 *>(xy);
+        if (k <= 16)
+            hipLaunchKernelGGL((kmeans_f32_pair_kernel<16, kAccumulate>), grid, dim3(kThreads), 0, s, p4, n, cent, k,
+                               thr, thr2, acc, n_copies, st, labels);
+        else
+            hipLaunchKernelGGL((kmeans_f32_pair_kernel<32, kAccumulate>), grid, dim3(kThreads), 0, s, p4, n, cent, k,
+                               thr, thr2, acc, n_copies, st, labels);
     } else {
         if (k <= 16) ECC_F32_LAUNCH(16, false);
         else ECC_F32_LAUNCH(32, false);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """eps-neighbourhood / grid-DBSCAN kernels on the bench workload (the representatives of the
 20 M-event 346x260 stream, 2442 windows of 8192): a few calls each, for rocprofv3 counter passes.
-Usage: eps_probe.py [counts|dbscan|lists|all]"""
+Usage: eps_probe.py [counts|dbscan|lists|all]  (lists: eps_lists + dbscan_extract)"""
 import sys
 from pathlib import Path
 
@@ -19,7 +19,20 @@ rep_xy, rep_idx, uniq, rep, nw = ctx.downsample_hash(d_xy, n)
 tot = nw * WIN
 cnt = ecc.DeviceArray(tot, np.int32)
 core = ecc.DeviceArray(tot, np.float64)
+if what in ("lists", "all"):  # the list chain: counts -> ascending lists -> extraction
+    e_cnt = ecc.DeviceArray(tot, np.int32)
+    ctx.eps_counts(rep_xy, nw, WIN, uniq, 20.0, 20, e_cnt, None)
+    ctx.sync()
+    valid = (np.arange(WIN)[None, :] < uniq.numpy()[:, None]).ravel()
+    nbr_cap = int(e_cnt.numpy()[valid].sum()) + 16
+    d_off, d_nbr = ecc.DeviceArray(tot + 1, np.int64), ecc.DeviceArray(nbr_cap, np.int32)
+    d_lab, d_nc, d_nd = ecc.DeviceArray(tot, np.int32), ecc.DeviceArray(nw, np.int32), ecc.DeviceArray(1, np.int64)
+    d_dups = ecc.DeviceArray(2 << 22, np.int64)
+    print("list entries", nbr_cap - 16)
 for _ in range(3):
+    if what in ("lists", "all"):
+        ctx.eps_lists(rep_xy, nw, WIN, uniq, 20.0, e_cnt, d_off, d_nbr, nbr_cap)
+        ctx.dbscan_extract(nw, WIN, uniq, d_off, d_nbr, 20, 100, 25000, d_lab, d_nc, d_dups, 1 << 22, d_nd)
     if what in ("counts", "all"):
         ctx.eps_counts(rep_xy, nw, WIN, uniq, 20.0, 20, cnt, None)
         ctx.eps_counts(rep_xy, nw, WIN, uniq, 10.0, 2, cnt, core)

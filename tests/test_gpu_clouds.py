@@ -166,7 +166,9 @@ def test_radius_f32_counts_core_lists_match_oracle(ecc, orc, gpu, min_pts):
     gpu.radius_counts_f32(d_p, n, 3, eps, min_pts, d_cnt, d_core)
     assert np.array_equal(d_cnt.numpy(), o_cnt)
     assert np.array_equal(d_core.numpy().view(np.int64), o_core.view(np.int64))
-    assert (o_core >= 0).any() and (o_core < 0).any()
+    assert (o_core >= 0).any() and np.array_equal(o_core >= 0, o_cnt >= min_pts)
+    if min_pts > 1:
+        assert (o_core < 0).any()
     total = int(o_off[-1])
     d_off, d_nbr = ecc.DeviceArray(n + 1, np.int64), ecc.DeviceArray(total, np.int32)
     d_nd = ecc.DeviceArray(total, np.float64)

@@ -271,6 +271,29 @@ def test_kmeans_assign_ties_and_threshold(ecc, orc, gpu):
     assert list(g[:7]) == [0, 0, 1, 1, 3, 255, 1]
 
 
+@pytest.mark.parametrize("engine", [1, 2])
+def test_kmeans_f32_threshold_and_tie_boundaries_ulps(ecc, orc, gpu, engine):
+    """The f32 engines' fast screens (the vector engine's 32-ulp buckets + d2 < thr2, the matrix
+    engine's margin) against assign_to_centers' rule at its edges: points a few ulps either side
+    of the threshold circle (sqrt(d2) < 50) and of the bisector between two centres."""
+    rng = np.random.default_rng(17 + engine)
+    c = np.array([100, 100, 180, 100, 100, 180, 35.5, 41.25], np.float32)
+    th = rng.uniform(0, 2 * np.pi, 60000)
+    ring = np.stack([100 + 50 * np.cos(th), 100 + 50 * np.sin(th)], 1).astype(np.float32)
+    bis = np.stack([np.full(60000, 140.0), rng.uniform(60, 140, 60000)], 1).astype(np.float32)
+    pts = np.concatenate([ring, bis])
+    steps = rng.integers(-4, 5, pts.shape).astype(np.int32)
+    pts = (pts.view(np.int32) + steps).view(np.float32)  # +-4 ulps
+    flat = pts.ravel()
+    o = orc.kmeans_assign_f32(flat, c)
+    assert 0 < (o == 255).sum() < len(o) and (o == 1).sum() > 1000
+    d_c = dev(ecc, c)
+    d_lab = ecc.DeviceArray(len(pts), np.uint8)
+    gpu.kmeans_f32_engine(dev(ecc, flat), len(pts), d_c, ecc.kmeans_cfg(k=4, max_iters=0, tol=-1.0), engine, d_lab)
+    gpu.sync()
+    assert (d_lab.numpy() == o).all()
+
+
 # ------------------------------------------------------------------------------ SAE + arc corners
 def _fast_gpu(ecc, gpu, xy, t, W, H, border_mode=0, first_detect=1, sae0=None, slice_events=16384):
     cfg = ecc.corner_cfg(width=W, height=H, border_mode=border_mode, first_detect_slice=first_detect,
@@ -333,15 +356,17 @@ def test_fast_detect_stream_continuation(ecc, orc, gpu):
     assert (s2 == o_sae).all()
 
 
-def test_fast_detect_dense_overflow_path(ecc, orc, gpu):
-    """>= 3 groups of 32 slices where whole slices land in a 30x30-pixel patch: every window of
-    the patch holds more values than the compact per-pixel lists take, so those items run on the
-    dense-plane kernel (asserted through ecc_fast_detect_stats) — flags and SAE still bit-exact."""
+@pytest.mark.parametrize("side,groups", [(30, 1.5), (200, 16)])
+def test_fast_detect_dense_overflow_path(ecc, orc, gpu, side, groups):
+    """Whole slices landing in a side x side patch: every window of the patch holds more values
+    than the compact per-pixel lists take, so those items run on the dense-plane kernel (asserted
+    through ecc_fast_detect_stats): a few dozen items (30 px) and thousands (200 px, 16 groups).
+    Flags and SAE bit-exact."""
     W, H = 346, 260
     rng = np.random.default_rng(5)
-    n_dense = 16384 * 48
-    xd = rng.integers(150, 180, n_dense)
-    yd = rng.integers(100, 130, n_dense)
+    n_dense = int(16384 * 32 * groups)
+    xd = rng.integers(150, 150 + side, n_dense)
+    yd = rng.integers(100, 100 + side, n_dense)
     td = np.cumsum(rng.integers(0, 3, n_dense)).astype(np.int64)
     xy2, t2, _ = ecc.gen_events(16384 * 50 + 333, seed=17, width=W, height=H)
     xy = np.concatenate([ecc.pack_xy(xd, yd), xy2])
@@ -350,6 +375,7 @@ def test_fast_detect_dense_overflow_path(ecc, orc, gpu):
     g_flags, g_sae = _fast_gpu(ecc, gpu, xy, t, W, H)
     st = gpu.fast_detect_stats()
     assert st["groups"] >= 3 and st["overflow_items"] > 0, st
+    assert (st["overflow_items"] > 1000) == (side == 200), st
     assert o_flags[:n_dense].sum() > 0 and o_flags[n_dense:].sum() > 0
     assert (g_flags == o_flags).all(), f"{(g_flags != o_flags).sum()} corner labels differ"
     assert (g_sae == o_sae).all()
