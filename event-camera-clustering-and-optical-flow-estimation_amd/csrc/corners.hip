@@ -134,7 +134,6 @@ __device__ __forceinline__ int slice_in_group(uint32_t el, const CornerGeom &g) 
 // the CU idle outside its load phase).
 constexpr int kSortThreads = 1024;
 constexpr int kSortEPT = 16;
-constexpr int kSortFence = 4;  // events whose loads may be in flight together
 constexpr int kSortChunk = kSortThreads * kSortEPT;
 
 // Block-wide exclusive scan in place of a[0, n) (kSortThreads threads, each a contiguous run).
@@ -161,7 +160,7 @@ __device__ __forceinline__ void block_excl_scan_inplace(int32_t *a, int n, int32
     }
 }
 
-__global__ void __launch_bounds__(kSortThreads, 8)  // 8 waves/SIMD: two workgroups per CU
+__global__ void __launch_bounds__(kSortThreads, 4)  // one workgroup per CU: a lane's 16 events' loads in flight at once
 slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g, Sorted so,
                   int32_t *__restrict__ first_border, int32_t *__restrict__ err) {
     extern __shared__ int32_t hist[];  // [nb]: counts, then offsets, then (long slices) cursors;
@@ -185,25 +184,40 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
     // per event only its final key and tile << 16 | rank stay in registers (single slices:
     // rank < 2^14); the key is formed at load time
     uint32_t kv[kSortEPT], br[kSortEPT];
-    const uint32_t *__restrict__ xs = xy + lo;
-    const int64_t *__restrict__ ts = t + lo;
+    // buffer views of the slice: loads past its end return 0, so every load is unconditional and
+    // nothing branches between them (a load under a per-lane condition, or a branch after each
+    // event's loads, made each event wait for its own loads: 16 serial HBM round trips per slice).
+    // The time-order check takes the previous event's t from the neighbouring lane (DPP wave
+    // shift); each wave's first event is checked against its predecessor afterwards.
+    const __amdgpu_buffer_rsrc_t vx = ecc::buffer_view(xy + lo, (uint32_t)len * 4u);
+    const __amdgpu_buffer_rsrc_t vt = ecc::buffer_view(t + lo, (uint32_t)len * 8u);
     for (int c0 = 0; c0 < len; c0 += kSortChunk) {  // one iteration for single slices
+        uint32_t vv[kSortEPT];
+        int64_t tt[kSortEPT];
+#pragma unroll
+        for (int u = 0; u < kSortEPT; ++u) {  // every load of the lane first (su rides in soffset)
+            const uint32_t su = (uint32_t)(c0 + u * kSortThreads);
+            vv[u] = ecc::buffer_load_u32(vx, (uint32_t)tid * 4u, su * 4u);
+            tt[u] = ecc::buffer_load_i64(vt, (uint32_t)tid * 8u, su * 8u);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the compiler from interleaving uses between them
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u) {
-            // a compiler fence every kSortFence events keeps later loads from being hoisted above
-            // earlier uses (all 16 events' loads in flight would spill)
-            if (u > 0 && u % kSortFence == 0) asm volatile("" ::: "memory");
             const int i = c0 + u * kSortThreads + tid;
             const bool ok = i < len;
-            const int ic = ok ? i : len - 1;  // clamped: unconditional loads off uniform bases
-            const uint32_t v = xs[ic];
-            const int64_t tc = ts[ic];
-            // the previous event's t: a coalesced load of the neighbouring element (cache hit)
-            const int64_t tp = (ic > 0 || lo > 0) ? ts[ic - 1] : INT64_MIN;
-            bad |= ok && tp > tc;
+            const uint32_t v = vv[u];
+            const int64_t tc = tt[u];
+            const uint32_t plo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)tc, 0x138, 0xf, 0xf, false);
+            const uint32_t phi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)tc >> 32), 0x138, 0xf, 0xf, false);
+            const int64_t tp = (int64_t)(((uint64_t)phi << 32) | plo);  // lane - 1's t (wave_shr:1)
+            bad |= ok & (lane > 0) & (tp > tc);
             kv[u] = tile_key(v, fmt4 ? (uint32_t)(tc - t_first) : (uint32_t)(lo + i - grp_first));
             br[u] = ok ? (uint32_t)tile_of(v, g) << 16 : 0xffffffffu;
-            if (ok && is_border(ecc::xy_x(v), ecc::xy_y(v), g)) fb = min(fb, i);
+            fb = min(fb, (ok && is_border(ecc::xy_x(v), ecc::xy_y(v), g)) ? i : 0x7fffffff);
+        }
+        if (tid < kSortEPT * (kSortThreads / 64)) {  // each wave's first event against its predecessor
+            const int i = c0 + tid * 64;  // u = tid / 16, wave = tid % 16
+            if (i < len && lo + i > 0) bad |= t[lo + i - 1] > t[lo + i];
         }
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u) {
@@ -392,11 +406,14 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
             uint32_t k[kBuildUnroll];
             int r[kBuildUnroll];
 #pragma unroll
-            for (int u = 0; u < kBuildUnroll; ++u) {
+            for (int u = 0; u < kBuildUnroll; ++u) {  // clamped index: the loads are unconditional
                 const int i = i0 + u * kThreads + tid;
-                const int64_t gi = (i < total) ? seg_at(segs, i, r[u]) : 0;
-                k[u] = (i < total) ? so.key[gi] : 0xffffffffu;
+                const int64_t gi = seg_at(segs, i < total ? i : total - 1, r[u]);
+                k[u] = so.key[gi];
             }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < kBuildUnroll; ++u) k[u] = i0 + u * kThreads + tid < total ? k[u] : 0xffffffffu;
 #pragma unroll
             for (int u = 0; u < kBuildUnroll; ++u) {
                 if (k[u] == 0xffffffffu) continue;
@@ -407,13 +424,16 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
         for (int i0 = 0; i0 < total; i0 += kBuildUnroll * kThreads) {
             uint32_t k[kBuildUnroll], tv[kBuildUnroll];
 #pragma unroll
-            for (int u = 0; u < kBuildUnroll; ++u) {
+            for (int u = 0; u < kBuildUnroll; ++u) {  // clamped index: the loads are unconditional
                 const int i = i0 + u * kThreads + tid;
                 int r_unused;
-                const int64_t gi = (i < total) ? seg_at(segs, i, r_unused) : 0;
-                k[u] = (i < total) ? so.key[gi] : 0xffffffffu;
-                tv[u] = (i < total && gr.narrow) ? so.t32[gi] : 0u;
+                const int64_t gi = seg_at(segs, i < total ? i : total - 1, r_unused);
+                k[u] = so.key[gi];
+                tv[u] = gr.narrow ? so.t32[gi] : 0u;
             }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < kBuildUnroll; ++u) k[u] = i0 + u * kThreads + tid < total ? k[u] : 0xffffffffu;
 #pragma unroll
             for (int u = 0; u < kBuildUnroll; ++u) {
                 if (k[u] == 0xffffffffu) continue;
@@ -1231,20 +1251,39 @@ flags_event_kernel(const uint32_t *__restrict__ xy, CornerGeom g, const uint32_t
     const int n4 = vec ? len / 4 : 0;
     // a lane's quads (<= kFlagQuads of them for slices up to 16384 events) are loaded before the
     // staging, so the two latencies overlap
+    // all of them unconditional through a buffer view of the slice's whole quads (0 past them):
+    // a load under a per-lane condition made each quad wait for the previous one
     uint4 pre[kFlagQuads];
+    const __amdgpu_buffer_rsrc_t vq = ecc::buffer_view(xy + lo, (uint32_t)n4 * 16u);
 #pragma unroll
-    for (int u = 0; u < kFlagQuads; ++u) {
-        const int q = u * kFlagThreads + (int)threadIdx.x;
-        pre[u] = (q < n4 && 4 * q < live_end) ? *reinterpret_cast<const uint4 *>(xy + lo + 4 * q) : make_uint4(0u, 0u, 0u, 0u);
-    }
+    for (int u = 0; u < kFlagQuads; ++u)
+        pre[u] = ecc::buffer_load_u128(vq, threadIdx.x * 16u, (uint32_t)(u * kFlagThreads) * 16u);
+    __builtin_amdgcn_sched_barrier(0);
     if (kStaged && live_end > 0) {
+        // four words per lane per trip, loads unconditional through a buffer view of the group's
+        // result words (0 past them; the word past an item's end is selected away afterwards)
         const int b0 = j * kTilePix, w0 = b0 >> 5, sh = b0 & 31;
-        for (int k = threadIdx.x; k < g.n_tiles * kSegWords; k += kFlagThreads) {
-            const int tile = k / kSegWords, w = k % kSegWords;
-            const uint32_t *r = rg + (int64_t)tile * kPairWords + w0 + w;
-            const uint32_t a = w0 + w < kPairWords ? r[0] : 0u;
-            const uint32_t c = (sh && w0 + w + 1 < kPairWords) ? r[1] : 0u;
-            sb[k] = sh ? (a >> sh) | (c << (32 - sh)) : a;
+        const int total = g.n_tiles * kSegWords;
+        const __amdgpu_buffer_rsrc_t vr = ecc::buffer_view(rg, (uint32_t)g.n_tiles * kPairWords * 4u);
+        for (int k0 = 0; k0 < total; k0 += 4 * kFlagThreads) {
+            uint32_t a[4], c[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int k = k0 + b * kFlagThreads + (int)threadIdx.x;
+                const int tile = k / kSegWords, w = k % kSegWords;
+                const uint32_t off = ((uint32_t)tile * kPairWords + w0 + w) * 4u;
+                a[b] = ecc::buffer_load_u32(vr, off);
+                c[b] = ecc::buffer_load_u32(vr, off + 4u);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int k = k0 + b * kFlagThreads + (int)threadIdx.x;
+                const int w = k % kSegWords;
+                const uint32_t av = w0 + w < kPairWords ? a[b] : 0u;
+                const uint32_t cv = (sh && w0 + w + 1 < kPairWords) ? c[b] : 0u;
+                if (k < total) sb[k] = sh ? (av >> sh) | (cv << (32 - sh)) : av;
+            }
         }
     }
     __syncthreads();

@@ -98,6 +98,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_view(const void *p, uin
 __device__ __forceinline__ uint32_t buffer_load_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
 }
+__device__ __forceinline__ int64_t buffer_load_i64(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
+    return (int64_t)(((uint64_t)v[1] << 32) | v[0]);
+}
+__device__ __forceinline__ uint4 buffer_load_u128(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
 
 // Inclusive prefix sum over the 64 lanes of a wave with DPP moves (no LDS round trip): row_shr
 // 1/2/4/8 scans each row of 16 (bound_ctrl fills zeros at the row start), then row_bcast:15

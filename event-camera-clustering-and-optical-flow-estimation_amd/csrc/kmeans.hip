@@ -306,7 +306,7 @@ __device__ __forceinline__ float uniform_f32(float v) {
 // Replicated accumulators: the per-WG flush goes to replica blockIdx % n_copies, which spreads
 // the same-address global atomics; the update kernel sums the replicas.
 constexpr int kAccStride = 3 * kMaxK;
-constexpr int kAccCopies = 4;
+constexpr int kAccCopies = 16;  // replicas: 256 pixel-pass WGs -> 16 atomics per address
 
 // One Lloyd pass (kAccumulate) or the final labelling.  Accumulation: every point adds
 // (1 << 52) | (x << 26) | y to its cluster's u64 slot of its WAVE in LDS with one no-return
@@ -806,11 +806,16 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     const int64_t nblk = (npair + 63) / 64;  // 64 pairs per wave block
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     const int64_t span = stride * kPairUnroll;
+    // a trip's loads through a buffer view based at its first pair: unconditional (0 past the
+    // last pair), one VGPR of lane offset for all of them, the u part in the scalar offset
     auto load = [&](int64_t b0, float4 (&q)[kPairUnroll]) {
+        const int64_t first = b0 * 64 < npair ? b0 * 64 : npair;
+        const int64_t rem = (npair - first) * 16;
+        const __amdgpu_buffer_rsrc_t v = ecc::buffer_view(xy4 + first, rem < 0xffffffffll ? (uint32_t)rem : 0xffffffffu);
 #pragma unroll
-        for (int u = 0; u < kPairUnroll; ++u) {  // clamped, unconditional
-            const int64_t pp = (b0 + u * stride) * 64 + lane;
-            q[u] = xy4[pp < npair ? pp : npair - 1];
+        for (int u = 0; u < kPairUnroll; ++u) {
+            const uint4 w = ecc::buffer_load_u128(v, (uint32_t)lane * 16u, (uint32_t)(u * stride * 64 * 16));
+            q[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
         }
     };
     auto test = [&](int64_t b0, const float4 (&q)[kPairUnroll]) {
@@ -833,7 +838,7 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     // trips and no branch around the loads, so the wait before each trip's tests covers only
     // that trip's own loads while the other buffer's are in flight.
     float4 qa[kPairUnroll], qb[kPairUnroll];
-    int64_t b0 = (int64_t)blockIdx.x * kWaves + wave;
+    int64_t b0 = (int64_t)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(wave);  // uniform: scalar descriptors
     if (npair > 0 && b0 < nblk) {
         load(b0, qa);
         for (;;) {
@@ -920,13 +925,18 @@ kmeans_update_kernel(AccT *__restrict__ acc, int n_copies, float *__restrict__ c
     float shift = 0.f;
     if (lane < k) {
         AccT a[3] = {0, 0, 0};
-        for (int r = 0; r < n_copies; ++r) {
+        AccT v[kAccCopies][3];  // every replica's loads in flight together
+#pragma unroll
+        for (int r = 0; r < kAccCopies; ++r)
+#pragma unroll
+            for (int f = 0; f < 3; ++f) v[r][f] = r < n_copies ? acc[r * kAccStride + 3 * lane + f] : (AccT)0;
+#pragma unroll
+        for (int r = 0; r < kAccCopies; ++r)
 #pragma unroll
             for (int f = 0; f < 3; ++f) {
-                a[f] += acc[r * kAccStride + 3 * lane + f];
-                acc[r * kAccStride + 3 * lane + f] = 0;
+                a[f] += v[r][f];
+                if (r < n_copies) acc[r * kAccStride + 3 * lane + f] = 0;
             }
-        }
         const double n_pts = (double)a[0];
         if (n_pts > 0.0) {
             const float nx = (float)((double)a[1] / n_pts);
@@ -1178,8 +1188,11 @@ kmeans_step_kernel(StepArgs a, const uint32_t *__restrict__ ext, int n_ext, uint
     if (update) {
         if (tid < 3 * a.k) {
             const int c = tid / 3, f = tid - 3 * c;
-            unsigned long long v = 0;
-            for (int r = 0; r < a.n_copies; ++r) v += a.acc_in[r * kAccStride + 3 * c + f];
+            unsigned long long t[kAccCopies], v = 0;  // all replicas' loads in flight together
+#pragma unroll
+            for (int r = 0; r < kAccCopies; ++r) t[r] = r < a.n_copies ? a.acc_in[r * kAccStride + 3 * c + f] : 0ull;
+#pragma unroll
+            for (int r = 0; r < kAccCopies; ++r) v += t[r];
             s_sum[f][c] = v;
         }
         if (blockIdx.x == 0)

@@ -862,7 +862,8 @@ def test_eps_neighbourhoods_match_oracle(ecc, orc, gpu, eps, min_pts):
 
 @pytest.mark.parametrize("eps,min_pts", [(6.0, 64), (12.5, 20), (3.0, 3)])
 def test_eps_counts_wide_segments(ecc, orc, gpu, eps, min_pts):
-    """16384-point segments (dynamic LDS above 64 KiB) and the min_pts-sized core networks."""
+    """16384-point segments (dynamic LDS above 64 KiB) and the min_pts-sized core networks; the
+    lists of the same segments (bitmap words of 4 per lane, thousands of neighbours per query)."""
     rng = np.random.default_rng(61)
     n_segs, stride = 2, 16384
     counts = np.array([16384, 9001], np.int32)
@@ -873,11 +874,19 @@ def test_eps_counts_wide_segments(ecc, orc, gpu, eps, min_pts):
     pts = np.clip(np.rint(np.where(pick[:, None], blob, noise)), 0, [345, 259]).astype(np.int64)
     pts[100:140] = pts[99]  # duplicates
     xy = ecc.pack_xy(pts[:, 0], pts[:, 1])
-    o_cnt, o_core, _, _ = orc.eps_neighbours(xy, n_segs, stride, counts, eps, min_pts, want_lists=False)
+    o_cnt, o_core, o_off, o_nbr = orc.eps_neighbours(xy, n_segs, stride, counts, eps, min_pts)
     d_cnt = ecc.DeviceArray(n, np.int32)
     d_core = ecc.DeviceArray(n, np.float64)
     gpu.eps_counts(dev(ecc, xy), n_segs, stride, dev(ecc, counts), eps, min_pts, d_cnt, d_core)
+    d_off = ecc.DeviceArray(n + 1, np.int64)
+    d_nbr = ecc.DeviceArray(int(o_off[-1]) + 16, np.int32)
+    gpu.eps_lists(dev(ecc, xy), n_segs, stride, dev(ecc, counts), eps, d_cnt, d_off, d_nbr, int(o_off[-1]) + 16)
     gpu.sync()
+    import ctypes as C
+    total = C.c_int64(0)
+    assert ecc.lib.ecc_eps_total(gpu.ctx, d_off.ptr, n, C.byref(total), gpu.stream) == 0  # no list error
+    assert (d_off.numpy() == o_off).all() and total.value == o_off[-1]
+    assert (d_nbr.numpy()[:o_off[-1]] == o_nbr[:o_off[-1]]).all()
     g_cnt, g_core = d_cnt.numpy(), d_core.numpy()
     for sgi in range(n_segs):
         sl = slice(sgi * stride, sgi * stride + counts[sgi])
