@@ -134,6 +134,7 @@ __device__ __forceinline__ int slice_in_group(uint32_t el, const CornerGeom &g) 
 // the CU idle outside its load phase).
 constexpr int kSortThreads = 1024;
 constexpr int kSortEPT = 16;
+constexpr int kSortFence = 4;  // events whose loads may be in flight together
 constexpr int kSortChunk = kSortThreads * kSortEPT;
 
 // Block-wide exclusive scan in place of a[0, n) (kSortThreads threads, each a contiguous run).
@@ -160,7 +161,7 @@ __device__ __forceinline__ void block_excl_scan_inplace(int32_t *a, int n, int32
     }
 }
 
-__global__ void __launch_bounds__(kSortThreads, 4)  // one workgroup per CU: a lane's 16 events' loads in flight at once
+__global__ void __launch_bounds__(kSortThreads, 8)  // 8 waves/SIMD: two workgroups per CU
 slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g, Sorted so,
                   int32_t *__restrict__ first_border, int32_t *__restrict__ err) {
     extern __shared__ int32_t hist[];  // [nb]: counts, then offsets, then (long slices) cursors;
@@ -184,40 +185,25 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
     // per event only its final key and tile << 16 | rank stay in registers (single slices:
     // rank < 2^14); the key is formed at load time
     uint32_t kv[kSortEPT], br[kSortEPT];
-    // buffer views of the slice: loads past its end return 0, so every load is unconditional and
-    // nothing branches between them (a load under a per-lane condition, or a branch after each
-    // event's loads, made each event wait for its own loads: 16 serial HBM round trips per slice).
-    // The time-order check takes the previous event's t from the neighbouring lane (DPP wave
-    // shift); each wave's first event is checked against its predecessor afterwards.
-    const __amdgpu_buffer_rsrc_t vx = ecc::buffer_view(xy + lo, (uint32_t)len * 4u);
-    const __amdgpu_buffer_rsrc_t vt = ecc::buffer_view(t + lo, (uint32_t)len * 8u);
+    const uint32_t *__restrict__ xs = xy + lo;
+    const int64_t *__restrict__ ts = t + lo;
     for (int c0 = 0; c0 < len; c0 += kSortChunk) {  // one iteration for single slices
-        uint32_t vv[kSortEPT];
-        int64_t tt[kSortEPT];
-#pragma unroll
-        for (int u = 0; u < kSortEPT; ++u) {  // every load of the lane first (su rides in soffset)
-            const uint32_t su = (uint32_t)(c0 + u * kSortThreads);
-            vv[u] = ecc::buffer_load_u32(vx, (uint32_t)tid * 4u, su * 4u);
-            tt[u] = ecc::buffer_load_i64(vt, (uint32_t)tid * 8u, su * 8u);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep the compiler from interleaving uses between them
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u) {
+            // a compiler fence every kSortFence events keeps later loads from being hoisted above
+            // earlier uses (all 16 events' loads in flight would spill)
+            if (u > 0 && u % kSortFence == 0) asm volatile("" ::: "memory");
             const int i = c0 + u * kSortThreads + tid;
             const bool ok = i < len;
-            const uint32_t v = vv[u];
-            const int64_t tc = tt[u];
-            const uint32_t plo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)tc, 0x138, 0xf, 0xf, false);
-            const uint32_t phi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)tc >> 32), 0x138, 0xf, 0xf, false);
-            const int64_t tp = (int64_t)(((uint64_t)phi << 32) | plo);  // lane - 1's t (wave_shr:1)
-            bad |= ok & (lane > 0) & (tp > tc);
+            const int ic = ok ? i : len - 1;  // clamped: unconditional loads off uniform bases
+            const uint32_t v = xs[ic];
+            const int64_t tc = ts[ic];
+            // the previous event's t: a coalesced load of the neighbouring element (cache hit)
+            const int64_t tp = (ic > 0 || lo > 0) ? ts[ic - 1] : INT64_MIN;
+            bad |= ok && tp > tc;
             kv[u] = tile_key(v, fmt4 ? (uint32_t)(tc - t_first) : (uint32_t)(lo + i - grp_first));
             br[u] = ok ? (uint32_t)tile_of(v, g) << 16 : 0xffffffffu;
-            fb = min(fb, (ok && is_border(ecc::xy_x(v), ecc::xy_y(v), g)) ? i : 0x7fffffff);
-        }
-        if (tid < kSortEPT * (kSortThreads / 64)) {  // each wave's first event against its predecessor
-            const int i = c0 + tid * 64;  // u = tid / 16, wave = tid % 16
-            if (i < len && lo + i > 0) bad |= t[lo + i - 1] > t[lo + i];
+            if (ok && is_border(ecc::xy_x(v), ecc::xy_y(v), g)) fb = min(fb, i);
         }
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u) {
@@ -406,14 +392,11 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
             uint32_t k[kBuildUnroll];
             int r[kBuildUnroll];
 #pragma unroll
-            for (int u = 0; u < kBuildUnroll; ++u) {  // clamped index: the loads are unconditional
+            for (int u = 0; u < kBuildUnroll; ++u) {
                 const int i = i0 + u * kThreads + tid;
-                const int64_t gi = seg_at(segs, i < total ? i : total - 1, r[u]);
-                k[u] = so.key[gi];
+                const int64_t gi = (i < total) ? seg_at(segs, i, r[u]) : 0;
+                k[u] = (i < total) ? so.key[gi] : 0xffffffffu;
             }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < kBuildUnroll; ++u) k[u] = i0 + u * kThreads + tid < total ? k[u] : 0xffffffffu;
 #pragma unroll
             for (int u = 0; u < kBuildUnroll; ++u) {
                 if (k[u] == 0xffffffffu) continue;
@@ -424,16 +407,13 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
         for (int i0 = 0; i0 < total; i0 += kBuildUnroll * kThreads) {
             uint32_t k[kBuildUnroll], tv[kBuildUnroll];
 #pragma unroll
-            for (int u = 0; u < kBuildUnroll; ++u) {  // clamped index: the loads are unconditional
+            for (int u = 0; u < kBuildUnroll; ++u) {
                 const int i = i0 + u * kThreads + tid;
                 int r_unused;
-                const int64_t gi = seg_at(segs, i < total ? i : total - 1, r_unused);
-                k[u] = so.key[gi];
-                tv[u] = gr.narrow ? so.t32[gi] : 0u;
+                const int64_t gi = (i < total) ? seg_at(segs, i, r_unused) : 0;
+                k[u] = (i < total) ? so.key[gi] : 0xffffffffu;
+                tv[u] = (i < total && gr.narrow) ? so.t32[gi] : 0u;
             }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < kBuildUnroll; ++u) k[u] = i0 + u * kThreads + tid < total ? k[u] : 0xffffffffu;
 #pragma unroll
             for (int u = 0; u < kBuildUnroll; ++u) {
                 if (k[u] == 0xffffffffu) continue;

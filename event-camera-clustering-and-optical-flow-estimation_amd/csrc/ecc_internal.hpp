@@ -92,8 +92,14 @@ __host__ __device__ inline int xy_y(uint32_t v) { return (int)(v >> 16); }
 // Raw buffer view of [p, p + bytes) (stride 0, gfx9 resource word 3): loads at or past `bytes`
 // return 0 by the hardware range check, so a wave can issue all its loads over a ragged range
 // unconditionally (a load under a per-lane condition waits for every earlier one).
+// The view must be wave-uniform (a divergent resource becomes a waterfall loop per load), so its
+// words go through readfirstlane: callers pass uniform values, the compiler need not prove it.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_view(const void *p, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint64_t ua = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(ua), (short)0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 __device__ __forceinline__ uint32_t buffer_load_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);

@@ -125,7 +125,10 @@ __device__ __forceinline__ void emit_list(const CellGrid &g, const uint32_t *cen
     // read per lane, all in flight together), then the wave takes them with readlane
     int idx = 0;
     {
-        const int r = lane >> 1, ry = cy + r - ecc::epsg::kMaxR, kx = lane < 2 * kRows ? g.kx[r] : -1;
+        const int r = lane >> 1, ry = cy + r - ecc::epsg::kMaxR;
+        int kx = -1;  // g.kx[r] by selects (a runtime index would put g.kx in scratch memory)
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) kx = r == q ? g.kx[q] : kx;
         if (kx >= 0 && ry >= 0 && ry < g.gy) {
             const int cl = ry * g.gx + max(cx - kx, 0), ch = ry * g.gx + min(cx + kx, g.gx - 1);
             idx = (lane & 1) ? ch : (cl > 0 ? cl - 1 : -1);
@@ -143,15 +146,14 @@ __device__ __forceinline__ void emit_list(const CellGrid &g, const uint32_t *cen
         pre[r + 1] = pre[r] + (hi - lo);
     }
     const int total_c = pre[kRows];
-    auto pos_of = [&](int f) {
-        int a = f + off[0];
-#pragma unroll
-        for (int r = 1; r < kRows; ++r) a = f >= pre[r] ? f + off[r] : a;
-        return a;
-    };
     for (int f = lane; f < total_c; f += 128) {
-        const int f2 = f + 64;
-        const int a0 = pos_of(f), a1 = pos_of(f2 < total_c ? f2 : f);
+        const int f2 = f + 64, f2c = f2 < total_c ? f2 : f;
+        int a0 = f + off[0], a1 = f2c + off[0];
+#pragma unroll
+        for (int r = 1; r < kRows; ++r) {
+            a0 = f >= pre[r] ? f + off[r] : a0;
+            a1 = f2c >= pre[r] ? f2c + off[r] : a1;
+        }
         const uint32_t w0 = spt[a0], w1 = spt[a1];
         const int j0 = sidx[a0], j1 = sidx[a1];
         asm volatile("" ::"v"(j0), "v"(j1));  // both index reads issued with the point reads

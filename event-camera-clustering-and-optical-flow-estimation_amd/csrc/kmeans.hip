@@ -347,24 +347,20 @@ kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__re
             ty += w & ((1ull << 26) - 1);
         }
     };
-    const bool vec_ok = (segs.stride & 3) == 0;
     for (int64_t s = blockIdx.x; s < segs.n_segs; s += gridDim.x) {
         const int64_t cnt = segs.count(s);
         const int64_t base = s * segs.stride;
         // Two 4-point batches per lane per trip: both loads and all eight label gathers are in
         // flight before the first LDS add, halving the dependent load -> gather -> add rounds.
+        // the segment through a buffer view rounded up to 16 B (inside the allocation's last 16-B
+        // block; points past cnt are masked): unconditional 16-B loads (4-B alignment suffices)
+        const __amdgpu_buffer_rsrc_t vs = ecc::buffer_view(xy + base, (uint32_t)((cnt * 4 + 15) & ~15ll));
         for (int64_t j0 = 0; j0 < cnt; j0 += 8 * kThreads) {  // uniform trip count per WG
             uint32_t v[8], lab[8];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                const int64_t j = j0 + u * 4 * kThreads + 4 * tid;
-                if (vec_ok && j + 3 < cnt) {
-                    const uint4 q = *reinterpret_cast<const uint4 *>(xy + base + j);
-                    v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[4 * u + e] = (j + e < cnt) ? xy[base + j + e] : 0u;
-                }
+                const uint4 q = ecc::buffer_load_u128(vs, (uint32_t)tid * 16u, (uint32_t)(j0 + u * 4 * kThreads) * 4u);
+                v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -454,26 +450,21 @@ kmeans_img_labels_kernel(const uint32_t *__restrict__ xy, Segs segs, const float
     }
     __syncthreads();
     const uint32_t img_w = img_wh[0], img_h = img_wh[1];
-    const bool vec_ok = (segs.stride & 3) == 0;
     for (int64_t s = blockIdx.x; s < segs.n_segs; s += gridDim.x) {
         const int64_t base = s * segs.stride;
         // readable extent: the whole stride (the next segment starts after it), except in the
         // last segment, whose buffer may end at its count
         const int64_t cnt = segs.count(s);
         const int64_t lim = s + 1 < segs.n_segs ? segs.stride : cnt;
+        const __amdgpu_buffer_rsrc_t vs = ecc::buffer_view(xy + base, (uint32_t)((lim * 4 + 15) & ~15ll));
         for (int64_t j0 = 0; j0 < cnt; j0 += kLabPer * kThreads) {
             uint32_t v[kLabPer], lab[kLabPer];
 #pragma unroll
-            for (int u = 0; u < kLabPer / 4; ++u) {
-                const int64_t j = j0 + u * 4 * kThreads + 4 * tid;
-                if (vec_ok && j + 3 < lim) {
-                    const uint4 q = *reinterpret_cast<const uint4 *>(xy + base + j);
-                    v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[4 * u + e] = (j + e < lim) ? xy[base + j + e] : 0u;
-                }
+            for (int u = 0; u < kLabPer / 4; ++u) {  // unconditional 16-B loads (see kmeans_fast_kernel)
+                const uint4 q = ecc::buffer_load_u128(vs, (uint32_t)tid * 16u, (uint32_t)(j0 + u * 4 * kThreads) * 4u);
+                v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
             }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < kLabPer / 4; ++u) {
                 const int64_t j = j0 + u * 4 * kThreads + 4 * tid;
@@ -531,9 +522,9 @@ kmeans_lds_labels_kernel(const uint32_t *__restrict__ xy, Segs segs, const float
     for (uint32_t i0 = 0; i0 < n_words; i0 += 8 * kLabLdsThreads) {
         uint32_t wv[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t i = i0 + u * kLabLdsThreads + tid, r = i / wq;
-            wv[u] = i < n_words ? *reinterpret_cast<const uint32_t *>(img + r * kImgSide + 4 * (i - r * wq)) : 0u;
+        for (int u = 0; u < 8; ++u) {  // clamped word: unconditional loads, all eight in flight
+            const uint32_t i0u = i0 + u * kLabLdsThreads + tid, i = i0u < n_words ? i0u : n_words - 1, r = i / wq;
+            wv[u] = *reinterpret_cast<const uint32_t *>(img + r * kImgSide + 4 * (i - r * wq));
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -542,26 +533,23 @@ kmeans_lds_labels_kernel(const uint32_t *__restrict__ xy, Segs segs, const float
         }
     }
     __syncthreads();
-    const bool vec_ok = (segs.stride & 3) == 0;
     for (int64_t s0 = 4 * (int64_t)blockIdx.x; s0 < segs.n_segs; s0 += 4 * (int64_t)gridDim.x) {
         const int64_t s = s0 + sub;
         if (s >= segs.n_segs) continue;  // no barrier below
         const int64_t base = s * segs.stride;
         const int64_t cnt = segs.count(s);
         const int64_t lim = s + 1 < segs.n_segs ? segs.stride : cnt;
+        // the segment through a buffer view rounded up to 16 B (inside the allocation's last 16-B
+        // block; points past cnt are masked): one unconditional 16-B load per quad
+        const __amdgpu_buffer_rsrc_t vs = ecc::buffer_view(xy + base, (uint32_t)((lim * 4 + 15) & ~15ll));
         for (int64_t j0 = 0; j0 < cnt; j0 += kLabPer * 256) {
             uint32_t v[kLabPer], lab[kLabPer];
 #pragma unroll
-            for (int u = 0; u < kLabPer / 4; ++u) {
-                const int64_t j = j0 + u * 4 * 256 + 4 * t;
-                if (vec_ok && j + 3 < lim) {
-                    const uint4 q = *reinterpret_cast<const uint4 *>(xy + base + j);
-                    v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[4 * u + e] = (j + e < lim) ? xy[base + j + e] : 0u;
-                }
+            for (int u = 0; u < kLabPer / 4; ++u) {  // (16-B buffer loads need only 4-B alignment)
+                const uint4 q = ecc::buffer_load_u128(vs, (uint32_t)t * 16u, (uint32_t)(j0 + u * 4 * 256) * 4u);
+                v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
             }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < kLabPer / 4; ++u) {
                 const int64_t j = j0 + u * 4 * 256 + 4 * t;
@@ -1085,21 +1073,33 @@ kmeans_count_kernel(const uint32_t *__restrict__ xy, Segs segs, const uint32_t *
         // trips latency-bound: 30 dependent trips per part)
         for (int64_t sg = s0; sg < s1; sg += kHistSegs) {
             int64_t cnt[kHistSegs], base[kHistSegs], cmax = 0;
+            int32_t cl[kHistSegs];  // the counts' loads together (clamped segment, no branch between)
+            if (segs.counts) {
+#pragma unroll
+                for (int i = 0; i < kHistSegs; ++i) cl[i] = segs.counts[sg + i < s1 ? sg + i : s1 - 1];
+            } else {
+#pragma unroll
+                for (int i = 0; i < kHistSegs; ++i) cl[i] = (int32_t)segs.count(sg + i);
+            }
 #pragma unroll
             for (int i = 0; i < kHistSegs; ++i) {
-                cnt[i] = sg + i < s1 ? segs.count(sg + i) : 0;
+                cnt[i] = sg + i < s1 ? cl[i] : 0;
                 base[i] = (sg + i) * segs.stride;
                 cmax = cnt[i] > cmax ? cnt[i] : cmax;
             }
+            // per segment a buffer view (0 past its count): the 16 loads are unconditional, so all
+            // of them are in flight together (a load under a per-lane condition waited for the last)
+            __amdgpu_buffer_rsrc_t vs[kHistSegs];
+#pragma unroll
+            for (int i = 0; i < kHistSegs; ++i) vs[i] = ecc::buffer_view(xy + base[i], (uint32_t)cnt[i] * 4u);
             for (int64_t j0 = 0; j0 < cmax; j0 += kHistUnroll * kHistThreads) {
                 uint32_t v[kHistSegs][kHistUnroll];
 #pragma unroll
                 for (int i = 0; i < kHistSegs; ++i)
 #pragma unroll
-                    for (int u = 0; u < kHistUnroll; ++u) {
-                        const int64_t j = j0 + u * kHistThreads + tid;
-                        v[i][u] = j < cnt[i] ? xy[base[i] + j] : 0xffffffffu;
-                    }
+                    for (int u = 0; u < kHistUnroll; ++u)
+                        v[i][u] = ecc::buffer_load_u32(vs[i], (uint32_t)tid * 4u, (uint32_t)(j0 + u * kHistThreads) * 4u);
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < kHistSegs; ++i)
 #pragma unroll

@@ -175,14 +175,20 @@ nms_compact_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ 
     const int64_t lo = s * (int64_t)S;
     const int64_t len = ((lo + S < n) ? lo + S : n) - lo;
     int run = 0;
+    // 16-B aligned slices: one unconditional 16-B load per lane through a buffer view of the
+    // slice rounded up to 16 B (the round-up stays inside the allocation's last 16-B block; bytes
+    // past len are masked) -- a per-lane choice of load form waited for every load
+    const bool vec = ((reinterpret_cast<uintptr_t>(flags) + lo) & 15) == 0;  // uniform
+    const __amdgpu_buffer_rsrc_t vf = ecc::buffer_view(flags + lo, (uint32_t)((len + 15) & ~15ll));
     for (int64_t c0 = 0; c0 < len; c0 += kCompactThreads * 16) {
         const int64_t my0 = c0 + (int64_t)tid * 16;
         uint32_t bits = 0;
-        if (my0 + 15 < len && ((lo + my0) & 15) == 0) {
-            const uint4 q = *reinterpret_cast<const uint4 *>(flags + lo + my0);
+        if (vec) {
+            const uint4 q = ecc::buffer_load_u128(vf, (uint32_t)my0);
             const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-            for (int k = 0; k < 16; ++k) bits |= (((w4[k >> 2] >> (8 * (k & 3))) & 0xffu) ? 1u : 0u) << k;
+            for (int k = 0; k < 16; ++k)
+                bits |= (((w4[k >> 2] >> (8 * (k & 3))) & 0xffu) && my0 + k < len ? 1u : 0u) << k;
         } else {
             for (int k = 0; k < 16; ++k)
                 if (my0 + k < len && flags[lo + my0 + k]) bits |= 1u << k;

@@ -157,7 +157,7 @@ def test_dbscan_cloud_duplicate_capacity_and_edge_cases(ecc, orc, gpu):
 
 @pytest.mark.parametrize("min_pts", [1, 8, 64, 65, 100, 300])
 def test_radius_f32_counts_core_lists_match_oracle(ecc, orc, gpu, min_pts):
-    pts = event_cloud(ecc, 6000, 21, 0.05, 0.45)  # up to ~220 neighbours: core points at every min_pts here
+    pts = event_cloud(ecc, 6000, 21, 0.05, 0.45)  # up to 218 neighbours: core points up to min_pts 100, none at 300
     n = len(pts)
     eps = 12.5
     o_cnt, o_core, o_off, o_nbr = orc.radius_f32(pts, eps, min_pts)
@@ -166,7 +166,9 @@ def test_radius_f32_counts_core_lists_match_oracle(ecc, orc, gpu, min_pts):
     gpu.radius_counts_f32(d_p, n, 3, eps, min_pts, d_cnt, d_core)
     assert np.array_equal(d_cnt.numpy(), o_cnt)
     assert np.array_equal(d_core.numpy().view(np.int64), o_core.view(np.int64))
-    assert (o_core >= 0).any() and np.array_equal(o_core >= 0, o_cnt >= min_pts)
+    assert np.array_equal(o_core >= 0, o_cnt >= min_pts)
+    if min_pts <= 100:  # the register network up to 64, the radix select above
+        assert (o_core >= 0).any()
     if min_pts > 1:
         assert (o_core < 0).any()
     total = int(o_off[-1])
