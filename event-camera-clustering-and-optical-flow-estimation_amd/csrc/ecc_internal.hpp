@@ -104,6 +104,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_view(const void *p, uin
 __device__ __forceinline__ uint32_t buffer_load_u32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
 }
+__device__ __forceinline__ void buffer_store_u32(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, 0);
+}
 __device__ __forceinline__ int64_t buffer_load_i64(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
     return (int64_t)(((uint64_t)v[1] << 32) | v[0]);

@@ -114,6 +114,7 @@ _sigs = {
     "ecc_memcpy_d2h": (C.c_int, [P, P, C.c_size_t, P]),
     "ecc_memcpy_d2d": (C.c_int, [P, P, C.c_size_t, P]),
     "ecc_stream_create": (C.c_int, [C.POINTER(P)]),
+    "ecc_stream_create_priority": (C.c_int, [C.POINTER(P), C.c_int32]),
     "ecc_stream_destroy": (C.c_int, [P]),
     "ecc_event_create": (C.c_int, [C.POINTER(P)]),
     "ecc_event_destroy": (C.c_int, [P]),
