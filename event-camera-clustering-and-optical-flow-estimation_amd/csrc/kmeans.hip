@@ -22,6 +22,10 @@
 // Algorithmic bytes: 4 B/point/iteration (packed u16 xy) + 1 B/point for the final labels.
 #include "ecc_internal.hpp"
 
+#ifndef ECC_KM_ACC_SUB
+#define ECC_KM_ACC_SUB 1
+#endif
+
 #include <cmath>
 
 namespace {
@@ -752,6 +756,290 @@ kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__
     }
 }
 
+// ---- candidate table for the vector engine (k <= 32, 16-B aligned points) ---------------------
+// Each Lloyd pass labels every point by the first centre of smallest sqrt_rn(d2); with k = 16
+// that is ~105 VALU per point in the screen above, and the pass is VALU-bound (r03j counters:
+// 84 M VALU wave-instructions for 50 M points, 71 % busy).  Here a 64 x 64 grid of square cells
+// over the points' bounding box holds, per cell and pass, the centres that can win ANYWHERE in
+// the cell (computed in fp64 by the update kernel right after the centres move):
+//   candidate i  <=>  dmin2_i(cell) <= min_j dmax2_j(cell) * (1 + 2^-12) + 1e-30,
+// the cell grown by cs * 2^-12 on each side (covers the fp32 cell-index rounding, < cs * 2^-16).
+// A non-candidate's fp32 d2 then exceeds the winner's by more than 2^-13 relative, beyond the
+// fp32 rounding of d2 (< 2^-21) and assign_fast's 2^-20 square-root tie band: it can neither win
+// nor make the tie test fire, so testing the (at most 3) candidates in ascending index with
+// assign_fast's own steps gives assign_fast's label.  A cell whose every point lies beyond the
+// threshold (dmin2 > thr2 (1 + 2^-12) for all centres) is flagged 255.  More than 3 candidates,
+// a point outside the grid (or NaN), or a tie-band hit take assign_fast itself.  The bounding box
+// comes from a 64 K-point sample (points outside it are only slower, never wrong).
+constexpr int kLutSide = 64;
+constexpr int kLutCells = kLutSide * kLutSide;
+constexpr int kLutBlocks = kLutCells / kThreads;
+constexpr int kBoxBlocks = 64, kBoxPerThread = 4;
+constexpr uint32_t kLutFar = 1u << 30, kLutFull = 1u << 31;
+
+struct LutGeom {
+    float x0, y0, inv_cs, fgx, fgy, cs;
+    int32_t gx, gy, ok, pad[7];
+};
+static_assert(sizeof(LutGeom) == 64, "LutGeom is one 64-B record");
+
+// float -> u32 with the same order (so u32 atomic max gives float max; max of ~u gives the min)
+__device__ __forceinline__ uint32_t ordered_u32(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float from_ordered(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// box[4 b + 0..3] = workgroup b's max ord(x), max ~ord(x), max ord(y), max ~ord(y) over its finite
+// sampled points (0 = none); kmeans_update_lut_kernel reduces the kBoxBlocks records.  (One u32
+// atomic max per wave into a single record measured 15 us: 1024 same-address atomics.)
+__global__ void __launch_bounds__(kThreads)
+kmeans_bbox_sample_kernel(const float2 *__restrict__ xy, int64_t n, uint32_t *__restrict__ box) {
+    constexpr int64_t kSamples = (int64_t)kBoxBlocks * kThreads * kBoxPerThread;
+    __shared__ uint32_t s_r[kThreads / 64][4];
+    const int64_t step = n > kSamples ? n / kSamples : 1;
+    const int tid = threadIdx.x;
+    float2 p[kBoxPerThread + 1];
+#pragma unroll
+    for (int u = 0; u < kBoxPerThread; ++u) {
+        const int64_t j = (((int64_t)blockIdx.x * kThreads + tid) * kBoxPerThread + u) * step;
+        p[u] = xy[j < n ? j : n - 1];
+    }
+    p[kBoxPerThread] = xy[n - 1];  // the last point too
+    uint32_t r[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int u = 0; u <= kBoxPerThread; ++u) {
+        if (__builtin_isfinite(p[u].x) && __builtin_isfinite(p[u].y)) {
+            const uint32_t ox = ordered_u32(p[u].x), oy = ordered_u32(p[u].y);
+            r[0] = max(r[0], ox);
+            r[1] = max(r[1], ~ox);
+            r[2] = max(r[2], oy);
+            r[3] = max(r[3], ~oy);
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) r[f] = max(r[f], (uint32_t)__shfl_xor((int)r[f], o));
+    }
+    if ((tid & 63) == 0)
+        for (int f = 0; f < 4; ++f) s_r[tid >> 6][f] = r[f];
+    __syncthreads();
+    if (tid < 4) {
+        uint32_t v = 0u;
+        for (int w = 0; w < kThreads / 64; ++w) v = max(v, s_r[w][tid]);
+        box[4 * blockIdx.x + tid] = v;
+    }
+}
+
+// The grid over the sampled box (deterministic: every launch derives the same record).
+__device__ inline LutGeom lut_geometry(const uint32_t (&box)[4]) {
+    LutGeom g{};
+    g.ok = 0;
+    if (box[0] == 0u) return g;
+    const float xmax = from_ordered(box[0]), xmin = from_ordered(~box[1]);
+    const float ymax = from_ordered(box[2]), ymin = from_ordered(~box[3]);
+    const double mag = fmax(fmax(fabs((double)xmin), fabs((double)xmax)), fmax(fabs((double)ymin), fabs((double)ymax)));
+    if (!(mag < 1e18)) return g;  // keeps every candidate's fp32 d2 finite
+    const double w = (double)xmax - xmin, h = (double)ymax - ymin;
+    double cs = fmax(w, h) / kLutSide * (1.0 + 0x1p-10);
+    cs = fmax(cs, fmax(mag * 0x1p-20, 1e-12));
+    g.cs = (float)cs;
+    g.inv_cs = __fdiv_rn(1.0f, g.cs);
+    g.gx = min(kLutSide, (int)(w / (double)g.cs) + 1);
+    g.gy = min(kLutSide, (int)(h / (double)g.cs) + 1);
+    g.x0 = xmin;
+    g.y0 = ymin;
+    g.fgx = (float)g.gx;
+    g.fgy = (float)g.gy;
+    g.ok = 1;
+    return g;
+}
+
+// One cell's entry: candidate indices in bits 0-4, 5-9, 10-14 (ascending, padded with the last),
+// kLutFar when no point of the cell can be within the threshold, kLutFull past 3 candidates.
+__device__ inline uint32_t lut_entry(int ix, int iy, const LutGeom &g, const float2 *__restrict__ s_c, int k,
+                                     float thr2) {
+    const double cs = g.cs, e = cs * 0x1p-12;
+    const double x0 = (double)g.x0 + ix * cs - e, x1 = (double)g.x0 + (ix + 1) * cs + e;
+    const double y0 = (double)g.y0 + iy * cs - e, y1 = (double)g.y0 + (iy + 1) * cs + e;
+    auto dmin2 = [&](float2 c) {
+        const double dx = fmax(fmax(x0 - c.x, c.x - x1), 0.0), dy = fmax(fmax(y0 - c.y, c.y - y1), 0.0);
+        return dx * dx + dy * dy;
+    };
+    double best = __builtin_inf(), near = __builtin_inf();
+    for (int i = 0; i < k; ++i) {
+        const float2 c = s_c[i];
+        const double dx = fmax(fabs(c.x - x0), fabs(c.x - x1)), dy = fmax(fabs(c.y - y0), fabs(c.y - y1));
+        best = fmin(best, dx * dx + dy * dy);
+        near = fmin(near, dmin2(c));
+    }
+    const double bound = best * (1.0 + 0x1p-12) + 1e-30;
+    uint32_t ent = 0u;
+    int cnt = 0, last = 0;
+    for (int i = 0; i < k; ++i) {
+        if (dmin2(s_c[i]) <= bound) {
+            if (cnt < 3) ent |= (uint32_t)i << (5 * cnt);
+            last = i;
+            ++cnt;
+        }
+    }
+    // every point beyond the threshold: 255 whatever the candidates (far from all centres, many
+    // of them are nearly equidistant, so such cells would otherwise overflow)
+    if (near > (double)thr2 * (1.0 + 0x1p-12) + 1e-30) return kLutFar;
+    if (cnt == 0 || cnt > 3) ent |= kLutFull;  // (none: non-finite centres) -> assign_fast
+    for (int j = cnt; j < 3; ++j) ent |= (uint32_t)last << (5 * j);
+    return ent;
+}
+
+// Centroid update fused with the candidate table.  kLutBlocks workgroups each sum the replicas
+// (the same fp64 arithmetic as kmeans_update_kernel), keep the new centres in LDS and build 256
+// cells; workgroup 0 writes the centres and the state.  Accumulators ping-pong between two sets:
+// this launch reads acc_rd and zeroes acc_zero (read by the previous update), so no workgroup
+// zeroes what another still reads.  iter < 0: table for the current centres only (before pass 0;
+// also writes the grid record).  st->done holds iter + 1 of the converging update, so workgroups
+// of that same launch still build its table.
+__global__ void __launch_bounds__(kThreads)
+kmeans_update_lut_kernel(const double *__restrict__ acc_rd, double *__restrict__ acc_zero, int n_copies,
+                         float *__restrict__ cent, int k, float tol, KmState *__restrict__ st, int iter,
+                         const uint32_t *__restrict__ box, LutGeom *__restrict__ geom, uint32_t *__restrict__ lut,
+                         float thr2) {
+    if (iter >= 0) {
+        const int d = __builtin_amdgcn_readfirstlane(st->done);
+        if (d != 0 && d <= iter) return;
+    }
+    __shared__ float2 s_c[kFastMaxK];
+    __shared__ LutGeom s_g;
+    const int tid = threadIdx.x;
+    if (tid >= 64 && tid < 128) {  // wave 1: the grid record (reduced from the samples before pass 0)
+        if (iter < 0) {
+            const int l = tid - 64;
+            uint32_t r[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                r[f] = l < kBoxBlocks ? box[4 * l + f] : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) r[f] = max(r[f], (uint32_t)__shfl_xor((int)r[f], o));
+            }
+            if (l == 0) {
+                s_g = lut_geometry(r);
+                if (blockIdx.x == 0) *geom = s_g;
+            }
+        } else if (tid == 64) {
+            s_g = *geom;
+        }
+    }
+    if (iter >= 0) {
+        const int z = blockIdx.x * kThreads + tid;
+        if (z < n_copies * kAccStride) acc_zero[z] = 0.0;
+    }
+    if (tid < 64) {  // wave 0: centres (k <= 32 lanes) and, in workgroup 0, the state
+        float shift = 0.f;
+        if (tid < k) {
+            const float ox = cent[2 * tid], oy = cent[2 * tid + 1];
+            float nx = ox, ny = oy;
+            if (iter >= 0) {
+                double a[3] = {0.0, 0.0, 0.0}, v[kAccCopies][3];
+#pragma unroll
+                for (int r = 0; r < kAccCopies; ++r)
+#pragma unroll
+                    for (int f = 0; f < 3; ++f) v[r][f] = r < n_copies ? acc_rd[r * kAccStride + 3 * tid + f] : 0.0;
+#pragma unroll
+                for (int r = 0; r < kAccCopies; ++r)
+#pragma unroll
+                    for (int f = 0; f < 3; ++f) a[f] += v[r][f];
+                if (a[0] > 0.0) {
+                    nx = (float)(a[1] / a[0]);
+                    ny = (float)(a[2] / a[0]);
+                    shift = fmaxf(fabsf(nx - ox), fabsf(ny - oy));
+                    if (blockIdx.x == 0) {
+                        cent[2 * tid] = nx;
+                        cent[2 * tid + 1] = ny;
+                    }
+                }
+            }
+            s_c[tid] = make_float2(nx, ny);
+        }
+        if (iter >= 0 && blockIdx.x == 0) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) shift = fmaxf(shift, __shfl_xor(shift, o));
+            if (tid == 0) {
+                st->iters += 1;
+                if (tol >= 0.f && shift <= tol) st->done = iter + 1;
+            }
+        }
+    }
+    __syncthreads();
+    const LutGeom g = s_g;
+    if (!g.ok) return;
+    const int c = blockIdx.x * kThreads + tid;
+    if (c < g.gx * g.gy) lut[c] = lut_entry(c % g.gx, c / g.gx, g, s_c, k, thr2);
+}
+
+// What the assignment kernels need of the grid record.
+struct LutView {
+    float x0, y0, inv_cs, fgx, fgy, fmx, fmy;  // fmx, fmy: the last cell index as float
+    int32_t gx;
+};
+
+// assign_fast's steps with the centres read from LDS (the table kernels keep no centres in
+// registers; this is their rare fallback)
+template <int K>
+__device__ __forceinline__ uint32_t assign_lds2(float px, float py, const float2 *__restrict__ s_c, float thr) {
+    float m = __builtin_inff(), m_prev = __builtin_inff();
+    int ia = 0;
+#pragma unroll 4
+    for (int i = 0; i < K; ++i) {
+        const float2 c = s_c[i];
+        const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
+        const float d2 = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+        const bool lt = d2 < m;
+        m_prev = lt ? m : m_prev;
+        ia = lt ? i : ia;
+        m = lt ? d2 : m;
+    }
+    if (m_prev <= __fmul_rn(m, 1.0f + 0x1p-20f)) {
+        uint32_t best = 255u;
+        float best_s = thr;
+        for (int i = 0; i < K; ++i) {
+            const float2 c = s_c[i];
+            const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
+            const float sd = ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
+            if (sd < best_s) { best_s = sd; best = (uint32_t)i; }
+        }
+        return best;
+    }
+    return ecc::sqrt_rn(m) < thr ? (uint32_t)ia : 255u;
+}
+
+// One point through the table: assign_fast's steps over the cell's 3 candidate slots.  full =
+// the caller must take assign_fast (outside the grid, > 3 candidates, or a tie-band hit).
+__device__ __forceinline__ uint32_t lut_point(float px, float py, const LutView &g, const uint32_t *__restrict__ s_lut,
+                                              const float2 *__restrict__ s_c, float thr2, bool &full) {
+    const float tx = __fmul_rn(__fsub_rn(px, g.x0), g.inv_cs), ty = __fmul_rn(__fsub_rn(py, g.y0), g.inv_cs);
+    const bool inside = (tx >= 0.f) & (tx < g.fgx) & (ty >= 0.f) & (ty < g.fgy);
+    const int ix = (int)fminf(fmaxf(tx, 0.f), g.fmx), iy = (int)fminf(fmaxf(ty, 0.f), g.fmy);
+    const uint32_t e = s_lut[iy * g.gx + ix];
+    float m = __builtin_inff(), m_prev = __builtin_inff();
+    uint32_t ia = 0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const uint32_t i = (e >> (5 * j)) & 31u;
+        const float2 c = s_c[i];
+        const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
+        const float d2 = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+        const bool lt = d2 < m;
+        m_prev = lt ? m : m_prev;
+        ia = lt ? i : ia;
+        m = lt ? d2 : m;
+    }
+    const bool far = (e & kLutFar) != 0u;
+    full = !inside || (!far && ((e & kLutFull) != 0u || m_prev <= __fmul_rn(m, 1.0f + 0x1p-20f)));
+    return (!far && m < thr2) ? ia : 255u;
+}
+
 // Vector engine, streaming form: a lane takes two consecutive points per 16-B load (the pair the
 // packed screen tests together), kPairUnroll such loads per trip, and the NEXT trip's loads are
 // issued before this trip's tests, so a wave keeps 2 x kPairUnroll x 16 B in flight across its
@@ -760,34 +1048,68 @@ kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__
 // aligned); an odd last point is taken by lane 0 of workgroup 0.
 constexpr int kPairUnroll = 4;
 
-template <int K, bool kAccumulate>
+template <int K, bool kAccumulate, bool kLut>
 __global__ void __launch_bounds__(kThreads)
 kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *__restrict__ cent, int k, float thr,
                        float thr2, double *__restrict__ acc, int n_copies, const KmState *__restrict__ st,
-                       uint8_t *__restrict__ labels) {
+                       uint8_t *__restrict__ labels, const LutGeom *__restrict__ geom,
+                       const uint32_t *__restrict__ lut) {
     if (kAccumulate && st->done) return;
-    __shared__ uint32_t s_n[kWaves][K];
-    __shared__ double s_sx[kWaves][K], s_sy[kWaves][K];
+    // accumulator slots per wave, kSub copies (lane % kSub) to spread same-address LDS atomics
+    constexpr int kSub = ECC_KM_ACC_SUB;
+    __shared__ uint32_t s_n[kWaves * kSub][K];
+    __shared__ double s_sx[kWaves * kSub][K], s_sy[kWaves * kSub][K];
     __shared__ float2 s_c[K];
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[kLut ? kLutCells : 4];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    float cx[K], cy[K];
+    // The grid record as scalars (a struct copy of the 64-B record went to the stack).  Without a
+    // grid (non-finite or huge box) every point is outside: fgx = 0, one cell, assign_lds2.
+    LutView g{};
+    if constexpr (kLut) {
+        const bool ok = geom->ok != 0;
+        g.x0 = geom->x0;
+        g.y0 = geom->y0;
+        g.inv_cs = geom->inv_cs;
+        g.fgx = ok ? geom->fgx : 0.f;
+        g.fgy = ok ? geom->fgy : 0.f;
+        g.fmx = ok ? geom->fgx - 1.f : 0.f;
+        g.fmy = ok ? geom->fgy - 1.f : 0.f;
+        g.gx = ok ? geom->gx : 1;
+        // the table into LDS: all of a lane's 16-B loads in flight at once (a strided word loop
+        // paid one L2 round trip per word, at the start of every workgroup)
+        const __amdgpu_buffer_rsrc_t v = ecc::buffer_view(lut, ok ? (uint32_t)(g.gx * geom->gy) * 4u : 0u);
+        uint4 q[kLutCells / (4 * kThreads)];
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
-        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+        for (int u = 0; u < kLutCells / (4 * kThreads); ++u)
+            q[u] = ecc::buffer_load_u128(v, (uint32_t)tid * 16u, (uint32_t)(u * kThreads * 16));
+#pragma unroll
+        for (int u = 0; u < kLutCells / (4 * kThreads); ++u)
+            reinterpret_cast<uint4 *>(s_lut)[u * kThreads + tid] = q[u];
+        if (!ok && tid == 0) s_lut[0] = kLutFull;
+    }
+    float cx[K], cy[K];  // the screen's centres in scalar registers (not with the table)
+    if constexpr (!kLut) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
+            cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+        }
     }
     if (tid < K) s_c[tid] = make_float2(tid < k ? cent[2 * tid] : 1e30f, tid < k ? cent[2 * tid + 1] : 1e30f);
     if (kAccumulate && lane < K) {
-        s_n[wave][lane] = 0u;
-        s_sx[wave][lane] = 0.0;
-        s_sy[wave][lane] = 0.0;
+        for (int b = 0; b < kSub; ++b) {
+            s_n[wave * kSub + b][lane] = 0u;
+            s_sx[wave * kSub + b][lane] = 0.0;
+            s_sy[wave * kSub + b][lane] = 0.0;
+        }
     }
+    const int slot = wave * kSub + lane % kSub;
     __syncthreads();
-    auto account = [&](float2 q, uint32_t l) {
+    auto account = [&](float2 q, uint32_t l) __attribute__((always_inline)) {
         if (kAccumulate && l < (uint32_t)K) {
-            atomicAdd(&s_n[wave][l], 1u);
-            atomicAdd(&s_sx[wave][l], (double)q.x);
-            atomicAdd(&s_sy[wave][l], (double)q.y);
+            atomicAdd(&s_n[slot][l], 1u);
+            atomicAdd(&s_sx[slot][l], (double)q.x);
+            atomicAdd(&s_sy[slot][l], (double)q.y);
         }
     };
     const int64_t npair = n / 2;
@@ -796,7 +1118,7 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     const int64_t span = stride * kPairUnroll;
     // a trip's loads through a buffer view based at its first pair: unconditional (0 past the
     // last pair), one VGPR of lane offset for all of them, the u part in the scalar offset
-    auto load = [&](int64_t b0, float4 (&q)[kPairUnroll]) {
+    auto load = [&](int64_t b0, float4 (&q)[kPairUnroll]) __attribute__((always_inline)) {
         const int64_t first = b0 * 64 < npair ? b0 * 64 : npair;
         const int64_t rem = (npair - first) * 16;
         const __amdgpu_buffer_rsrc_t v = ecc::buffer_view(xy4 + first, rem < 0xffffffffll ? (uint32_t)rem : 0xffffffffu);
@@ -806,7 +1128,7 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
             q[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
         }
     };
-    auto test = [&](int64_t b0, const float4 (&q)[kPairUnroll]) {
+    auto test = [&](int64_t b0, const float4 (&q)[kPairUnroll]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < kPairUnroll; ++u) {
             const int64_t blk = b0 + u * stride;
@@ -814,7 +1136,20 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
             const int64_t pp = blk * 64 + lane;
             const float2 p0 = make_float2(q[u].x, q[u].y), p1 = make_float2(q[u].z, q[u].w);
             uint32_t l0, l1;
-            assign_pair<K>(p0, p1, cx, cy, s_c, thr, thr2, l0, l1);
+            if constexpr (kLut) {
+                bool f0, f1;
+                l0 = lut_point(p0.x, p0.y, g, s_lut, s_c, thr2, f0);
+                l1 = lut_point(p1.x, p1.y, g, s_lut, s_c, thr2, f1);
+                // one fallback round for the wave when no lane needs both of its points
+                while (f0 | f1) {
+                    const float qx = f0 ? p0.x : p1.x, qy = f0 ? p0.y : p1.y;
+                    const uint32_t l = assign_lds2<K>(qx, qy, s_c, thr);
+                    if (f0) { l0 = l; f0 = false; }
+                    else { l1 = l; f1 = false; }
+                }
+            } else {
+                assign_pair<K>(p0, p1, cx, cy, s_c, thr, thr2, l0, l1);
+            }
             if (pp < npair) {
                 if (labels) reinterpret_cast<uint16_t *>(labels)[pp] = (uint16_t)(l0 | l1 << 8);
                 account(p0, l0);
@@ -842,7 +1177,9 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     }
     if ((n & 1) && blockIdx.x == 0 && tid == 0) {  // the odd last point
         const float2 q = reinterpret_cast<const float2 *>(xy4)[n - 1];
-        const uint32_t l = assign_fast<K>(q.x, q.y, cx, cy, thr);
+        uint32_t l;
+        if constexpr (kLut) l = assign_lds2<K>(q.x, q.y, s_c, thr);
+        else l = assign_fast<K>(q.x, q.y, cx, cy, thr);
         if (labels) labels[n - 1] = (uint8_t)l;
         account(q, l);
     }
@@ -852,7 +1189,7 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
         const int f = tid / k, c = tid - f * k;
         double v = 0.0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) v += f == 0 ? (double)s_n[w][c] : (f == 1 ? s_sx[w][c] : s_sy[w][c]);
+        for (int w = 0; w < kWaves * kSub; ++w) v += f == 0 ? (double)s_n[w][c] : (f == 1 ? s_sx[w][c] : s_sy[w][c]);
         if (v != 0.0) atomicAdd(&acc[(int)(blockIdx.x % n_copies) * kAccStride + 3 * c + f], v);
     }
 }
@@ -876,7 +1213,8 @@ inline float sqrt_threshold(float thr) {
 
 template <bool kAccumulate>
 bool launch_f32_fast(int k, int method, dim3 grid, hipStream_t s, const float *xy, int64_t n, const float *cent,
-                     float thr, double *acc, int n_copies, const KmState *st, uint8_t *labels) {
+                     float thr, double *acc, int n_copies, const KmState *st, uint8_t *labels,
+                     const LutGeom *geom = nullptr, const uint32_t *lut = nullptr) {
     const float thr2 = sqrt_threshold(thr);
     if (k > kFastMaxK) return false;
     const float2 *p = reinterpret_cast<const float2 *>(xy);
@@ -888,12 +1226,17 @@ bool launch_f32_fast(int k, int method, dim3 grid, hipStream_t s, const float *x
         else ECC_F32_LAUNCH(32, true);
     } else if ((reinterpret_cast<uintptr_t>(xy) & 15) == 0 && (reinterpret_cast<uintptr_t>(labels) & 1) == 0) {  // 16-B loads of point pairs
         const float4 *p4 = reinterpret_cast<const float4 *>(xy);
-        if (k <= 16)
-            hipLaunchKernelGGL((kmeans_f32_pair_kernel<16, kAccumulate>), grid, dim3(kThreads), 0, s, p4, n, cent, k,
-                               thr, thr2, acc, n_copies, st, labels);
-        else
-            hipLaunchKernelGGL((kmeans_f32_pair_kernel<32, kAccumulate>), grid, dim3(kThreads), 0, s, p4, n, cent, k,
-                               thr, thr2, acc, n_copies, st, labels);
+#define ECC_PAIR_LAUNCH(KK, LUT)                                                                                 \
+    hipLaunchKernelGGL((kmeans_f32_pair_kernel<KK, kAccumulate, LUT>), grid, dim3(kThreads), 0, s, p4, n, cent, k, \
+                       thr, thr2, acc, n_copies, st, labels, geom, lut)
+        if (geom) {
+            if (k <= 16) ECC_PAIR_LAUNCH(16, true);
+            else ECC_PAIR_LAUNCH(32, true);
+        } else {
+            if (k <= 16) ECC_PAIR_LAUNCH(16, false);
+            else ECC_PAIR_LAUNCH(32, false);
+        }
+#undef ECC_PAIR_LAUNCH
     } else {
         if (k <= 16) ECC_F32_LAUNCH(16, false);
         else ECC_F32_LAUNCH(32, false);
@@ -1527,18 +1870,69 @@ static int kmeans_run_f32_impl(ecc_ctx *ctx, const float *xy, int64_t n_points, 
     if ((reinterpret_cast<uintptr_t>(xy) & 7) != 0) return ECC_ERR_INVALID;  // float2 loads
     const bool fast = cfg->k <= kFastMaxK;
     const int n_copies = fast ? kAccCopies : 1;
+    const int eng = method == 0 ? 1 : method;  // auto = the vector engine (measured faster, DESIGN.md §5)
+    // the vector engine's pair kernel (16-B aligned points) runs on the candidate table
+    const bool use_lut = fast && eng == 1 && n_points > 0 && (reinterpret_cast<uintptr_t>(xy) & 15) == 0;
     const size_t acc_bytes = (size_t)n_copies * kAccStride * 8;
-    rc = ecc::ws_reserve(ctx, acc_bytes + 64);
+    // workspace: accumulator set 0 | set 1 (the table path ping-pongs) | state | box | grid | table
+    const size_t st_off = 2 * acc_bytes, box_off = st_off + 64, geom_off = box_off + 16 * kBoxBlocks, lut_off = geom_off + 64;
+    const size_t ws_bytes = lut_off + (size_t)kLutCells * 4;
+    rc = ecc::ws_reserve(ctx, ws_bytes);
     if (rc) return rc;
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t s = ecc::as_stream(stream);
-    auto *acc = reinterpret_cast<double *>(ctx->ws);
-    auto *st = reinterpret_cast<KmState *>(reinterpret_cast<char *>(ctx->ws) + acc_bytes);
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, acc_bytes + 64, s), "memset(kmeans acc)");
-    const int eng = method == 0 ? 1 : method;  // auto = the vector engine (measured faster, DESIGN.md §5)
+    char *ws = reinterpret_cast<char *>(ctx->ws);
+    auto *acc = reinterpret_cast<double *>(ws);
+    auto *st = reinterpret_cast<KmState *>(ws + st_off);
+    auto *box = reinterpret_cast<uint32_t *>(ws + box_off);
+    auto *geom = reinterpret_cast<LutGeom *>(ws + geom_off);
+    auto *lut = reinterpret_cast<uint32_t *>(ws + lut_off);
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, box_off, s), "memset(kmeans acc)");
     const char *name = eng == 2 ? "kmeans_f32_mfma_kernel" : "kmeans_f32_vec_kernel";
     const int grid = fast ? (int)std::max<int64_t>(1, std::min<int64_t>((n_points + 255) / 256, 4096))
                           : grid_for((n_points + kThreads - 1) / kThreads);
+    const float thr2 = sqrt_threshold(cfg->threshold);
+    if (use_lut) {
+        {
+            ECC_TIMED(ctx, s, "kmeans_bbox_sample_kernel");
+            hipLaunchKernelGGL(kmeans_bbox_sample_kernel, dim3(kBoxBlocks), dim3(kThreads), 0, s,
+                               reinterpret_cast<const float2 *>(xy), n_points, box);
+        }
+        {
+            ECC_TIMED(ctx, s, "kmeans_update_lut_kernel");
+            hipLaunchKernelGGL(kmeans_update_lut_kernel, dim3(kLutBlocks), dim3(kThreads), 0, s, acc, acc, n_copies,
+                               centroids, cfg->k, cfg->tol, st, -1, box, geom, lut, thr2);
+        }
+        // one round of resident workgroups (4 per CU at <= 128 VGPRs): each loads the table once
+        const int lgrid = (int)std::max<int64_t>(1, std::min<int64_t>((n_points + 255) / 256, 4 * ctx->n_cu));
+        for (int it = 0; it < cfg->max_iters; ++it) {
+            double *acc_it = acc + (size_t)(it & 1) * n_copies * kAccStride;
+            double *acc_next = acc + (size_t)((it + 1) & 1) * n_copies * kAccStride;
+            {
+                ECC_TIMED(ctx, s, name);
+                launch_f32_fast<true>(cfg->k, eng, dim3(lgrid), s, xy, n_points, centroids, cfg->threshold, acc_it,
+                                      n_copies, st, nullptr, geom, lut);
+            }
+            {
+                ECC_TIMED(ctx, s, "kmeans_update_lut_kernel");
+                hipLaunchKernelGGL(kmeans_update_lut_kernel, dim3(kLutBlocks), dim3(kThreads), 0, s, acc_it,
+                                   acc_next, n_copies, centroids, cfg->k, cfg->tol, st, it, box, geom, lut, thr2);
+            }
+        }
+        ECC_CHECK_LAUNCH(ctx, "kmeans_f32 iteration");
+        if (labels) {
+            {
+                ECC_TIMED(ctx, s, "kmeans_f32_labels");
+                const bool lab_ok = (reinterpret_cast<uintptr_t>(labels) & 1) == 0;
+                launch_f32_fast<false>(cfg->k, eng, dim3(lab_ok ? lgrid : grid), s, xy, n_points, centroids, cfg->threshold, nullptr,
+                                       1, st, labels, lab_ok ? geom : nullptr, lut);
+            }
+            ECC_CHECK_LAUNCH(ctx, "kmeans_f32 labels");
+        }
+        if (iters_out)
+            ECC_CHECK_HIP(ctx, hipMemcpyAsync(iters_out, &st->iters, 4, hipMemcpyDeviceToDevice, s), "copy iters");
+        return ECC_OK;
+    }
     for (int it = 0; it < cfg->max_iters && n_points > 0; ++it) {
         {
             ECC_TIMED(ctx, s, fast ? name : "kmeans_f32_kernel");

@@ -294,6 +294,57 @@ def test_kmeans_f32_threshold_and_tie_boundaries_ulps(ecc, orc, gpu, engine):
     assert (d_lab.numpy() == o).all()
 
 
+@pytest.mark.parametrize("case", ["stacked", "outliers", "tiny", "far", "converge"])
+def test_kmeans_f32_candidate_table_edges(ecc, orc, gpu, case):
+    """The vector engine's candidate table (64 x 64 cells over a sampled bounding box, <= 3
+    candidates per cell): labels and centroids equal the oracle's where the table's cases meet —
+    five coinciding centres (cells with > 3 candidates), a few points far outside the sampled box
+    plus NaN / inf points, a sub-pixel extent (the minimum cell size), every cell beyond the
+    threshold, and a run that converges on tol (the table of the converging update is the one the
+    labels use)."""
+    rng = np.random.default_rng({"stacked": 1, "outliers": 2, "tiny": 3, "far": 4, "converge": 5}[case])
+    n = 400_000
+    pts = np.floor(rng.uniform(0, 346, (n, 2))).astype(np.float32)
+    c0 = _init_centroids(16, seed=21, w=346, h=260)
+    iters, tol, thr, exact = 4, -1.0, 50.0, True
+    if case == "stacked":
+        c0.reshape(-1, 2)[3:8] = [120.0, 90.0]  # five centres on one point: > 3 candidates nearby
+        c0.reshape(-1, 2)[8:10] = [121.0, 90.0]
+    elif case == "outliers":
+        pts[rng.integers(0, n, 40)] = rng.uniform(-3e4, 3e4, (40, 2))
+    elif case == "tiny":
+        pts = (100.0 + rng.uniform(0, 1e-3, (n, 2))).astype(np.float32)
+        c0 = (100.0 + rng.uniform(0, 1e-3, (16, 2))).astype(np.float32).ravel()
+        exact = False
+    elif case == "far":
+        thr = 0.25  # most cells hold no point within the threshold of any centre
+    else:
+        iters, tol = 40, 0.05
+    flat = pts.ravel()
+    o_c, o_lab, o_it = orc.kmeans_run_f32(flat, c0, iters, thr, tol)
+    d_c, d_lab, d_it = dev(ecc, c0), ecc.DeviceArray(n, np.uint8), ecc.DeviceArray(1, np.int32)
+    gpu.kmeans_f32_engine(dev(ecc, flat), n, d_c, ecc.kmeans_cfg(k=16, max_iters=iters, tol=tol, threshold=thr), 1,
+                          d_lab, d_it)
+    gpu.sync()
+    assert d_it.numpy()[0] == o_it
+    if exact:  # integer-valued points: fp64 sums exact, centroids bit-equal
+        assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32))
+        assert (d_lab.numpy() == o_lab).all()
+    else:
+        assert np.allclose(d_c.numpy(), o_c, atol=1e-6, rtol=0)
+        assert (d_lab.numpy() != o_lab).mean() < 1e-4
+    # labels of non-finite points with the final centres (labels-only pass, max_iters 0)
+    bad = pts[:1000].copy()
+    bad[::7, 0] = np.nan
+    bad[1::7, 1] = np.inf
+    bad[2::7] = -np.inf
+    d_lab2 = ecc.DeviceArray(len(bad), np.uint8)
+    gpu.kmeans_f32_engine(dev(ecc, bad.ravel()), len(bad), d_c, ecc.kmeans_cfg(k=16, max_iters=0, threshold=thr), 1,
+                          d_lab2)
+    gpu.sync()
+    assert (d_lab2.numpy() == orc.kmeans_assign_f32(bad.ravel(), d_c.numpy(), thr)).all()
+
+
 # ------------------------------------------------------------------------------ SAE + arc corners
 def _fast_gpu(ecc, gpu, xy, t, W, H, border_mode=0, first_detect=1, sae0=None, slice_events=16384):
     cfg = ecc.corner_cfg(width=W, height=H, border_mode=border_mode, first_detect_slice=first_detect,
