@@ -23,7 +23,7 @@
 #include "ecc_internal.hpp"
 
 #ifndef ECC_KM_ACC_SUB
-#define ECC_KM_ACC_SUB 1
+#define ECC_KM_ACC_SUB 4
 #endif
 
 #include <cmath>
@@ -768,14 +768,22 @@ kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__
 // fp32 rounding of d2 (< 2^-21) and assign_fast's 2^-20 square-root tie band: it can neither win
 // nor make the tie test fire, so testing the (at most 3) candidates in ascending index with
 // assign_fast's own steps gives assign_fast's label.  A cell whose every point lies beyond the
-// threshold (dmin2 > thr2 (1 + 2^-12) for all centres) is flagged 255.  More than 3 candidates,
-// a point outside the grid (or NaN), or a tie-band hit take assign_fast itself.  The bounding box
-// comes from a 64 K-point sample (points outside it are only slower, never wrong).
+// threshold (dmin2 > thr2 (1 + 2^-12) for all centres) names a NaN sentinel centre three times
+// (d2 NaN: no tie, label 255); more than 3 candidates name an infinite one (d2 = inf: the tie
+// test fires).  A point outside the grid (or NaN) and a tie-band hit take assign_fast's steps over
+// all centres.  The bounding box comes from a 64 K-point sample (points outside it are only
+// slower, never wrong).  An entry holds the three candidates' BYTE offsets into the kernels' LDS
+// centre table (10 bits each), so the lookup needs no shifts.
 constexpr int kLutSide = 64;
 constexpr int kLutCells = kLutSide * kLutSide;
 constexpr int kLutBlocks = kLutCells / kThreads;
 constexpr int kBoxBlocks = 64, kBoxPerThread = 4;
-constexpr uint32_t kLutFar = 1u << 30, kLutFull = 1u << 31;
+constexpr int kLutInf = kFastMaxK, kLutNan = kFastMaxK + 1;  // sentinel slots of the centre table
+__host__ __device__ constexpr uint32_t lut_pack(uint32_t a, uint32_t b, uint32_t c) {
+    return (a * 8u) | (b * 8u) << 10 | (c * 8u) << 20;
+}
+constexpr uint32_t kLutFull = lut_pack(kLutInf, kLutInf, kLutInf);
+constexpr uint32_t kLutFar = lut_pack(kLutNan, kLutNan, kLutNan);
 
 struct LutGeom {
     float x0, y0, inv_cs, fgx, fgy, cs;
@@ -858,7 +866,7 @@ __device__ inline LutGeom lut_geometry(const uint32_t (&box)[4]) {
     return g;
 }
 
-// One cell's entry: candidate indices in bits 0-4, 5-9, 10-14 (ascending, padded with the last),
+// One cell's entry: the candidates (ascending, padded with the last) as lut_pack offsets,
 // kLutFar when no point of the cell can be within the threshold, kLutFull past 3 candidates.
 __device__ inline uint32_t lut_entry(int ix, int iy, const LutGeom &g, const float2 *__restrict__ s_c, int k,
                                      float thr2) {
@@ -877,21 +885,21 @@ __device__ inline uint32_t lut_entry(int ix, int iy, const LutGeom &g, const flo
         near = fmin(near, dmin2(c));
     }
     const double bound = best * (1.0 + 0x1p-12) + 1e-30;
-    uint32_t ent = 0u;
-    int cnt = 0, last = 0;
+    uint32_t cand[3] = {0u, 0u, 0u};
+    int cnt = 0;
     for (int i = 0; i < k; ++i) {
         if (dmin2(s_c[i]) <= bound) {
-            if (cnt < 3) ent |= (uint32_t)i << (5 * cnt);
-            last = i;
+            if (cnt < 3) cand[cnt] = (uint32_t)i;
             ++cnt;
         }
     }
     // every point beyond the threshold: 255 whatever the candidates (far from all centres, many
     // of them are nearly equidistant, so such cells would otherwise overflow)
     if (near > (double)thr2 * (1.0 + 0x1p-12) + 1e-30) return kLutFar;
-    if (cnt == 0 || cnt > 3) ent |= kLutFull;  // (none: non-finite centres) -> assign_fast
-    for (int j = cnt; j < 3; ++j) ent |= (uint32_t)last << (5 * j);
-    return ent;
+    if (cnt == 0 || cnt > 3) return kLutFull;  // (none: non-finite centres) -> all centres
+    if (cnt < 2) cand[1] = cand[0];
+    if (cnt < 3) cand[2] = cand[1];
+    return lut_pack(cand[0], cand[1], cand[2]);
 }
 
 // Centroid update fused with the candidate table.  kLutBlocks workgroups each sum the replicas
@@ -980,8 +988,8 @@ kmeans_update_lut_kernel(const double *__restrict__ acc_rd, double *__restrict__
 
 // What the assignment kernels need of the grid record.
 struct LutView {
-    float x0, y0, inv_cs, fgx, fgy, fmx, fmy;  // fmx, fmy: the last cell index as float
-    int32_t gx;
+    float x0, y0, inv_cs, fgx_m, fgy_m;  // fgx_m: the largest float below the column count
+    int32_t gx4;                          // row stride of the table in bytes
 };
 
 // assign_fast's steps with the centres read from LDS (the table kernels keep no centres in
@@ -1015,29 +1023,45 @@ __device__ __forceinline__ uint32_t assign_lds2(float px, float py, const float2
 }
 
 // One point through the table: assign_fast's steps over the cell's 3 candidate slots.  full =
-// the caller must take assign_fast (outside the grid, > 3 candidates, or a tie-band hit).
+// the caller must take the steps over all centres (outside the grid, > 3 candidates, or a
+// tie-band hit).  ~35 VALU per point: med3 clamps the cell coordinates and tells inside from
+// outside in one compare, the entry's byte offsets address the centre table directly, and the
+// first candidate seeds the running minimum (a real candidate's d2 is finite; the sentinels' inf /
+// NaN propagate as described above).
 __device__ __forceinline__ uint32_t lut_point(float px, float py, const LutView &g, const uint32_t *__restrict__ s_lut,
                                               const float2 *__restrict__ s_c, float thr2, bool &full) {
     const float tx = __fmul_rn(__fsub_rn(px, g.x0), g.inv_cs), ty = __fmul_rn(__fsub_rn(py, g.y0), g.inv_cs);
-    const bool inside = (tx >= 0.f) & (tx < g.fgx) & (ty >= 0.f) & (ty < g.fgy);
-    const int ix = (int)fminf(fmaxf(tx, 0.f), g.fmx), iy = (int)fminf(fmaxf(ty, 0.f), g.fmy);
-    const uint32_t e = s_lut[iy * g.gx + ix];
-    float m = __builtin_inff(), m_prev = __builtin_inff();
-    uint32_t ia = 0;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const uint32_t i = (e >> (5 * j)) & 31u;
-        const float2 c = s_c[i];
+    const float cxf = __builtin_amdgcn_fmed3f(tx, 0.f, g.fgx_m), cyf = __builtin_amdgcn_fmed3f(ty, 0.f, g.fgy_m);
+    const bool inside = (cxf == tx) & (cyf == ty);  // false for NaN
+    const uint32_t a = __umul24((uint32_t)(int)cyf, (uint32_t)g.gx4) + ((uint32_t)(int)cxf << 2);
+    const uint32_t e = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_lut) + a);
+    const uint32_t o0 = e & 0x3ffu, o1 = (e >> 10) & 0x3ffu, o2 = e >> 20;
+    const char *cb = reinterpret_cast<const char *>(s_c);
+    const float2 c0 = *reinterpret_cast<const float2 *>(cb + o0);
+    const float2 c1 = *reinterpret_cast<const float2 *>(cb + o1);
+    const float2 c2 = *reinterpret_cast<const float2 *>(cb + o2);
+    auto d2 = [&](float2 c) {
         const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
-        const float d2 = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
-        const bool lt = d2 < m;
+        return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+    };
+    float m = d2(c0), m_prev = __builtin_inff();
+    uint32_t ia = o0;
+    {
+        const float d = d2(c1);
+        const bool lt = d < m;
         m_prev = lt ? m : m_prev;
-        ia = lt ? i : ia;
-        m = lt ? d2 : m;
+        ia = lt ? o1 : ia;
+        m = lt ? d : m;
     }
-    const bool far = (e & kLutFar) != 0u;
-    full = !inside || (!far && ((e & kLutFull) != 0u || m_prev <= __fmul_rn(m, 1.0f + 0x1p-20f)));
-    return (!far && m < thr2) ? ia : 255u;
+    {
+        const float d = d2(c2);
+        const bool lt = d < m;
+        m_prev = lt ? m : m_prev;
+        ia = lt ? o2 : ia;
+        m = lt ? d : m;
+    }
+    full = !inside | (m_prev <= __fmul_rn(m, 1.0f + 0x1p-20f));
+    return m < thr2 ? ia >> 3 : 255u;
 }
 
 // Vector engine, streaming form: a lane takes two consecutive points per 16-B load (the pair the
@@ -1059,7 +1083,7 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     constexpr int kSub = ECC_KM_ACC_SUB;
     __shared__ uint32_t s_n[kWaves * kSub][K];
     __shared__ double s_sx[kWaves * kSub][K], s_sy[kWaves * kSub][K];
-    __shared__ float2 s_c[K];
+    __shared__ float2 s_c[kLut ? kFastMaxK + 2 : K];  // + the table's inf and NaN sentinels
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[kLut ? kLutCells : 4];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     // The grid record as scalars (a struct copy of the 64-B record went to the stack).  Without a
@@ -1070,14 +1094,15 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
         g.x0 = geom->x0;
         g.y0 = geom->y0;
         g.inv_cs = geom->inv_cs;
-        g.fgx = ok ? geom->fgx : 0.f;
-        g.fgy = ok ? geom->fgy : 0.f;
-        g.fmx = ok ? geom->fgx - 1.f : 0.f;
-        g.fmy = ok ? geom->fgy - 1.f : 0.f;
-        g.gx = ok ? geom->gx : 1;
+        if (!ok) g.inv_cs = __builtin_nanf("");  // no grid: every point is outside (NaN compares false)
+        g.fgx_m = ok ? __uint_as_float(__float_as_uint(geom->fgx) - 1u) : 0.f;  // fgx >= 1
+        g.fgy_m = ok ? __uint_as_float(__float_as_uint(geom->fgy) - 1u) : 0.f;
+        g.gx4 = ok ? 4 * geom->gx : 4;
+        if (tid == kLutInf) s_c[kLutInf] = make_float2(__builtin_inff(), __builtin_inff());
+        if (tid == kLutNan) s_c[kLutNan] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
         // the table into LDS: all of a lane's 16-B loads in flight at once (a strided word loop
         // paid one L2 round trip per word, at the start of every workgroup)
-        const __amdgpu_buffer_rsrc_t v = ecc::buffer_view(lut, ok ? (uint32_t)(g.gx * geom->gy) * 4u : 0u);
+        const __amdgpu_buffer_rsrc_t v = ecc::buffer_view(lut, ok ? (uint32_t)(geom->gx * geom->gy) * 4u : 0u);
         uint4 q[kLutCells / (4 * kThreads)];
 #pragma unroll
         for (int u = 0; u < kLutCells / (4 * kThreads); ++u)
