@@ -302,6 +302,8 @@ __device__ __forceinline__ uint32_t assign_lds(float px, float py, const float *
     return ecc::sqrt_rn(m) < thr ? (uint32_t)ia : 255u;
 }
 
+__device__ __forceinline__ uint64_t lanes_below_mask(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
 __device__ __forceinline__ float uniform_f32(float v) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
@@ -779,6 +781,10 @@ constexpr int kLutCells = kLutSide * kLutSide;
 constexpr int kLutBlocks = kLutCells / kThreads;
 constexpr int kBoxBlocks = 64, kBoxPerThread = 4;
 constexpr int kLutInf = kFastMaxK, kLutNan = kFastMaxK + 1;  // sentinel slots of the centre table
+// Candidate slots the assignment tests per point.  With pairwise domination (lut_entry) about 1 %
+// of the cells near the centres keep 3 candidates: their points go through the wave's fallback
+// queue, which is cheaper than a third distance for every point.
+constexpr int kLutSlots = 2;
 __host__ __device__ constexpr uint32_t lut_pack(uint32_t a, uint32_t b, uint32_t c) {
     return (a * 8u) | (b * 8u) << 10 | (c * 8u) << 20;
 }
@@ -884,22 +890,60 @@ __device__ inline uint32_t lut_entry(int ix, int iy, const LutGeom &g, const flo
         best = fmin(best, dx * dx + dy * dy);
         near = fmin(near, dmin2(c));
     }
-    const double bound = best * (1.0 + 0x1p-12) + 1e-30;
-    uint32_t cand[3] = {0u, 0u, 0u};
-    int cnt = 0;
-    for (int i = 0; i < k; ++i) {
-        if (dmin2(s_c[i]) <= bound) {
-            if (cnt < 3) cand[cnt] = (uint32_t)i;
-            ++cnt;
-        }
-    }
     // every point beyond the threshold: 255 whatever the candidates (far from all centres, many
     // of them are nearly equidistant, so such cells would otherwise overflow)
     if (near > (double)thr2 * (1.0 + 0x1p-12) + 1e-30) return kLutFar;
-    if (cnt == 0 || cnt > 3) return kLutFull;  // (none: non-finite centres) -> all centres
+    const double bound = best * (1.0 + 0x1p-12) + 1e-30;
+    constexpr int kPre = 4;
+    int pre[kPre] = {0, 0, 0, 0};
+    int np = 0;
+    for (int i = 0; i < k; ++i) {
+        if (dmin2(s_c[i]) <= bound) {
+            pre[np < kPre ? np : kPre - 1] = np < kPre ? i : pre[kPre - 1];
+            ++np;
+        }
+    }
+    if (np == 0 || np > kPre) return kLutFull;  // (none: non-finite centres) -> all centres
+    // Pairwise domination (the bound above is per centre): i cannot win in the cell if some other
+    // candidate j has d_i^2 > (1 + 2^-12) d_j^2 + 1e-30 at every point of it.  d_i^2 - (1+eps) d_j^2
+    // is concave in the point (its quadratic part is -eps |p|^2), so its minimum over the cell is
+    // at a corner: four evaluations decide.  A pruned centre then stays 2^-13 above the winner, as
+    // the per-centre bound guarantees.  This leaves 1-2 candidates in nearly every cell (the bound
+    // alone left 4+ near Voronoi vertices).  Fixed-size, fully unrolled (register arrays).
+    double dc[kPre][4];
+#pragma unroll
+    for (int a = 0; a < kPre; ++a) {
+        const float2 c = s_c[pre[a]];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double dx = c.x - ((q & 1) ? x1 : x0), dy = c.y - ((q & 2) ? y1 : y0);
+            dc[a][q] = dx * dx + dy * dy;
+        }
+    }
+    uint32_t keep = (1u << np) - 1u;
+#pragma unroll
+    for (int a = 0; a < kPre; ++a) {
+#pragma unroll
+        for (int b = 0; b < kPre; ++b) {
+            if (a == b) continue;
+            bool dom = a < np && b < np;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dom = dom && (dc[a][q] - (1.0 + 0x1p-12) * dc[b][q] > 1e-30);
+            keep &= dom ? ~(1u << a) : ~0u;
+        }
+    }
+    uint32_t cand[3] = {0u, 0u, 0u};
+    int cnt = 0;
+#pragma unroll
+    for (int a = 0; a < kPre; ++a) {
+        if (keep >> a & 1u) {
+            if (cnt < 3) cand[cnt] = (uint32_t)pre[a];
+            ++cnt;
+        }
+    }
+    if (cnt == 0 || cnt > kLutSlots) return kLutFull;
     if (cnt < 2) cand[1] = cand[0];
-    if (cnt < 3) cand[2] = cand[1];
-    return lut_pack(cand[0], cand[1], cand[2]);
+    return lut_pack(cand[0], cand[1], cand[1]);
 }
 
 // Centroid update fused with the candidate table.  kLutBlocks workgroups each sum the replicas
@@ -1022,9 +1066,9 @@ __device__ __forceinline__ uint32_t assign_lds2(float px, float py, const float2
     return ecc::sqrt_rn(m) < thr ? (uint32_t)ia : 255u;
 }
 
-// One point through the table: assign_fast's steps over the cell's 3 candidate slots.  full =
+// One point through the table: assign_fast's steps over the cell's kLutSlots candidates.  full =
 // the caller must take the steps over all centres (outside the grid, > 3 candidates, or a
-// tie-band hit).  ~35 VALU per point: med3 clamps the cell coordinates and tells inside from
+// tie-band hit).  ~33 VALU per point: med3 clamps the cell coordinates and tells inside from
 // outside in one compare, the entry's byte offsets address the centre table directly, and the
 // first candidate seeds the running minimum (a real candidate's d2 is finite; the sentinels' inf /
 // NaN propagate as described above).
@@ -1035,11 +1079,10 @@ __device__ __forceinline__ uint32_t lut_point(float px, float py, const LutView 
     const bool inside = (cxf == tx) & (cyf == ty);  // false for NaN
     const uint32_t a = __umul24((uint32_t)(int)cyf, (uint32_t)g.gx4) + ((uint32_t)(int)cxf << 2);
     const uint32_t e = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_lut) + a);
-    const uint32_t o0 = e & 0x3ffu, o1 = (e >> 10) & 0x3ffu, o2 = e >> 20;
+    const uint32_t o0 = e & 0x3ffu, o1 = (e >> 10) & 0x3ffu;
     const char *cb = reinterpret_cast<const char *>(s_c);
     const float2 c0 = *reinterpret_cast<const float2 *>(cb + o0);
     const float2 c1 = *reinterpret_cast<const float2 *>(cb + o1);
-    const float2 c2 = *reinterpret_cast<const float2 *>(cb + o2);
     auto d2 = [&](float2 c) {
         const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
         return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
@@ -1051,13 +1094,6 @@ __device__ __forceinline__ uint32_t lut_point(float px, float py, const LutView 
         const bool lt = d < m;
         m_prev = lt ? m : m_prev;
         ia = lt ? o1 : ia;
-        m = lt ? d : m;
-    }
-    {
-        const float d = d2(c2);
-        const bool lt = d < m;
-        m_prev = lt ? m : m_prev;
-        ia = lt ? o2 : ia;
         m = lt ? d : m;
     }
     full = !inside | (m_prev <= __fmul_rn(m, 1.0f + 0x1p-20f));
@@ -1085,6 +1121,7 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     __shared__ double s_sx[kWaves * kSub][K], s_sy[kWaves * kSub][K];
     __shared__ float2 s_c[kLut ? kFastMaxK + 2 : K];  // + the table's inf and NaN sentinels
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[kLut ? kLutCells : 4];
+    __shared__ float4 s_q[kWaves][kLut ? 192 : 1];  // fallback queues: < 64 + 2 x 64 entries
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     // The grid record as scalars (a struct copy of the 64-B record went to the stack).  Without a
     // grid (non-finite or huge box) every point is outside: fgx = 0, one cell, assign_lds2.
@@ -1153,6 +1190,43 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
             q[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
         }
     };
+    // Fallback queue of this wave (table path): points the table cannot decide (outside the grid,
+    // > kLutSlots candidates, a tie-band hit) are appended with their index and labelled 64 at a
+    // time by assign_lds2 with every lane busy, instead of one divergent round per trip.  The
+    // queue is wave-private LDS; a wave's LDS operations execute in order, so only the compiler
+    // is fenced.  A queued point's byte label is stored after the trip's 2-byte store of its pair.
+    uint32_t qn = 0;  // wave-uniform fill
+    auto drain = [&](uint32_t cnt) __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t i = qn - cnt + (uint32_t)lane;
+        if ((uint32_t)lane < cnt) {
+            const float4 e = s_q[wave][i];
+            const float2 q2 = make_float2(e.x, e.y);
+            const uint32_t l = assign_lds2<K>(q2.x, q2.y, s_c, thr);
+            const int64_t idx = (int64_t)__float_as_uint(e.z) | ((int64_t)__float_as_uint(e.w) << 32);
+            if (labels) labels[idx] = (uint8_t)l;
+            account(q2, l);
+        }
+        qn -= cnt;
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto enqueue = [&](float2 p0, float2 p1, int64_t pp, bool f0, bool f1) __attribute__((always_inline)) {
+        if constexpr (kLut) {
+            const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
+            if ((m0 | m1) == 0ull) return;  // uniform
+            const uint32_t n0 = (uint32_t)__popcll(m0);
+            const uint64_t below = lanes_below_mask(lane);
+            auto put = [&](uint32_t slot, float2 pt, int64_t idx) {
+                s_q[wave][slot] = make_float4(pt.x, pt.y, __uint_as_float((uint32_t)idx),
+                                              __uint_as_float((uint32_t)((uint64_t)idx >> 32)));
+            };
+            if (f0) put(qn + (uint32_t)__popcll(m0 & below), p0, 2 * pp);
+            if (f1) put(qn + n0 + (uint32_t)__popcll(m1 & below), p1, 2 * pp + 1);
+            qn += n0 + (uint32_t)__popcll(m1);
+            if (qn >= 64u) drain(64u);
+        }
+    };
     auto test = [&](int64_t b0, const float4 (&q)[kPairUnroll]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < kPairUnroll; ++u) {
@@ -1161,25 +1235,22 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
             const int64_t pp = blk * 64 + lane;
             const float2 p0 = make_float2(q[u].x, q[u].y), p1 = make_float2(q[u].z, q[u].w);
             uint32_t l0, l1;
+            bool f0 = false, f1 = false;
             if constexpr (kLut) {
-                bool f0, f1;
                 l0 = lut_point(p0.x, p0.y, g, s_lut, s_c, thr2, f0);
                 l1 = lut_point(p1.x, p1.y, g, s_lut, s_c, thr2, f1);
-                // one fallback round for the wave when no lane needs both of its points
-                while (f0 | f1) {
-                    const float qx = f0 ? p0.x : p1.x, qy = f0 ? p0.y : p1.y;
-                    const uint32_t l = assign_lds2<K>(qx, qy, s_c, thr);
-                    if (f0) { l0 = l; f0 = false; }
-                    else { l1 = l; f1 = false; }
-                }
+                f0 = f0 && pp < npair;
+                f1 = f1 && pp < npair;
             } else {
                 assign_pair<K>(p0, p1, cx, cy, s_c, thr, thr2, l0, l1);
             }
             if (pp < npair) {
                 if (labels) reinterpret_cast<uint16_t *>(labels)[pp] = (uint16_t)(l0 | l1 << 8);
-                account(p0, l0);
-                account(p1, l1);
+                if (!f0) account(p0, l0);
+                if (!f1) account(p1, l1);
             }
+            // after the pair's store: a drain rewrites the queued points' bytes
+            if constexpr (kLut) enqueue(p0, p1, pp, f0, f1);
         }
     };
     // Two buffers in ping-pong with unconditional (clamped) loads: no register copies between
@@ -1199,6 +1270,9 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
             b0 += span;
             if (b0 >= nblk) break;
         }
+    }
+    if constexpr (kLut) {
+        if (qn) drain(qn);
     }
     if ((n & 1) && blockIdx.x == 0 && tid == 0) {  // the odd last point
         const float2 q = reinterpret_cast<const float2 *>(xy4)[n - 1];
