@@ -22,6 +22,15 @@
 // Algorithmic bytes: 4 B/point/iteration (packed u16 xy) + 1 B/point for the final labels.
 #include "ecc_internal.hpp"
 
+#ifndef ECC_KM_LUT_WG_PER_CU
+#define ECC_KM_LUT_WG_PER_CU 5
+#endif
+#ifndef ECC_KM_LAB_WG_PER_CU
+#define ECC_KM_LAB_WG_PER_CU 6
+#endif
+#ifndef ECC_KM_LUT_UNROLL
+#define ECC_KM_LUT_UNROLL 4
+#endif
 #ifndef ECC_KM_ACC_SUB
 #define ECC_KM_ACC_SUB 4
 #endif
@@ -1121,7 +1130,7 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     __shared__ double s_sx[kWaves * kSub][K], s_sy[kWaves * kSub][K];
     __shared__ float2 s_c[kLut ? kFastMaxK + 2 : K];  // + the table's inf and NaN sentinels
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[kLut ? kLutCells : 4];
-    __shared__ float4 s_q[kWaves][kLut ? 192 : 1];  // fallback queues: < 64 + 2 x 64 entries
+    __shared__ float4 s_q[kWaves][kLut ? 128 : 1];  // fallback queues: < 64 + 64 entries
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     // The grid record as scalars (a struct copy of the 64-B record went to the stack).  Without a
     // grid (non-finite or huge box) every point is outside: fgx = 0, one cell, assign_lds2.
@@ -1177,15 +1186,17 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     const int64_t npair = n / 2;
     const int64_t nblk = (npair + 63) / 64;  // 64 pairs per wave block
     const int64_t stride = (int64_t)gridDim.x * kWaves;
-    const int64_t span = stride * kPairUnroll;
+    // table path: loads per trip (8 measured slower than 4: 117 vs 110 us per accumulate pass)
+    constexpr int kU = kLut ? ECC_KM_LUT_UNROLL : kPairUnroll;
+    const int64_t span = stride * kU;
     // a trip's loads through a buffer view based at its first pair: unconditional (0 past the
     // last pair), one VGPR of lane offset for all of them, the u part in the scalar offset
-    auto load = [&](int64_t b0, float4 (&q)[kPairUnroll]) __attribute__((always_inline)) {
+    auto load = [&](int64_t b0, float4 (&q)[kU]) __attribute__((always_inline)) {
         const int64_t first = b0 * 64 < npair ? b0 * 64 : npair;
         const int64_t rem = (npair - first) * 16;
         const __amdgpu_buffer_rsrc_t v = ecc::buffer_view(xy4 + first, rem < 0xffffffffll ? (uint32_t)rem : 0xffffffffu);
 #pragma unroll
-        for (int u = 0; u < kPairUnroll; ++u) {
+        for (int u = 0; u < kU; ++u) {
             const uint4 w = ecc::buffer_load_u128(v, (uint32_t)lane * 16u, (uint32_t)(u * stride * 64 * 16));
             q[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
         }
@@ -1221,15 +1232,18 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
                 s_q[wave][slot] = make_float4(pt.x, pt.y, __uint_as_float((uint32_t)idx),
                                               __uint_as_float((uint32_t)((uint64_t)idx >> 32)));
             };
+            // one half at a time with a drain check between: the queue never holds 128 entries
             if (f0) put(qn + (uint32_t)__popcll(m0 & below), p0, 2 * pp);
-            if (f1) put(qn + n0 + (uint32_t)__popcll(m1 & below), p1, 2 * pp + 1);
-            qn += n0 + (uint32_t)__popcll(m1);
+            qn += n0;
+            if (qn >= 64u) drain(64u);
+            if (f1) put(qn + (uint32_t)__popcll(m1 & below), p1, 2 * pp + 1);
+            qn += (uint32_t)__popcll(m1);
             if (qn >= 64u) drain(64u);
         }
     };
-    auto test = [&](int64_t b0, const float4 (&q)[kPairUnroll]) __attribute__((always_inline)) {
+    auto test = [&](int64_t b0, const float4 (&q)[kU]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < kPairUnroll; ++u) {
+        for (int u = 0; u < kU; ++u) {
             const int64_t blk = b0 + u * stride;
             if (blk >= nblk) break;  // wave-uniform
             const int64_t pp = blk * 64 + lane;
@@ -1256,7 +1270,7 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     // Two buffers in ping-pong with unconditional (clamped) loads: no register copies between
     // trips and no branch around the loads, so the wait before each trip's tests covers only
     // that trip's own loads while the other buffer's are in flight.
-    float4 qa[kPairUnroll], qb[kPairUnroll];
+    float4 qa[kU], qb[kU];
     int64_t b0 = (int64_t)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(wave);  // uniform: scalar descriptors
     if (npair > 0 && b0 < nblk) {
         load(b0, qa);
@@ -2002,8 +2016,15 @@ static int kmeans_run_f32_impl(ecc_ctx *ctx, const float *xy, int64_t n_points, 
             hipLaunchKernelGGL(kmeans_update_lut_kernel, dim3(kLutBlocks), dim3(kThreads), 0, s, acc, acc, n_copies,
                                centroids, cfg->k, cfg->tol, st, -1, box, geom, lut, thr2);
         }
-        // one round of resident workgroups (4 per CU at <= 128 VGPRs): each loads the table once
-        const int lgrid = (int)std::max<int64_t>(1, std::min<int64_t>((n_points + 255) / 256, 4 * ctx->n_cu));
+        // one round of resident workgroups, as many per CU as registers and LDS allow (a
+        // latency-bound stream: the labels pass took 104 us at four per CU, 93 at five): the
+        // accumulate pass 5 (k <= 16: 86 VGPRs, 30 KB) or 4 (k <= 32: 35 KB of slots and table),
+        // the labels pass 6 (80 VGPRs, 25 KB)
+        auto rgrid = [&](int per_cu) {
+            return (int)std::max<int64_t>(1, std::min<int64_t>((n_points + 255) / 256, (int64_t)per_cu * ctx->n_cu));
+        };
+        const int lgrid = rgrid(cfg->k <= 16 ? ECC_KM_LUT_WG_PER_CU : 4);
+        const int lgrid_lab = rgrid(ECC_KM_LAB_WG_PER_CU);
         for (int it = 0; it < cfg->max_iters; ++it) {
             double *acc_it = acc + (size_t)(it & 1) * n_copies * kAccStride;
             double *acc_next = acc + (size_t)((it + 1) & 1) * n_copies * kAccStride;
@@ -2023,7 +2044,7 @@ static int kmeans_run_f32_impl(ecc_ctx *ctx, const float *xy, int64_t n_points, 
             {
                 ECC_TIMED(ctx, s, "kmeans_f32_labels");
                 const bool lab_ok = (reinterpret_cast<uintptr_t>(labels) & 1) == 0;
-                launch_f32_fast<false>(cfg->k, eng, dim3(lab_ok ? lgrid : grid), s, xy, n_points, centroids, cfg->threshold, nullptr,
+                launch_f32_fast<false>(cfg->k, eng, dim3(lab_ok ? lgrid_lab : grid), s, xy, n_points, centroids, cfg->threshold, nullptr,
                                        1, st, labels, lab_ok ? geom : nullptr, lut);
             }
             ECC_CHECK_LAUNCH(ctx, "kmeans_f32 labels");
