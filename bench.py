@@ -858,9 +858,17 @@ def cpu_leg(ecc, args, W, H, K, I, xy, t, n, c0, ctx, g):
                     and np.array_equal(p_c.view(np.uint32), o_c.view(np.uint32)) and np.array_equal(p_lab, o_lab)
                     and np.array_equal(p_flags, o_flags) and np.array_equal(p_sae, o_sae)
                     and np.array_equal(p_cnt, o_cnt) and nms_mismatches(p_out, p_cnt, o_out, o_cnt, g["cap"])[0] == 0)
-    base["all_cores"] = {
+    # the threads it may use: the job's CPU affinity and OMP_NUM_THREADS (the GPU box sets 16 for a
+    # share of a larger host), not the machine's core count
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = None
+    base["omp_threads"] = {
         "value": round(n / dt_omp / 1e6, 3), "unit": "Mevents/s", "cores": nt, "kind": "port",
         "equals_single_thread": omp_same,
+        "limit": {"omp_threads": nt, "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
+                  "affinity_cpus": aff, "host_cpus": os.cpu_count()},
         "sample": f"same {n} events and pipeline, oracle/cpu_omp.cpp (OpenMP, {nt} threads: windows, k-means "
                   f"assignment, per-slice arc tests, per-slice NMS in parallel; SAE update sequential); {dt_omp:.2f} s"}
 
