@@ -900,7 +900,7 @@ struct SparseLds {
     uint16_t q4[kQ4Cap];
     int64_t wave_min[kWaves];
     int32_t wave_tot[kWaves];
-    int32_t exact_only, mixed, n_tasks, q4n;
+    int32_t exact_only, mixed, n_tasks, q4n, redo;
     int64_t seg_lo[16];
     int32_t seg_pref[16];
     int32_t seg_off[16];
@@ -941,6 +941,9 @@ __device__ __noinline__ bool sparse_exact_test(const SparseLds *L, int wp0, int6
     return arc_streak<20, 4, 8>(v4);
 }
 
+#ifndef ECC_ARC_WAVES
+#define ECC_ARC_WAVES 8
+#endif
 constexpr int kSparseHold = kValCap / kArcThreads;  // entries per lane, held between the two passes
 
 #ifndef ECC_ARC_PROFILE
@@ -961,7 +964,7 @@ __device__ unsigned long long g_arc_prof[8];
 #define ARC_MARK(k) do { } while (0)
 #endif
 
-__global__ void __launch_bounds__(kArcThreads, 6)  // 6 waves/SIMD: three 8-wave workgroups per CU
+__global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)  // waves/SIMD: 8 = four 8-wave workgroups per CU
 arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
            const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
            const int64_t *__restrict__ gB, uint32_t *__restrict__ res, int64_t *__restrict__ over,
@@ -1002,6 +1005,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         L.mixed = 0;
         L.n_tasks = 0;
         L.q4n = 0;
+        L.redo = 0;
     }
     if (tid < kMaxSeg) {
         // segment geometry packed into integer constants (a per-lane table read would be a load):
@@ -1114,11 +1118,35 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     __syncthreads();
 
     ARC_MARK(2);  // (c, d) list offsets, B_g slots, value scatter
-    // (e) tests, as the dense kernel's (lookups through the compact lists)
+    // (e) tests through the compact lists.  The circle-3 loop holds no call: its survivors and
+    //     the tasks its clamped keys cannot decide share one LDS queue (bit 15 = exact circle 3
+    //     first), drained after a barrier.  Without the call's saved registers the kernel fits
+    //     64 VGPRs: four 8-wave workgroups per CU.  Wide groups, and a queue overflow (redo),
+    //     take every task through the full path in a cold loop.
     const int n_tasks = L.n_tasks;
     const bool fast = !L.exact_only;
     const bool ties_exact = !L.mixed;
     const ExactCtx ec{Bg, t, grp_first, Lt, g.W, narrow};
+    if (fast) {
+        for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+            const int pi = L.tasks[ti];
+            const int j = pi / kTilePix, lp = pi % kTilePix;
+            const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+            const uint32_t below = below_mask(j);
+            uint32_t k3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) k3[k] = (sparse_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
+            const int r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+            if (r3 != 0) {
+                const int qi = atomicAdd(&L.q4n, 1);
+                if (qi < kQ4Cap) L.q4[qi] = (uint16_t)(pi | (r3 < 0 ? 0x8000 : 0));
+                else L.redo = 1;
+            }
+        }
+    }
+    __syncthreads();
+    ARC_MARK(3);  // circle 3
+    const bool redo = !fast || L.redo;  // uniform
     auto circle4 = [&](int pi) {
         const int j = pi / kTilePix, lp = pi % kTilePix;
         const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
@@ -1138,35 +1166,39 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         }
         if (r4 == 1) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
     };
-    for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
-        const int pi = L.tasks[ti];
+    auto exact3 = [&](int pi) {
         const int j = pi / kTilePix, lp = pi % kTilePix;
         const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-        const uint32_t below = below_mask(j);
-        int r3 = -1;
-        if (fast) {
-            uint32_t k3[16];
+        const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
+        return sparse_exact_test(&L, wp0, q0, j, true, ec);
+    };
+    if (!redo) {
+        const int n4 = L.q4n;
+#if ECC_ARC_PROFILE
+        if (tid == 0) atomicAdd(&g_arc_prof[6], (unsigned long long)n4);
+#endif
+        for (int qi = tid; qi < n4; qi += kArcThreads) {
+            const int e = L.q4[qi], pi = e & 0x7fff;
+            if (!(e & 0x8000) || exact3(pi)) circle4(pi);
+        }
+    } else {
+        // cold: wide groups (every test exact) or more queued tasks than kQ4Cap
+        for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+            const int pi = L.tasks[ti];
+            int r3 = -1;
+            if (fast) {
+                const int j = pi / kTilePix, lp = pi % kTilePix;
+                const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+                const uint32_t below = below_mask(j);
+                uint32_t k3[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) k3[k] = (sparse_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
-            r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
-        }
-        if (r3 < 0) {
-            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
-            r3 = sparse_exact_test(&L, wp0, q0, j, true, ec) ? 1 : 0;
-        }
-        if (r3 == 1) {
-            const int qi = atomicAdd(&L.q4n, 1);
-            if (qi < kQ4Cap) L.q4[qi] = (uint16_t)pi;
-            else circle4(pi);  // queue full (rare): test here
+                for (int k = 0; k < 16; ++k) k3[k] = (sparse_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
+                r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+            }
+            if (r3 < 0) r3 = exact3(pi) ? 1 : 0;
+            if (r3 == 1) circle4(pi);
         }
     }
-    __syncthreads();
-    ARC_MARK(3);  // circle 3
-    const int n4 = min(L.q4n, kQ4Cap);
-#if ECC_ARC_PROFILE
-    if (tid == 0) atomicAdd(&g_arc_prof[6], (unsigned long long)n4);
-#endif
-    for (int qi = tid; qi < n4; qi += kArcThreads) circle4(L.q4[qi]);
     __syncthreads();
     ARC_MARK(4);  // circle 4
 #if ECC_ARC_PROFILE
