@@ -883,7 +883,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
 // ascending j, at vals[pix[wp].off ...]; the value an event of slice j sees is
 // vals[off + popc(mask & ((2 << j) - 1))] — index off (the B_g slot) when no slice <= j touched
 // the pixel, so a lookup is one 8-B pixel read and one value read, no select.  ~34 KB of LDS
-// instead of the dense planes' ~80 KB: three 8-wave workgroups per CU.  Windows with more than
+// instead of the dense planes' ~80 KB: four 8-wave workgroups per CU.  Windows with more than
 // kValCap values go to the overflow list (arc_dense_kernel).
 constexpr int kValCap = 4096;
 
