@@ -231,8 +231,8 @@ def main():
                                                 d_c.ptr, labels.ptr, None, ks), "kmeans")
         ecc.check(lib.ecc_event_record(ev_join, ks))
         ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
-        ctx.fast_detect(d_xy, d_t, n, ccfg, sae, flags)
-        ctx.corner_nms(d_xy, flags, n, SLICE, W, H, 15, cap, nms_out[nb], nms_cnt[nb])
+        # detect + per-slice NMS in one call: the flag pass writes the NMS candidate lists
+        ctx.fast_detect_nms(d_xy, d_t, n, ccfg, sae, flags, 15, cap, nms_out[nb], nms_cnt[nb])
         ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_join))
 
     for _ in range(args.warmup):

@@ -1247,10 +1247,15 @@ __device__ __forceinline__ uint32_t corner_bit(uint32_t v, const CornerGeom &g, 
     return (rg[(int64_t)tile * kPairWords + (pi >> 5)] >> (pi & 31)) & 1u;
 }
 
-template <bool kStaged>
+// kCand (ecc_fast_detect_nms): the pass also writes each slice's NMS candidate list — the
+// flagged events' xy in event order at cand[s * S ...], their count in n_cand[s] — which is
+// what nms_compact_kernel would rebuild from the flags (the host takes this form only for
+// slices of at most 16384 events, a multiple of 4).
+template <bool kStaged, bool kCand>
 __global__ void __launch_bounds__(kFlagThreads)
 flags_event_kernel(const uint32_t *__restrict__ xy, CornerGeom g, const uint32_t *__restrict__ res,
-                   const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags) {
+                   const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags, uint32_t *__restrict__ cand,
+                   int32_t *__restrict__ n_cand) {
     extern __shared__ uint32_t sb[];  // [n_tiles][kSegWords]: bit lp of tile = pair (j, lp)
     const int64_t s = blockIdx.x;
     const int64_t lo = s * g.S;
@@ -1304,6 +1309,55 @@ flags_event_kernel(const uint32_t *__restrict__ xy, CornerGeom g, const uint32_t
                (i + 2 < live_end ? corner_bit<kStaged>(v.z, g, sb, rg, j) << 16 : 0u) |
                (i + 3 < live_end ? corner_bit<kStaged>(v.w, g, sb, rg, j) << 24 : 0u);
     };
+    if constexpr (kCand) {
+        // quad u of lane tid holds events 4 (u * 512 + tid) .. + 3: event order is u, then lane;
+        // a quad has <= 4 flags, so three ballots give each lane its prefix inside the wave
+        __shared__ int ctot[kFlagQuads][kFlagThreads / 64];
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        uint32_t f[kFlagQuads];
+        int pfx[kFlagQuads];
+#pragma unroll
+        for (int u = 0; u < kFlagQuads; ++u) {
+            const int q = u * kFlagThreads + (int)threadIdx.x;
+            const int i = 4 * q;
+            f[u] = (q < n4 && i < live_end) ? quad_flags(i, pre[u]) : 0u;
+            if (q < n4) *reinterpret_cast<uint32_t *>(flags + lo + i) = f[u];
+            const int c = __popc(f[u]);  // flag bytes are 0 or 1
+            const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+            pfx[u] = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+            if (lane == 0) ctot[u][wave] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+        }
+        __syncthreads();
+        int base = 0;
+        uint32_t *dst = cand + lo;
+#pragma unroll
+        for (int u = 0; u < kFlagQuads; ++u) {
+            int off = base + pfx[u];
+#pragma unroll
+            for (int w = 0; w < kFlagThreads / 64; ++w) {
+                const int tw = ctot[u][w];
+                off += w < wave ? tw : 0;
+                base += tw;
+            }
+            if (f[u]) {
+                if (f[u] & 0x1u) dst[off++] = pre[u].x;
+                if (f[u] & 0x100u) dst[off++] = pre[u].y;
+                if (f[u] & 0x10000u) dst[off++] = pre[u].z;
+                if (f[u] & 0x1000000u) dst[off++] = pre[u].w;
+            }
+        }
+        if (threadIdx.x == 0) {
+            for (int i = 4 * n4; i < len; ++i) {  // the batch's last < 4 events
+                const uint32_t v = xy[lo + i];
+                const uint32_t fb = i < live_end ? corner_bit<kStaged>(v, g, sb, rg, j) : 0u;
+                flags[lo + i] = (uint8_t)fb;
+                if (fb) dst[base++] = v;
+            }
+            n_cand[s] = base;
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < kFlagQuads; ++u) {
         const int q = u * kFlagThreads + (int)threadIdx.x;
@@ -1469,7 +1523,7 @@ ECC_API void ecc_corner_cfg_default(ecc_corner_cfg *cfg) {
 // carve (same n and cfg), so prepare/finish may be separate calls with a collective between.
 static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
                               const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags, int64_t *local_last,
-                              int phases, ecc_stream_t stream) {
+                              int phases, ecc_stream_t stream, uint32_t *cand = nullptr, int32_t *n_cand = nullptr) {
     if (!ctx || !cfg || n < 0) return ECC_ERR_INVALID;
     if ((phases & 2) && !sae) return ECC_ERR_INVALID;
     if (n > 0 && (!xy || !t || ((phases & 2) && !corner_flags))) return ECC_ERR_INVALID;
@@ -1580,18 +1634,27 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         constexpr size_t kLdsMax = 160 * 1024;
         const size_t lds = (size_t)g.n_tiles * kSegWords * sizeof(uint32_t);
         if (lds <= kLdsMax) {
-            static bool lds_set = false;
-            if (lds > 65536 && !lds_set) {
-                ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&flags_event_kernel<true>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax),
+            static bool lds_set[2] = {false, false};
+            const void *fn = cand ? reinterpret_cast<const void *>(&flags_event_kernel<true, true>)
+                                  : reinterpret_cast<const void *>(&flags_event_kernel<true, false>);
+            if (lds > 65536 && !lds_set[cand ? 1 : 0]) {
+                ECC_CHECK_HIP(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax),
                               "flags LDS");
-                lds_set = true;
+                lds_set[cand ? 1 : 0] = true;
             }
-            hipLaunchKernelGGL(flags_event_kernel<true>, dim3((unsigned)g.n_slices), dim3(kFlagThreads), lds, s, xy, g,
-                               (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
+            if (cand)
+                hipLaunchKernelGGL((flags_event_kernel<true, true>), dim3((unsigned)g.n_slices), dim3(kFlagThreads), lds, s,
+                                   xy, g, (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags, cand,
+                                   n_cand);
+            else
+                hipLaunchKernelGGL((flags_event_kernel<true, false>), dim3((unsigned)g.n_slices), dim3(kFlagThreads), lds,
+                                   s, xy, g, (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags,
+                                   nullptr, nullptr);
         } else {
-            hipLaunchKernelGGL(flags_event_kernel<false>, dim3((unsigned)g.n_slices), dim3(kFlagThreads), 0, s, xy, g,
-                               (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags);
+            if (cand) return ECC_ERR_INVALID;  // the caller checks ecc_fast_detect_nms' conditions
+            hipLaunchKernelGGL((flags_event_kernel<false, false>), dim3((unsigned)g.n_slices), dim3(kFlagThreads), 0, s,
+                               xy, g, (const uint32_t *)gi.res, (const int32_t *)first_border, corner_flags, nullptr,
+                               nullptr);
         }
     }
     ECC_CHECK_LAUNCH(ctx, "fast_detect");
@@ -1616,6 +1679,38 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
                             const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
                             ecc_stream_t stream) {
     return fast_detect_phases(ctx, xy, t, n, cfg, sae, corner_flags, nullptr, 3, stream);
+}
+
+ECC_API int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                                const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags, int32_t box_size,
+                                int32_t cap, ecc_corner *out, int32_t *out_count, ecc_stream_t stream) {
+    if (!ctx || !cfg) return ECC_ERR_INVALID;
+    if (ecc::nms_check_args(n, cfg->slice_events, cfg->width, cfg->height, box_size, cap)) return ECC_ERR_INVALID;
+    if (n > 0 && (!out_count || (cap > 0 && !out))) return ECC_ERR_INVALID;
+    const int64_t tiles = (int64_t)((cfg->width + kTile - 1) / kTile) * ((cfg->height + kTile - 1) / kTile);
+    uint32_t *cand = nullptr;
+    int32_t *n_cand = nullptr;
+    if (n > 0 && cfg->slice_events % 4 == 0 && cfg->slice_events <= kFlagQuads * kFlagThreads * 4 &&
+        tiles * kSegWords * 4 <= 160 * 1024) {
+        int rc = ecc::nms_candidates(ctx, n, cfg->slice_events, cfg->width, cfg->height, box_size, &cand, &n_cand);
+        if (rc) return rc;
+    }
+    if (!cand) {  // the two calls
+        int rc = ecc_fast_detect(ctx, xy, t, n, cfg, sae, corner_flags, stream);
+        if (rc) return rc;
+        return ecc_corner_nms(ctx, xy, corner_flags, n, cfg->slice_events, cfg->width, cfg->height, box_size, cap, out,
+                              out_count, stream);
+    }
+    hipStream_t s = ecc::as_stream(stream);
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + 1, 0, 4, s), "memset(nms err)");
+    int rc = fast_detect_phases(ctx, xy, t, n, cfg, sae, corner_flags, nullptr, 3, stream, cand, n_cand);
+    if (rc) return rc;
+    rc = ecc::nms_greedy(ctx, cand, n_cand, n, cfg->slice_events, cfg->width, cfg->height, box_size, cap, out,
+                         out_count, s);
+    if (rc) return rc;
+    ECC_CHECK_LAUNCH(ctx, "fast_detect_nms");
+    return ECC_OK;
 }
 
 ECC_API int ecc_fast_detect_prepare(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,

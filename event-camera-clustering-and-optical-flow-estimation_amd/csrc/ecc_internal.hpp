@@ -71,6 +71,17 @@ int exclusive_scan_i32_i64(ecc_ctx *ctx, const int32_t *in, int64_t n, int64_t *
 void corner_state_release(const ecc_ctx *ctx);
 // Frees the per-context NMS candidate buffer (nms.hip); called by ecc_ctx_destroy.
 void nms_state_release(const ecc_ctx *ctx);
+// Grid NMS in two steps (nms.hip), so that a producer of the per-slice candidate lists (the
+// corner flag pass of ecc_fast_detect_nms) can replace nms_compact_kernel: the argument check of
+// ecc_corner_nms; the per-context candidate buffer (n xy words at cand[s * S ...], counts
+// n_cand[s]; both null when the grid form does not apply: a grid above 64 KiB of LDS); the
+// greedy pass over the lists.
+int nms_check_args(int64_t n, int32_t slice_events, int32_t width, int32_t height, int32_t box_size, int32_t cap);
+int nms_candidates(ecc_ctx *ctx, int64_t n, int32_t slice_events, int32_t width, int32_t height, int32_t box_size,
+                   uint32_t **cand, int32_t **n_cand);
+int nms_greedy(ecc_ctx *ctx, const uint32_t *cand, const int32_t *n_cand, int64_t n, int32_t slice_events,
+               int32_t width, int32_t height, int32_t box_size, int32_t cap, ecc_corner *out, int32_t *out_count,
+               hipStream_t s);
 
 // Launch-error check: kernel launches are asynchronous; this surfaces configuration errors.
 #define ECC_CHECK_LAUNCH(ctx, what)                                  \

@@ -301,13 +301,66 @@ std::map<const ecc_ctx *, NmsState> g_nms;
 
 }  // namespace
 
+namespace ecc {
+int nms_check_args(int64_t n, int32_t slice_events, int32_t width, int32_t height, int32_t box_size, int32_t cap) {
+    if (n < 0 || slice_events < 1 || slice_events > kMaxCand || width < 1 || height < 1 || width > 32767 ||
+        height > 32767 || box_size < 1 || cap < 0)
+        return ECC_ERR_INVALID;
+    return ECC_OK;
+}
+
+int nms_candidates(ecc_ctx *ctx, int64_t n, int32_t slice_events, int32_t width, int32_t height, int32_t box_size,
+                   uint32_t **cand, int32_t **n_cand) {
+    *cand = nullptr;
+    *n_cand = nullptr;
+    const int cs = 2 * (box_size / 2) + 1;
+    const int gw = (width + cs - 1) / cs, gh = (height + cs - 1) / cs;
+    if ((int64_t)(gw + 2) * (gh + 2) > kGridMaxCells) return ECC_OK;  // the one-kernel form takes it
+    const int64_t n_slices = (n + slice_events - 1) / slice_events;
+    // candidate lists: n xy words + n_slices counts, per context (grown, never shrunk)
+    const size_t need = ecc::align_up((size_t)n * 4, 256) + (size_t)n_slices * 4;
+    NmsState *st;
+    {
+        std::lock_guard<std::mutex> lk(g_nms_mu);
+        st = &g_nms[ctx];
+    }
+    if (need > st->bytes) {
+        if (st->buf) {
+            ECC_CHECK_HIP(ctx, hipDeviceSynchronize(), "sync(nms buffer)");
+            (void)hipFree(st->buf);
+            st->buf = nullptr;
+            st->bytes = 0;
+        }
+        const size_t want = ecc::align_up(need + need / 8, 1 << 20);
+        if (hipMalloc(&st->buf, want) != hipSuccess) {
+            st->buf = nullptr;
+            return ECC_ERR_NOMEM;
+        }
+        st->bytes = want;
+    }
+    *cand = static_cast<uint32_t *>(st->buf);
+    *n_cand = reinterpret_cast<int32_t *>(static_cast<char *>(st->buf) + ecc::align_up((size_t)n * 4, 256));
+    return ECC_OK;
+}
+
+int nms_greedy(ecc_ctx *ctx, const uint32_t *cand, const int32_t *n_cand, int64_t n, int32_t slice_events,
+               int32_t width, int32_t height, int32_t box_size, int32_t cap, ecc_corner *out, int32_t *out_count,
+               hipStream_t s) {
+    const int64_t n_slices = (n + slice_events - 1) / slice_events;
+    const int half = box_size / 2, cs = 2 * half + 1;
+    const int gw = (width + cs - 1) / cs, gh = (height + cs - 1) / cs;
+    ECC_TIMED(ctx, s, "nms_kernel");
+    hipLaunchKernelGGL(nms_greedy_kernel, dim3((unsigned)n_slices), dim3(kGridThreads), (size_t)(gw + 2) * (gh + 2) * 4,
+                       s, cand, n_cand, slice_events, width, height, half, gw, gh, cap, out, out_count, ctx->flags + 1);
+    return ECC_OK;
+}
+}  // namespace ecc
+
 ECC_API int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corner_flags,
                            int64_t n, int32_t slice_events, int32_t width, int32_t height,
                            int32_t box_size, int32_t cap, ecc_corner *out, int32_t *out_count,
                            ecc_stream_t stream) {
-    if (!ctx || n < 0 || slice_events < 1 || slice_events > kMaxCand || width < 1 ||
-        height < 1 || width > 32767 || height > 32767 || box_size < 1 || cap < 0)
-        return ECC_ERR_INVALID;
+    if (!ctx || ecc::nms_check_args(n, slice_events, width, height, box_size, cap)) return ECC_ERR_INVALID;
     if (n == 0) return ECC_OK;
     if (!xy || !corner_flags || !out_count || (cap > 0 && !out)) return ECC_ERR_INVALID;
     const int64_t n_slices = (n + slice_events - 1) / slice_events;
@@ -315,42 +368,18 @@ ECC_API int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corn
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + 1, 0, 4, s), "memset(nms err)");
-    const int half = box_size / 2, cs = 2 * half + 1;
-    const int gw = (width + cs - 1) / cs, gh = (height + cs - 1) / cs;
-    if ((int64_t)(gw + 2) * (gh + 2) <= kGridMaxCells) {
-        // candidate lists: n xy words + n_slices counts, per context (grown, never shrunk)
-        const size_t need = ecc::align_up((size_t)n * 4, 256) + (size_t)n_slices * 4;
-        NmsState *st;
-        {
-            std::lock_guard<std::mutex> lk(g_nms_mu);
-            st = &g_nms[ctx];
-        }
-        if (need > st->bytes) {
-            if (st->buf) {
-                ECC_CHECK_HIP(ctx, hipDeviceSynchronize(), "sync(nms buffer)");
-                (void)hipFree(st->buf);
-                st->buf = nullptr;
-                st->bytes = 0;
-            }
-            const size_t want = ecc::align_up(need + need / 8, 1 << 20);
-            if (hipMalloc(&st->buf, want) != hipSuccess) {
-                st->buf = nullptr;
-                return ECC_ERR_NOMEM;
-            }
-            st->bytes = want;
-        }
-        auto *cand = static_cast<uint32_t *>(st->buf);
-        auto *n_cand = reinterpret_cast<int32_t *>(static_cast<char *>(st->buf) + ecc::align_up((size_t)n * 4, 256));
+    uint32_t *cand = nullptr;
+    int32_t *n_cand = nullptr;
+    int rc = ecc::nms_candidates(ctx, n, slice_events, width, height, box_size, &cand, &n_cand);
+    if (rc) return rc;
+    if (cand) {
         {
             ECC_TIMED(ctx, s, "nms_compact_kernel");
             hipLaunchKernelGGL(nms_compact_kernel, dim3((unsigned)n_slices), dim3(kCompactThreads), 0, s, xy,
                                corner_flags, n, slice_events, cand, n_cand);
         }
-        ECC_TIMED(ctx, s, "nms_kernel");
-        hipLaunchKernelGGL(nms_greedy_kernel, dim3((unsigned)n_slices), dim3(kGridThreads),
-                           (size_t)(gw + 2) * (gh + 2) * 4, s,
-                           (const uint32_t *)cand, (const int32_t *)n_cand, slice_events, width, height, half, gw, gh,
-                           cap, out, out_count, ctx->flags + 1);
+        rc = ecc::nms_greedy(ctx, cand, n_cand, n, slice_events, width, height, box_size, cap, out, out_count, s);
+        if (rc) return rc;
     } else {
         ECC_TIMED(ctx, s, "nms_kernel");
         hipLaunchKernelGGL(nms_kernel, dim3((unsigned)n_slices), dim3(kThreads), 0, s, xy,

@@ -149,6 +149,7 @@ _sigs = {
     "ecc_sae_max_combine": (C.c_int, [P, P, i32, i64, P, P]),
     "ecc_corner_cfg_default": (None, [C.POINTER(CornerCfg)]),
     "ecc_fast_detect": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, P]),
+    "ecc_fast_detect_nms": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, i32, i32, P, P, P]),
     "ecc_fast_detect_prepare": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P]),
     "ecc_fast_detect_finish": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, P]),
     "ecc_fast_detect_status": (C.c_int, [P, P]),
@@ -382,6 +383,13 @@ class Context:
                     sae: DeviceArray, flags: DeviceArray):
         check(lib.ecc_fast_detect(self.ctx, xy.ptr, t.ptr, n, C.byref(cfg), sae.ptr, flags.ptr,
                                   self.stream), "ecc_fast_detect")
+
+    def fast_detect_nms(self, xy: DeviceArray, t: DeviceArray, n: int, cfg: CornerCfg, sae: DeviceArray,
+                        flags: DeviceArray, box: int, cap: int, out: DeviceArray, counts: DeviceArray):
+        """fast_detect then corner_nms over cfg's slices, with the flag pass writing the NMS
+        candidate lists (FCT/…group_track.cpp:832-837: detect, then filterCorners per slice)."""
+        check(lib.ecc_fast_detect_nms(self.ctx, xy.ptr, t.ptr, n, C.byref(cfg), sae.ptr, flags.ptr, box, cap,
+                                      out.ptr, counts.ptr, self.stream), "ecc_fast_detect_nms")
 
     def fast_detect_status(self) -> int:
         return lib.ecc_fast_detect_status(self.ctx, self.stream)

@@ -301,8 +301,18 @@ int ecc_corner_nms(ecc_ctx *ctx, const uint32_t *xy, const uint8_t *corner_flags
                    int32_t slice_events, int32_t width, int32_t height, int32_t box_size,
                    int32_t cap, ecc_corner *out, int32_t *out_count, ecc_stream_t stream);
 /* Synchronises `stream`; ECC_ERR_CAPACITY if a slice kept more than `cap` corners in the last
- * ecc_corner_nms, ECC_ERR_INVALID if a flagged event lay outside the image (it was skipped). */
+ * ecc_corner_nms / ecc_fast_detect_nms, ECC_ERR_INVALID if a flagged event lay outside the image
+ * (it was skipped). */
 int ecc_corner_nms_status(ecc_ctx *ctx, ecc_stream_t stream);
+/* Detection followed by the per-slice NMS, as the reference's slice loop runs them
+ * (FCT/…group_track.cpp:832-837: detect, then filterCorners on the slice's corners):
+ * == ecc_fast_detect(ctx, xy, t, n, cfg, sae, corner_flags) then ecc_corner_nms(ctx, xy,
+ * corner_flags, n, cfg->slice_events, cfg->width, cfg->height, box_size, cap, out, out_count),
+ * same outputs and status calls.  With slices of at most 16384 events (a multiple of 4) the
+ * flag pass writes the NMS candidate lists itself, so NMS does not re-read the flags. */
+int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                        const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags, int32_t box_size,
+                        int32_t cap, ecc_corner *out, int32_t *out_count, ecc_stream_t stream);
 /* Dense form of ecc_corner_nms' per-slice lists (multi-GPU corner gather): with
  * counts[s] <= cap as ecc_corner_nms writes them, offsets[0..n_slices] (DEVICE int64) = the
  * exclusive scan of counts (offsets[n_slices] = total) and out[offsets[s] + d] = in[s*cap + d]. */

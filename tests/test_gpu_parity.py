@@ -566,6 +566,38 @@ def test_nms_matches_oracle(ecc, orc, gpu):
         assert (g_out[s * cap: s * cap + k] == o_out[s * cap: s * cap + k]).all(), s
 
 
+@pytest.mark.parametrize("W,H,n,S,box,cap", [
+    (346, 260, 16384 * 40 + 333, 16384, 15, 4096),  # fused candidates, ragged last slice (333 % 4 = 1)
+    (346, 260, 4096 * 30 + 2, 4096, 15, 40),        # short slices, capacity hit
+    (240, 180, 12288 * 9, 12288, 8, 4096),          # even box
+    (346, 260, 6000 * 12, 6000, 15, 4096),          # S % 4 == 0 but not a power of two
+    (346, 260, 1001 * 40, 1001, 15, 4096),          # S % 4 != 0: the two-call path
+    (346, 260, 16384 * 8, 16384, 1, 4096),          # 1-px cells: the kept-list NMS kernel
+])
+def test_fast_detect_nms_matches_two_calls_and_oracle(ecc, orc, gpu, W, H, n, S, box, cap):
+    """ecc_fast_detect_nms (the flag pass writes the NMS candidate lists) == ecc_fast_detect +
+    ecc_corner_nms == the oracle: flags, final SAE, per-slice kept corners and the status."""
+    xy, t, _ = ecc.gen_events(n, seed=n % 1000 + box, width=W, height=H)
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H, slice_events=S)
+    o_out, o_cnt, rc = orc.corner_nms(xy, o_flags, W, H, box=box, cap=cap, slice_events=S)
+    ns = len(o_cnt)
+    cfg = ecc.corner_cfg(width=W, height=H, slice_events=S)
+    sae = dev(ecc, np.zeros(W * H, np.int64))
+    flags = ecc.DeviceArray(n, np.uint8)
+    d_out = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE)
+    d_cnt = ecc.DeviceArray(ns, np.int32)
+    gpu.fast_detect_nms(dev(ecc, xy), dev(ecc, t), n, cfg, sae, flags, box, cap, d_out, d_cnt)
+    assert gpu.fast_detect_status() == 0
+    assert gpu.corner_nms_status() == (ecc.ERR_CAPACITY if rc else 0)
+    assert (flags.numpy() == o_flags).all()
+    assert (sae.numpy() == o_sae).all()
+    assert (d_cnt.numpy() == o_cnt).all()
+    g_out = d_out.numpy()
+    for s in range(ns):
+        k = o_cnt[s]
+        assert (g_out[s * cap: s * cap + k] == o_out[s * cap: s * cap + k]).all(), s
+
+
 def test_nms_dense_candidates(ecc, orc, gpu):
     """Many overlapping candidates in one slice (within-chunk dependency resolution)."""
     W, H = 200, 200
