@@ -1458,7 +1458,13 @@ __host__ __device__ inline int parts_used(int parts, int64_t cells) {
 }
 constexpr int kHistUnroll = 4;
 constexpr int kHistSegs = 4;
-constexpr int kPixGrid = 256;  // pixel-pass workgroups (64 measured slower: the per-pixel assignment dominates)
+#ifndef ECC_KM_PIX_GRID
+#define ECC_KM_PIX_GRID 128
+#endif
+// pixel-pass workgroups: on the k-means chain alone 256 were fastest (64: 102 us per ten passes
+// against 82), but that chain runs beside the corner chain and has slack; 128 (87 us) leaves the
+// corner chain more room: two-stream step 0.636 -> 0.630 ms
+constexpr int kPixGrid = ECC_KM_PIX_GRID;
 
 __device__ __forceinline__ void reduce_extent(const uint32_t *__restrict__ ext, int n_ext, uint32_t *s_red,
                                               uint32_t &w, uint32_t &h) {
@@ -1485,13 +1491,19 @@ __device__ __forceinline__ void reduce_extent(const uint32_t *__restrict__ ext, 
 // The slot count is the frame's chunk count when the caller gives the frame (3 at 346x260, so
 // no workgroup of a fourth slot idles), else 4; parts fill the 256 CUs: 8 * (32 / slots).
 constexpr int kCountSlots = 4;
+#ifndef ECC_KM_COUNT_MUL
+#define ECC_KM_COUNT_MUL 8
+#endif
+#ifndef ECC_KM_LAB_GRID
+#define ECC_KM_LAB_GRID 256
+#endif
 
 __host__ __device__ inline int count_grid(int parts, int slots) { return 8 * ((parts + 7) / 8) * slots; }
 
 inline void count_layout(int64_t n_segs, int64_t cells, int &parts, int &slots) {
     const int64_t ch = (cells + kHistChunk - 1) / kHistChunk;
     slots = cells > 0 ? (int)(ch < 1 ? 1 : (ch < kCountSlots ? ch : kCountSlots)) : kCountSlots;
-    parts = (int)std::min<int64_t>(8 * (32 / slots), std::max<int64_t>(n_segs, 1));
+    parts = (int)std::min<int64_t>(ECC_KM_COUNT_MUL * (32 / slots), std::max<int64_t>(n_segs, 1));
 }
 
 __global__ void __launch_bounds__(kHistThreads)
@@ -1942,7 +1954,7 @@ static int kmeans_run_xy16_impl(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
             const int64_t frame_lds = (int64_t)ecc::align_up((size_t)frame_w, 4) * frame_h;
             if (frame_px > 0 && frame_lds <= kLabLdsBytes) {  // the frame's label image fits in LDS
                 const int lds = (int)frame_lds;
-                const dim3 g((unsigned)std::min<int64_t>((segs.n_segs + 3) / 4, 256));
+                const dim3 g((unsigned)std::min<int64_t>((segs.n_segs + 3) / 4, ECC_KM_LAB_GRID));
                 static bool lab_lds_ok = false;
                 if (!lab_lds_ok) {
                     ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&kmeans_lds_labels_kernel<16>),
