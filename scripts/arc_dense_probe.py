@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""arc_dense_kernel phase split on the bench workload (20 M events, 346x260): per heavy item,
+the average wall-clock of each phase and the longest item.  Needs a profiling library (make
+ARC_PROFILE=1 into another LIBDIR, selected with ECC_LIB).  Usage: arc_dense_probe.py"""
+import ctypes as C
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "event-camera-clustering-and-optical-flow-estimation_amd"))
+import eccpy as ecc  # noqa: E402
+
+n, W, H = 1221 * 16384, 346, 260
+ctx = ecc.Context(0)
+xy, t, _ = ecc.gen_events(n, seed=1, width=W, height=H)
+d_xy, d_t = ecc.DeviceArray.from_numpy(xy, ctx.stream), ecc.DeviceArray.from_numpy(t, ctx.stream)
+cfg = ecc.corner_cfg(width=W, height=H)
+sae = ecc.DeviceArray(W * H, np.int64)
+flags = ecc.DeviceArray(n, np.uint8)
+prof = ecc.lib.ecc_arc_dense_profile
+o, tpu = (C.c_ulonglong * 8)(), C.c_double()
+for rep in range(3):
+    ecc.check(ecc.lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
+    ctx.fast_detect(d_xy, d_t, n, cfg, sae, flags)
+    ctx.sync()
+    prof(o, C.byref(tpu))
+    items = max(o[7], 1)
+    names = ["(a) segments + B_g", "(b) staging", "(c) clamp", "circle 3", "circle 4"]
+    print(f"rep {rep}: {items} heavy items, {o[6] / items:.0f} tasks/item, longest item {o[5] / tpu.value:.1f} us; "
+          "per item (us): " + ", ".join(f"{nm} {o[k] / tpu.value / items:.2f}" for k, nm in enumerate(names)), flush=True)
