@@ -712,14 +712,38 @@ constexpr int kStageUnroll = 4;
 // covers (own tile: all; edge neighbours: the 3 facing sub-regions; corners: 1) — 13 at most.
 constexpr int kMaxSeg = 13;
 
+#ifndef ECC_ARC_PROFILE
+#define ECC_ARC_PROFILE 0
+#endif
+#if ECC_ARC_PROFILE
+// profiling builds: arc_dense_kernel's per-item phases summed (thread 0), [5] = the longest item,
+// [6] = tasks, [7] = items
+__device__ unsigned long long g_dense_prof[8];
+#define DENSE_MARK(k)                                                                \
+    do {                                                                             \
+        if (tid == 0) {                                                              \
+            const unsigned long long now_ = wall_clock64();                          \
+            atomicAdd(&g_dense_prof[k], now_ - dense_t_);                            \
+            dense_t_ = now_;                                                         \
+        }                                                                            \
+    } while (0)
+#else
+#define DENSE_MARK(k) do { } while (0)
+#endif
+
 __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const int64_t *__restrict__ t, const CornerGeom &g,
                                                const int64_t *__restrict__ item_base,
                                                const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
-                                               const int64_t *__restrict__ gB, uint32_t *__restrict__ res) {
+                                               const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask,
+                                               uint32_t *__restrict__ res) {
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
     if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if ECC_ARC_PROFILE
+    const unsigned long long dense_t0_ = wall_clock64();
+    unsigned long long dense_t_ = dense_t0_;
+#endif
     const int64_t HW = (int64_t)g.H * g.W;
     int tx, ty;
     tile_origin_xy(g, tile, tx, ty);
@@ -737,7 +761,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
     const bool in = win_lane && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
     const int64_t bq = in ? Bg[(int64_t)wy * g.W + wx] : INT64_MAX;  // INT64_MAX: outside (never read)
-    if (win_lane) L.mb[wp].mask = 0u;
+    if (win_lane) L.mb[wp].mask = in ? gmask[grp * HW + (int64_t)wy * g.W + wx] : 0u;  // as in arc_kernel
     for (int w = tid; w < kPairWords; w += kArcThreads) L.res[w] = 0u;
     if (tid == 0) {
         L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
@@ -773,6 +797,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         if (tid == 0) L.seg_pref[0] = 0;
     }
     __syncthreads();
+    DENSE_MARK(0);  // (a) segment table + B_g window
     if (L.seg_pref[1] == 0) return;  // no events in the tile: nothing to flag
     const int total = L.seg_pref[kMaxSeg];
     int pref[kMaxSeg + 1];
@@ -800,7 +825,6 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
             const int lp = (int)(ent[u].meta & 255u), j = (int)(ent[u].meta >> 8);
             const int ewp = L.seg_off[sg[u]] + (lp / kTile) * kWin + lp % kTile;
             L.T[j][ewp] = ent[u].v;
-            atomicOr(&L.mb[ewp].mask, 1u << j);
             if (sg[u] == 0 && (int64_t)grp * kGroup + j >= g.first_detect &&
                 !is_border(x0 + lp % kTile, y0 + lp / kTile, g))
                 L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)(j * kTilePix + lp);
@@ -814,6 +838,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     }
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
+    DENSE_MARK(1);  // (b) staging
 
     // (c) clamped B_g per window pixel
     if (win_lane) {
@@ -823,6 +848,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         L.mb[wp].bc = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
     }
     __syncthreads();
+    DENSE_MARK(2);  // (c)
 
     // (d) each eligible pair of the tile is tested once; circle-3 survivors are queued so that
     //     circle 4 runs on as few waves as possible
@@ -872,9 +898,18 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         }
     }
     __syncthreads();
+    DENSE_MARK(3);  // circle 3
     const int n4 = min(L.q4n, kQ4Cap);
     for (int qi = tid; qi < n4; qi += kArcThreads) circle4(L.q4[qi]);
     __syncthreads();
+    DENSE_MARK(4);  // circle 4
+#if ECC_ARC_PROFILE
+    if (tid == 0) {
+        atomicMax(&g_dense_prof[5], wall_clock64() - dense_t0_);
+        atomicAdd(&g_dense_prof[6], (unsigned long long)n_tasks);
+        atomicAdd(&g_dense_prof[7], 1ull);
+    }
+#endif
     if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
 }
 
@@ -946,9 +981,6 @@ __device__ __noinline__ bool sparse_exact_test(const SparseLds *L, int wp0, int6
 #endif
 constexpr int kSparseHold = kValCap / kArcThreads;  // entries per lane, held between the two passes
 
-#ifndef ECC_ARC_PROFILE
-#define ECC_ARC_PROFILE 0
-#endif
 #if ECC_ARC_PROFILE
 // profiling builds: per-workgroup wall-clock of arc_kernel's phases, summed (thread 0); [7] = items
 __device__ unsigned long long g_arc_prof[8];
@@ -967,8 +999,8 @@ __device__ unsigned long long g_arc_prof[8];
 __global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)  // waves/SIMD: 8 = four 8-wave workgroups per CU
 arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
            const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
-           const int64_t *__restrict__ gB, uint32_t *__restrict__ res, int64_t *__restrict__ over,
-           uint32_t *__restrict__ n_over) {
+           const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
+           int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
     __shared__ SparseLds L;
     // XCD-aware order: workgroup b runs on XCD b % 8, so XCD x takes the contiguous item range
     // [x * per, (x + 1) * per) — neighbouring tiles of one group share that XCD's L2.
@@ -998,7 +1030,10 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
     const bool in = win_lane && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
     const int64_t bq = in ? Bg[(int64_t)wy * g.W + wx] : INT64_MAX;  // INT64_MAX: outside (never read)
-    if (win_lane) L.pix[wp].mask = 0u;
+    // the slices of the group that touched the pixel, as pair_build recorded them: the OR of the
+    // window's entries for that pixel, without one LDS atomic per entry (a pixel's entries are
+    // adjacent, so those atomics hit one word from many lanes of a wave)
+    if (win_lane) L.pix[wp].mask = in ? gmask[grp * HW + (int64_t)wy * g.W + wx] : 0u;
     for (int w = tid; w < kPairWords; w += kArcThreads) L.res[w] = 0u;
     if (tid == 0) {
         L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
@@ -1067,7 +1102,6 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         const int r = ewp[u];
         const int lp = (int)(ent[u].meta & 255u), j = (int)(ent[u].meta >> 8);
         ewp[u] = L.seg_off[r] + (lp / kTile) * kWin + lp % kTile;
-        atomicOr(&L.pix[ewp[u]].mask, 1u << j);
         if (r == 0 && (int64_t)grp * kGroup + j >= g.first_detect && !is_border(x0 + lp % kTile, y0 + lp / kTile, g))
             L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)(j * kTilePix + lp);
     }
@@ -1213,11 +1247,11 @@ __global__ void __launch_bounds__(kArcThreads, 4)  // 4 waves/SIMD: two 8-wave w
 arc_dense_kernel(const int64_t *__restrict__ t, CornerGeom g, const int64_t *__restrict__ over,
                  const uint32_t *__restrict__ n_over, const int64_t *__restrict__ item_base,
                  const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
-                 const int64_t *__restrict__ gB, uint32_t *__restrict__ res) {
+                 const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res) {
     __shared__ ArcLds L;
     const uint32_t n = *n_over;
     for (uint32_t li = blockIdx.x; li < n; li += gridDim.x) {
-        arc_dense_item(L, over[li], t, g, item_base, entries, sub_end, gB, res);
+        arc_dense_item(L, over[li], t, g, item_base, entries, sub_end, gB, gmask, res);
         __syncthreads();
     }
 }
@@ -1621,13 +1655,13 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
         hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
                            (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
-                           (const int64_t *)gi.B, gi.res, gi.over, gi.n_over);
+                           (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over);
     }
     {
         ECC_TIMED(ctx, s, "arc_dense_kernel");  // the overflow list, dense planes
         hipLaunchKernelGGL(arc_dense_kernel, dim3(512), dim3(kArcThreads), 0, s, t, g, (const int64_t *)gi.over,
                            (const uint32_t *)gi.n_over, (const int64_t *)gi.item_base, (const PairEntry *)gi.entries,
-                           (const int32_t *)gi.sub_end, (const int64_t *)gi.B, gi.res);
+                           (const int32_t *)gi.sub_end, (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res);
     }
     {
         ECC_TIMED(ctx, s, "flags_kernel");
@@ -1664,6 +1698,16 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
 #if ECC_ARC_PROFILE
 // Profiling builds only (make ARC_PROFILE=1): arc_kernel's summed per-workgroup phase ticks
 // since the last call (reset after reading); out[7] = items timed; ticks_per_us from the device.
+ECC_API int ecc_arc_dense_profile(unsigned long long *out8, double *ticks_per_us) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_dense_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return ECC_ERR_HIP;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_dense_prof), z, sizeof(z));
+    int khz = 0;
+    hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
+    *ticks_per_us = khz / 1000.0;
+    return ECC_OK;
+}
+
 ECC_API int ecc_arc_profile(unsigned long long *out8, double *ticks_per_us) {
     if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_arc_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return ECC_ERR_HIP;
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
