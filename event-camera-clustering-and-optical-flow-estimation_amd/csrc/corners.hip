@@ -335,6 +335,15 @@ __device__ __forceinline__ GroupRef group_ref(const int64_t *__restrict__ t, con
 constexpr int kSub = 9;
 __host__ __device__ constexpr int sub_band(int c) { return c < kHalo ? 0 : (c < kTile - kHalo ? 1 : 2); }
 __host__ __device__ constexpr int sub_of(int lp) { return sub_band(lp / kTile) * 3 + sub_band(lp % kTile); }
+// The arc kernels stage a window's values from exactly these sub-regions and read each window
+// pixel's slice mask from pair_build's mask image: a mask bit without a staged value would read
+// stale LDS.  That holds only while a neighbour tile's facing band is the window's halo.
+static_assert(kWin == kTile + 2 * kHalo, "window = tile + halo on both sides");
+static_assert(kHalo >= 4, "the circles reach 4 px from the pixel under test");
+static_assert(kTile >= 2 * kHalo, "the two border bands of a tile must not overlap");
+static_assert(sub_band(kHalo - 1) == 0 && sub_band(kHalo) == 1 && sub_band(kTile - kHalo - 1) == 1 &&
+                  sub_band(kTile - kHalo) == 2 && sub_band(kTile - 1) == 2,
+              "a tile's border bands are exactly kHalo pixels wide (the neighbours' halo)");
 
 // Tile pixels in (sub-region, pixel) order.
 struct SubOrder {
@@ -641,6 +650,7 @@ struct ArcLds {
     int32_t mixed;       // clamped values not all equal to the window minimum of B
     int32_t n_tasks;
     int32_t q4n;
+    int32_t n_exact;      // some task needs the exact int64 test
     int64_t seg_lo[16];   // window segments: first entry (absolute) ...
     int32_t seg_pref[16]; // ... exclusive prefix of their lengths ...
     int32_t seg_off[16];  // ... and the window offset of the neighbour tile's origin
@@ -683,6 +693,8 @@ __device__ __forceinline__ void exact_values(const ArcLds *L, int wp0, int64_t q
                                              const int8_t *dy, const int8_t *dx, const ExactCtx &c, int64_t (&v)[N]) {
 #pragma unroll
     for (int k = 0; k < N; ++k) {
+        // four neighbours' loads in flight at a time: all of them at once spilled (rare path)
+        if (k > 0 && k % 4 == 0) __builtin_amdgcn_sched_barrier(0);
         const int wp = wp0 + dy[k] * kWin + dx[k];
         const uint32_t mk = L->mb[wp].mask & below;
         const uint32_t tv = mk ? L->T[31 - __clz(mk)][wp] : 0u;
@@ -692,12 +704,15 @@ __device__ __forceinline__ void exact_values(const ArcLds *L, int wp0, int64_t q
     }
 }
 
-__device__ __noinline__ bool exact_circle_test(const ArcLds *L, int wp0, int64_t q0, int j, bool c3, const ExactCtx c) {
-    const uint32_t below = below_mask(j);
-    if (c3) {
+
+// Both circles exactly (circle 3 skipped when it already passed on keys).  Out of line, called
+// only from arc_dense_item's exact phase, where nothing else is live.
+__device__ __noinline__ bool exact_pair_test(const ArcLds *L, int wp0, int64_t q0, uint32_t below, bool c3_passed,
+                                             const ExactCtx c) {
+    if (!c3_passed) {
         int64_t v3[16];
         exact_values<16>(L, wp0, q0, below, c3dy, c3dx, c, v3);
-        return arc_streak<16, 3, 6>(v3);
+        if (!arc_streak<16, 3, 6>(v3)) return false;
     }
     int64_t v4[20];
     exact_values<20>(L, wp0, q0, below, c4dy, c4dx, c, v4);
@@ -768,6 +783,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         L.mixed = 0;
         L.n_tasks = 0;
         L.q4n = 0;
+        L.n_exact = 0;
     }
     if (tid < kMaxSeg) {
         // own tile: every sub-region; above/below: their facing rows; corners: one sub-region;
@@ -850,59 +866,73 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     __syncthreads();
     DENSE_MARK(2);  // (c)
 
-    // (d) each eligible pair of the tile is tested once; circle-3 survivors are queued so that
-    //     circle 4 runs on as few waves as possible
+    // (d) each eligible pair of the tile is tested once, in three phases so that no phase holds
+    //     another's registers (and no call): circle 3 on clamped keys, its survivors queued so
+    //     that circle 4 runs on as few waves as possible; circle 4 on clamped keys; then the
+    //     exact int64 tests of whatever the keys could not decide, marked in the task list
+    //     itself (bit 14: circle 3 undecided; bit 15: circle 3 passed, circle 4 still open).
+    //     Wide groups and values above t_last (exact_only) take every task exactly.
     const int n_tasks = L.n_tasks;
     const bool fast = !L.exact_only;
     const bool ties_exact = !L.mixed;
-    const ExactCtx ec{Bg, t, grp_first, Lt, g.W, narrow};
-    auto circle4 = [&](int pi) {
-        const int j = pi / kTilePix, lp = pi % kTilePix;
-        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-        const uint32_t below = below_mask(j);
-        int r4 = -1;
-        if (fast) {
-            uint32_t k4[32];
-#pragma unroll
-            for (int k = 0; k < 20; ++k) k4[k] = (win_value(L, wp0 + c4dy[k] * kWin + c4dx[k], below) << 5) | k;
-#pragma unroll
-            for (int k = 20; k < 32; ++k) k4[k] = 0u;
-            r4 = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
-        }
-        if (r4 < 0) {
-            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
-            r4 = exact_circle_test(&L, wp0, q0, j, false, ec) ? 1 : 0;
-        }
-        if (r4 == 1) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
-    };
-    for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
-        const int pi = L.tasks[ti];
-        const int j = pi / kTilePix, lp = pi % kTilePix;
-        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-        const uint32_t below = below_mask(j);
-        int r3 = -1;
-        if (fast) {
+    constexpr uint16_t kOpen3 = 0x4000, kOpen4 = 0x8000;
+    if (fast) {
+        for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+            const int pi = L.tasks[ti];
+            const int j = pi / kTilePix, lp = pi % kTilePix;
+            const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+            const uint32_t below = below_mask(j);
             uint32_t k3[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) k3[k] = (win_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
-            r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
-        }
-        if (r3 < 0) {
-            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
-            r3 = exact_circle_test(&L, wp0, q0, j, true, ec) ? 1 : 0;
-        }
-        if (r3 == 1) {
-            const int qi = atomicAdd(&L.q4n, 1);
-            if (qi < kQ4Cap) L.q4[qi] = (uint16_t)pi;
-            else circle4(pi);  // queue full (rare): test here
+            const int r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+            if (r3 > 0) {
+                const int qi = atomicAdd(&L.q4n, 1);
+                if (qi < kQ4Cap) L.q4[qi] = (uint16_t)ti;
+                else { L.tasks[ti] = (uint16_t)(pi | kOpen4); L.n_exact = 1; }  // queue full (rare)
+            } else if (r3 < 0) {
+                L.tasks[ti] = (uint16_t)(pi | kOpen3);
+                L.n_exact = 1;
+            }
         }
     }
     __syncthreads();
     DENSE_MARK(3);  // circle 3
     const int n4 = min(L.q4n, kQ4Cap);
-    for (int qi = tid; qi < n4; qi += kArcThreads) circle4(L.q4[qi]);
+    for (int qi = tid; qi < n4; qi += kArcThreads) {
+        const int ti = L.q4[qi];
+        const int pi = L.tasks[ti];
+        const int j = pi / kTilePix, lp = pi % kTilePix;
+        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        const uint32_t below = below_mask(j);
+        uint32_t k4[32];
+#pragma unroll
+        for (int k = 0; k < 20; ++k) k4[k] = (win_value(L, wp0 + c4dy[k] * kWin + c4dx[k], below) << 5) | k;
+#pragma unroll
+        for (int k = 20; k < 32; ++k) k4[k] = 0u;
+        const int r4 = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
+        if (r4 > 0) {
+            atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
+        } else if (r4 < 0) {
+            L.tasks[ti] = (uint16_t)(pi | kOpen4);
+            L.n_exact = 1;
+        }
+    }
     __syncthreads();
     DENSE_MARK(4);  // circle 4
+    if (!fast || L.n_exact) {  // uniform; rare: the exact int64 tests
+        const ExactCtx ec{Bg, t, grp_first, Lt, g.W, narrow};
+        for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+            const int e = L.tasks[ti], pi = e & 0x3fff;
+            if (fast && !(e & (kOpen3 | kOpen4))) continue;
+            const int j = pi / kTilePix, lp = pi % kTilePix;
+            const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
+            const uint32_t below = below_mask(j);
+            if (exact_pair_test(&L, wp0, q0, below, (e & kOpen4) != 0, ec)) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
+        }
+        __syncthreads();
+    }
 #if ECC_ARC_PROFILE
     if (tid == 0) {
         atomicMax(&g_dense_prof[5], wall_clock64() - dense_t0_);
@@ -949,33 +979,6 @@ __device__ __forceinline__ uint32_t sparse_value(const SparseLds &L, int wp, uin
     return L.vals[p.y + __popc(p.x & below)];
 }
 
-template <int N>
-__device__ __forceinline__ void sparse_exact_values(const SparseLds *L, int wp0, int64_t q0, uint32_t below,
-                                                    const int8_t *dy, const int8_t *dx, const ExactCtx &c,
-                                                    int64_t (&v)[N]) {
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        const int wp = wp0 + dy[k] * kWin + dx[k];
-        const uint32_t mk = L->pix[wp].mask & below;
-        const uint32_t tv = mk ? L->vals[L->pix[wp].off + __popc(mk)] : 0u;
-        v[k] = !mk      ? c.Bg[q0 + (int64_t)dy[k] * c.W + dx[k]]
-               : c.narrow ? c.Lt + (int64_t)tv
-                          : c.t[c.grp_first + tv - 1u];
-    }
-}
-
-__device__ __noinline__ bool sparse_exact_test(const SparseLds *L, int wp0, int64_t q0, int j, bool c3, const ExactCtx c) {
-    const uint32_t below = below_mask(j);
-    if (c3) {
-        int64_t v3[16];
-        sparse_exact_values<16>(L, wp0, q0, below, c3dy, c3dx, c, v3);
-        return arc_streak<16, 3, 6>(v3);
-    }
-    int64_t v4[20];
-    sparse_exact_values<20>(L, wp0, q0, below, c4dy, c4dx, c, v4);
-    return arc_streak<20, 4, 8>(v4);
-}
-
 #ifndef ECC_ARC_WAVES
 #define ECC_ARC_WAVES 8
 #endif
@@ -1020,7 +1023,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     const int x0 = tx * kTile, y0 = ty * kTile;
     const int wx0 = x0 - kHalo, wy0 = y0 - kHalo;
     const GroupRef gr = group_ref(t, g, grp);
-    const int64_t grp_first = gr.first, Lt = gr.Lt;
+    const int64_t Lt = gr.Lt;
     const bool narrow = gr.narrow;
     const int64_t *Bg = gB + grp * HW;
 
@@ -1133,6 +1136,10 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         bcv = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
     }
     __syncthreads();
+    if (L.exact_only) {  // uniform: a wide group or a value above t_last — the exact kernel takes it
+        if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
+        return;
+    }
     if (win_lane) {
         int off = incl - cnt;
         for (int w = 0; w < wave; ++w) off += L.wave_tot[w];
@@ -1152,92 +1159,63 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     __syncthreads();
 
     ARC_MARK(2);  // (c, d) list offsets, B_g slots, value scatter
-    // (e) tests through the compact lists.  The circle-3 loop holds no call: its survivors and
-    //     the tasks its clamped keys cannot decide share one LDS queue (bit 15 = exact circle 3
-    //     first), drained after a barrier.  Without the call's saved registers the kernel fits
-    //     64 VGPRs: four 8-wave workgroups per CU.  Wide groups, and a queue overflow (redo),
-    //     take every task through the full path in a cold loop.
+    // (e) tests through the compact lists, on clamped 32-bit keys only.  This kernel holds no
+    //     exact int64 path and no call: an item its keys cannot decide (a wide group, a value
+    //     above t_last, a tie the clamping may have merged) or whose circle-3 survivors overflow
+    //     the queue goes whole to arc_dense_kernel, which redoes it exactly.  So the kernel fits
+    //     64 VGPRs without spills: four 8-wave workgroups per CU.
     const int n_tasks = L.n_tasks;
-    const bool fast = !L.exact_only;
     const bool ties_exact = !L.mixed;
-    const ExactCtx ec{Bg, t, grp_first, Lt, g.W, narrow};
-    if (fast) {
-        for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
-            const int pi = L.tasks[ti];
-            const int j = pi / kTilePix, lp = pi % kTilePix;
-            const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-            const uint32_t below = below_mask(j);
-            uint32_t k3[16];
+    for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+        const int pi = L.tasks[ti];
+        const int j = pi / kTilePix, lp = pi % kTilePix;
+        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        const uint32_t below = below_mask(j);
+        uint32_t k3[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) k3[k] = (sparse_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
-            const int r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
-            if (r3 != 0) {
-                const int qi = atomicAdd(&L.q4n, 1);
-                if (qi < kQ4Cap) L.q4[qi] = (uint16_t)(pi | (r3 < 0 ? 0x8000 : 0));
-                else L.redo = 1;
-            }
+        for (int k = 0; k < 16; ++k) k3[k] = (sparse_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
+        const int r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+        if (r3 > 0) {
+            const int qi = atomicAdd(&L.q4n, 1);
+            if (qi < kQ4Cap) L.q4[qi] = (uint16_t)pi;
+            else L.redo = 1;
+        } else if (r3 < 0) {
+            L.redo = 1;
         }
     }
     __syncthreads();
     ARC_MARK(3);  // circle 3
-    const bool redo = !fast || L.redo;  // uniform
-    auto circle4 = [&](int pi) {
+    if (L.redo) {  // uniform
+        if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
+        return;
+    }
+    const int n4 = L.q4n;
+#if ECC_ARC_PROFILE
+    if (tid == 0) atomicAdd(&g_arc_prof[6], (unsigned long long)n4);
+#endif
+    for (int qi = tid; qi < n4; qi += kArcThreads) {
+        const int pi = L.q4[qi];
         const int j = pi / kTilePix, lp = pi % kTilePix;
         const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
         const uint32_t below = below_mask(j);
-        int r4 = -1;
-        if (fast) {
-            uint32_t k4[32];
+        uint32_t k4[32];
 #pragma unroll
-            for (int k = 0; k < 20; ++k) k4[k] = (sparse_value(L, wp0 + c4dy[k] * kWin + c4dx[k], below) << 5) | k;
+        for (int k = 0; k < 20; ++k) k4[k] = (sparse_value(L, wp0 + c4dy[k] * kWin + c4dx[k], below) << 5) | k;
 #pragma unroll
-            for (int k = 20; k < 32; ++k) k4[k] = 0u;
-            r4 = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
-        }
-        if (r4 < 0) {
-            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
-            r4 = sparse_exact_test(&L, wp0, q0, j, false, ec) ? 1 : 0;
-        }
-        if (r4 == 1) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
-    };
-    auto exact3 = [&](int pi) {
-        const int j = pi / kTilePix, lp = pi % kTilePix;
-        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-        const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
-        return sparse_exact_test(&L, wp0, q0, j, true, ec);
-    };
-    if (!redo) {
-        const int n4 = L.q4n;
-#if ECC_ARC_PROFILE
-        if (tid == 0) atomicAdd(&g_arc_prof[6], (unsigned long long)n4);
-#endif
-        for (int qi = tid; qi < n4; qi += kArcThreads) {
-            const int e = L.q4[qi], pi = e & 0x7fff;
-            if (!(e & 0x8000) || exact3(pi)) circle4(pi);
-        }
-    } else {
-        // cold: wide groups (every test exact) or more queued tasks than kQ4Cap
-        for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
-            const int pi = L.tasks[ti];
-            int r3 = -1;
-            if (fast) {
-                const int j = pi / kTilePix, lp = pi % kTilePix;
-                const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-                const uint32_t below = below_mask(j);
-                uint32_t k3[16];
-#pragma unroll
-                for (int k = 0; k < 16; ++k) k3[k] = (sparse_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
-                r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
-            }
-            if (r3 < 0) r3 = exact3(pi) ? 1 : 0;
-            if (r3 == 1) circle4(pi);
-        }
+        for (int k = 20; k < 32; ++k) k4[k] = 0u;
+        const int r4 = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
+        if (r4 > 0) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
+        else if (r4 < 0) L.redo = 1;
     }
     __syncthreads();
     ARC_MARK(4);  // circle 4
 #if ECC_ARC_PROFILE
     if (tid == 0) atomicAdd(&g_arc_prof[7], 1ull);
 #endif
+    if (L.redo) {  // uniform: a circle-4 tie the clamped keys cannot decide
+        if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
+        return;
+    }
     if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
 }
 

@@ -390,14 +390,14 @@ ECC_API int ecc_dbscan_cloud_f64(ecc_ctx *ctx, const double *pts, int64_t n, int
                                 dups, dup_cap, n_dups, stream);
 }
 
+// Only the duplicate-capacity bit of this path's own word (a radius call in between cannot change
+// it).  Non-finite points are not an error: as in the reference's radiusSearch they are nobody's
+// neighbour, so they come out as noise (label -1) and the other clusters are unaffected.
 ECC_API int ecc_dbscan_cloud_status(ecc_ctx *ctx, ecc_stream_t stream) {
     if (!ctx) return ECC_ERR_INVALID;
-    int32_t f = 0, bad = 0;
+    int32_t f = 0;
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipMemcpyAsync(&f, ctx->flags + kFlagWord, 4, hipMemcpyDeviceToHost, s), "read dbscan err");
-    ECC_CHECK_HIP(ctx, hipMemcpyAsync(&bad, ctx->flags + ecc::rgrid::kBadWord, 4, hipMemcpyDeviceToHost, s),
-                  "read dbscan bad");
     ECC_CHECK_HIP(ctx, hipStreamSynchronize(s), "sync");
-    if (bad) return ECC_ERR_INVALID;
     return (f & 2) ? ECC_ERR_CAPACITY : ECC_OK;
 }

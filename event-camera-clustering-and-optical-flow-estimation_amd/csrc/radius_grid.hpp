@@ -27,7 +27,7 @@ namespace rgrid {
 
 constexpr int kThreads = 256;
 constexpr int kGridWord = 16;  // ctx->flags[16..]: bounding-box keys, then the grid geometry
-constexpr int kBadWord = 7;    // ctx->flags[7]: bit 1 = a non-finite coordinate was seen
+constexpr int kBadWord = 7;    // ctx->flags[7]: bit 1 = a non-finite coordinate was seen (radius status)
 
 struct Grid {
     double mn[3];
@@ -59,12 +59,23 @@ bbox_kernel(const T *__restrict__ pts, int64_t n, int dim, int64_t *keys, int32_
     int64_t mx[3] = {(int64_t)0x8000000000000000ull, (int64_t)0x8000000000000000ull, (int64_t)0x8000000000000000ull};
     bool fin = true;
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+        // a point with a non-finite coordinate is left out of the box: its distance to every
+        // point, itself included, is NaN or inf, never <= eps^2 (the reference's `d2 <= r2`), so
+        // whatever cell it lands in it is nobody's neighbour
+        double v[3] = {0.0, 0.0, 0.0};
+        bool pf = true;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             if (d >= dim) break;
-            const double v = (double)pts[i * dim + d];
-            fin = fin && isfinite(v);
-            const int64_t k = dkey(v);
+            v[d] = (double)pts[i * dim + d];
+            pf = pf && isfinite(v[d]);
+        }
+        fin = fin && pf;
+        if (!pf) continue;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            if (d >= dim) break;
+            const int64_t k = dkey(v[d]);
             mn[d] = k < mn[d] ? k : mn[d];
             mx[d] = k > mx[d] ? k : mx[d];
         }
@@ -86,8 +97,7 @@ bbox_kernel(const T *__restrict__ pts, int64_t n, int dim, int64_t *keys, int32_
         }
 }
 
-static __global__ void grid_setup_kernel(const int64_t *keys, int dim, double eps, int64_t max_cells, const int32_t *bad,
-                                  Grid *g) {
+static __global__ void grid_setup_kernel(const int64_t *keys, int dim, double eps, int64_t max_cells, Grid *g) {
     if (threadIdx.x != 0) return;
     Grid r{};
     r.dim = dim;
@@ -96,7 +106,7 @@ static __global__ void grid_setup_kernel(const int64_t *keys, int dim, double ep
     for (int d = 0; d < dim; ++d) {
         r.mn[d] = dval(keys[d]);
         span[d] = dval(keys[3 + d]) - r.mn[d];
-        if (*bad || !(span[d] >= 0.0)) span[d] = 0.0;  // non-finite input: one cell (status reports it)
+        if (!(span[d] >= 0.0)) span[d] = 0.0;  // no finite point at all: one cell
     }
     for (;;) {
         int64_t cells = 1;
@@ -226,7 +236,7 @@ int build(ecc_ctx *ctx, const T *pts, int64_t n, int dim, double eps, hipStream_
         ECC_TIMED(ctx, s, "radius_grid_kernels");
         hipLaunchKernelGGL(bbox_kernel<T>, dim3(blocks), dim3(kThreads), 0, s, pts, n, dim, w.keys, bad);
         hipLaunchKernelGGL(grid_setup_kernel, dim3(1), dim3(64), 0, s, (const int64_t *)w.keys, dim, eps, w.max_cells,
-                           (const int32_t *)bad, w.grid);
+                           w.grid);
         ECC_CHECK_HIP(ctx, hipMemsetAsync(w.cell_cnt, 0, (size_t)w.max_cells * 4, s), "memset(cells)");
         hipLaunchKernelGGL(cell_count_kernel<T>, dim3(blocks), dim3(kThreads), 0, s, pts, n, (const Grid *)w.grid,
                            w.cell_of, w.cell_cnt);

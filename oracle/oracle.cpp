@@ -765,7 +765,9 @@ static int dbscan_cloud(const T *pts, int n, int dim, double eps, int min_pts, i
     return (int)clusters.size();
 }
 
-// 3-D float points (x, y, z per point); labels = the first output cluster holding the point
+// 3-D float points (x, y, z per point); labels = the LAST output cluster holding the point (the
+// shared body above overwrites in output order).  The GPU label is the first-claim cluster's rank,
+// so where border points have duplicate memberships compare cluster lists, not labels.
 ORC_API int orc_dbscan(const float *pts, int n, double eps, int min_pts, int min_size, int max_size,
                        int32_t *labels) {
     return dbscan_cloud<float>(pts, n, 3, eps, min_pts, min_size, max_size, labels, nullptr, nullptr, 0);

@@ -146,13 +146,38 @@ def test_dbscan_cloud_duplicate_capacity_and_edge_cases(ecc, orc, gpu):
     same = np.full((500, 3), 7.25, np.float32)
     _, _, _, got = gpu_dbscan_cloud(ecc, gpu, same, 0.0, 500, 1, 1 << 30)
     assert len(got) == 1 and len(got[0]) == 500
-    # a non-finite coordinate is reported, not clustered
-    bad = np.ones((10, 3), np.float32)
-    bad[3, 1] = np.nan
-    d_p = dev(ecc, bad.ravel())
-    d_lab, d_nc, d_nd = ecc.DeviceArray(10, np.int32), ecc.DeviceArray(1, np.int32), ecc.DeviceArray(1, np.int64)
-    gpu.dbscan_cloud(d_p, 10, 3, 1.0, 1, 1, 10, d_lab, d_nc, None, 0, d_nd)
-    assert gpu.dbscan_cloud_status() == ecc.ERR_INVALID
+
+
+def test_dbscan_cloud_non_finite_points_are_noise(ecc, orc, gpu):
+    """A point with a NaN or inf coordinate: `d2 <= r2` (DBSCAN_simple.h:132-136) is false for
+    every pair it is in, itself included, so the reference makes it noise and clusters the rest
+    as without it (a non-dense PCL cloud).  Same here, with no error status — and a radius call
+    in between does not change the status of the DBSCAN call before it."""
+    pts = event_cloud(ecc, 8000, 31, 0.3, 0.45)
+    rng = np.random.default_rng(3)
+    bad = rng.choice(len(pts), 40, replace=False)
+    vals = [np.nan, np.inf, -np.inf]
+    for k, i in enumerate(bad):
+        pts[i, k % 3] = vals[k % 3]
+    pts[bad[0]] = np.nan  # all coordinates
+    _, ref = orc.dbscan_cloud(pts, 6.0, 5, 1, 1 << 30)
+    st, _, lab, got = gpu_dbscan_cloud(ecc, gpu, pts, 6.0, 5, 1, 1 << 30)
+    assert st == 0 and (lab[bad] == -1).all()
+    assert_same_clusters(got, ref)
+    assert len(got) > 5
+    # an all-non-finite cloud: all noise
+    allbad = np.full((50, 3), np.nan, np.float32)
+    st, _, lab, got = gpu_dbscan_cloud(ecc, gpu, allbad, 1.0, 1, 1, 10)
+    assert st == 0 and got == [] and (lab == -1).all()
+    # the radius path still reports non-finite input; DBSCAN's own status is its own word
+    d_p = dev(ecc, pts.ravel())
+    d_lab, d_nc, d_nd = ecc.DeviceArray(len(pts), np.int32), ecc.DeviceArray(1, np.int32), ecc.DeviceArray(1, np.int64)
+    d_d = ecc.DeviceArray(2 << 20, np.int64)
+    gpu.dbscan_cloud(d_p, len(pts), 3, 6.0, 5, 1, 1 << 30, d_lab, d_nc, d_d, 1 << 20, d_nd)
+    cnt = ecc.DeviceArray(len(pts), np.int32)
+    gpu.radius_counts_f32(d_p, len(pts), 3, 6.0, 0, cnt)
+    assert gpu.radius_status() == ecc.ERR_INVALID
+    assert gpu.dbscan_cloud_status() == 0
 
 
 @pytest.mark.parametrize("min_pts", [1, 8, 64, 65, 100, 300])
