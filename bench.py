@@ -81,10 +81,6 @@ def parse():
                     help="run the sharded step even at world size 1: a 1-rank process group of --dist-backend "
                          "(nccl = RCCL), so the C5 code path — collectives, SAE combine, corner pack/gather, "
                          "track merge — executes on a single GPU")
-    ap.add_argument("--kmeans-priority", type=int, default=0, choices=(-1, 0, 1),
-                    help="priority of the k-means chain's stream (1 high, 0 default, -1 low)")
-    ap.add_argument("--kmeans-cus", type=int, default=0,
-                    help="single GPU: run the k-means chain on this many CUs and the corner chain on the rest (0: shared)")
     ap.add_argument("--overlap", action="store_true",
                     help="keep the two-stream sharded schedule under gloo too (correctness rehearsals; gloo "
                          "collectives block the host, so it is not a timing configuration)")
@@ -190,29 +186,9 @@ def main():
     # single GPU: downsample -> k-means and the corner chain read the same resident batch and are
     # independent, so they run on two streams (fork/join with events) and overlap
     s2, ev_fork, ev_join = ecc.P(), ecc.P(), ecc.P()
-    split_restore = None
     if not dist:
-        # stream priority of the k-means chain (--kmeans-priority): measured without effect on
-        # the step (0.682 / 0.681 / 0.672 ms at high / default / low), so the default stays
-        ecc.check(lib.ecc_stream_create_priority(ecc.C.byref(s2), args.kmeans_priority), "stream")
-        if args.kmeans_cus > 0:
-            # spatial split: the latency-bound k-means chain gets its own CUs and the corner chain
-            # the rest, so neither queues behind the other's workgroups.  Measured slower than the
-            # shared default (0.68 ms): 16 CUs 1.296, 24 0.934, 32 0.709, 48 0.724, 64 0.745 ms/step
-            # (scripts/gpu_cusplit_ab.sh), so the default stays 0
-            ncu = ecc.C.c_int32(0)
-            ecc.check(lib.ecc_device_cu_count(local, ecc.C.byref(ncu)), "cu count")
-            words = (ncu.value + 31) // 32
-            km = (ecc.C.c_uint32 * words)()
-            cm = (ecc.C.c_uint32 * words)()
-            for c in range(ncu.value):
-                (km if c < args.kmeans_cus else cm)[c // 32] |= 1 << (c % 32)
-            s_km, s_cn = ecc.P(), ecc.P()
-            ecc.check(lib.ecc_stream_create_cu_mask(ecc.C.byref(s_km), km, words), "k-means stream")
-            ecc.check(lib.ecc_stream_create_cu_mask(ecc.C.byref(s_cn), cm, words), "corner stream")
-            s2 = s_km
-            split_restore = ctx.stream  # the later measurements run unrestricted again
-            ctx.stream = s_cn.value
+        # the k-means chain's stream (a priority or a CU split for it measured no faster: DESIGN §5)
+        ecc.check(lib.ecc_stream_create(ecc.C.byref(s2)), "stream")
         ecc.check(lib.ecc_event_create(ecc.C.byref(ev_fork)), "event")
         ecc.check(lib.ecc_event_create(ecc.C.byref(ev_join)), "event")
 
@@ -282,8 +258,6 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_step = elapsed / args.steps * 1e3
-    if split_restore is not None:
-        ctx.stream = split_restore
 
     # 2. the kernel-timing pass: the same K steps again with HIP events recorded around every
     #    launch on its stream (ecc_ctx_set_timing) -> per-kernel average durations.  It runs on
@@ -527,9 +501,7 @@ def main():
             "events_per_gpu": n, "reps_per_gpu": n_reps, "width": W, "height": H, "k": K,
             "kmeans_iters": I, "parallelism": f"time-window shards x{world}",
             "launch": "hipGraph replay of the captured step" if graph is not None else "eager launches",
-            "streams": (f"k-means chain on {args.kmeans_cus} CUs, corner chain on the others (CU-masked streams)"
-                        if split_restore is not None else
-                        "two streams sharing all CUs" if not (dist or args.serial) else "see parallelism"),
+            "streams": "two streams sharing all CUs" if not (dist or args.serial) else "see parallelism",
         },
         "roofline": {
             "kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -1191,7 +1191,10 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     }
     const int n4 = L.q4n;
 #if ECC_ARC_PROFILE
-    if (tid == 0) atomicAdd(&g_arc_prof[6], (unsigned long long)n4);
+    if (tid == 0) {
+        atomicAdd(&g_arc_prof[5], (unsigned long long)n_tasks);
+        atomicAdd(&g_arc_prof[6], (unsigned long long)n4);
+    }
 #endif
     for (int qi = tid; qi < n4; qi += kArcThreads) {
         const int pi = L.q4[qi];

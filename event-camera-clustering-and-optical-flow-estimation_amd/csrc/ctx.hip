@@ -208,35 +208,6 @@ ECC_API int ecc_stream_create(ecc_stream_t *stream) {
     *stream = reinterpret_cast<ecc_stream_t>(s);
     return ECC_OK;
 }
-// A non-blocking stream at a scheduling priority: > 0 the device's highest, < 0 its lowest, 0 the
-// default.  A short latency-bound chain (the k-means passes) on a high-priority stream gets its
-// workgroups dispatched ahead of a saturating chain's as CUs free up.
-ECC_API int ecc_stream_create_priority(ecc_stream_t *stream, int32_t priority) {
-    if (!stream) return ECC_ERR_INVALID;
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return ECC_ERR_HIP;
-    const int p = priority > 0 ? greatest : (priority < 0 ? least : 0);
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, p) != hipSuccess) return ECC_ERR_HIP;
-    *stream = reinterpret_cast<ecc_stream_t>(s);
-    return ECC_OK;
-}
-// A non-blocking stream whose kernels run only on the CUs whose bits are set in mask[0..n_words)
-// (bit i of word w = CU 32 w + i): two concurrent chains can be given disjoint parts of the GPU.
-ECC_API int ecc_stream_create_cu_mask(ecc_stream_t *stream, const uint32_t *mask, int32_t n_words) {
-    if (!stream || !mask || n_words < 1) return ECC_ERR_INVALID;
-    hipStream_t s = nullptr;
-    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask) != hipSuccess) return ECC_ERR_HIP;
-    *stream = reinterpret_cast<ecc_stream_t>(s);
-    return ECC_OK;
-}
-ECC_API int ecc_device_cu_count(int32_t device, int32_t *n_cu) {
-    if (!n_cu) return ECC_ERR_INVALID;
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return ECC_ERR_HIP;
-    *n_cu = v;
-    return ECC_OK;
-}
 ECC_API int ecc_stream_destroy(ecc_stream_t stream) { ECC_RT(hipStreamDestroy(ecc::as_stream(stream))); }
 ECC_API int ecc_event_create(void **event) {
     if (!event) return ECC_ERR_INVALID;

@@ -114,9 +114,6 @@ _sigs = {
     "ecc_memcpy_d2h": (C.c_int, [P, P, C.c_size_t, P]),
     "ecc_memcpy_d2d": (C.c_int, [P, P, C.c_size_t, P]),
     "ecc_stream_create": (C.c_int, [C.POINTER(P)]),
-    "ecc_stream_create_priority": (C.c_int, [C.POINTER(P), C.c_int32]),
-    "ecc_stream_create_cu_mask": (C.c_int, [C.POINTER(P), C.POINTER(C.c_uint32), C.c_int32]),
-    "ecc_device_cu_count": (C.c_int, [C.c_int32, C.POINTER(C.c_int32)]),
     "ecc_stream_destroy": (C.c_int, [P]),
     "ecc_event_create": (C.c_int, [C.POINTER(P)]),
     "ecc_event_destroy": (C.c_int, [P]),

@@ -69,11 +69,6 @@ int ecc_memcpy_h2d(void *dst, const void *src, size_t bytes, ecc_stream_t stream
 int ecc_memcpy_d2h(void *dst, const void *src, size_t bytes, ecc_stream_t stream);
 int ecc_memcpy_d2d(void *dst, const void *src, size_t bytes, ecc_stream_t stream);
 int ecc_stream_create(ecc_stream_t *stream);
-/* priority > 0: the device's highest stream priority, < 0: its lowest, 0: default */
-int ecc_stream_create_priority(ecc_stream_t *stream, int32_t priority);
-/* kernels of this stream run only on the CUs set in mask (bit i of word w = CU 32 w + i) */
-int ecc_stream_create_cu_mask(ecc_stream_t *stream, const uint32_t *mask, int32_t n_words);
-int ecc_device_cu_count(int32_t device, int32_t *n_cu);
 int ecc_stream_destroy(ecc_stream_t stream);
 int ecc_event_create(void **event);
 int ecc_event_destroy(void *event);

@@ -51,6 +51,8 @@ def main():
         args.remove(out)
     srcs = [Path(a) for a in args] or sorted((PKG / "csrc").glob("*.hip"))
     rows = [k for s in srcs for k in resources(s)]
+    # rocPRIM's own sort kernels (sort.hip instantiates them): library code, not listed
+    rows = [k for k in rows if "rocprim::" not in k["kernel"]]
     print(f"{'kernel':58s} {'vgpr':>4s} {'agpr':>4s} {'sgpr':>4s} {'vspill':>6s} {'scratch':>7s} {'lds':>6s} {'waves/SIMD':>10s}")
     for k in rows:
         print(f"{k['kernel'][:58]:58s} {k.get('vgpr', 0):4d} {k.get('agpr', 0):4d} {k.get('sgpr', 0):4d} "

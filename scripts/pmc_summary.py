@@ -2,10 +2,12 @@
 """Per-kernel SQ counters and occupancy from rocprofv3 --pmc passes (gpu_evidence.sh).
 
 Occupancy follows rocprofiler-sdk's gfx950 definitions (counter_defs.yaml):
-  MeanOccupancyPerCU = 4 * SQ_WAVE_CYCLES / GRBM_GUI_ACTIVE / CU_NUM   (SQ_WAVE_CYCLES in quad-cycles)
-  OccupancyPercent   = 100 * MeanOccupancyPerCU / 32                  (32 wave slots per CU)
+  MeanOccupancyPerCU = 4 * SQ_WAVE_CYCLES / max(GRBM_GUI_ACTIVE) / CU_NUM   (SQ_WAVE_CYCLES in quad-cycles)
+  OccupancyPercent   = 100 * MeanOccupancyPerCU / 32                       (32 wave slots per CU)
+rocprofv3's CSV sums GRBM_GUI_ACTIVE over the 8 XCD instances (measured: 7.8x the kernel's
+duration in 2.4 GHz cycles for arc_kernel), so the per-instance value is the sum / 8.
 Counters are summed per dispatch and averaged over a kernel's dispatches.
-Usage: pmc_summary.py <dir with p*/ subdirs> <out.json> [n_cu]
+Usage: pmc_summary.py <dir with p*/ subdirs> <out.json> [n_cu] [n_xcd]
 """
 import csv
 import glob
@@ -22,6 +24,7 @@ from traffic import short  # noqa: E402
 def main():
     d, out = sys.argv[1], sys.argv[2]
     n_cu = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    n_xcd = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     # (kernel, counter) -> {dispatch id: summed value}
     per = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(d + "/p*/**/*counter_collection.csv", recursive=True):
@@ -38,7 +41,9 @@ def main():
     res = {}
     for k, c in sorted(acc.items()):
         row = {kk: (round(v, 1) if isinstance(v, float) else v) for kk, v in sorted(c.items())}
-        g = c.get("GRBM_GUI_ACTIVE", 0.0)
+        g = c.get("GRBM_GUI_ACTIVE", 0.0) / n_xcd
+        if g > 0:
+            row["gpu_cycles"] = round(g)
         if g > 0 and "SQ_WAVE_CYCLES" in c:
             occ = 4.0 * c["SQ_WAVE_CYCLES"] / g / n_cu
             row["mean_waves_per_cu"] = round(occ, 2)
