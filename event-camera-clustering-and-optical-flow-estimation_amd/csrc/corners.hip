@@ -42,6 +42,12 @@
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef ECC_ARC_PERSIST
+#define ECC_ARC_PERSIST 0  // 1: persistent arc kernel, the next item's loads issued during the tests
+#endif
+#ifndef ECC_ARC_PLAN
+#define ECC_ARC_PLAN 0  // 1: heavy items listed before the arc tests, arc_dense_kernel on a second stream
+#endif
 constexpr int kBuildUnroll = 8;
 constexpr int kArcThreads = 512;  // 8 waves: one lane per window pixel (484) when staging
 constexpr int kGroup = 32;         // slices per group (mask bits)
@@ -57,6 +63,7 @@ struct CornerGeom {
     int W, H, S, margin, border_mode, first_detect;
     int any_order;         // timestamps in any order: every group wide (index values, exact tests)
     int tiles_x, n_tiles;  // bin n_tiles of each group holds the events outside the sensor
+    int seg_stride;        // words per slice of the slice-major corner pairs: n_tiles * 7, to 16 B
     float inv_S;
     int64_t n, n_slices;
 };
@@ -378,6 +385,7 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
                   int64_t *__restrict__ item_base, int32_t *__restrict__ sub_end, uint32_t *__restrict__ gmask,
                   int64_t *__restrict__ glast) {
     __shared__ uint32_t tab[kGroup][kTilePix];  // 24.5 KiB
+    __shared__ uint32_t pmask[kTilePix];        // slices that touched each tile pixel
     __shared__ int32_t wtot[kThreads / 64];
     __shared__ TileSegs segs;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -390,6 +398,7 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
     {
         uint4 *z = reinterpret_cast<uint4 *>(&tab[0][0]);
         for (int i = tid; i < (int)(sizeof(tab) / 16); i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (tid < kTilePix) pmask[tid] = 0u;
     }
     tile_segs(g, so, grp, tile, segs);
     const GroupRef gr = group_ref(t, g, grp);
@@ -410,6 +419,7 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
             for (int u = 0; u < kBuildUnroll; ++u) {
                 if (k[u] == 0xffffffffu) continue;
                 atomicMax(&tab[r[u]][k[u] & 255u], (k[u] >> 8) + gr.dlt);
+                atomicOr(&pmask[k[u] & 255u], 1u << r[u]);
             }
         }
     } else {
@@ -427,17 +437,17 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
             for (int u = 0; u < kBuildUnroll; ++u) {
                 if (k[u] == 0xffffffffu) continue;
                 const uint32_t el = k[u] >> 8;
-                atomicMax(&tab[slice_in_group(el, g)][k[u] & 255u], gr.narrow ? tv[u] + gr.dlt : el + 1u);
+                const int jr = slice_in_group(el, g);
+                atomicMax(&tab[jr][k[u] & 255u], gr.narrow ? tv[u] + gr.dlt : el + 1u);
+                atomicOr(&pmask[k[u] & 255u], 1u << jr);
             }
         }
     }
     __syncthreads();
     // lane k owns pixel c_sub.pix[k]: slice mask, entry count, exclusive prefix in sub-region order
-    uint32_t m = 0u;
-    if (tid < kTilePix) {
-#pragma unroll
-        for (int j = 0; j < kGroup; ++j) m |= (tab[j][lp] != 0u ? 1u : 0u) << j;
-    }
+    // the pixel's slice mask, kept by one LDS atomicOr per event beside its atomicMax (reading
+    // the pixel's 32 table words instead cost 32 LDS reads per pixel lane: 107 -> 100 us)
+    const uint32_t m = tid < kTilePix ? pmask[lp] : 0u;
     const int cnt = __popc(m);
     int incl = cnt;
 #pragma unroll
@@ -631,6 +641,24 @@ __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
 // The value an event of slice j sees at wp is T[j*][wp] with j* the highest set bit of
 // mask & ((2 << j) - 1), else bc: no forward fill, and T is never cleared.
 constexpr int kPairWords = kGroup * kTilePix / 32;  // 196: one bit per (slice, tile pixel)
+constexpr int kSegWords = (kTilePix + 31) / 32;     // 7: one slice's 196 bits of a tile
+
+// The corner pairs leave the arc kernels SLICE-major: res[group][j][tile][kSegWords], bit lp of
+// word w = pair (j, pixel 32 w + lp), so that the flag pass of slice j stages its segment of every
+// tile as one contiguous run (item-major words put one 4-B read of each tile in its own 128-B
+// line, and the 32 slices of a group, on 8 XCDs, fetched every line ~8 times: ~90 MB per step).
+// Lane w < 32 * 7 of an item's workgroup writes word w from the item's LDS bits `bits`
+// (pair j * 196 + lp); neighbouring tiles' words are adjacent, so the writes combine in L2.
+__device__ __forceinline__ void store_res_slice_major(const uint32_t *bits, int64_t grp, int tile, const CornerGeom &g,
+                                                      uint32_t *__restrict__ res, int tid) {
+    if (tid >= kGroup * kSegWords) return;
+    const int j = tid / kSegWords, w = tid % kSegWords;
+    const int b0 = j * kTilePix + 32 * w, w0 = b0 >> 5, sh = b0 & 31;
+    uint32_t v = bits[w0] >> sh;
+    if (sh && w0 + 1 < kPairWords) v |= bits[w0 + 1] << (32 - sh);
+    if (w == kSegWords - 1) v &= (1u << (kTilePix - 32 * (kSegWords - 1))) - 1u;  // 4 bits of the last word
+    res[(grp * kGroup + j) * g.seg_stride + tile * kSegWords + w] = v;
+}
 constexpr int kWaves = kArcThreads / 64;
 constexpr int kQ4Cap = 1024;  // two 8-wave workgroups per CU fit the 160 KiB LDS
 
@@ -720,7 +748,7 @@ __device__ __noinline__ bool exact_pair_test(const ArcLds *L, int wp0, int64_t q
 }
 
 // 5. Arc test of one (group, tile) item, all items of all groups in one launch.  The item's
-// corner pairs go to res[item][kPairWords] (bit j*196 + pixel); flags_event_kernel applies them.
+// corner pairs go to res (slice-major, store_res_slice_major); flags_event_kernel applies them.
 constexpr int kStageUnroll = 4;
 
 // Window segments: the sub-regions of the 3x3 tiles around the item's tile that its window
@@ -940,7 +968,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         atomicAdd(&g_dense_prof[7], 1ull);
     }
 #endif
-    if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
+    store_res_slice_major(L.res, grp, tile, g, res, tid);
 }
 
 // ---- compact window values (the common case) -------------------------------------------------
@@ -986,12 +1014,15 @@ constexpr int kSparseHold = kValCap / kArcThreads;  // entries per lane, held be
 
 #if ECC_ARC_PROFILE
 // profiling builds: per-workgroup wall-clock of arc_kernel's phases, summed (thread 0); [7] = items
-__device__ unsigned long long g_arc_prof[8];
+// per item (no global atomics on shared words: 18 K workgroups adding to 8 words serialised at
+// the memory side and distorted the very phases they timed); summed on the host
+constexpr int kProfItems = 1 << 15;
+__device__ unsigned long long g_arc_items[kProfItems][8];
 #define ARC_MARK(k)                                                                  \
     do {                                                                             \
         if (tid == 0) {                                                              \
             const unsigned long long now_ = wall_clock64();                          \
-            atomicAdd(&g_arc_prof[k], now_ - arc_t_);                                \
+            arc_ph_[k] = now_ - arc_t_;                                              \
             arc_t_ = now_;                                                           \
         }                                                                            \
     } while (0)
@@ -999,44 +1030,91 @@ __device__ unsigned long long g_arc_prof[8];
 #define ARC_MARK(k) do { } while (0)
 #endif
 
-__global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)  // waves/SIMD: 8 = four 8-wave workgroups per CU
-arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
-           const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
-           const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
-           int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
-    __shared__ SparseLds L;
-    // XCD-aware order: workgroup b runs on XCD b % 8, so XCD x takes the contiguous item range
-    // [x * per, (x + 1) * per) — neighbouring tiles of one group share that XCD's L2.
-    const int64_t per = gridDim.x / 8;
-    const int64_t item = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (item >= n_items) return;
+// One item's phase-A loads (B_g and slice mask of window pixel `tid`, the segment `tid` < 13 of the
+// window), issued by arc_prefetch ahead of their use: the persistent arc kernel issues the next
+// item's while the current item's tests run.
+struct ArcPre {
+    int64_t bq;   // B_g (INT64_MAX outside the sensor / past the window)
+    uint32_t mk;  // slices of the group that touched the pixel
+    int64_t b0;   // segment: first entry
+    int len;      // segment: entries
+};
+
+__device__ __forceinline__ void arc_prefetch(ArcPre &p, int64_t item, const CornerGeom &g,
+                                             const int64_t *__restrict__ item_base, const int32_t *__restrict__ sub_end,
+                                             const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask) {
+    const int tid = threadIdx.x;
+    p.bq = INT64_MAX;
+    p.mk = 0u;
+    p.b0 = 0;
+    p.len = 0;
+    if (item < 0) return;  // uniform
+    const int64_t HW = (int64_t)g.H * g.W;
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
-    if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
+    const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
+    const int wx = tx * kTile - kHalo + tid % kWin, wy = ty * kTile - kHalo + tid / kWin;
+    if (tid < kWinPix && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
+        const int64_t q = (int64_t)wy * g.W + wx;
+        p.bq = gB[grp * HW + q];
+        p.mk = gmask[grp * HW + q];
+    }
+    if (tid < kMaxSeg) {
+        // segment geometry packed into integer constants (a per-lane table read would be a load):
+        // dx, dy in {-1,0,1} (2 bits + 1), first/last sub-region (4 bits)
+        const int sxt = (int)((0x2222215u >> (2 * tid)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * tid)) & 3u) - 1;
+        const int r0t = (int)((0x6835020268060ull >> (4 * tid)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * tid)) & 15u);
+        const int nx = tx + sxt, ny = ty + syt;
+        if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
+            const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
+            const int s0 = r0t ? sub_end[bi * kSub + r0t - 1] : 0;
+            p.b0 = item_base[bi] + s0;
+            p.len = sub_end[bi * kSub + r1t] - s0;
+        }
+    }
+}
+
+// The arc tests of one (group, tile) item from its prefetched phase-A loads `pre`.  kPersist:
+// the next item's loads are issued into `nxt` (after barrier 3, or at an early exit), and the
+// caller syncs before the next item reuses the LDS.
+//   A: segment table, wave scans of the value counts and of min B_g     -> barrier 1
+//   B: entry loads issued; pixel records, B_g slots, clamp               -> barrier 2
+//   C: tasks, value scatter                                              -> barrier 3
+//   circle 3 -> barrier 4 -> circle 4 -> barrier 5
+// The slice mask of every window pixel comes from pair_build's mask image, so its value count,
+// the wave prefix of the counts and the window minimum of B_g are all known before the first
+// barrier; the entries are loaded right after it, while the pixel records and B_g slots are
+// written, and scattered after the second.
+template <bool kPersist>
+__device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPre &pre, ArcPre &nxt, int64_t next_item,
+                                         const int64_t *__restrict__ t, const CornerGeom &g,
+                                         const int64_t *__restrict__ item_base, const PairEntry *__restrict__ entries,
+                                         const int32_t *__restrict__ sub_end, const int64_t *__restrict__ gB,
+                                         const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
+                                         int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
+    auto prefetch_next = [&]() {
+        if constexpr (kPersist) arc_prefetch(nxt, next_item, g, item_base, sub_end, gB, gmask);
+    };
+    const int64_t grp = item / g.n_tiles;
+    const int tile = (int)(item % g.n_tiles);
+    if ((grp + 1) * kGroup <= g.first_detect) {  // every slice of the group precedes detection
+        prefetch_next();
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #if ECC_ARC_PROFILE
-    unsigned long long arc_t_ = wall_clock64();
+    unsigned long long arc_t_ = wall_clock64(), arc_ph_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    const int64_t HW = (int64_t)g.H * g.W;
     int tx, ty;
     tile_origin_xy(g, tile, tx, ty);
     const int x0 = tx * kTile, y0 = ty * kTile;
-    const int wx0 = x0 - kHalo, wy0 = y0 - kHalo;
     const GroupRef gr = group_ref(t, g, grp);
     const int64_t Lt = gr.Lt;
     const bool narrow = gr.narrow;
-    const int64_t *Bg = gB + grp * HW;
-
-    // (a) the window pixel's B_g (lane wp < 484), the segment table (lanes 0..12), cleared masks
     const int wp = tid;
     const bool win_lane = wp < kWinPix;
-    const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
-    const bool in = win_lane && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
-    const int64_t bq = in ? Bg[(int64_t)wy * g.W + wx] : INT64_MAX;  // INT64_MAX: outside (never read)
-    // the slices of the group that touched the pixel, as pair_build recorded them: the OR of the
-    // window's entries for that pixel, without one LDS atomic per entry (a pixel's entries are
-    // adjacent, so those atomics hit one word from many lanes of a wave)
-    if (win_lane) L.pix[wp].mask = in ? gmask[grp * HW + (int64_t)wy * g.W + wx] : 0u;
+    const int64_t bq = pre.bq;
+    const uint32_t mk_w = pre.mk;
     for (int w = tid; w < kPairWords; w += kArcThreads) L.res[w] = 0u;
     if (tid == 0) {
         L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
@@ -1046,44 +1124,46 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         L.redo = 0;
     }
     if (tid < kMaxSeg) {
-        // segment geometry packed into integer constants (a per-lane table read would be a load):
-        // dx, dy in {-1,0,1} (2 bits + 1), first/last sub-region (4 bits)
         const int sxt = (int)((0x2222215u >> (2 * tid)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * tid)) & 3u) - 1;
-        const int r0t = (int)((0x6835020268060ull >> (4 * tid)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * tid)) & 15u);
-        const int nx = tx + sxt, ny = ty + syt;
-        int64_t b0 = 0;
-        int len = 0;
-        if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
-            const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
-            const int s0 = r0t ? sub_end[bi * kSub + r0t - 1] : 0;
-            b0 = item_base[bi] + s0;
-            len = sub_end[bi * kSub + r1t] - s0;
-        }
-        int incl = len;
+        int incl = pre.len;
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
             const int v = __shfl_up(incl, o, 16);
             if (tid >= o) incl += v;
         }
-        L.seg_lo[tid] = b0;
+        L.seg_lo[tid] = pre.b0;
         L.seg_pref[tid + 1] = incl;
         L.seg_off[tid] = (syt * kTile) * kWin + sxt * kTile + kHalo * kWin + kHalo;
         if (tid == 0) L.seg_pref[0] = 0;
     }
-    __syncthreads();
-    ARC_MARK(0);  // (a) segment table + B_g window
-    if (L.seg_pref[1] == 0) return;  // no events in the tile: nothing to flag
+    const int cnt = win_lane ? __popc(mk_w) + 1 : 0;  // the pixel's values + its B_g slot
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) L.wave_tot[wave] = incl;
+    int64_t bmin = bq;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t x = __shfl_xor(bmin, o);
+        bmin = x < bmin ? x : bmin;
+    }
+    if (lane == 0) L.wave_min[wave] = bmin;
+    __syncthreads();  // 1
+    ARC_MARK(0);  // A
     const int total = L.seg_pref[kMaxSeg];
-    if (total > kValCap) {  // too many values for the compact list: the dense kernel takes it
-        if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
+    if (L.seg_pref[1] == 0 || total > kValCap) {  // uniform
+        // no events in the tile: nothing to flag; too many values for the compact list: the
+        // dense kernel takes it (listed by arc_plan_kernel with ECC_ARC_PLAN)
+        if (!ECC_ARC_PLAN && total > kValCap && L.seg_pref[1] != 0 && tid == 0) over[atomicAdd(n_over, 1u)] = item;
+        prefetch_next();
         return;
     }
     int pref[kMaxSeg + 1];
 #pragma unroll
     for (int c = 0; c <= kMaxSeg; ++c) pref[c] = L.seg_pref[c];  // uniform
-
-    // (b) pass 1: slice bits of every window pixel; the own tile's eligible pairs become tasks;
-    //     the entries stay in registers for pass 2
     PairEntry ent[kSparseHold];
     int ewp[kSparseHold];
     const int slots = (total + kArcThreads - 1) / kArcThreads;  // uniform: the slots in use
@@ -1098,73 +1178,46 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         ent[u] = (i < total) ? entries[L.seg_lo[r] + (i - L.seg_pref[r])] : PairEntry{0u, 0u};
         ewp[u] = (i < total) ? r : -1;
     }
+    if (win_lane) {
+        int off = incl - cnt;
+        for (int w = 0; w < wave; ++w) off += L.wave_tot[w];
+        int64_t vz = INT64_MAX;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
+        const uint32_t bcv = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
+        reinterpret_cast<uint2 *>(L.pix)[wp] = make_uint2(mk_w, (uint32_t)off);
+        L.vals[off] = bcv;
+    }
+    __syncthreads();  // 2
+    ARC_MARK(1);  // B
+    if (L.exact_only) {  // uniform: a wide group or a value above t_last — the exact kernel takes it
+        if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
+        prefetch_next();
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < kSparseHold; ++u) {
         if (u >= slots) break;
         if (ewp[u] < 0) continue;
         const int r = ewp[u];
         const int lp = (int)(ent[u].meta & 255u), j = (int)(ent[u].meta >> 8);
-        ewp[u] = L.seg_off[r] + (lp / kTile) * kWin + lp % kTile;
+        const int e = L.seg_off[r] + (lp / kTile) * kWin + lp % kTile;
         if (r == 0 && (int64_t)grp * kGroup + j >= g.first_detect && !is_border(x0 + lp % kTile, y0 + lp / kTile, g))
             L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)(j * kTilePix + lp);
+        const PixInfo pq = L.pix[e];
+        L.vals[pq.off + 1u + __popc(pq.mask & ((1u << j) - 1u))] = ent[u].v;
     }
-    int64_t bmin = bq;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int64_t x = __shfl_xor(bmin, o);
-        bmin = x < bmin ? x : bmin;
-    }
-    if (lane == 0) L.wave_min[wave] = bmin;
-    __syncthreads();
-
-    ARC_MARK(1);  // (b) pass 1: entries, slice bits, tasks
-    // (c) per window pixel: clamped B_g, value count (+ the B_g slot), wave prefix of the counts
-    const uint32_t mk_w = win_lane ? L.pix[wp].mask : 0u;
-    const int cnt = win_lane ? __popc(mk_w) + 1 : 0;
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
-    if (lane == 63) L.wave_tot[wave] = incl;
-    uint32_t bcv = 0u;
-    if (win_lane) {
-        int64_t vz = INT64_MAX;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
-        bcv = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
-    }
-    __syncthreads();
-    if (L.exact_only) {  // uniform: a wide group or a value above t_last — the exact kernel takes it
-        if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
-        return;
-    }
-    if (win_lane) {
-        int off = incl - cnt;
-        for (int w = 0; w < wave; ++w) off += L.wave_tot[w];
-        L.pix[wp].off = (uint32_t)off;
-        L.vals[off] = bcv;
-    }
-    __syncthreads();
-    // (d) pass 2: each value at its pixel's list position (ascending slice)
-#pragma unroll
-    for (int u = 0; u < kSparseHold; ++u) {
-        if (u >= slots) break;
-        if (ewp[u] < 0) continue;
-        const int j = (int)(ent[u].meta >> 8);
-        const PixInfo p = L.pix[ewp[u]];
-        L.vals[p.off + 1u + __popc(p.mask & ((1u << j) - 1u))] = ent[u].v;
-    }
-    __syncthreads();
-
-    ARC_MARK(2);  // (c, d) list offsets, B_g slots, value scatter
-    // (e) tests through the compact lists, on clamped 32-bit keys only.  This kernel holds no
-    //     exact int64 path and no call: an item its keys cannot decide (a wide group, a value
-    //     above t_last, a tie the clamping may have merged) or whose circle-3 survivors overflow
-    //     the queue goes whole to arc_dense_kernel, which redoes it exactly.  So the kernel fits
-    //     64 VGPRs without spills: four 8-wave workgroups per CU.
-    const int n_tasks = L.n_tasks;
+    __syncthreads();  // 3
+    ARC_MARK(2);  // C
+    prefetch_next();  // the next item's loads fly during the tests
+    // Tests through the compact lists, on clamped 32-bit keys only.  No exact int64 path and no
+    // call: an item its keys cannot decide (a wide group, a value above t_last, a tie the clamping
+    // may have merged) or whose circle-3 survivors overflow the queue goes whole to
+    // arc_dense_kernel, which redoes it exactly.  So the kernel fits 64 VGPRs without spills.
+#ifndef ECC_ARC_SKIP
+#define ECC_ARC_SKIP 0  // timing experiments only (wrong results): 1 = no circle 4, 2 = no tests
+#endif
+    const int n_tasks = ECC_ARC_SKIP >= 2 ? 0 : L.n_tasks;
     const bool ties_exact = !L.mixed;
     for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
         const int pi = L.tasks[ti];
@@ -1183,17 +1236,17 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
             L.redo = 1;
         }
     }
-    __syncthreads();
+    __syncthreads();  // 4
     ARC_MARK(3);  // circle 3
     if (L.redo) {  // uniform
         if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
         return;
     }
-    const int n4 = L.q4n;
+    const int n4 = ECC_ARC_SKIP >= 1 ? 0 : L.q4n;
 #if ECC_ARC_PROFILE
     if (tid == 0) {
-        atomicAdd(&g_arc_prof[5], (unsigned long long)n_tasks);
-        atomicAdd(&g_arc_prof[6], (unsigned long long)n4);
+        arc_ph_[5] = (unsigned long long)n_tasks;
+        arc_ph_[6] = (unsigned long long)n4;
     }
 #endif
     for (int qi = tid; qi < n4; qi += kArcThreads) {
@@ -1210,16 +1263,93 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
         if (r4 > 0) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
         else if (r4 < 0) L.redo = 1;
     }
-    __syncthreads();
+    __syncthreads();  // 5
     ARC_MARK(4);  // circle 4
 #if ECC_ARC_PROFILE
-    if (tid == 0) atomicAdd(&g_arc_prof[7], 1ull);
+    if (tid == 0 && item < kProfItems) {
+        arc_ph_[7] = 1ull;
+        for (int k = 0; k < 8; ++k) g_arc_items[item][k] = arc_ph_[k];
+    }
 #endif
     if (L.redo) {  // uniform: a circle-4 tie the clamped keys cannot decide
         if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
         return;
     }
-    if (tid < kPairWords) res[item * kPairWords + tid] = L.res[tid];
+    store_res_slice_major(L.res, grp, tile, g, res, tid);
+}
+
+// One workgroup per item, all items of all groups in one launch, in XCD-aware order: workgroup b
+// runs on XCD b % 8, so XCD x takes the contiguous item range [x * per, (x + 1) * per) —
+// neighbouring tiles of one group share that XCD's L2.
+__global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)  // waves/SIMD: 8 = four 8-wave workgroups per CU
+arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
+           const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
+           const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
+           int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
+    __shared__ SparseLds L;
+    const int64_t per = gridDim.x / 8;
+    const int64_t item = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (item >= n_items) return;
+    ArcPre pre, unused;
+    arc_prefetch(pre, item, g, item_base, sub_end, gB, gmask);
+    arc_item<false>(L, item, pre, unused, -1, t, g, item_base, entries, sub_end, gB, gmask, res, over, n_over);
+}
+
+// Persistent form: a resident grid (four workgroups per CU) walks the items of its XCD's range,
+// workgroup l of an XCD taking items l, l + G, l + 2G, ... of the range (G workgroups per XCD),
+// and loads each next item's B_g window, masks and segment table while the current item's tests
+// run, so one of the item's two dependent global round trips is off its critical path.
+__global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)
+arc_persist_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
+                   const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
+                   const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
+                   int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
+    __shared__ SparseLds L;
+    const int64_t per = (n_items + 7) / 8;
+    const int64_t x = blockIdx.x % 8, G = gridDim.x / 8;
+    const int64_t lo = x * per, hi = min(n_items, lo + per);
+    int64_t item = lo + blockIdx.x / 8;
+    if (item >= hi) return;
+    ArcPre cur, nxt;
+    arc_prefetch(cur, item, g, item_base, sub_end, gB, gmask);
+    for (;;) {
+        const int64_t next = item + G < hi ? item + G : -1;
+        arc_item<true>(L, item, cur, nxt, next, t, g, item_base, entries, sub_end, gB, gmask, res, over, n_over);
+        if (next < 0) break;
+        __syncthreads();  // the LDS of this item is read out before the next one's phase A
+        cur = nxt;
+        item = next;
+    }
+}
+
+// Items whose window holds more values than the compact list (and whose own tile has pairs),
+// listed BEFORE the arc tests: arc_dense_kernel then works through them on a second stream beside
+// arc_kernel instead of after it (its ~430 heavy items take one long round at two workgroups per
+// CU: a 45 us tail of the corner chain when run after arc_kernel).  One thread per item; the
+// window's 13 segments exactly as arc_kernel builds them.
+__global__ void __launch_bounds__(kThreads)
+arc_plan_kernel(CornerGeom g, int64_t n_items, const int32_t *__restrict__ sub_end, int64_t *__restrict__ over,
+                uint32_t *__restrict__ n_over) {
+    const int64_t item = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (item >= n_items) return;
+    const int64_t grp = item / g.n_tiles;
+    if ((grp + 1) * kGroup <= g.first_detect) return;
+    const int tile = (int)(item % g.n_tiles);
+    const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
+    int total = 0, own = 0;
+#pragma unroll
+    for (int c = 0; c < kMaxSeg; ++c) {
+        const int sxt = (int)((0x2222215u >> (2 * c)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * c)) & 3u) - 1;
+        const int r0t = (int)((0x6835020268060ull >> (4 * c)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * c)) & 15u);
+        const int nx = tx + sxt, ny = ty + syt;
+        if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
+            const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
+            const int len = sub_end[bi * kSub + r1t] - (r0t ? sub_end[bi * kSub + r0t - 1] : 0);
+            total += len;
+            own = c == 0 ? len : own;
+        }
+    }
+    if (own > 0 && total > kValCap) over[atomicAdd(n_over, 1u)] = item;
 }
 
 // The windows above the compact list's capacity (arc_kernel's overflow list), each with the
@@ -1244,9 +1374,13 @@ arc_dense_kernel(const int64_t *__restrict__ t, CornerGeom g, const int64_t *__r
 // written, 0 or 1, four per lane and store.  The per-event eligibility of the reference loop: the
 // first-detect rule (Q15) and, in ref_compat mode (Q11), "before the slice's first border event";
 // corner pairs are never border pixels.
-constexpr int kFlagThreads = 512;
-constexpr int kFlagQuads = 8;  // 4-event quads a lane loads up front (16384-event slices)
-constexpr int kSegWords = (kTilePix + 31) / 32 + 1;  // 7: a 196-bit segment at any bit offset
+#ifndef ECC_FLAG_THREADS
+#define ECC_FLAG_THREADS 256
+#endif
+constexpr int kFlagThreads = ECC_FLAG_THREADS;  // 256: every slice's workgroup resident at once (8 per CU)
+constexpr int kFlagQuads = 8;  // 4-event quads a lane has in flight per batch
+constexpr int kFlagBatch = kFlagQuads * kFlagThreads;  // quads per batch
+constexpr int kFlagCandMax = 16384;  // slices up to this many events take the candidate-list form
 
 // kStaged: bit lp of tile in the LDS segments; otherwise (sensors whose segments exceed the
 // LDS) straight from the group's result words.
@@ -1258,63 +1392,65 @@ __device__ __forceinline__ uint32_t corner_bit(uint32_t v, const CornerGeom &g, 
     const int tile = (y / kTile) * g.tiles_x + x / kTile;
     const int lp = (y % kTile) * kTile + x % kTile;
     if (kStaged) return (sb[tile * kSegWords + (lp >> 5)] >> (lp & 31)) & 1u;
-    const int pi = j * kTilePix + lp;
-    return (rg[(int64_t)tile * kPairWords + (pi >> 5)] >> (pi & 31)) & 1u;
+    return (rg[(int64_t)tile * kSegWords + (lp >> 5)] >> (lp & 31)) & 1u;
 }
 
 // kCand (ecc_fast_detect_nms): the pass also writes each slice's NMS candidate list — the
 // flagged events' xy in event order at cand[s * S ...], their count in n_cand[s] — which is
 // what nms_compact_kernel would rebuild from the flags (the host takes this form only for
-// slices of at most 16384 events, a multiple of 4).
+// slices of at most kFlagCandMax events, a multiple of 4).
+// 256-lane workgroups, one per slice, so that all 1221 slices of the bench batch are resident at
+// once (eight per CU; 512-lane ones left a second round of 197 workgroups as a tail).  A slice's
+// quads are taken in batches of kFlagQuads per lane: the first batch's loads are issued before
+// the staging of the result segments, so the two latencies overlap.
 template <bool kStaged, bool kCand>
 __global__ void __launch_bounds__(kFlagThreads)
 flags_event_kernel(const uint32_t *__restrict__ xy, CornerGeom g, const uint32_t *__restrict__ res,
                    const int32_t *__restrict__ first_border, uint8_t *__restrict__ flags, uint32_t *__restrict__ cand,
                    int32_t *__restrict__ n_cand) {
     extern __shared__ uint32_t sb[];  // [n_tiles][kSegWords]: bit lp of tile = pair (j, lp)
+    __shared__ int ctot[kFlagQuads][kFlagThreads / 64];
     const int64_t s = blockIdx.x;
     const int64_t lo = s * g.S;
     const int len = (int)((lo + g.S < g.n ? lo + g.S : g.n) - lo);
     const int j = (int)(s % kGroup);
     // events [0, live_end) of the slice can be corners
     const int live_end = s < g.first_detect ? 0 : (g.border_mode == 1 ? min(len, max(first_border[s], 0)) : len);
-    const uint32_t *rg = res + (s / kGroup) * g.n_tiles * kPairWords;
+    const uint32_t *rg = res + s * g.seg_stride;  // slice s's segment of every tile (16-B aligned)
     const bool vec = (lo & 3) == 0;  // 4-event quads: 16-B loads, 4-B flag stores
     const int n4 = vec ? len / 4 : 0;
-    // a lane's quads (<= kFlagQuads of them for slices up to 16384 events) are loaded before the
-    // staging, so the two latencies overlap
-    // all of them unconditional through a buffer view of the slice's whole quads (0 past them):
-    // a load under a per-lane condition made each quad wait for the previous one
-    uint4 pre[kFlagQuads];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // all loads unconditional through a buffer view of the slice's whole quads (0 past them): a
+    // load under a per-lane condition made each quad wait for the previous one
     const __amdgpu_buffer_rsrc_t vq = ecc::buffer_view(xy + lo, (uint32_t)n4 * 16u);
+    uint4 pre[kFlagQuads];
+    auto load_batch = [&](int q0) {
 #pragma unroll
-    for (int u = 0; u < kFlagQuads; ++u)
-        pre[u] = ecc::buffer_load_u128(vq, threadIdx.x * 16u, (uint32_t)(u * kFlagThreads) * 16u);
-    __builtin_amdgcn_sched_barrier(0);
+        for (int u = 0; u < kFlagQuads; ++u)
+            pre[u] = ecc::buffer_load_u128(vq, threadIdx.x * 16u, (uint32_t)(q0 + u * kFlagThreads) * 16u);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    load_batch(0);
     if (kStaged && live_end > 0) {
-        // four words per lane per trip, loads unconditional through a buffer view of the group's
-        // result words (0 past them; the word past an item's end is selected away afterwards)
-        const int b0 = j * kTilePix, w0 = b0 >> 5, sh = b0 & 31;
+        // the slice's words of every tile are one contiguous run: 16-B loads, four per lane per
+        // trip, unconditional through a buffer view (0 past the run)
         const int total = g.n_tiles * kSegWords;
-        const __amdgpu_buffer_rsrc_t vr = ecc::buffer_view(rg, (uint32_t)g.n_tiles * kPairWords * 4u);
-        for (int k0 = 0; k0 < total; k0 += 4 * kFlagThreads) {
-            uint32_t a[4], c[4];
+        const __amdgpu_buffer_rsrc_t vr = ecc::buffer_view(rg, (uint32_t)total * 4u);
+        for (int k0 = 0; k0 < total; k0 += 16 * kFlagThreads) {
+            uint4 a[4];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int k = k0 + b * kFlagThreads + (int)threadIdx.x;
-                const int tile = k / kSegWords, w = k % kSegWords;
-                const uint32_t off = ((uint32_t)tile * kPairWords + w0 + w) * 4u;
-                a[b] = ecc::buffer_load_u32(vr, off);
-                c[b] = ecc::buffer_load_u32(vr, off + 4u);
-            }
+            for (int b = 0; b < 4; ++b) a[b] = ecc::buffer_load_u128(vr, (uint32_t)(k0 + 4 * (b * kFlagThreads + (int)threadIdx.x)) * 4u);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                const int k = k0 + b * kFlagThreads + (int)threadIdx.x;
-                const int w = k % kSegWords;
-                const uint32_t av = w0 + w < kPairWords ? a[b] : 0u;
-                const uint32_t cv = (sh && w0 + w + 1 < kPairWords) ? c[b] : 0u;
-                if (k < total) sb[k] = sh ? (av >> sh) | (cv << (32 - sh)) : av;
+                const int k = k0 + 4 * (b * kFlagThreads + (int)threadIdx.x);
+                if (k + 3 < total) {
+                    *reinterpret_cast<uint4 *>(sb + k) = a[b];
+                } else {
+                    if (k < total) sb[k] = a[b].x;
+                    if (k + 1 < total) sb[k + 1] = a[b].y;
+                    if (k + 2 < total) sb[k + 2] = a[b].z;
+                }
             }
         }
     }
@@ -1324,46 +1460,52 @@ flags_event_kernel(const uint32_t *__restrict__ xy, CornerGeom g, const uint32_t
                (i + 2 < live_end ? corner_bit<kStaged>(v.z, g, sb, rg, j) << 16 : 0u) |
                (i + 3 < live_end ? corner_bit<kStaged>(v.w, g, sb, rg, j) << 24 : 0u);
     };
-    if constexpr (kCand) {
-        // quad u of lane tid holds events 4 (u * 512 + tid) .. + 3: event order is u, then lane;
-        // a quad has <= 4 flags, so three ballots give each lane its prefix inside the wave
-        __shared__ int ctot[kFlagQuads][kFlagThreads / 64];
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int base = 0;  // candidates written so far (uniform)
+    uint32_t *dst = cand + lo;
+    for (int q0 = 0; q0 < n4; q0 += kFlagBatch) {  // uniform
+        if (q0 > 0) load_batch(q0);
         uint32_t f[kFlagQuads];
         int pfx[kFlagQuads];
 #pragma unroll
         for (int u = 0; u < kFlagQuads; ++u) {
-            const int q = u * kFlagThreads + (int)threadIdx.x;
+            const int q = q0 + u * kFlagThreads + (int)threadIdx.x;
             const int i = 4 * q;
             f[u] = (q < n4 && i < live_end) ? quad_flags(i, pre[u]) : 0u;
             if (q < n4) *reinterpret_cast<uint32_t *>(flags + lo + i) = f[u];
-            const int c = __popc(f[u]);  // flag bytes are 0 or 1
-            const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
-            pfx[u] = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
-            if (lane == 0) ctot[u][wave] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-        }
-        __syncthreads();
-        int base = 0;
-        uint32_t *dst = cand + lo;
-#pragma unroll
-        for (int u = 0; u < kFlagQuads; ++u) {
-            int off = base + pfx[u];
-#pragma unroll
-            for (int w = 0; w < kFlagThreads / 64; ++w) {
-                const int tw = ctot[u][w];
-                off += w < wave ? tw : 0;
-                base += tw;
-            }
-            if (f[u]) {
-                if (f[u] & 0x1u) dst[off++] = pre[u].x;
-                if (f[u] & 0x100u) dst[off++] = pre[u].y;
-                if (f[u] & 0x10000u) dst[off++] = pre[u].z;
-                if (f[u] & 0x1000000u) dst[off++] = pre[u].w;
+            if constexpr (kCand) {
+                // quad u of lane tid holds events 4 (q0 + u * T + tid) .. + 3: event order is u,
+                // then lane; a quad has <= 4 flags, so three ballots give each lane its prefix
+                const int c = __popc(f[u]);  // flag bytes are 0 or 1
+                const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+                pfx[u] = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+                if (lane == 0) ctot[u][wave] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
             }
         }
+        if constexpr (kCand) {
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < kFlagQuads; ++u) {
+                int off = base + pfx[u];
+#pragma unroll
+                for (int w = 0; w < kFlagThreads / 64; ++w) {
+                    const int tw = ctot[u][w];
+                    off += w < wave ? tw : 0;
+                    base += tw;
+                }
+                if (f[u]) {
+                    if (f[u] & 0x1u) dst[off++] = pre[u].x;
+                    if (f[u] & 0x100u) dst[off++] = pre[u].y;
+                    if (f[u] & 0x10000u) dst[off++] = pre[u].z;
+                    if (f[u] & 0x1000000u) dst[off++] = pre[u].w;
+                }
+            }
+            __syncthreads();  // ctot is rewritten by the next batch
+        }
+    }
+    if constexpr (kCand) {
         if (threadIdx.x == 0) {
-            for (int i = 4 * n4; i < len; ++i) {  // the batch's last < 4 events
+            for (int i = 4 * n4; i < len; ++i) {  // the batch's last < 4 events, in order
                 const uint32_t v = xy[lo + i];
                 const uint32_t fb = i < live_end ? corner_bit<kStaged>(v, g, sb, rg, j) : 0u;
                 flags[lo + i] = (uint8_t)fb;
@@ -1371,28 +1513,10 @@ flags_event_kernel(const uint32_t *__restrict__ xy, CornerGeom g, const uint32_t
             }
             n_cand[s] = base;
         }
-        return;
+    } else {
+        for (int i = 4 * n4 + threadIdx.x; i < len; i += kFlagThreads)  // last < 4 events, or unaligned slices
+            flags[lo + i] = (uint8_t)(i < live_end ? corner_bit<kStaged>(xy[lo + i], g, sb, rg, j) : 0u);
     }
-#pragma unroll
-    for (int u = 0; u < kFlagQuads; ++u) {
-        const int q = u * kFlagThreads + (int)threadIdx.x;
-        if (q >= n4) break;
-        const int i = 4 * q;
-        *reinterpret_cast<uint32_t *>(flags + lo + i) = i < live_end ? quad_flags(i, pre[u]) : 0u;
-    }
-    for (int q = kFlagQuads * kFlagThreads + threadIdx.x; q < n4; q += kFlagThreads) {  // slices > 16384 events
-        const int i = 4 * q;
-        uint32_t f = 0u;
-        if (i < live_end) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(xy + lo + i);
-            f = corner_bit<kStaged>(v.x, g, sb, rg, j) | (i + 1 < live_end ? corner_bit<kStaged>(v.y, g, sb, rg, j) << 8 : 0u) |
-                (i + 2 < live_end ? corner_bit<kStaged>(v.z, g, sb, rg, j) << 16 : 0u) |
-                (i + 3 < live_end ? corner_bit<kStaged>(v.w, g, sb, rg, j) << 24 : 0u);
-        }
-        *reinterpret_cast<uint32_t *>(flags + lo + i) = f;
-    }
-    for (int i = 4 * n4 + threadIdx.x; i < len; i += kFlagThreads)
-        flags[lo + i] = (uint8_t)(i < live_end ? corner_bit<kStaged>(xy[lo + i], g, sb, rg, j) : 0u);
 }
 
 // Plain final-SAE scatter (no detection): sae[q] = max t.
@@ -1427,6 +1551,9 @@ struct CornerState {
     // diagnostics of the last detection (ecc_fast_detect_stats)
     const uint32_t *n_over = nullptr;
     int64_t n_items = 0, n_slices = 0, n_groups = 0;
+    // the second stream arc_dense_kernel runs on beside arc_kernel (ECC_ARC_PLAN), fork/join events
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 
 std::mutex g_state_mu;
@@ -1455,12 +1582,13 @@ struct Carve {
 struct GroupImages {
     uint32_t *mask;       // [n_groups][H*W] slices of the group that touched the pixel
     int64_t *B;           // [n_groups][H*W] last t of the group, then (in place) B_g
-    uint32_t *res;        // [n_items][kPairWords] corner (slice, pixel) pairs per item
+    uint32_t *res;        // [n_groups][32][n_tiles][kSegWords] corner (slice, pixel) pairs, slice-major
     PairEntry *entries;   // [n] distinct (slice, pixel) pairs per item, at item_base[item]
     int64_t *item_base;   // [n_items]
     int32_t *sub_end;     // [n_items][kSub] sub-region ends inside each item's entries
     int64_t *over;        // [n_items] items whose windows exceed the compact list (arc_dense_kernel)
-    uint32_t *n_over;
+    int64_t *over2;       // [n_items] items arc_kernel defers to the exact path (ECC_ARC_PLAN)
+    uint32_t *n_over;     // [0]: heavy items, [1]: deferred items
 };
 
 Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_items, int64_t n_groups, int32_t **first_border,
@@ -1473,11 +1601,12 @@ Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_items, int64_t n_g
     const size_t img = (size_t)n_groups * g.W * g.H;
     gi->mask = cv.take<uint32_t>(img);
     gi->B = cv.take<int64_t>(img);
-    gi->res = cv.take<uint32_t>((size_t)n_items * kPairWords);
+    gi->res = cv.take<uint32_t>((size_t)n_groups * kGroup * g.seg_stride);
     gi->entries = cv.take<PairEntry>((size_t)g.n);
     gi->item_base = cv.take<int64_t>((size_t)n_items);
     gi->sub_end = cv.take<int32_t>((size_t)n_items * kSub);
     gi->over = cv.take<int64_t>((size_t)n_items);
+    gi->over2 = cv.take<int64_t>((size_t)n_items);
     gi->n_over = cv.take<uint32_t>(64);
     return so;
 }
@@ -1518,6 +1647,9 @@ void corner_state_release(const ecc_ctx *ctx) {
         g_states.erase(it);
     }
     if (st->evt) (void)hipFree(st->evt);
+    if (st->side) (void)hipStreamDestroy(st->side);
+    if (st->fork) (void)hipEventDestroy(st->fork);
+    if (st->join) (void)hipEventDestroy(st->join);
     delete st;
 }
 }  // namespace ecc
@@ -1561,6 +1693,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     g.any_order = cfg->any_order;
     g.tiles_x = (g.W + kTile - 1) / kTile;
     g.n_tiles = g.tiles_x * ((g.H + kTile - 1) / kTile);
+    g.seg_stride = (g.n_tiles * kSegWords + 3) & ~3;
     if (g.n_tiles > kMaxTiles) return ECC_ERR_INVALID;  // > 8191 16x16 tiles (~2.1 Mpixel)
     g.n = n;
     g.n_slices = (n + g.S - 1) / g.S;
@@ -1619,7 +1752,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         ECC_CHECK_LAUNCH(ctx, "fast_detect_prepare");
         return ECC_OK;
     }
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 8, s), "memset(overflow counts)");
     st->n_over = gi.n_over;
     st->n_items = n_items;
     st->n_slices = g.n_slices;
@@ -1631,19 +1764,48 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         hipLaunchKernelGGL(sae_prefix_kernel, dim3(blocks), dim3(kThreads), 0, s, g, n_groups,
                            (const uint32_t *)gi.mask, gi.B, sae);
     }
+    // heavy items (n_over[0], list `over`) and the items arc_kernel defers to the exact path
+    // (n_over[1], list `over2`; the same list as the heavy ones without the plan)
+    int64_t *const over2 = ECC_ARC_PLAN ? gi.over2 : gi.over;
+    uint32_t *const n_over2 = ECC_ARC_PLAN ? gi.n_over + 1 : gi.n_over;
+    auto dense = [&](hipStream_t sd, const int64_t *list, const uint32_t *cnt) {
+        ECC_TIMED(ctx, sd, "arc_dense_kernel");  // dense planes
+        hipLaunchKernelGGL(arc_dense_kernel, dim3(512), dim3(kArcThreads), 0, sd, t, g, list, cnt,
+                           (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
+                           (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res);
+    };
+    if (ECC_ARC_PLAN) {
+        {
+            ECC_TIMED(ctx, s, "arc_plan_kernel");
+            hipLaunchKernelGGL(arc_plan_kernel, dim3(blocks_for(n_items, kThreads)), dim3(kThreads), 0, s, g, n_items,
+                               (const int32_t *)gi.sub_end, gi.over, gi.n_over);
+        }
+        if (!st->side) {
+            ECC_CHECK_HIP(ctx, hipStreamCreateWithFlags(&st->side, hipStreamNonBlocking), "corner side stream");
+            ECC_CHECK_HIP(ctx, hipEventCreateWithFlags(&st->fork, hipEventDisableTiming), "corner fork event");
+            ECC_CHECK_HIP(ctx, hipEventCreateWithFlags(&st->join, hipEventDisableTiming), "corner join event");
+        }
+        ECC_CHECK_HIP(ctx, hipEventRecord(st->fork, s), "fork");
+        ECC_CHECK_HIP(ctx, hipStreamWaitEvent(st->side, st->fork, 0), "fork wait");
+        dense(st->side, gi.over, gi.n_over);
+        ECC_CHECK_HIP(ctx, hipEventRecord(st->join, st->side), "join");
+    }
     {
         ECC_TIMED(ctx, s, "arc_kernel");
-        const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
-        hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
-                           (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
-                           (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over);
+        if (ECC_ARC_PERSIST) {
+            const unsigned grid = (unsigned)(8 * std::min<int64_t>((n_items + 7) / 8, ctx->n_cu / 2));  // 4 per CU
+            hipLaunchKernelGGL(arc_persist_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
+                               (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
+                               (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, over2, n_over2);
+        } else {
+            const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
+            hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
+                               (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
+                               (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, over2, n_over2);
+        }
     }
-    {
-        ECC_TIMED(ctx, s, "arc_dense_kernel");  // the overflow list, dense planes
-        hipLaunchKernelGGL(arc_dense_kernel, dim3(512), dim3(kArcThreads), 0, s, t, g, (const int64_t *)gi.over,
-                           (const uint32_t *)gi.n_over, (const int64_t *)gi.item_base, (const PairEntry *)gi.entries,
-                           (const int32_t *)gi.sub_end, (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res);
-    }
+    if (ECC_ARC_PLAN) ECC_CHECK_HIP(ctx, hipStreamWaitEvent(s, st->join, 0), "join wait");
+    dense(s, over2, n_over2);  // the deferred items (with the plan: none on ordinary streams)
     {
         ECC_TIMED(ctx, s, "flags_kernel");
         constexpr size_t kLdsMax = 160 * 1024;
@@ -1690,9 +1852,14 @@ ECC_API int ecc_arc_dense_profile(unsigned long long *out8, double *ticks_per_us
 }
 
 ECC_API int ecc_arc_profile(unsigned long long *out8, double *ticks_per_us) {
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_arc_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return ECC_ERR_HIP;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    hipMemcpyToSymbol(HIP_SYMBOL(g_arc_prof), z, sizeof(z));
+    std::vector<unsigned long long> h((size_t)kProfItems * 8);
+    if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_arc_items), h.size() * 8) != hipSuccess) return ECC_ERR_HIP;
+    for (int k = 0; k < 8; ++k) out8[k] = 0;
+    for (size_t it = 0; it < (size_t)kProfItems; ++it)
+        if (h[it * 8 + 7])
+            for (int k = 0; k < 8; ++k) out8[k] += h[it * 8 + k];
+    std::fill(h.begin(), h.end(), 0ull);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_arc_items), h.data(), h.size() * 8);
     int khz = 0;
     hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
     *ticks_per_us = khz / 1000.0;
@@ -1715,7 +1882,7 @@ ECC_API int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t 
     const int64_t tiles = (int64_t)((cfg->width + kTile - 1) / kTile) * ((cfg->height + kTile - 1) / kTile);
     uint32_t *cand = nullptr;
     int32_t *n_cand = nullptr;
-    if (n > 0 && cfg->slice_events % 4 == 0 && cfg->slice_events <= kFlagQuads * kFlagThreads * 4 &&
+    if (n > 0 && cfg->slice_events % 4 == 0 && cfg->slice_events <= kFlagCandMax &&
         tiles * kSegWords * 4 <= 160 * 1024) {
         int rc = ecc::nms_candidates(ctx, n, cfg->slice_events, cfg->width, cfg->height, box_size, &cand, &n_cand);
         if (rc) return rc;
@@ -1761,14 +1928,16 @@ ECC_API int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream) {
 ECC_API int ecc_fast_detect_stats(ecc_ctx *ctx, int64_t *out, int32_t n_out, ecc_stream_t stream) {
     if (!ctx || n_out < 0 || (n_out > 0 && !out)) return ECC_ERR_INVALID;
     CornerState *st = state_of(ctx);
-    uint32_t over = 0;
+    uint32_t ov[2] = {0, 0};
     if (st->n_over) {
-        ECC_CHECK_HIP(ctx, hipMemcpyAsync(&over, st->n_over, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
+        ECC_CHECK_HIP(ctx, hipMemcpyAsync(ov, st->n_over, 8, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
                       "read overflow count");
         ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
     }
-    const int64_t v[4] = {st->n_items, (int64_t)over, st->n_slices, st->n_groups};
-    for (int i = 0; i < n_out && i < 4; ++i) out[i] = v[i];
+    // [1] = items taken by arc_dense_kernel (windows above the compact list + deferred exact items),
+    // [4] = the deferred ones among them
+    const int64_t v[5] = {st->n_items, (int64_t)ov[0] + ov[1], st->n_slices, st->n_groups, (int64_t)ov[1]};
+    for (int i = 0; i < n_out && i < 5; ++i) out[i] = v[i];
     return ECC_OK;
 }
 
