@@ -42,12 +42,6 @@
 namespace {
 
 constexpr int kThreads = 256;
-#ifndef ECC_ARC_PERSIST
-#define ECC_ARC_PERSIST 0  // 1: persistent arc kernel, the next item's loads issued during the tests
-#endif
-#ifndef ECC_ARC_PLAN
-#define ECC_ARC_PLAN 0  // 1: heavy items listed before the arc tests, arc_dense_kernel on a second stream
-#endif
 constexpr int kBuildUnroll = 8;
 constexpr int kArcThreads = 512;  // 8 waves: one lane per window pixel (484) when staging
 constexpr int kGroup = 32;         // slices per group (mask bits)
@@ -736,7 +730,9 @@ __device__ __forceinline__ void exact_values(const ArcLds *L, int wp0, int64_t q
 // Both circles exactly (circle 3 skipped when it already passed on keys).  Out of line, called
 // only from arc_dense_item's exact phase, where nothing else is live.
 __device__ __noinline__ bool exact_pair_test(const ArcLds *L, int wp0, int64_t q0, uint32_t below, bool c3_passed,
-                                             const ExactCtx c) {
+                                             const int64_t *Bg, const int64_t *t, int64_t grp_first, int64_t Lt, int W,
+                                             bool narrow) {
+    const ExactCtx c{Bg, t, grp_first, Lt, W, narrow};  // scalars in registers, not a by-value struct on the stack
     if (!c3_passed) {
         int64_t v3[16];
         exact_values<16>(L, wp0, q0, below, c3dy, c3dx, c, v3);
@@ -750,6 +746,50 @@ __device__ __noinline__ bool exact_pair_test(const ArcLds *L, int wp0, int64_t q
 // 5. Arc test of one (group, tile) item, all items of all groups in one launch.  The item's
 // corner pairs go to res (slice-major, store_res_slice_major); flags_event_kernel applies them.
 constexpr int kStageUnroll = 4;
+
+// Window segment c (< 13) of item (grp, tile): the sub-regions of the 3x3 tiles around the tile
+// that its window covers (own tile: all; edge neighbours: the 3 facing sub-regions; corners: 1),
+// as (first entry, entries).  The geometry is packed into integer constants (a per-lane table
+// read would be a load): dx, dy in {-1,0,1} (2 bits + 1), first/last sub-region (4 bits).  The
+// three loads are unconditional and independent (clamped to the own item when the neighbour is
+// off the sensor), so they are in flight together: a load under a per-lane condition, or one
+// whose address waits on another, made them one round trip each.
+__device__ __forceinline__ void window_segment(const CornerGeom &g, int64_t grp, int tile, int c,
+                                               const int64_t *__restrict__ item_base,
+                                               const int32_t *__restrict__ sub_end, int64_t &b0, int &len) {
+    const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
+    const int sxt = (int)((0x2222215u >> (2 * c)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * c)) & 3u) - 1;
+    const int r0t = (int)((0x6835020268060ull >> (4 * c)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * c)) & 15u);
+    const int nx = tx + sxt, ny = ty + syt;
+    const bool ok = nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x;
+#ifndef ECC_SEG_NEW
+#define ECC_SEG_NEW 1
+#endif
+#if ECC_SEG_NEW
+    const int64_t bi = grp * g.n_tiles + (ok ? (int64_t)ny * g.tiles_x + nx : (int64_t)tile);
+    const int s0r = sub_end[bi * kSub + (r0t ? r0t - 1 : 0)];
+    const int s1 = sub_end[bi * kSub + r1t];
+    const int64_t ib = item_base[bi];
+    asm volatile("" ::"v"(s0r), "v"(s1), "v"(ib));  // keeps the loads out of an exec-mask branch
+    const int s0 = r0t ? s0r : 0;
+    b0 = ok ? ib + s0 : 0;
+    len = ok ? s1 - s0 : 0;
+#else
+    b0 = 0; len = 0;
+    if (ok) {
+        const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
+        const int s0 = r0t ? sub_end[bi * kSub + r0t - 1] : 0;
+        b0 = item_base[bi] + s0;
+        len = sub_end[bi * kSub + r1t] - s0;
+    }
+#endif
+}
+
+// window offset of segment c's tile origin
+__device__ __forceinline__ int window_segment_offset(int c) {
+    const int sxt = (int)((0x2222215u >> (2 * c)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * c)) & 3u) - 1;
+    return (syt * kTile) * kWin + sxt * kTile + kHalo * kWin + kHalo;
+}
 
 // Window segments: the sub-regions of the 3x3 tiles around the item's tile that its window
 // covers (own tile: all; edge neighbours: the 3 facing sub-regions; corners: 1) — 13 at most.
@@ -814,21 +854,9 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         L.n_exact = 0;
     }
     if (tid < kMaxSeg) {
-        // own tile: every sub-region; above/below: their facing rows; corners: one sub-region;
-        // left/right: their facing columns (3 sub-regions, one segment each)
-        // segment geometry packed into integer constants (a per-lane table read would be a load):
-        // dx, dy in {-1,0,1} (2 bits + 1), first/last sub-region (4 bits)
-        const int sxt = (int)((0x2222215u >> (2 * tid)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * tid)) & 3u) - 1;
-        const int r0t = (int)((0x6835020268060ull >> (4 * tid)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * tid)) & 15u);
-        const int nx = tx + sxt, ny = ty + syt;
-        int64_t b0 = 0;
-        int len = 0;
-        if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
-            const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
-            const int s0 = r0t ? sub_end[bi * kSub + r0t - 1] : 0;
-            b0 = item_base[bi] + s0;
-            len = sub_end[bi * kSub + r1t] - s0;
-        }
+        int64_t b0;
+        int len;
+        window_segment(g, grp, tile, tid, item_base, sub_end, b0, len);
         int incl = len;  // prefix over lanes 0..12 of wave 0
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
@@ -837,7 +865,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         }
         L.seg_lo[tid] = b0;
         L.seg_pref[tid + 1] = incl;
-        L.seg_off[tid] = (syt * kTile) * kWin + sxt * kTile + kHalo * kWin + kHalo;
+        L.seg_off[tid] = window_segment_offset(tid);
         if (tid == 0) L.seg_pref[0] = 0;
     }
     __syncthreads();
@@ -854,15 +882,22 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     for (int i0 = 0; i0 < total; i0 += kStageUnroll * kArcThreads) {
         PairEntry ent[kStageUnroll];
         int sg[kStageUnroll];
+        int64_t ea[kStageUnroll];
+        // segment starts first, then the loads unconditional on clamped indices (in flight together)
 #pragma unroll
         for (int u = 0; u < kStageUnroll; ++u) {
-            const int i = i0 + u * kArcThreads + tid;
+            const int i = min(i0 + u * kArcThreads + tid, total - 1);
             int r = 0;
 #pragma unroll
             for (int c = 1; c < kMaxSeg; ++c) r += (i >= pref[c]) ? 1 : 0;
-            sg[u] = (i < total) ? r : -1;
-            ent[u] = (i < total) ? entries[L.seg_lo[r] + (i - L.seg_pref[r])] : PairEntry{0u, 0u};
+            int pr = 0;
+#pragma unroll
+            for (int c = 1; c < kMaxSeg; ++c) pr = (r == c) ? pref[c] : pr;
+            sg[u] = (i0 + u * kArcThreads + tid < total) ? r : -1;
+            ea[u] = L.seg_lo[r] + (i - pr);
         }
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; ++u) ent[u] = entries[ea[u]];
 #pragma unroll
         for (int u = 0; u < kStageUnroll; ++u) {
             if (sg[u] < 0) continue;
@@ -949,7 +984,6 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     __syncthreads();
     DENSE_MARK(4);  // circle 4
     if (!fast || L.n_exact) {  // uniform; rare: the exact int64 tests
-        const ExactCtx ec{Bg, t, grp_first, Lt, g.W, narrow};
         for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
             const int e = L.tasks[ti], pi = e & 0x3fff;
             if (fast && !(e & (kOpen3 | kOpen4))) continue;
@@ -957,7 +991,8 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
             const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
             const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
             const uint32_t below = below_mask(j);
-            if (exact_pair_test(&L, wp0, q0, below, (e & kOpen4) != 0, ec)) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
+            if (exact_pair_test(&L, wp0, q0, below, (e & kOpen4) != 0, Bg, t, grp_first, Lt, g.W, narrow))
+                atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
         }
         __syncthreads();
     }
@@ -1059,24 +1094,10 @@ __device__ __forceinline__ void arc_prefetch(ArcPre &p, int64_t item, const Corn
         p.bq = gB[grp * HW + q];
         p.mk = gmask[grp * HW + q];
     }
-    if (tid < kMaxSeg) {
-        // segment geometry packed into integer constants (a per-lane table read would be a load):
-        // dx, dy in {-1,0,1} (2 bits + 1), first/last sub-region (4 bits)
-        const int sxt = (int)((0x2222215u >> (2 * tid)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * tid)) & 3u) - 1;
-        const int r0t = (int)((0x6835020268060ull >> (4 * tid)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * tid)) & 15u);
-        const int nx = tx + sxt, ny = ty + syt;
-        if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
-            const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
-            const int s0 = r0t ? sub_end[bi * kSub + r0t - 1] : 0;
-            p.b0 = item_base[bi] + s0;
-            p.len = sub_end[bi * kSub + r1t] - s0;
-        }
-    }
+    if (tid < kMaxSeg) window_segment(g, grp, tile, tid, item_base, sub_end, p.b0, p.len);
 }
 
-// The arc tests of one (group, tile) item from its prefetched phase-A loads `pre`.  kPersist:
-// the next item's loads are issued into `nxt` (after barrier 3, or at an early exit), and the
-// caller syncs before the next item reuses the LDS.
+// The arc tests of one (group, tile) item from its phase-A loads `pre`.
 //   A: segment table, wave scans of the value counts and of min B_g     -> barrier 1
 //   B: entry loads issued; pixel records, B_g slots, clamp               -> barrier 2
 //   C: tasks, value scatter                                              -> barrier 3
@@ -1085,22 +1106,15 @@ __device__ __forceinline__ void arc_prefetch(ArcPre &p, int64_t item, const Corn
 // the wave prefix of the counts and the window minimum of B_g are all known before the first
 // barrier; the entries are loaded right after it, while the pixel records and B_g slots are
 // written, and scattered after the second.
-template <bool kPersist>
-__device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPre &pre, ArcPre &nxt, int64_t next_item,
+__device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPre &pre,
                                          const int64_t *__restrict__ t, const CornerGeom &g,
                                          const int64_t *__restrict__ item_base, const PairEntry *__restrict__ entries,
                                          const int32_t *__restrict__ sub_end, const int64_t *__restrict__ gB,
                                          const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
                                          int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
-    auto prefetch_next = [&]() {
-        if constexpr (kPersist) arc_prefetch(nxt, next_item, g, item_base, sub_end, gB, gmask);
-    };
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
-    if ((grp + 1) * kGroup <= g.first_detect) {  // every slice of the group precedes detection
-        prefetch_next();
-        return;
-    }
+    if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #if ECC_ARC_PROFILE
     unsigned long long arc_t_ = wall_clock64(), arc_ph_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1124,7 +1138,6 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         L.redo = 0;
     }
     if (tid < kMaxSeg) {
-        const int sxt = (int)((0x2222215u >> (2 * tid)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * tid)) & 3u) - 1;
         int incl = pre.len;
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
@@ -1133,7 +1146,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         }
         L.seg_lo[tid] = pre.b0;
         L.seg_pref[tid + 1] = incl;
-        L.seg_off[tid] = (syt * kTile) * kWin + sxt * kTile + kHalo * kWin + kHalo;
+        L.seg_off[tid] = window_segment_offset(tid);
         if (tid == 0) L.seg_pref[0] = 0;
     }
     const int cnt = win_lane ? __popc(mk_w) + 1 : 0;  // the pixel's values + its B_g slot
@@ -1156,9 +1169,8 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     const int total = L.seg_pref[kMaxSeg];
     if (L.seg_pref[1] == 0 || total > kValCap) {  // uniform
         // no events in the tile: nothing to flag; too many values for the compact list: the
-        // dense kernel takes it (listed by arc_plan_kernel with ECC_ARC_PLAN)
-        if (!ECC_ARC_PLAN && total > kValCap && L.seg_pref[1] != 0 && tid == 0) over[atomicAdd(n_over, 1u)] = item;
-        prefetch_next();
+        // dense kernel takes it
+        if (total > kValCap && L.seg_pref[1] != 0 && tid == 0) over[atomicAdd(n_over, 1u)] = item;
         return;
     }
     int pref[kMaxSeg + 1];
@@ -1167,6 +1179,13 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     PairEntry ent[kSparseHold];
     int ewp[kSparseHold];
     const int slots = (total + kArcThreads - 1) / kArcThreads;  // uniform: the slots in use
+    // every slot's segment start first (LDS reads all in flight), then every entry load, with
+    // clamped indices and no per-lane condition: a load inside an exec-mask branch, or behind its
+    // own LDS round trip, issued the eight loads one LDS round trip apart
+#ifndef ECC_EB_NEW
+#define ECC_EB_NEW 0
+#endif
+#if !ECC_EB_NEW
 #pragma unroll
     for (int u = 0; u < kSparseHold; ++u) {
         ewp[u] = -1;
@@ -1178,6 +1197,27 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         ent[u] = (i < total) ? entries[L.seg_lo[r] + (i - L.seg_pref[r])] : PairEntry{0u, 0u};
         ewp[u] = (i < total) ? r : -1;
     }
+#else
+    int64_t ea[kSparseHold];
+#pragma unroll
+    for (int u = 0; u < kSparseHold; ++u) {
+        if (u >= slots) break;
+        const int i = min(u * kArcThreads + tid, total - 1);
+        int r = 0;
+#pragma unroll
+        for (int c = 1; c < kMaxSeg; ++c) r += (i >= pref[c]) ? 1 : 0;
+        int pr = 0;
+#pragma unroll
+        for (int c = 1; c < kMaxSeg; ++c) pr = (r == c) ? pref[c] : pr;
+        ea[u] = L.seg_lo[r] + (i - pr);
+        ewp[u] = (u * kArcThreads + tid < total) ? r : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kSparseHold; ++u) {
+        if (u >= slots) break;
+        ent[u] = entries[ea[u]];
+    }
+#endif
     if (win_lane) {
         int off = incl - cnt;
         for (int w = 0; w < wave; ++w) off += L.wave_tot[w];
@@ -1192,7 +1232,6 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     ARC_MARK(1);  // B
     if (L.exact_only) {  // uniform: a wide group or a value above t_last — the exact kernel takes it
         if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
-        prefetch_next();
         return;
     }
 #pragma unroll
@@ -1209,7 +1248,6 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     }
     __syncthreads();  // 3
     ARC_MARK(2);  // C
-    prefetch_next();  // the next item's loads fly during the tests
     // Tests through the compact lists, on clamped 32-bit keys only.  No exact int64 path and no
     // call: an item its keys cannot decide (a wide group, a value above t_last, a tie the clamping
     // may have merged) or whose circle-3 survivors overflow the queue goes whole to
@@ -1290,67 +1328,11 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     const int64_t per = gridDim.x / 8;
     const int64_t item = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
     if (item >= n_items) return;
-    ArcPre pre, unused;
+    ArcPre pre;
     arc_prefetch(pre, item, g, item_base, sub_end, gB, gmask);
-    arc_item<false>(L, item, pre, unused, -1, t, g, item_base, entries, sub_end, gB, gmask, res, over, n_over);
+    arc_item(L, item, pre, t, g, item_base, entries, sub_end, gB, gmask, res, over, n_over);
 }
 
-// Persistent form: a resident grid (four workgroups per CU) walks the items of its XCD's range,
-// workgroup l of an XCD taking items l, l + G, l + 2G, ... of the range (G workgroups per XCD),
-// and loads each next item's B_g window, masks and segment table while the current item's tests
-// run, so one of the item's two dependent global round trips is off its critical path.
-__global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)
-arc_persist_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
-                   const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
-                   const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
-                   int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
-    __shared__ SparseLds L;
-    const int64_t per = (n_items + 7) / 8;
-    const int64_t x = blockIdx.x % 8, G = gridDim.x / 8;
-    const int64_t lo = x * per, hi = min(n_items, lo + per);
-    int64_t item = lo + blockIdx.x / 8;
-    if (item >= hi) return;
-    ArcPre cur, nxt;
-    arc_prefetch(cur, item, g, item_base, sub_end, gB, gmask);
-    for (;;) {
-        const int64_t next = item + G < hi ? item + G : -1;
-        arc_item<true>(L, item, cur, nxt, next, t, g, item_base, entries, sub_end, gB, gmask, res, over, n_over);
-        if (next < 0) break;
-        __syncthreads();  // the LDS of this item is read out before the next one's phase A
-        cur = nxt;
-        item = next;
-    }
-}
-
-// Items whose window holds more values than the compact list (and whose own tile has pairs),
-// listed BEFORE the arc tests: arc_dense_kernel then works through them on a second stream beside
-// arc_kernel instead of after it (its ~430 heavy items take one long round at two workgroups per
-// CU: a 45 us tail of the corner chain when run after arc_kernel).  One thread per item; the
-// window's 13 segments exactly as arc_kernel builds them.
-__global__ void __launch_bounds__(kThreads)
-arc_plan_kernel(CornerGeom g, int64_t n_items, const int32_t *__restrict__ sub_end, int64_t *__restrict__ over,
-                uint32_t *__restrict__ n_over) {
-    const int64_t item = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (item >= n_items) return;
-    const int64_t grp = item / g.n_tiles;
-    if ((grp + 1) * kGroup <= g.first_detect) return;
-    const int tile = (int)(item % g.n_tiles);
-    const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
-    int total = 0, own = 0;
-#pragma unroll
-    for (int c = 0; c < kMaxSeg; ++c) {
-        const int sxt = (int)((0x2222215u >> (2 * c)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * c)) & 3u) - 1;
-        const int r0t = (int)((0x6835020268060ull >> (4 * c)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * c)) & 15u);
-        const int nx = tx + sxt, ny = ty + syt;
-        if (nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x) {
-            const int64_t bi = grp * g.n_tiles + (int64_t)ny * g.tiles_x + nx;
-            const int len = sub_end[bi * kSub + r1t] - (r0t ? sub_end[bi * kSub + r0t - 1] : 0);
-            total += len;
-            own = c == 0 ? len : own;
-        }
-    }
-    if (own > 0 && total > kValCap) over[atomicAdd(n_over, 1u)] = item;
-}
 
 // The windows above the compact list's capacity (arc_kernel's overflow list), each with the
 // dense per-slice planes.
@@ -1551,9 +1533,6 @@ struct CornerState {
     // diagnostics of the last detection (ecc_fast_detect_stats)
     const uint32_t *n_over = nullptr;
     int64_t n_items = 0, n_slices = 0, n_groups = 0;
-    // the second stream arc_dense_kernel runs on beside arc_kernel (ECC_ARC_PLAN), fork/join events
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
 };
 
 std::mutex g_state_mu;
@@ -1586,9 +1565,8 @@ struct GroupImages {
     PairEntry *entries;   // [n] distinct (slice, pixel) pairs per item, at item_base[item]
     int64_t *item_base;   // [n_items]
     int32_t *sub_end;     // [n_items][kSub] sub-region ends inside each item's entries
-    int64_t *over;        // [n_items] items whose windows exceed the compact list (arc_dense_kernel)
-    int64_t *over2;       // [n_items] items arc_kernel defers to the exact path (ECC_ARC_PLAN)
-    uint32_t *n_over;     // [0]: heavy items, [1]: deferred items
+    int64_t *over;        // [n_items] items arc_kernel leaves to arc_dense_kernel (heavy or undecidable)
+    uint32_t *n_over;     // [0]: their count
 };
 
 Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_items, int64_t n_groups, int32_t **first_border,
@@ -1606,7 +1584,6 @@ Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_items, int64_t n_g
     gi->item_base = cv.take<int64_t>((size_t)n_items);
     gi->sub_end = cv.take<int32_t>((size_t)n_items * kSub);
     gi->over = cv.take<int64_t>((size_t)n_items);
-    gi->over2 = cv.take<int64_t>((size_t)n_items);
     gi->n_over = cv.take<uint32_t>(64);
     return so;
 }
@@ -1647,9 +1624,6 @@ void corner_state_release(const ecc_ctx *ctx) {
         g_states.erase(it);
     }
     if (st->evt) (void)hipFree(st->evt);
-    if (st->side) (void)hipStreamDestroy(st->side);
-    if (st->fork) (void)hipEventDestroy(st->fork);
-    if (st->join) (void)hipEventDestroy(st->join);
     delete st;
 }
 }  // namespace ecc
@@ -1752,7 +1726,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         ECC_CHECK_LAUNCH(ctx, "fast_detect_prepare");
         return ECC_OK;
     }
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 8, s), "memset(overflow counts)");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
     st->n_over = gi.n_over;
     st->n_items = n_items;
     st->n_slices = g.n_slices;
@@ -1764,48 +1738,19 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         hipLaunchKernelGGL(sae_prefix_kernel, dim3(blocks), dim3(kThreads), 0, s, g, n_groups,
                            (const uint32_t *)gi.mask, gi.B, sae);
     }
-    // heavy items (n_over[0], list `over`) and the items arc_kernel defers to the exact path
-    // (n_over[1], list `over2`; the same list as the heavy ones without the plan)
-    int64_t *const over2 = ECC_ARC_PLAN ? gi.over2 : gi.over;
-    uint32_t *const n_over2 = ECC_ARC_PLAN ? gi.n_over + 1 : gi.n_over;
-    auto dense = [&](hipStream_t sd, const int64_t *list, const uint32_t *cnt) {
-        ECC_TIMED(ctx, sd, "arc_dense_kernel");  // dense planes
-        hipLaunchKernelGGL(arc_dense_kernel, dim3(512), dim3(kArcThreads), 0, sd, t, g, list, cnt,
-                           (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
-                           (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res);
-    };
-    if (ECC_ARC_PLAN) {
-        {
-            ECC_TIMED(ctx, s, "arc_plan_kernel");
-            hipLaunchKernelGGL(arc_plan_kernel, dim3(blocks_for(n_items, kThreads)), dim3(kThreads), 0, s, g, n_items,
-                               (const int32_t *)gi.sub_end, gi.over, gi.n_over);
-        }
-        if (!st->side) {
-            ECC_CHECK_HIP(ctx, hipStreamCreateWithFlags(&st->side, hipStreamNonBlocking), "corner side stream");
-            ECC_CHECK_HIP(ctx, hipEventCreateWithFlags(&st->fork, hipEventDisableTiming), "corner fork event");
-            ECC_CHECK_HIP(ctx, hipEventCreateWithFlags(&st->join, hipEventDisableTiming), "corner join event");
-        }
-        ECC_CHECK_HIP(ctx, hipEventRecord(st->fork, s), "fork");
-        ECC_CHECK_HIP(ctx, hipStreamWaitEvent(st->side, st->fork, 0), "fork wait");
-        dense(st->side, gi.over, gi.n_over);
-        ECC_CHECK_HIP(ctx, hipEventRecord(st->join, st->side), "join");
-    }
     {
         ECC_TIMED(ctx, s, "arc_kernel");
-        if (ECC_ARC_PERSIST) {
-            const unsigned grid = (unsigned)(8 * std::min<int64_t>((n_items + 7) / 8, ctx->n_cu / 2));  // 4 per CU
-            hipLaunchKernelGGL(arc_persist_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
-                               (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
-                               (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, over2, n_over2);
-        } else {
-            const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
-            hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
-                               (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
-                               (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, over2, n_over2);
-        }
+        const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
+        hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items, (const int64_t *)gi.item_base,
+                           (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end, (const int64_t *)gi.B,
+                           (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over);
     }
-    if (ECC_ARC_PLAN) ECC_CHECK_HIP(ctx, hipStreamWaitEvent(s, st->join, 0), "join wait");
-    dense(s, over2, n_over2);  // the deferred items (with the plan: none on ordinary streams)
+    {
+        ECC_TIMED(ctx, s, "arc_dense_kernel");  // the items arc_kernel left: dense planes, exact tests
+        hipLaunchKernelGGL(arc_dense_kernel, dim3(512), dim3(kArcThreads), 0, s, t, g, (const int64_t *)gi.over,
+                           (const uint32_t *)gi.n_over, (const int64_t *)gi.item_base, (const PairEntry *)gi.entries,
+                           (const int32_t *)gi.sub_end, (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res);
+    }
     {
         ECC_TIMED(ctx, s, "flags_kernel");
         constexpr size_t kLdsMax = 160 * 1024;
@@ -1928,16 +1873,14 @@ ECC_API int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream) {
 ECC_API int ecc_fast_detect_stats(ecc_ctx *ctx, int64_t *out, int32_t n_out, ecc_stream_t stream) {
     if (!ctx || n_out < 0 || (n_out > 0 && !out)) return ECC_ERR_INVALID;
     CornerState *st = state_of(ctx);
-    uint32_t ov[2] = {0, 0};
+    uint32_t ov = 0;
     if (st->n_over) {
-        ECC_CHECK_HIP(ctx, hipMemcpyAsync(ov, st->n_over, 8, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
+        ECC_CHECK_HIP(ctx, hipMemcpyAsync(&ov, st->n_over, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
                       "read overflow count");
         ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
     }
-    // [1] = items taken by arc_dense_kernel (windows above the compact list + deferred exact items),
-    // [4] = the deferred ones among them
-    const int64_t v[5] = {st->n_items, (int64_t)ov[0] + ov[1], st->n_slices, st->n_groups, (int64_t)ov[1]};
-    for (int i = 0; i < n_out && i < 5; ++i) out[i] = v[i];
+    const int64_t v[4] = {st->n_items, (int64_t)ov, st->n_slices, st->n_groups};
+    for (int i = 0; i < n_out && i < 4; ++i) out[i] = v[i];
     return ECC_OK;
 }
 

@@ -392,10 +392,9 @@ class Context:
         return lib.ecc_fast_detect_status(self.ctx, self.stream)
 
     def fast_detect_stats(self) -> dict:
-        out = np.zeros(5, np.int64)
-        check(lib.ecc_fast_detect_stats(self.ctx, out.ctypes.data, 5, self.stream), "ecc_fast_detect_stats")
-        return {"items": int(out[0]), "overflow_items": int(out[1]), "slices": int(out[2]), "groups": int(out[3]),
-                "exact_items": int(out[4])}
+        out = np.zeros(4, np.int64)
+        check(lib.ecc_fast_detect_stats(self.ctx, out.ctypes.data, 4, self.stream), "ecc_fast_detect_stats")
+        return {"items": int(out[0]), "overflow_items": int(out[1]), "slices": int(out[2]), "groups": int(out[3])}
 
     def sae_scatter(self, xy: DeviceArray, t: DeviceArray, n: int, w: int, h: int,
                     sae: DeviceArray):

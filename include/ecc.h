@@ -270,7 +270,7 @@ int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream);
  * out[0] = (group of 32 slices, 14x14 tile) work items, out[1] = items tested by the dense-plane
  * kernel (windows holding more values than the compact per-pixel lists take, and items whose
  * clamped 32-bit keys could not decide a test: those take the exact int64 path), out[2] =
- * slices, out[3] = groups, out[4] = the undecided items among out[1].  Writes min(n_out, 5). */
+ * slices, out[3] = groups.  Writes min(n_out, 4). */
 int ecc_fast_detect_stats(ecc_ctx *ctx, int64_t *out, int32_t n_out, ecc_stream_t stream);
 /* Multi-GPU SAE hand-off: out[q] = max over images[i*hw + q], i < n_images (the shards'
  * local final SAEs of all LOWER ranks give a rank its exact initial SAE; max == last writer
