@@ -117,14 +117,17 @@ __device__ __forceinline__ int wave_first_comp(const int *parent, const int32_t 
     return first;
 }
 
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, 8)  // 64 VGPRs: two 16-wave workgroups per CU
 dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict__ seg_counts,
                       const int64_t *__restrict__ offsets, const int32_t *__restrict__ nbr, int64_t nbr_len,
                       int min_pts, int min_size,
                       int max_size, int32_t *__restrict__ labels, int32_t *__restrict__ n_clusters,
                       int64_t *__restrict__ dups, int64_t dup_cap, unsigned long long *n_dups, int32_t *err) {
-    __shared__ int parent[kMaxPts];
-    __shared__ int c_size[kMaxComp], c_front[kMaxComp], c_rank[kMaxComp];
+    // parent[] sized by the stride (dynamic), the ranks in 16 bits: 72 KB at stride 8192, so
+    // two workgroups share a CU (the static 16384-entry parent[] held one per CU)
+    extern __shared__ int parent[];  // [stride]
+    __shared__ int c_size[kMaxComp], c_front[kMaxComp];
+    __shared__ int16_t c_rank[kMaxComp];
     __shared__ int wsum[kThreads / 64];
     __shared__ int s_kept;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -157,23 +160,20 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         __syncthreads();
         // 3. compress; roots -> component ids in ascending root order (block scan over j)
         constexpr int kPer = kMaxPts / kThreads;  // 16 consecutive points per lane
-        int roots[kPer], nr = 0;
+        uint32_t roots = 0;  // bit u: point j0 + u is a root
+        int nr = 0;
         const int j0 = tid * kPer;
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
             const int j = j0 + u;
-            roots[u] = 0;
-            if (j < m && parent[j] != -1) {
-                const int r = uf_find(parent, j);
-                roots[u] = r == j;
-                nr += roots[u];
-            }
+            if (j < m && parent[j] != -1 && uf_find(parent, j) == j) roots |= 1u << u;
         }
+        nr = __popc(roots);
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {  // non-roots point at their root (only root values are written)
             const int j = j0 + u;
-            if (j < m && parent[j] != -1 && !roots[u]) parent[j] = uf_root(parent, j);
+            if (j < m && parent[j] != -1 && !((roots >> u) & 1u)) parent[j] = uf_root(parent, j);
         }
         int x = nr;
 #pragma unroll
@@ -192,7 +192,7 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         if (nc <= kMaxComp) {
 #pragma unroll
             for (int u = 0; u < kPer; ++u)
-                if (roots[u]) parent[j0 + u] = -(cid++) - 2;
+                if ((roots >> u) & 1u) parent[j0 + u] = -(cid++) - 2;
         }
         __syncthreads();
         if (nc > kMaxComp) {  // too many components for the LDS tables
@@ -249,7 +249,7 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
                 }
                 atomicAdd(&s_kept, 1);
             }
-            c_rank[c] = r;
+            c_rank[c] = (int16_t)r;
         }
         __syncthreads();
         if (tid == 0) n_clusters[s] = s_kept;
@@ -612,8 +612,18 @@ ECC_API int ecc_dbscan_extract(ecc_ctx *ctx, int64_t n_segs, int64_t seg_stride,
     if (n_dups) ECC_CHECK_HIP(ctx, hipMemsetAsync(n_dups, 0, 8, s), "memset(n_dups)");
     if (n_segs == 0) return ECC_OK;
     const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 4096);
+    const size_t lds = (size_t)seg_stride * sizeof(int);
+    if (lds > 65536) {
+        static bool lds_set = false;
+        if (!lds_set) {
+            ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&dbscan_extract_kernel),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kMaxPts * (int)sizeof(int)),
+                          "dbscan_extract LDS");
+            lds_set = true;
+        }
+    }
     ECC_TIMED(ctx, s, "dbscan_extract_kernel");
-    hipLaunchKernelGGL(dbscan_extract_kernel, dim3(grid), dim3(kThreads), 0, s, n_segs, seg_stride, seg_counts,
+    hipLaunchKernelGGL(dbscan_extract_kernel, dim3(grid), dim3(kThreads), lds, s, n_segs, seg_stride, seg_counts,
                        offsets, nbr, nbr_len, min_pts, min_cluster_size, max_cluster_size, labels, n_clusters, dups, dup_cap,
                        reinterpret_cast<unsigned long long *>(n_dups), err);
     ECC_CHECK_LAUNCH(ctx, "dbscan_extract");

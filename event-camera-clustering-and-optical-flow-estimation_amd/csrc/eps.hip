@@ -25,7 +25,12 @@ namespace {
 using ecc::epsg::CellGrid;
 using ecc::epsg::kCells;
 using ecc::epsg::kNT;
+using ecc::buffer_load_u32;
+using ecc::buffer_view;
+using ecc::xy_x;
+using ecc::xy_y;
 constexpr int kMaxPts = 16384;
+constexpr int kLeftWord = 9;  // ctx->flags[9]: segments the row-run counts left to the candidate walk
 
 struct SegView {
     const int32_t *counts;
@@ -41,10 +46,12 @@ __device__ __forceinline__ int seg_points(const SegView &sv, int64_t s) {
 // cend[kCells + 1] | spt[stride] | sidx[stride] and, when kStage, st_cnt[stride] (u16) |
 // st_d2[stride] (u32, K > 0): the results by segment index, written out coalesced after the
 // queries.  ~120 KB at stride 8192 with core distances.
+// `left` (row-run leftovers mode, K == 0): only the segments eps_run_counts_kernel marked
+// (counts[base] == -1; *left = how many) are processed.
 template <int K, bool kStage>
 __global__ void __launch_bounds__(kNT)
 eps_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32_t r2i, int min_pts,
-                  int32_t *__restrict__ counts, double *__restrict__ core) {
+                  int32_t *__restrict__ counts, double *__restrict__ core, const int32_t *__restrict__ left) {
     extern __shared__ uint32_t lds_c[];
     uint32_t *cend = lds_c;
     uint32_t *spt = cend + kCells + 1;
@@ -53,9 +60,11 @@ eps_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32
     uint32_t *st_d2 = reinterpret_cast<uint32_t *>(st_cnt + ((sv.stride + 1) & ~1ll));
     __shared__ int red[64];
     const int tid = threadIdx.x;
+    if (left && *left == 0) return;  // uniform: no leftovers
     for (int64_t s = blockIdx.x; s < sv.n_segs; s += gridDim.x) {
         const int m = seg_points(sv, s);
         const int64_t base = s * sv.stride;
+        if (left && (m == 0 || counts[base] != -1)) continue;  // uniform: done by the row-run kernel
         const CellGrid g = ecc::epsg::bin_cells(xy, base, m, e_int, r2i, cend, spt, sidx, red, false, true);
         ecc::epsg::with_narrow(g, [&](auto narrow) {
             constexpr bool kN = decltype(narrow)::value;
@@ -105,6 +114,168 @@ eps_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32
             }
         }
         __syncthreads();
+    }
+}
+
+// Row-run form.  A segment's points are distinct pixels whenever it is a downsample window (one
+// representative per hash bucket, and a pixel always hashes to the same bucket), so the segment is
+// an occupancy bitmap over its bounding box, one bit per pixel, 32 pixels a word, each word paired
+// with the number of points in the words before it (row-major).  The points of row y in [xl, xh)
+// then number prefix(y, xh) - prefix(y, xl), with prefix(y, x) = base[word] + popc(bits[word]
+// below x): a query's count is a sum over the 2*eps + 1 rows of the disk (half-width w(dy) =
+// floor(sqrt(floor(eps^2) - dy^2)), the same integer test d^2 <= floor(eps^2) as the candidate
+// walk), two LDS reads per row, no candidate loop and no test.  With core distances (K > 0) each
+// row's run is walked bit by bit instead (the run IS the row's neighbours: no test), keeping the
+// K smallest d^2 in the same insertion network as eps_counts_kernel.  The bitmap of a 346 x 260
+// sensor is 3120 words (25 KB): four 8-wave workgroups per CU share the CU's LDS, so one
+// segment's set-up barriers overlap the others' queries.  A segment whose bitmap exceeds
+// kRunWords or that repeats a pixel is left to eps_counts_kernel (marked by counts[base] = -1,
+// counted in *left).
+constexpr int kRT = 512;
+constexpr int kRunWords = 4992;  // (bits, prefix) pairs: 39 KB, four workgroups per CU
+
+template <int K>
+__global__ void __launch_bounds__(kRT)
+eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32_t r2i, int min_pts,
+                      int32_t *__restrict__ counts, double *__restrict__ core, int32_t *__restrict__ left) {
+    __shared__ uint2 wd[kRunWords + 1];  // [kRunWords]: a zero word for rows outside the box
+    __shared__ int box[kRT / 64][4];
+    __shared__ int wsum[kRT / 64];
+    __shared__ int dup[2];  // by segment parity: reset one segment ahead, behind two barriers
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kW = kRT / 64;
+    if (tid == 0) {
+        wd[kRunWords] = make_uint2(0u, 0u);
+        dup[0] = dup[1] = 0;
+    }
+    int par = 0;
+    for (int64_t s = blockIdx.x; s < sv.n_segs; s += gridDim.x, par ^= 1) {
+        if (tid == 0) dup[par ^ 1] = 0;  // last read in the previous segment, before its barrier 6
+        const int m = seg_points(sv, s);
+        const int64_t base = s * sv.stride;
+        const __amdgpu_buffer_rsrc_t seg = buffer_view(xy + base, (uint32_t)m * 4u);
+        int xmn = 0x7fffffff, ymn = 0x7fffffff, xmx = -1, ymx = -1;
+        for (int q = tid; q < m; q += kRT) {
+            const uint32_t v = buffer_load_u32(seg, (uint32_t)q * 4u);
+            xmn = min(xmn, xy_x(v)); ymn = min(ymn, xy_y(v));
+            xmx = max(xmx, xy_x(v)); ymx = max(ymx, xy_y(v));
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            xmn = min(xmn, __shfl_xor(xmn, o)); ymn = min(ymn, __shfl_xor(ymn, o));
+            xmx = max(xmx, __shfl_xor(xmx, o)); ymx = max(ymx, __shfl_xor(ymx, o));
+        }
+        if (lane == 0) {
+            box[wave][0] = xmn; box[wave][1] = ymn;
+            box[wave][2] = xmx; box[wave][3] = ymx;
+        }
+        __syncthreads();  // 1
+        xmn = box[0][0]; ymn = box[0][1]; xmx = box[0][2]; ymx = box[0][3];
+#pragma unroll
+        for (int w = 1; w < kW; ++w) {
+            xmn = min(xmn, box[w][0]); ymn = min(ymn, box[w][1]);
+            xmx = max(xmx, box[w][2]); ymx = max(ymx, box[w][3]);
+        }
+        const int Wb = m ? xmx - xmn + 1 : 1, H = m ? ymx - ymn + 1 : 1;
+        const int WW = (Wb >> 5) + 1;  // words per row: x == Wb (a run's end) still has a word
+        const int64_t words = (int64_t)H * WW;
+        bool leftover = words > kRunWords;  // uniform
+        if (!leftover) {
+            for (int w = tid; w < words; w += kRT) wd[w] = make_uint2(0u, 0u);
+        }
+        __syncthreads();  // 2
+        if (!leftover) {
+            for (int q = tid; q < m; q += kRT) {
+                const uint32_t v = buffer_load_u32(seg, (uint32_t)q * 4u);
+                const int x = xy_x(v) - xmn, y = xy_y(v) - ymn;
+                const uint32_t bit = 1u << (x & 31);
+                const uint32_t old = atomicOr(&wd[y * WW + (x >> 5)].x, bit);
+                if (old & bit) dup[par] = 1;
+            }
+        }
+        __syncthreads();  // 3
+        leftover = leftover || dup[par];  // uniform
+        if (leftover) {
+            if (tid == 0 && m > 0) {
+                counts[base] = -1;
+                atomicAdd(left, 1);
+            }
+        } else {
+            if (K == 0) {  // prefix of the word popcounts: thread t takes words [t * per, t * per + per)
+                const int per = (int)((words + kRT - 1) / kRT);
+                const int w0 = tid * per, w1 = min(w0 + per, (int)words);
+                int loc = 0;
+                for (int w = w0; w < w1; ++w) loc += __popc(wd[w].x);
+                const int inc = ecc::wave_incl_scan(loc);
+                if (lane == 63) wsum[wave] = inc;
+                __syncthreads();  // 4
+                int off = inc - loc;
+                for (int w = 0; w < wave; ++w) off += wsum[w];
+                for (int w = w0; w < w1; ++w) {
+                    wd[w].y = (uint32_t)off;
+                    off += __popc(wd[w].x);
+                }
+                __syncthreads();  // 5
+            }
+            // queries in segment order: lane q's results at base + q (coalesced)
+            const int amax = min(e_int, H - 1);  // rows beyond the box hold nothing
+            for (int q = tid; q < sv.stride; q += kRT) {
+                int cnt = 0;
+                int best[K > 0 ? K : 1];
+#pragma unroll
+                for (int k = 0; k < (K > 0 ? K : 1); ++k) best[k] = 0x7fffffff;
+                if (q < m) {
+                    const uint32_t v = buffer_load_u32(seg, (uint32_t)q * 4u);
+                    const int x = xy_x(v) - xmn, y = xy_y(v) - ymn;
+                    int hw = e_int;  // floor(sqrt(r2i - a^2)), non-increasing in a (uniform)
+                    for (int a = 0; a <= amax; ++a) {
+                        while (hw > 0 && (uint32_t)(hw * hw) > r2i - (uint32_t)(a * a)) --hw;
+                        const int xl = max(x - hw, 0), xh = min(x + hw + 1, Wb);
+                        const uint32_t ml = (1u << (xl & 31)) - 1u, mh = (1u << (xh & 31)) - 1u;
+                        const int cl = xl >> 5, ch = xh >> 5;
+#pragma unroll
+                        for (int sgn = 0; sgn < 2; ++sgn) {
+                            if (sgn && a == 0) break;
+                            const int yy = sgn ? y - a : y + a;
+                            const bool ok = (unsigned)yy < (unsigned)H;
+                            const int rb = yy * WW;
+                            if (K == 0) {
+                                const uint2 lo = wd[ok ? rb + cl : kRunWords], hi = wd[ok ? rb + ch : kRunWords];
+                                cnt += (int)(hi.y - lo.y) + __popc(hi.x & mh) - __popc(lo.x & ml);
+                            } else if (ok) {
+                                for (int wi = cl; wi <= ch; ++wi) {
+                                    uint32_t b = wd[rb + wi].x;
+                                    if (wi == cl) b &= ~ml;
+                                    if (wi == ch) b &= mh;
+                                    while (b) {
+                                        const int dx = wi * 32 + __builtin_ctz(b) - x;
+                                        b &= b - 1u;
+                                        int val = dx * dx + a * a;
+                                        ++cnt;
+#pragma unroll
+                                        for (int k = 0; k < (K > 0 ? K : 1); ++k) {
+                                            const int lo2 = min(best[k], val);
+                                            val = max(best[k], val);
+                                            best[k] = lo2;
+                                        }
+                                    }
+                                }
+                            }
+                        }
+                    }
+                }
+                counts[base + q] = cnt;
+                if (K > 0) {
+                    uint32_t sel = 0xffffffffu;  // not a core point (or padding)
+                    if (cnt >= min_pts) {
+#pragma unroll
+                        for (int k = 0; k < (K > 0 ? K : 1); ++k) sel = (k == min_pts - 1) ? (uint32_t)best[k] : sel;
+                    }
+                    core[base + q] = sel == 0xffffffffu ? -1.0 : sqrt((double)sel);  // correctly rounded
+                }
+            }
+        }
+        __syncthreads();  // 6: the LDS is reused by the next segment
     }
 }
 
@@ -269,23 +440,38 @@ ECC_API int ecc_eps_counts(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int
     const size_t grid_lds = (size_t)(kCells + 1 + seg_stride) * 4 + (size_t)seg_stride * 2;
     const size_t stage_lds = (size_t)((seg_stride + 1) & ~1ll) * 2 + (core_dist ? (size_t)seg_stride * 4 : 0);
     const bool stage = grid_lds + stage_lds + 256 <= 160 * 1024;
-    using Kern = void (*)(const uint32_t *, SegView, int, uint32_t, int, int32_t *, double *);
 #define ECC_EPS_PICK(S)                                                                                        \
     (K == 0 ? eps_counts_kernel<0, S> : K <= 1 ? eps_counts_kernel<1, S> : K <= 2 ? eps_counts_kernel<2, S>     \
      : K <= 4 ? eps_counts_kernel<4, S> : K <= 8 ? eps_counts_kernel<8, S> : K <= 16 ? eps_counts_kernel<16, S> \
      : K <= 32 ? eps_counts_kernel<32, S> : eps_counts_kernel<64, S>)
+    using Kern = void (*)(const uint32_t *, SegView, int, uint32_t, int, int32_t *, double *, const int32_t *);
     const Kern kern = stage ? (Kern)ECC_EPS_PICK(true) : (Kern)ECC_EPS_PICK(false);
 #undef ECC_EPS_PICK
     const size_t lds = grid_lds + (stage ? stage_lds : 0);
     ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                   "eps_counts lds");
-    // segments are grid-strided; enough workgroups for every CU at the occupancy the LDS allows
-    const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 2048);
+    hipStream_t s = ecc::as_stream(stream);
+    // the row-run kernel, then its leftovers (segments that repeat a pixel or whose bitmap is
+    // larger than its LDS) through the candidate walk; the second launch exits at once without any
+    int32_t *left = ctx->flags + kLeftWord;
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(left, 0, 4, s), "memset(eps leftovers)");
     {
-        ECC_TIMED(ctx, ecc::as_stream(stream), "eps_counts_kernel");
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(kNT), lds, ecc::as_stream(stream), xy, sv, e_int, (uint32_t)r2i,
-                           min_pts, counts, core_dist);
+        using RunKern = void (*)(const uint32_t *, SegView, int, uint32_t, int, int32_t *, double *, int32_t *);
+        const RunKern rk = K == 0 ? eps_run_counts_kernel<0> : K <= 1 ? eps_run_counts_kernel<1>
+                         : K <= 2 ? eps_run_counts_kernel<2> : K <= 4 ? eps_run_counts_kernel<4>
+                         : K <= 8 ? eps_run_counts_kernel<8> : K <= 16 ? eps_run_counts_kernel<16>
+                         : K <= 32 ? eps_run_counts_kernel<32> : eps_run_counts_kernel<64>;
+        ECC_TIMED(ctx, s, "eps_run_counts_kernel");
+        const unsigned grid = (unsigned)std::min<int64_t>(n_segs, (int64_t)4 * ctx->n_cu);
+        hipLaunchKernelGGL(rk, dim3(grid), dim3(kRT), 0, s, xy, sv, e_int, (uint32_t)r2i, min_pts, counts, core_dist,
+                           left);
+    }
+    {
+        ECC_TIMED(ctx, s, "eps_counts_left_kernel");
+        const unsigned grid = (unsigned)std::min<int64_t>(n_segs, ctx->n_cu);  // one WG per CU (LDS)
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kNT), lds, s, xy, sv, e_int, (uint32_t)r2i, min_pts, counts,
+                           core_dist, (const int32_t *)left);
     }
     ECC_CHECK_LAUNCH(ctx, "eps_counts_kernel");
     return ECC_OK;

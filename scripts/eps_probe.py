@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """eps-neighbourhood / grid-DBSCAN kernels on the bench workload (the representatives of the
 20 M-event 346x260 stream, 2442 windows of 8192): a few calls each, for rocprofv3 counter passes.
-Usage: eps_probe.py [counts|dbscan|lists|all]  (lists: eps_lists + dbscan_extract)"""
+Usage: eps_probe.py [counts|dbscan|lists|all|time]  (lists: eps_lists + dbscan_extract)"""
 import sys
 from pathlib import Path
 
@@ -43,6 +43,25 @@ for _ in range(3):
         ctx.dbscan_grid(rep_xy, nw, WIN, uniq, 20.0, 20, 100, 25000, lab, nc, None, 0, nd)
 ctx.sync()
 print("ok", nw, int(uniq.numpy().sum()))
+
+if what == "time":  # per-kernel times of the counts (ε 20 counts only, ε 10 with core distances)
+    for eps, mp, co in ((20.0, 20, None), (10.0, 2, core)):
+        ctx.eps_counts(rep_xy, nw, WIN, uniq, eps, mp, cnt, co)
+        ctx.sync()
+        tmr = ecc.Timer(ctx.stream)
+        tmr.start()
+        for _ in range(10):
+            ctx.eps_counts(rep_xy, nw, WIN, uniq, eps, mp, cnt, co)
+        ms = tmr.stop() / 10
+        ctx.set_timing(True)
+        ctx.timing_reset()
+        for _ in range(10):
+            ctx.eps_counts(rep_xy, nw, WIN, uniq, eps, mp, cnt, co)
+        st = ctx.timing_report()
+        ctx.set_timing(False)
+        print(f"eps {eps} min_pts {mp} core {co is not None}: {ms:.4f} ms/call;",
+              {k: round(v["total_ms"] / v["launches"] * 1e3, 1) for k, v in st.items()}, "us; checksum",
+              int(cnt.numpy().astype(np.int64).sum()))
 
 if what == "dbscan" and hasattr(ecc.lib, "ecc_dbscan_profile"):
     import ctypes as C

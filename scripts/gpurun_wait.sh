@@ -3,7 +3,7 @@
 # ("transient": nothing ran, nothing was charged).  Any other outcome — success, a failure of the
 # command itself, a refusal — ends the loop.  Usage: gpurun_wait.sh <timeout_s> <log> <command>
 TMO="$1"; LOG="$2"; shift 2
-for attempt in $(seq 1 20); do
+for attempt in $(seq 1 ${GPURUN_ATTEMPTS:-60}); do
   timeout $((TMO + 900)) /usr/local/graft/bin/gpurun --timeout "$TMO" -- "$@" > "$LOG" 2>&1
   rc=$?
   st=$(python3 -c "import json; print(json.load(open('$(dirname "$0")/../gpurun_out/.last_call.json')).get('status'))" 2>/dev/null)

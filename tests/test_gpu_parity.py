@@ -979,6 +979,49 @@ def test_eps_counts_wide_segments(ecc, orc, gpu, eps, min_pts):
         assert (g_cnt[pad] == 0).all() and (g_core[pad] == -1.0).all()
 
 
+@pytest.mark.parametrize("min_pts", [0, 2, 20])
+@pytest.mark.parametrize("eps", [0.5, 1.01, 10.0, 20.0, 37.9, 400.0])
+def test_eps_counts_row_run_matches_oracle(ecc, orc, gpu, eps, min_pts):
+    """The row-run bitmap kernel (counts; with min_pts > 0 also core distances) on downsample
+    windows (distinct pixels), plus segments it must leave to the candidate walk — a repeated
+    pixel, a bounding box above its LDS bitmap — an empty segment and a full 8192-point segment;
+    padding counts 0 and core distance -1."""
+    xy, _, _ = ecc.gen_events(60_000, seed=43)
+    rep_xy, _, u, _ = orc.downsample_hash(xy)
+    rng = np.random.default_rng(7)
+    stride = 8192
+    segs, counts = [], []
+    for w in range(len(u)):
+        segs.append(rep_xy[w * stride:(w + 1) * stride])
+        counts.append(int(u[w]))
+    dup = rep_xy[:stride].copy()
+    dup[5] = dup[17]  # one repeated pixel
+    segs.append(dup); counts.append(int(u[0]))
+    wide = ecc.pack_xy(rng.integers(0, 3000, stride), rng.integers(0, 2000, stride))  # 2000 x 94 words
+    segs.append(wide); counts.append(3000)
+    segs.append(np.zeros(stride, np.uint32)); counts.append(0)
+    pix = rng.permutation(346 * 260)[:stride]  # 8192 distinct pixels
+    segs.append(ecc.pack_xy(pix % 346, pix // 346)); counts.append(stride)
+    allxy = np.concatenate(segs).astype(np.uint32)
+    counts = np.array(counts, np.int32)
+    n_segs = len(counts)
+    o_cnt, o_core, _, _ = orc.eps_neighbours(allxy, n_segs, stride, counts, eps, max(min_pts, 1), want_lists=False)
+    d_cnt = ecc.DeviceArray(n_segs * stride, np.int32)
+    d_core = ecc.DeviceArray(n_segs * stride, np.float64) if min_pts else None
+    gpu.eps_counts(dev(ecc, allxy), n_segs, stride, dev(ecc, counts), eps, max(min_pts, 1), d_cnt, d_core)
+    gpu.sync()
+    g_cnt = d_cnt.numpy()
+    g_core = d_core.numpy() if min_pts else None
+    for sgi in range(n_segs):
+        sl = slice(sgi * stride, sgi * stride + counts[sgi])
+        pad = slice(sgi * stride + counts[sgi], (sgi + 1) * stride)
+        assert (g_cnt[sl] == o_cnt[sl]).all(), sgi
+        assert (g_cnt[pad] == 0).all(), sgi
+        if min_pts:
+            assert np.array_equal(g_core[sl], o_core[sl]), sgi
+            assert (g_core[pad] == -1.0).all(), sgi
+
+
 def test_eps_duplicates_and_kdtree_kat(ecc, gpu):
     """kd-tree KATs of OPT/test/test_main.cpp:595-720 (radius 1.01), 1-D cases mapped onto the
     x axis (+4), including the duplicate-point case."""
