@@ -45,7 +45,7 @@ WINDOW = 8192
 CORNER_KERNELS = ("slice_sort_kernel", "pair_build_kernel", "sae_prefix_kernel", "arc_kernel",
                   "arc_dense_kernel", "flags_kernel")
 KMEANS_KERNELS = ("kmeans_count_kernel", "kmeans_count_sum_kernel", "kmeans_extent_kernel",
-                  "kmeans_pixel_pass", "kmeans_lloyd_kernel", "kmeans_step_kernel", "kmeans_xy16_labels")
+                  "kmeans_pixel_pass", "kmeans_step_kernel", "kmeans_xy16_labels")
 NMS_KERNELS = ("nms_compact_kernel", "nms_kernel")
 
 

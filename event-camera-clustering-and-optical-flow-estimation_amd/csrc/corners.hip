@@ -1055,9 +1055,6 @@ __device__ unsigned long long g_arc_items[kProfItems][8];
 // One item's phase-A loads (B_g and slice mask of window pixel `tid`, the segment `tid` < 13 of the
 // window), issued by arc_prefetch ahead of their use: the persistent arc kernel issues the next
 // item's while the current item's tests run.
-#ifndef ECC_ARC_WSEG
-#define ECC_ARC_WSEG 1
-#endif
 struct ArcPre {
     int64_t bq;   // B_g (INT64_MAX outside the sensor / past the window)
     uint32_t mk;  // slices of the group that touched the pixel
@@ -1084,8 +1081,7 @@ __device__ __forceinline__ void arc_prefetch(ArcPre &p, int64_t item, const Corn
         p.bq = gB[grp * HW + q];
         p.mk = gmask[grp * HW + q];
     }
-    const int c = ECC_ARC_WSEG ? (tid & 63) : tid;  // ECC_ARC_WSEG: every wave takes the 13 segments
-    if (c < kMaxSeg) window_segment(g, grp, tile, c, item_base, sub_end, p.b0, p.len);
+    if (tid < kMaxSeg) window_segment(g, grp, tile, tid, item_base, sub_end, p.b0, p.len);
 }
 
 // The arc tests of one (group, tile) item from its phase-A loads `pre`.
@@ -1128,66 +1124,6 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         L.q4n = 0;
         L.redo = 0;
     }
-#if ECC_ARC_WSEG
-    // Every wave scans the 13 window segments itself (its lanes 0-12 loaded them), so the entry
-    // loads need neither an LDS segment table nor barrier 1: they are issued here and fly while
-    // the waves meet at the barrier and write the pixel records.
-    PairEntry ent[kSparseHold];
-    int ewp[kSparseHold];
-    int slots;
-    {
-        const int len = lane < kMaxSeg ? pre.len : 0;
-        int sincl = len;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            const int v = __shfl_up(sincl, o, 16);
-            if (lane >= o) sincl += v;
-        }
-        const int sexcl = sincl - len;
-        const int total = __builtin_amdgcn_readlane(sincl, kMaxSeg - 1);
-        const int own = __builtin_amdgcn_readlane(sincl, 0);
-        if (own == 0 || total > kValCap) {  // uniform (every wave computes the same)
-            // no events in the tile: nothing to flag; too many values for the compact list: the
-            // dense kernel takes it
-            if (own != 0 && tid == 0) over[atomicAdd(n_over, 1u)] = item;
-            return;
-        }
-        int pref[kMaxSeg];  // segment starts (wave-uniform)
-#pragma unroll
-        for (int c = 1; c < kMaxSeg; ++c) pref[c] = __builtin_amdgcn_readlane(sexcl, c);
-        slots = (total + kArcThreads - 1) / kArcThreads;  // uniform: the slots in use
-#pragma unroll
-        for (int u = 0; u < kSparseHold; ++u) {
-            ewp[u] = -1;
-            if (u >= slots) continue;
-            const int i = u * kArcThreads + tid;
-            int r = 0;
-#pragma unroll
-            for (int c = 1; c < kMaxSeg; ++c) r += (i >= pref[c]) ? 1 : 0;
-            const int64_t b0r = __shfl(pre.b0, r);
-            const int pr = __shfl(sexcl, r);
-            ent[u] = (i < total) ? entries[b0r + (i - pr)] : PairEntry{0u, 0u};
-            ewp[u] = (i < total) ? r : -1;
-        }
-    }
-    const int cnt = win_lane ? __popc(mk_w) + 1 : 0;  // the pixel's values + its B_g slot
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
-    if (lane == 63) L.wave_tot[wave] = incl;
-    int64_t bmin = bq;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int64_t x = __shfl_xor(bmin, o);
-        bmin = x < bmin ? x : bmin;
-    }
-    if (lane == 0) L.wave_min[wave] = bmin;
-    __syncthreads();  // 1
-    ARC_MARK(0);  // A
-#else
     if (tid < kMaxSeg) {
         int incl = pre.len;
 #pragma unroll
@@ -1230,7 +1166,8 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     PairEntry ent[kSparseHold];
     int ewp[kSparseHold];
     const int slots = (total + kArcThreads - 1) / kArcThreads;  // uniform: the slots in use
-    // (clamped unconditional entry loads behind a separate address pass measured 15 us slower)
+    // (measured slower: clamped unconditional entry loads behind a separate address pass, 15 us;
+    // every wave scanning the 13 segments itself so the loads issue before barrier 1, 10 us)
 #pragma unroll
     for (int u = 0; u < kSparseHold; ++u) {
         ewp[u] = -1;
@@ -1242,7 +1179,6 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         ent[u] = (i < total) ? entries[L.seg_lo[r] + (i - L.seg_pref[r])] : PairEntry{0u, 0u};
         ewp[u] = (i < total) ? r : -1;
     }
-#endif
     if (win_lane) {
         int off = incl - cnt;
         for (int w = 0; w < wave; ++w) off += L.wave_tot[w];
@@ -1358,33 +1294,6 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
     arc_item(L, item, pre, t, g, item_base, entries, sub_end, gB, gmask, res, over, n_over);
 }
 
-
-#ifndef ECC_ARC_LOOP
-#define ECC_ARC_LOOP 0  // 1: resident arc workgroups taking items from per-XCD queues
-#endif
-// Resident form (ECC_ARC_LOOP): four workgroups per CU, each taking the next item of its XCD's
-// contiguous item range from a device counter (queue[xcd]), until the range is exhausted.
-__global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)
-arc_loop_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
-                const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
-                const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
-                int64_t *__restrict__ over, uint32_t *__restrict__ n_over, uint32_t *__restrict__ queue) {
-    __shared__ SparseLds L;
-    __shared__ int64_t next;
-    const int x = (int)(blockIdx.x % 8);
-    const int64_t per = (n_items + 7) / 8;
-    const int64_t lo = x * per, hi = min(lo + per, n_items);
-    for (;;) {
-        if (threadIdx.x == 0) next = lo + (int64_t)atomicAdd(&queue[x], 1u);
-        __syncthreads();
-        const int64_t item = next;
-        if (item >= hi) break;  // uniform
-        ArcPre pre;
-        arc_prefetch(pre, item, g, item_base, sub_end, gB, gmask);
-        arc_item(L, item, pre, t, g, item_base, entries, sub_end, gB, gmask, res, over, n_over);
-        __syncthreads();  // every lane has read `next`; the LDS is free for the next item
-    }
-}
 
 // The windows above the compact list's capacity (arc_kernel's overflow list), each with the
 // dense per-slice planes.
@@ -1618,7 +1527,7 @@ struct GroupImages {
     int64_t *item_base;   // [n_items]
     int32_t *sub_end;     // [n_items][kSub] sub-region ends inside each item's entries
     int64_t *over;        // [n_items] items arc_kernel leaves to arc_dense_kernel (heavy or undecidable)
-    uint32_t *n_over;     // [0]: their count; [8..15]: arc_loop_kernel's per-XCD item queues
+    uint32_t *n_over;     // [0]: their count
 };
 
 Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_items, int64_t n_groups, int32_t **first_border,
@@ -1778,7 +1687,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         ECC_CHECK_LAUNCH(ctx, "fast_detect_prepare");
         return ECC_OK;
     }
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 64, s), "memset(overflow count, item queues)");
+    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
     st->n_over = gi.n_over;
     st->n_items = n_items;
     st->n_slices = g.n_slices;
@@ -1792,13 +1701,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     }
     {
         ECC_TIMED(ctx, s, "arc_kernel");
-        if (ECC_ARC_LOOP) {
-            const unsigned grid = (unsigned)(8 * std::min<int64_t>((n_items + 7) / 8, ctx->n_cu / 2));  // 4 per CU
-            hipLaunchKernelGGL(arc_loop_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
-                               (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
-                               (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over,
-                               gi.n_over + 8);
-        } else {
+        {
             const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
             hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
                                (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,

@@ -124,29 +124,37 @@ eps_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32
 // then number prefix(y, xh) - prefix(y, xl), with prefix(y, x) = base[word] + popc(bits[word]
 // below x): a query's count is a sum over the 2*eps + 1 rows of the disk (half-width w(dy) =
 // floor(sqrt(floor(eps^2) - dy^2)), the same integer test d^2 <= floor(eps^2) as the candidate
-// walk), two LDS reads per row, no candidate loop and no test.  With core distances (K > 0) each
-// row's run is walked bit by bit instead (the run IS the row's neighbours: no test), keeping the
-// K smallest d^2 in the same insertion network as eps_counts_kernel.  The bitmap of a 346 x 260
+// walk), two LDS reads per row, no candidate loop and no test.  (Core distances keep the
+// candidate walk: walking each row's run bit by bit for the K smallest d^2 measured 0.68 -> 0.92
+// ms at OPTICS eps 10.)  The bitmap of a 346 x 260
 // sensor is 3120 words (25 KB): four 8-wave workgroups per CU share the CU's LDS, so one
 // segment's set-up barriers overlap the others' queries.  A segment whose bitmap exceeds
 // kRunWords or that repeats a pixel is left to eps_counts_kernel (marked by counts[base] = -1,
 // counted in *left).
 constexpr int kRT = 512;
-constexpr int kRunWords = 4992;  // (bits, prefix) pairs: 39 KB, four workgroups per CU
+constexpr int kRunWords = 4864;  // (bits, prefix) pairs: 38 KB, four workgroups per CU
+constexpr int kHwTab = 512;      // eps < 512 (larger eps: the candidate walk)
 
-template <int K>
 __global__ void __launch_bounds__(kRT)
-eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32_t r2i, int min_pts,
-                      int32_t *__restrict__ counts, double *__restrict__ core, int32_t *__restrict__ left) {
+eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32_t r2i,
+                      int32_t *__restrict__ counts, int32_t *__restrict__ left) {
     __shared__ uint2 wd[kRunWords + 1];  // [kRunWords]: a zero word for rows outside the box
     __shared__ int box[kRT / 64][4];
     __shared__ int wsum[kRT / 64];
     __shared__ int dup[2];  // by segment parity: reset one segment ahead, behind two barriers
+    __shared__ uint16_t hwt[kHwTab];  // disk half-widths floor(sqrt(floor(eps^2) - a^2)), a < kHwTab
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kW = kRT / 64;
     if (tid == 0) {
         wd[kRunWords] = make_uint2(0u, 0u);
         dup[0] = dup[1] = 0;
+    }
+    for (int a = tid; a < kHwTab && a <= e_int; a += kRT) {  // exact integer square roots
+        const uint32_t v = r2i - (uint32_t)(a * a);
+        uint32_t h = (uint32_t)sqrtf((float)v);
+        while (h * h > v) --h;
+        while ((h + 1) * (h + 1) <= v) ++h;
+        hwt[a] = (uint16_t)h;
     }
     int par = 0;
     for (int64_t s = blockIdx.x; s < sv.n_segs; s += gridDim.x, par ^= 1) {
@@ -201,7 +209,7 @@ eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, ui
                 atomicAdd(left, 1);
             }
         } else {
-            if (K == 0) {  // prefix of the word popcounts: thread t takes words [t * per, t * per + per)
+            {  // prefix of the word popcounts: thread t takes words [t * per, t * per + per)
                 const int per = (int)((words + kRT - 1) / kRT);
                 const int w0 = tid * per, w1 = min(w0 + per, (int)words);
                 int loc = 0;
@@ -221,15 +229,12 @@ eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, ui
             const int amax = min(e_int, H - 1);  // rows beyond the box hold nothing
             for (int q = tid; q < sv.stride; q += kRT) {
                 int cnt = 0;
-                int best[K > 0 ? K : 1];
-#pragma unroll
-                for (int k = 0; k < (K > 0 ? K : 1); ++k) best[k] = 0x7fffffff;
                 if (q < m) {
                     const uint32_t v = buffer_load_u32(seg, (uint32_t)q * 4u);
                     const int x = xy_x(v) - xmn, y = xy_y(v) - ymn;
-                    int hw = e_int;  // floor(sqrt(r2i - a^2)), non-increasing in a (uniform)
+#pragma unroll 4
                     for (int a = 0; a <= amax; ++a) {
-                        while (hw > 0 && (uint32_t)(hw * hw) > r2i - (uint32_t)(a * a)) --hw;
+                        const int hw = hwt[a];  // a broadcast read; no loop-carried state
                         const int xl = max(x - hw, 0), xh = min(x + hw + 1, Wb);
                         const uint32_t ml = (1u << (xl & 31)) - 1u, mh = (1u << (xh & 31)) - 1u;
                         const int cl = xl >> 5, ch = xh >> 5;
@@ -239,40 +244,12 @@ eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, ui
                             const int yy = sgn ? y - a : y + a;
                             const bool ok = (unsigned)yy < (unsigned)H;
                             const int rb = yy * WW;
-                            if (K == 0) {
-                                const uint2 lo = wd[ok ? rb + cl : kRunWords], hi = wd[ok ? rb + ch : kRunWords];
-                                cnt += (int)(hi.y - lo.y) + __popc(hi.x & mh) - __popc(lo.x & ml);
-                            } else if (ok) {
-                                for (int wi = cl; wi <= ch; ++wi) {
-                                    uint32_t b = wd[rb + wi].x;
-                                    if (wi == cl) b &= ~ml;
-                                    if (wi == ch) b &= mh;
-                                    while (b) {
-                                        const int dx = wi * 32 + __builtin_ctz(b) - x;
-                                        b &= b - 1u;
-                                        int val = dx * dx + a * a;
-                                        ++cnt;
-#pragma unroll
-                                        for (int k = 0; k < (K > 0 ? K : 1); ++k) {
-                                            const int lo2 = min(best[k], val);
-                                            val = max(best[k], val);
-                                            best[k] = lo2;
-                                        }
-                                    }
-                                }
-                            }
+                            const uint2 lo = wd[ok ? rb + cl : kRunWords], hi = wd[ok ? rb + ch : kRunWords];
+                            cnt += (int)(hi.y - lo.y) + __popc(hi.x & mh) - __popc(lo.x & ml);
                         }
                     }
                 }
                 counts[base + q] = cnt;
-                if (K > 0) {
-                    uint32_t sel = 0xffffffffu;  // not a core point (or padding)
-                    if (cnt >= min_pts) {
-#pragma unroll
-                        for (int k = 0; k < (K > 0 ? K : 1); ++k) sel = (k == min_pts - 1) ? (uint32_t)best[k] : sel;
-                    }
-                    core[base + q] = sel == 0xffffffffu ? -1.0 : sqrt((double)sel);  // correctly rounded
-                }
             }
         }
         __syncthreads();  // 6: the LDS is reused by the next segment
@@ -452,26 +429,29 @@ ECC_API int ecc_eps_counts(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                   "eps_counts lds");
     hipStream_t s = ecc::as_stream(stream);
-    // the row-run kernel, then its leftovers (segments that repeat a pixel or whose bitmap is
-    // larger than its LDS) through the candidate walk; the second launch exits at once without any
-    int32_t *left = ctx->flags + kLeftWord;
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(left, 0, 4, s), "memset(eps leftovers)");
-    {
-        using RunKern = void (*)(const uint32_t *, SegView, int, uint32_t, int, int32_t *, double *, int32_t *);
-        const RunKern rk = K == 0 ? eps_run_counts_kernel<0> : K <= 1 ? eps_run_counts_kernel<1>
-                         : K <= 2 ? eps_run_counts_kernel<2> : K <= 4 ? eps_run_counts_kernel<4>
-                         : K <= 8 ? eps_run_counts_kernel<8> : K <= 16 ? eps_run_counts_kernel<16>
-                         : K <= 32 ? eps_run_counts_kernel<32> : eps_run_counts_kernel<64>;
-        ECC_TIMED(ctx, s, "eps_run_counts_kernel");
-        const unsigned grid = (unsigned)std::min<int64_t>(n_segs, (int64_t)4 * ctx->n_cu);
-        hipLaunchKernelGGL(rk, dim3(grid), dim3(kRT), 0, s, xy, sv, e_int, (uint32_t)r2i, min_pts, counts, core_dist,
-                           left);
-    }
-    {
+    if (K == 0 && e_int < kHwTab) {
+        // counts only: the row-run kernel, then its leftovers (segments that repeat a pixel or
+        // whose bitmap exceeds its LDS) through the candidate walk, which exits at once without any
+        int32_t *left = ctx->flags + kLeftWord;
+        ECC_CHECK_HIP(ctx, hipMemsetAsync(left, 0, 4, s), "memset(eps leftovers)");
+        {
+            ECC_TIMED(ctx, s, "eps_run_counts_kernel");
+            // one workgroup per segment (a resident grid of 4 per CU striding over 2442 segments
+            // left its last round 40 % full)
+            const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 1 << 20);
+            hipLaunchKernelGGL(eps_run_counts_kernel, dim3(grid), dim3(kRT), 0, s, xy, sv, e_int, (uint32_t)r2i, counts,
+                               left);
+        }
         ECC_TIMED(ctx, s, "eps_counts_left_kernel");
         const unsigned grid = (unsigned)std::min<int64_t>(n_segs, ctx->n_cu);  // one WG per CU (LDS)
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kNT), lds, s, xy, sv, e_int, (uint32_t)r2i, min_pts, counts,
                            core_dist, (const int32_t *)left);
+    } else {
+        // segments are grid-strided; enough workgroups for every CU at the occupancy the LDS allows
+        ECC_TIMED(ctx, s, "eps_counts_kernel");
+        const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 2048);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kNT), lds, s, xy, sv, e_int, (uint32_t)r2i, min_pts, counts,
+                           core_dist, (const int32_t *)nullptr);
     }
     ECC_CHECK_LAUNCH(ctx, "eps_counts_kernel");
     return ECC_OK;

@@ -1775,152 +1775,6 @@ kmeans_step_kernel(StepArgs a, const uint32_t *__restrict__ ext, int n_ext, uint
     }
 }
 
-// All non-final Lloyd passes of the pixel form in ONE launch: kLloydGrid resident workgroups run
-// pass it = 0 .. n_iters - 1 exactly as kmeans_step_kernel<K, true> would (the same replica sets
-// rotating by pass, the same update arithmetic, the same per-workgroup LDS sums added to replica
-// blockIdx % n_copies), with a grid barrier between passes instead of a launch boundary.  Every
-// workgroup derives the same update from the same integer sums, so a converged pass (tol >= 0)
-// ends the loop in all of them.  Ten passes were ten launches of ~8.6 us each, mostly launch gap
-// and the dependent replica reads.  The barrier needs every workgroup resident: the grid is far
-// below one workgroup per CU, and workgroups of other streams' kernels never wait on this one, so
-// the ones not yet dispatched always get a slot.
-#ifndef ECC_KM_LLOYD_GRID
-#define ECC_KM_LLOYD_GRID 64
-#endif
-constexpr int kLloydGrid = ECC_KM_LLOYD_GRID;
-
-__device__ __forceinline__ void grid_barrier(uint32_t *bar, uint32_t target) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
-    }
-    __syncthreads();
-}
-
-struct LloydArgs {
-    unsigned long long *acc[3];  // the rotating replica sets (pass it accumulates into acc[it % 3])
-    float *cb[2];                // centroid history: pass it's centres in cb[it & 1]
-    float *cent;                 // the caller's centroids (C_0 in, updated every pass)
-    int n_iters, n_copies, k;
-    float thr, tol;
-    uint32_t *bar;               // grid-barrier counter, zero at launch
-};
-
-template <int K>
-__global__ void __launch_bounds__(kThreads)
-kmeans_lloyd_kernel(LloydArgs a, KmState *st, PixArgs px) {
-    const int tid = threadIdx.x;
-    __shared__ unsigned long long s_sum[3][K];
-    __shared__ unsigned long long w_acc[3][K];
-    __shared__ float s_c[2][K];
-    __shared__ int s_done;
-    const uint32_t w = px.wh[0], h = px.wh[1];
-    const int64_t cells = (int64_t)w * h;
-    for (int it = 0; it < a.n_iters; ++it) {
-        const float *c_prev = it ? a.cb[(it - 1) & 1] : a.cent;
-        float *c_next = a.cb[it & 1];
-        for (int i = tid; i < 3 * K; i += kThreads) (&w_acc[0][0])[i] = 0ull;
-        if (it) {  // kmeans_step_kernel's update, same order of operations
-            const unsigned long long *acc_in = a.acc[(it - 1) % 3];
-            if (tid < 3 * a.k) {
-                const int c = tid / 3, f = tid - 3 * c;
-                unsigned long long t[kAccCopies], v = 0;
-#pragma unroll
-                for (int r = 0; r < kAccCopies; ++r) t[r] = r < a.n_copies ? acc_in[r * kAccStride + 3 * c + f] : 0ull;
-#pragma unroll
-                for (int r = 0; r < kAccCopies; ++r) v += t[r];
-                s_sum[f][c] = v;
-            }
-            if (blockIdx.x == 0) {
-                unsigned long long *acc_zero = a.acc[(it + 1) % 3];
-                for (int i = tid; i < a.n_copies * kAccStride; i += kThreads) acc_zero[i] = 0ull;
-            }
-            __syncthreads();
-            if (tid < 64) {
-                float shift = 0.f;
-                if (tid < a.k) {
-                    const float ox = c_prev[2 * tid], oy = c_prev[2 * tid + 1];
-                    float nx = ox, ny = oy;
-                    const double n_pts = (double)s_sum[0][tid];
-                    if (n_pts > 0.0) {
-                        nx = (float)((double)s_sum[1][tid] / n_pts);
-                        ny = (float)((double)s_sum[2][tid] / n_pts);
-                        shift = fmaxf(fabsf(nx - ox), fabsf(ny - oy));
-                    }
-                    s_c[0][tid] = nx;
-                    s_c[1][tid] = ny;
-                    if (blockIdx.x == 0) {
-                        c_next[2 * tid] = nx;
-                        c_next[2 * tid + 1] = ny;
-                        a.cent[2 * tid] = nx;
-                        a.cent[2 * tid + 1] = ny;
-                    }
-                }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) shift = fmaxf(shift, __shfl_xor(shift, o));
-                if (tid == 0) {
-                    const int done = (a.tol >= 0.f && shift <= a.tol) ? 1 : 0;
-                    s_done = done;
-                    if (blockIdx.x == 0) {
-                        st->iters += 1;
-                        st->done = done;
-                    }
-                }
-            }
-        } else {
-            if (tid < a.k) {
-                s_c[0][tid] = c_prev[2 * tid];
-                s_c[1][tid] = c_prev[2 * tid + 1];
-                if (blockIdx.x == 0) {
-                    c_next[2 * tid] = s_c[0][tid];
-                    c_next[2 * tid + 1] = s_c[1][tid];
-                }
-            }
-            if (tid == 0) s_done = 0;
-        }
-        __syncthreads();
-        if (s_done) break;  // uniform across the grid: the same sums in every workgroup
-        float cx[K], cy[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            cx[i] = uniform_f32(i < a.k ? s_c[0][i] : 1e30f);
-            cy[i] = uniform_f32(i < a.k ? s_c[1][i] : 1e30f);
-        }
-        for (uint32_t c = blockIdx.x * kThreads + tid; c < (uint32_t)cells; c += gridDim.x * kThreads) {
-            const uint32_t y = c / w, x = c - y * w;
-            const uint32_t n = px.cnt[c];
-            if (!n) continue;
-            const uint32_t l = assign_fast<K>((float)x, (float)y, cx, cy, a.thr);
-            if (l >= (uint32_t)K) continue;
-            atomicAdd(&w_acc[0][l], (unsigned long long)n);
-            atomicAdd(&w_acc[1][l], (unsigned long long)n * x);
-            atomicAdd(&w_acc[2][l], (unsigned long long)n * y);
-        }
-        const uint32_t n_out = *px.n_outside;
-        for (uint32_t i = blockIdx.x * kThreads + tid; i < n_out; i += gridDim.x * kThreads) {
-            const uint32_t v = px.outside[i], x = v & 0xffffu, y = v >> 16;
-            const uint32_t l = assign_fast<K>((float)x, (float)y, cx, cy, a.thr);
-            if (l >= (uint32_t)K) continue;
-            atomicAdd(&w_acc[0][l], 1ull);
-            atomicAdd(&w_acc[1][l], (unsigned long long)x);
-            atomicAdd(&w_acc[2][l], (unsigned long long)y);
-        }
-        __syncthreads();
-        if (tid < 3 * a.k) {
-            const int f = tid / a.k, c = tid - f * a.k;
-            const unsigned long long sum = w_acc[f][c];
-            if (sum) atomicAdd(&a.acc[it % 3][(int)(blockIdx.x % a.n_copies) * kAccStride + 3 * c + f], sum);
-        }
-        grid_barrier(a.bar, (uint32_t)(it + 1) * gridDim.x);
-    }
-}
-
-template <int K>
-void launch_lloyd(hipStream_t s, const LloydArgs &a, KmState *st, const PixArgs &px) {
-    hipLaunchKernelGGL((kmeans_lloyd_kernel<K>), dim3(kLloydGrid), dim3(kThreads), 0, s, a, st, px);
-}
-
 template <int K, bool kPix>
 void launch_step(dim3 grid, hipStream_t s, const StepArgs &a, const uint32_t *ext, int n_ext, uint8_t *img,
                  KmState *st, const PixArgs &px) {
@@ -2091,16 +1945,7 @@ static int kmeans_run_xy16_impl(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
                 else launch_step<32, true>(dim3(kPixGrid), s, a, ext, grid, img, st, px);
             }
         };
-        if (kLloydGrid > 0 && cfg->max_iters > 0) {  // the passes in one launch (grid barriers)
-            LloydArgs la{{accb[0], accb[1], accb[2]}, {cb[0], cb[1]}, centroids, cfg->max_iters, kAccCopies, cfg->k,
-                         cfg->threshold, cfg->tol, reinterpret_cast<uint32_t *>(ws + off_st + 32)};
-            const PixArgs px{cnt, outside, n_out, nullptr, wh};
-            ECC_TIMED(ctx, s, "kmeans_lloyd_kernel");
-            if (cfg->k <= 16) launch_lloyd<16>(s, la, st, px);
-            else launch_lloyd<32>(s, la, st, px);
-        } else {
-            for (int it = 0; it < cfg->max_iters; ++it) step(it, false);
-        }
+        for (int it = 0; it < cfg->max_iters; ++it) step(it, false);
         if (cfg->max_iters > 0 || labels) step(cfg->max_iters, true);  // last update (+ image for labels)
         ECC_CHECK_LAUNCH(ctx, "kmeans_xy16 iteration");
         if (labels) {
@@ -2488,16 +2333,7 @@ ECC_API int ecc_kmeans_run_counts(ecc_ctx *ctx, const uint32_t *counts, int32_t 
             else launch_step<32, true>(dim3(kPixGrid), s, a, nullptr, 0, nullptr, st, px);
         }
     };
-    if (kLloydGrid > 0 && cfg->max_iters > 0) {  // the passes in one launch (grid barriers)
-        LloydArgs la{{accb[0], accb[1], accb[2]}, {cb[0], cb[1]}, centroids, cfg->max_iters, kAccCopies, cfg->k,
-                     cfg->threshold, cfg->tol, reinterpret_cast<uint32_t *>(ws + off_st + 32)};
-        const PixArgs px{counts, (const uint32_t *)n_out, n_out, nullptr, wh};
-        ECC_TIMED(ctx, s, "kmeans_lloyd_kernel");
-        if (cfg->k <= 16) launch_lloyd<16>(s, la, st, px);
-        else launch_lloyd<32>(s, la, st, px);
-    } else {
-        for (int it = 0; it < cfg->max_iters; ++it) step(it, false);
-    }
+    for (int it = 0; it < cfg->max_iters; ++it) step(it, false);
     if (cfg->max_iters > 0) step(cfg->max_iters, true);  // the last pass's update
     ECC_CHECK_LAUNCH(ctx, "kmeans run_counts");
     if (iters_out)

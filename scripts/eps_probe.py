@@ -62,6 +62,35 @@ if what == "time":  # per-kernel times of the counts (ε 20 counts only, ε 10 w
         print(f"eps {eps} min_pts {mp} core {co is not None}: {ms:.4f} ms/call;",
               {k: round(v["total_ms"] / v["launches"] * 1e3, 1) for k, v in st.items()}, "us; checksum",
               int(cnt.numpy().astype(np.int64).sum()))
+    # the DBSCAN list chain: counts -> lists -> extraction (per-kernel times)
+    e_cnt = ecc.DeviceArray(tot, np.int32)
+    ctx.eps_counts(rep_xy, nw, WIN, uniq, 20.0, 20, e_cnt, None)
+    ctx.sync()
+    valid = (np.arange(WIN)[None, :] < uniq.numpy()[:, None]).ravel()
+    nbr_cap = int(e_cnt.numpy()[valid].sum()) + 16
+    d_off, d_nbr = ecc.DeviceArray(tot + 1, np.int64), ecc.DeviceArray(nbr_cap, np.int32)
+    d_lab, d_nc, d_nd = ecc.DeviceArray(tot, np.int32), ecc.DeviceArray(nw, np.int32), ecc.DeviceArray(1, np.int64)
+    d_dups = ecc.DeviceArray(2 << 22, np.int64)
+
+    def chain():
+        ctx.eps_counts(rep_xy, nw, WIN, uniq, 20.0, 20, e_cnt, None)
+        ctx.eps_lists(rep_xy, nw, WIN, uniq, 20.0, e_cnt, d_off, d_nbr, nbr_cap)
+        ctx.dbscan_extract(nw, WIN, uniq, d_off, d_nbr, 20, 100, 25000, d_lab, d_nc, d_dups, 1 << 22, d_nd)
+    chain()
+    ctx.sync()
+    tmr = ecc.Timer(ctx.stream)
+    tmr.start()
+    for _ in range(3):
+        chain()
+    ms = tmr.stop() / 3
+    ctx.set_timing(True)
+    ctx.timing_reset()
+    for _ in range(3):
+        chain()
+    st = ctx.timing_report()
+    ctx.set_timing(False)
+    print(f"dbscan chain: {ms:.3f} ms/call;", {k: round(v["total_ms"] / v["launches"] * 1e3, 1) for k, v in st.items()},
+          "us; clusters", int(d_nc.numpy().sum()), "labels checksum", int(d_lab.numpy().astype(np.int64).sum()))
 
 if what == "dbscan" and hasattr(ecc.lib, "ecc_dbscan_profile"):
     import ctypes as C
