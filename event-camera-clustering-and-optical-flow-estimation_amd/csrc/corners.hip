@@ -1181,7 +1181,8 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     }
     if (win_lane) {
         int off = incl - cnt;
-        for (int w = 0; w < wave; ++w) off += L.wave_tot[w];
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) off += w < wave ? L.wave_tot[w] : 0;  // reads in flight together
         int64_t vz = INT64_MAX;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
