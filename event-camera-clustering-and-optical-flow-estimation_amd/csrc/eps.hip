@@ -46,7 +46,7 @@ __device__ __forceinline__ int seg_points(const SegView &sv, int64_t s) {
 // cend[kCells + 1] | spt[stride] | sidx[stride] and, when kStage, st_cnt[stride] (u16) |
 // st_d2[stride] (u32, K > 0): the results by segment index, written out coalesced after the
 // queries.  ~120 KB at stride 8192 with core distances.
-// `left` (row-run leftovers mode, K == 0): only the segments eps_run_counts_kernel marked
+// `left` (row-run leftovers mode): only the segments eps_run_counts_kernel marked
 // (counts[base] == -1; *left = how many) are processed.
 template <int K, bool kStage>
 __global__ void __launch_bounds__(kNT)
@@ -124,9 +124,9 @@ eps_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32
 // then number prefix(y, xh) - prefix(y, xl), with prefix(y, x) = base[word] + popc(bits[word]
 // below x): a query's count is a sum over the 2*eps + 1 rows of the disk (half-width w(dy) =
 // floor(sqrt(floor(eps^2) - dy^2)), the same integer test d^2 <= floor(eps^2) as the candidate
-// walk), two LDS reads per row, no candidate loop and no test.  (Core distances keep the
-// candidate walk: walking each row's run bit by bit for the K smallest d^2 measured 0.68 -> 0.92
-// ms at OPTICS eps 10.)  The bitmap of a 346 x 260
+// walk), two LDS reads per row, no candidate loop and no test.  (Core distances by walking each
+// row's run bit by bit measured 0.68 -> 0.92 ms at OPTICS eps 10; see K > 0 below.)  The bitmap
+// of a 346 x 260
 // sensor is 3120 words (25 KB): four 8-wave workgroups per CU share the CU's LDS, so one
 // segment's set-up barriers overlap the others' queries.  A segment whose bitmap exceeds
 // kRunWords or that repeats a pixel is left to eps_counts_kernel (marked by counts[base] = -1,
@@ -135,9 +135,15 @@ constexpr int kRT = 512;
 constexpr int kRunWords = 4864;  // (bits, prefix) pairs: 38 KB, four workgroups per CU
 constexpr int kHwTab = 512;      // eps < 512 (larger eps: the candidate walk)
 
+// K > 0 (core distances, eps < 32): a disk row's chord lies inside the three bitmap words around
+// the query's column, so the row is two 64-bit masks — the pixels at or left of x within the
+// chord, and those right of it — whose popcounts give the count and whose K nearest set bits per
+// side (leading / trailing zero counts, no per-bit loop) feed the K-smallest insertion network:
+// a row holds at most K of the K nearest points on each side of x.
+template <int K>
 __global__ void __launch_bounds__(kRT)
-eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32_t r2i,
-                      int32_t *__restrict__ counts, int32_t *__restrict__ left) {
+eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32_t r2i, int min_pts,
+                      int32_t *__restrict__ counts, double *__restrict__ core, int32_t *__restrict__ left) {
     __shared__ uint2 wd[kRunWords + 1];  // [kRunWords]: a zero word for rows outside the box
     __shared__ int box[kRT / 64][4];
     __shared__ int wsum[kRT / 64];
@@ -209,7 +215,7 @@ eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, ui
                 atomicAdd(left, 1);
             }
         } else {
-            {  // prefix of the word popcounts: thread t takes words [t * per, t * per + per)
+            if (K == 0) {  // prefix of the word popcounts: thread t takes words [t * per, t * per + per)
                 const int per = (int)((words + kRT - 1) / kRT);
                 const int w0 = tid * per, w1 = min(w0 + per, (int)words);
                 int loc = 0;
@@ -229,7 +235,56 @@ eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, ui
             const int amax = min(e_int, H - 1);  // rows beyond the box hold nothing
             for (int q = tid; q < sv.stride; q += kRT) {
                 int cnt = 0;
-                if (q < m) {
+                int best[K > 0 ? K : 1];
+#pragma unroll
+                for (int k = 0; k < (K > 0 ? K : 1); ++k) best[k] = 0x7fffffff;
+                if (K > 0 && q < m) {
+                    const uint32_t v = buffer_load_u32(seg, (uint32_t)q * 4u);
+                    const int x = xy_x(v) - xmn, y = xy_y(v) - ymn;
+                    const int wx = x >> 5, xb = x & 31;
+                    for (int a = 0; a <= amax; ++a) {
+                        const int hw = hwt[a];  // <= 31
+                        const uint64_t lmask = ((2ull << (32 + xb)) - 1ull) & ~((1ull << (32 + xb - hw)) - 1ull);
+                        const uint64_t rmask = (1ull << hw) - 1ull;
+                        const int a2 = a * a;
+#pragma unroll
+                        for (int sgn = 0; sgn < 2; ++sgn) {
+                            if (sgn && a == 0) break;
+                            const int yy = sgn ? y - a : y + a;
+                            const bool ok = (unsigned)yy < (unsigned)H;
+                            const int rb = yy * WW;
+                            const uint32_t w0 = wd[ok && wx > 0 ? rb + wx - 1 : kRunWords].x;
+                            const uint32_t w1 = wd[ok ? rb + wx : kRunWords].x;
+                            const uint32_t w2 = wd[ok && wx + 1 < WW ? rb + wx + 1 : kRunWords].x;
+                            // bit 32 + xb of Lm is x itself; bit i of Rm is x + 1 + i
+                            uint64_t Lm = (((uint64_t)w1 << 32) | w0) & lmask;
+                            uint64_t Rm = ((((uint64_t)w2 << 32) | w1) >> (xb + 1)) & rmask;
+                            cnt += __popcll(Lm) + __popcll(Rm);
+#pragma unroll
+                            for (int t = 0; t < K; ++t) {
+                                const int pl = 63 - __clzll(Lm | 1ull);  // bit 0 is never in Lm
+                                const int dl = 32 + xb - pl;
+                                int vl = Lm ? dl * dl + a2 : 0x7fffffff;
+                                Lm &= ~(1ull << pl);
+                                const int dr = __ffsll((long long)Rm);  // 1-based: dx of the nearest
+                                int vr = Rm ? dr * dr + a2 : 0x7fffffff;
+                                Rm &= Rm - 1ull;
+#pragma unroll
+                                for (int k = 0; k < (K > 0 ? K : 1); ++k) {
+                                    const int l1 = min(best[k], vl);
+                                    vl = max(best[k], vl);
+                                    best[k] = l1;
+                                }
+#pragma unroll
+                                for (int k = 0; k < (K > 0 ? K : 1); ++k) {
+                                    const int l1 = min(best[k], vr);
+                                    vr = max(best[k], vr);
+                                    best[k] = l1;
+                                }
+                            }
+                        }
+                    }
+                } else if (q < m) {
                     const uint32_t v = buffer_load_u32(seg, (uint32_t)q * 4u);
                     const int x = xy_x(v) - xmn, y = xy_y(v) - ymn;
 #pragma unroll 4
@@ -250,6 +305,14 @@ eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, ui
                     }
                 }
                 counts[base + q] = cnt;
+                if (K > 0) {
+                    uint32_t sel = 0xffffffffu;  // not a core point (or padding)
+                    if (cnt >= min_pts) {
+#pragma unroll
+                        for (int k = 0; k < (K > 0 ? K : 1); ++k) sel = (k == min_pts - 1) ? (uint32_t)best[k] : sel;
+                    }
+                    core[base + q] = sel == 0xffffffffu ? -1.0 : sqrt((double)sel);  // correctly rounded
+                }
             }
         }
         __syncthreads();  // 6: the LDS is reused by the next segment
@@ -429,18 +492,24 @@ ECC_API int ecc_eps_counts(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, int
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                   "eps_counts lds");
     hipStream_t s = ecc::as_stream(stream);
-    if (K == 0 && e_int < kHwTab) {
-        // counts only: the row-run kernel, then its leftovers (segments that repeat a pixel or
-        // whose bitmap exceeds its LDS) through the candidate walk, which exits at once without any
+    // counts: the row-run kernel (eps < 512); with core distances when min_pts <= 8 and eps < 32.
+    // Its leftovers (segments that repeat a pixel or whose bitmap exceeds its LDS) go through the
+    // candidate walk, which exits at once without any; other cases take the candidate walk whole.
+    const bool run = K == 0 ? e_int < kHwTab : (K <= 8 && e_int < 32);
+    if (run) {
         int32_t *left = ctx->flags + kLeftWord;
         ECC_CHECK_HIP(ctx, hipMemsetAsync(left, 0, 4, s), "memset(eps leftovers)");
         {
+            using RunKern = void (*)(const uint32_t *, SegView, int, uint32_t, int, int32_t *, double *, int32_t *);
+            const RunKern rk = K == 0 ? eps_run_counts_kernel<0> : K <= 1 ? eps_run_counts_kernel<1>
+                             : K <= 2 ? eps_run_counts_kernel<2> : K <= 4 ? eps_run_counts_kernel<4>
+                             : eps_run_counts_kernel<8>;
             ECC_TIMED(ctx, s, "eps_run_counts_kernel");
             // one workgroup per segment (a resident grid of 4 per CU striding over 2442 segments
             // left its last round 40 % full)
             const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 1 << 20);
-            hipLaunchKernelGGL(eps_run_counts_kernel, dim3(grid), dim3(kRT), 0, s, xy, sv, e_int, (uint32_t)r2i, counts,
-                               left);
+            hipLaunchKernelGGL(rk, dim3(grid), dim3(kRT), 0, s, xy, sv, e_int, (uint32_t)r2i, min_pts, counts,
+                               core_dist, left);
         }
         ECC_TIMED(ctx, s, "eps_counts_left_kernel");
         const unsigned grid = (unsigned)std::min<int64_t>(n_segs, ctx->n_cu);  // one WG per CU (LDS)

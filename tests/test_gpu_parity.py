@@ -979,7 +979,7 @@ def test_eps_counts_wide_segments(ecc, orc, gpu, eps, min_pts):
         assert (g_cnt[pad] == 0).all() and (g_core[pad] == -1.0).all()
 
 
-@pytest.mark.parametrize("min_pts", [0, 2, 20])
+@pytest.mark.parametrize("min_pts", [0, 2, 5, 20])
 @pytest.mark.parametrize("eps", [0.5, 1.01, 10.0, 20.0, 37.9, 400.0])
 def test_eps_counts_row_run_matches_oracle(ecc, orc, gpu, eps, min_pts):
     """The row-run bitmap kernel (counts; with min_pts > 0 also core distances) on downsample
