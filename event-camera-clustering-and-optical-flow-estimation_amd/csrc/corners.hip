@@ -164,12 +164,19 @@ __device__ __forceinline__ void block_excl_scan_inplace(int32_t *a, int n, int32
 
 __global__ void __launch_bounds__(kSortThreads, 8)  // 8 waves/SIMD: two workgroups per CU
 slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g, Sorted so,
-                  int32_t *__restrict__ first_border, int32_t *__restrict__ err) {
+                  int32_t *__restrict__ first_border, int32_t *__restrict__ err, int32_t err_val,
+                  uint32_t *__restrict__ zero0, int32_t *__restrict__ zero1) {
     extern __shared__ int32_t hist[];  // [nb]: counts, then offsets, then (long slices) cursors;
                                        // then [kSortChunk] staging of the sorted slice
     __shared__ int32_t wsum[kSortThreads / 64];
     const int tid = threadIdx.x, lane = tid & 63;
     const int64_t s = blockIdx.x;
+    // the call's counters that later kernels of the call start from (a 4-B memset each was a
+    // fill launch on the critical path): arc_kernel's overflow count, the NMS error word
+    if (s == 0 && tid == 0) {
+        if (zero0) *zero0 = 0u;
+        if (zero1) *zero1 = 0;
+    }
     const int64_t lo = s * g.S;
     const int len = (int)((lo + g.S < g.n ? lo + g.S : g.n) - lo);
     const int64_t grp = s / kGroup;
@@ -212,7 +219,7 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
             br[u] |= (uint32_t)atomicAdd(&hist[br[u] >> 16], 1) & 0xffffu;
         }
     }
-    if (__any(bad) && lane == 0 && !g.any_order) *err = 1;
+    if (__any(bad) && lane == 0 && !g.any_order) *err = err_val;  // this call's tag: no reset needed
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) fb = min(fb, __shfl_xor(fb, o));
     if (lane == 0) wsum[tid >> 6] = fb;
@@ -1492,6 +1499,7 @@ sae_max_combine_kernel(const int64_t *__restrict__ images, int n_images, int64_t
 struct CornerState {
     void *evt = nullptr;
     size_t evt_bytes = 0;
+    int32_t epoch = 0;  // tag of the last sort phase: slice_sort writes it to ctx->flags[0] on error
     // diagnostics of the last detection (ecc_fast_detect_stats)
     const uint32_t *n_over = nullptr;
     int64_t n_items = 0, n_slices = 0, n_groups = 0;
@@ -1606,7 +1614,8 @@ ECC_API void ecc_corner_cfg_default(ecc_corner_cfg *cfg) {
 // carve (same n and cfg), so prepare/finish may be separate calls with a collective between.
 static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
                               const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags, int64_t *local_last,
-                              int phases, ecc_stream_t stream, uint32_t *cand = nullptr, int32_t *n_cand = nullptr) {
+                              int phases, ecc_stream_t stream, uint32_t *cand = nullptr, int32_t *n_cand = nullptr,
+                              int32_t *zero_nms_err = nullptr) {
     if (!ctx || !cfg || n < 0) return ECC_ERR_INVALID;
     if ((phases & 2) && !sae) return ECC_ERR_INVALID;
     if (n > 0 && (!xy || !t || ((phases & 2) && !corner_flags))) return ECC_ERR_INVALID;
@@ -1636,7 +1645,8 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     if (g.n_slices > INT32_MAX) return ECC_ERR_INVALID;
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    if (phases & 1) ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags, 0, 4, s), "memset(err flag)");
+    CornerState *st = state_of(ctx);
+    if (phases & 1) ++st->epoch;  // ecc_fast_detect_status: flags[0] == epoch <=> this call's sort failed
     if (n == 0) {
         if (local_last) ECC_CHECK_HIP(ctx, hipMemsetAsync(local_last, 0, (size_t)g.W * g.H * 8, s), "memset(local)");
         return ECC_OK;
@@ -1645,7 +1655,6 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     const int64_t n_groups = (g.n_slices + kGroup - 1) / kGroup;
     const int64_t n_items = n_groups * g.n_tiles;  // work items: (group, tile)
     if (n_items > (int64_t)INT32_MAX - 8) return ECC_ERR_INVALID;
-    CornerState *st = state_of(ctx);
     int32_t *first_border = nullptr;
     GroupImages gi{};
     Carve measure{nullptr};
@@ -1669,7 +1678,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         }
         ECC_TIMED(ctx, s, "slice_sort_kernel");
         hipLaunchKernelGGL(slice_sort_kernel, dim3((unsigned)g.n_slices), dim3(kSortThreads), lds, s, xy, t, g,
-                           so, first_border, ctx->flags);
+                           so, first_border, ctx->flags, st->epoch, (phases & 2) ? gi.n_over : nullptr, zero_nms_err);
     }
     {
         ECC_TIMED(ctx, s, "pair_build_kernel");
@@ -1688,7 +1697,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         ECC_CHECK_LAUNCH(ctx, "fast_detect_prepare");
         return ECC_OK;
     }
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
+    if (!(phases & 1)) ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
     st->n_over = gi.n_over;
     st->n_items = n_items;
     st->n_slices = g.n_slices;
@@ -1804,8 +1813,9 @@ ECC_API int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t 
     }
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->flags + 1, 0, 4, s), "memset(nms err)");
-    int rc = fast_detect_phases(ctx, xy, t, n, cfg, sae, corner_flags, nullptr, 3, stream, cand, n_cand);
+    // the NMS error word is zeroed by the sort kernel (n > 0 here: nms_candidates gave a buffer)
+    int rc = fast_detect_phases(ctx, xy, t, n, cfg, sae, corner_flags, nullptr, 3, stream, cand, n_cand,
+                                ctx->flags + 1);
     if (rc) return rc;
     rc = ecc::nms_greedy(ctx, cand, n_cand, n, cfg->slice_events, cfg->width, cfg->height, box_size, cap, out,
                          out_count, s);
@@ -1831,7 +1841,8 @@ ECC_API int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream) {
     ECC_CHECK_HIP(ctx, hipMemcpyAsync(&f, ctx->flags, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
                   "read err flag");
     ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
-    return f ? ECC_ERR_UNSORTED_TIME : ECC_OK;
+    const int32_t epoch = state_of(ctx)->epoch;
+    return (epoch != 0 && f == epoch) ? ECC_ERR_UNSORTED_TIME : ECC_OK;
 }
 
 ECC_API int ecc_fast_detect_stats(ecc_ctx *ctx, int64_t *out, int32_t n_out, ecc_stream_t stream) {
