@@ -1449,7 +1449,10 @@ kmeans_extent_kernel(const uint32_t *__restrict__ xy, Segs segs, uint32_t *__res
 // the chunk densely into partial[m]; kmeans_count_sum_kernel adds the parts.  Part 0's
 // workgroups of chunk 0 also list the points outside the kImgSide^2 image.
 constexpr int kHistThreads = 1024;
-constexpr int kHistChunk = 32768;  // pixels per LDS chunk (128 KiB)
+#ifndef ECC_KM_HIST_CHUNK
+#define ECC_KM_HIST_CHUNK 32768
+#endif
+constexpr int kHistChunk = ECC_KM_HIST_CHUNK;  // pixels per LDS chunk (128 KiB)
 constexpr int64_t kHistBudget = 16 << 20;  // partial-count entries (64 MiB): parts used = budget / cells
 
 __host__ __device__ inline int parts_used(int parts, int64_t cells) {
