@@ -441,6 +441,17 @@ def test_fast_detect_rejects_decreasing_time(ecc, gpu):
     flags = ecc.DeviceArray(len(xy), np.uint8)
     gpu.fast_detect(dev(ecc, xy), dev(ecc, t), len(xy), cfg, sae, flags)
     assert gpu.fast_detect_status() == ecc.ERR_UNSORTED_TIME
+    # the error word carries the failing call's tag (no per-call reset): a later sorted call, and
+    # a later empty call, report OK; the fused detect + NMS call reports a new failure again
+    t_ok = np.sort(t)
+    gpu.fast_detect(dev(ecc, xy), dev(ecc, t_ok), len(xy), cfg, sae, flags)
+    assert gpu.fast_detect_status() == 0
+    gpu.fast_detect(dev(ecc, xy), dev(ecc, t), 0, cfg, sae, flags)
+    assert gpu.fast_detect_status() == 0
+    ns = -(-len(xy) // cfg.slice_events)
+    out, cnt = ecc.DeviceArray(ns * 64, ecc.CORNER_DTYPE), ecc.DeviceArray(ns, np.int32)
+    gpu.fast_detect_nms(dev(ecc, xy), dev(ecc, t), len(xy), cfg, sae, flags, 15, 64, out, cnt)
+    assert gpu.fast_detect_status() == ecc.ERR_UNSORTED_TIME
 
 
 def _any_order_times(kind, n, seed):
@@ -980,7 +991,7 @@ def test_eps_counts_wide_segments(ecc, orc, gpu, eps, min_pts):
 
 
 @pytest.mark.parametrize("min_pts", [0, 2, 5, 20])
-@pytest.mark.parametrize("eps", [0.5, 1.01, 10.0, 20.0, 37.9, 400.0])
+@pytest.mark.parametrize("eps", [0.5, 1.01, 10.0, 20.0, 31.9, 37.9, 400.0])
 def test_eps_counts_row_run_matches_oracle(ecc, orc, gpu, eps, min_pts):
     """The row-run bitmap kernel (counts; with min_pts > 0 also core distances) on downsample
     windows (distinct pixels), plus segments it must leave to the candidate walk — a repeated
