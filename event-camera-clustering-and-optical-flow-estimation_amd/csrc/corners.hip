@@ -1329,7 +1329,10 @@ arc_dense_kernel(const int64_t *__restrict__ t, CornerGeom g, const int64_t *__r
 #define ECC_FLAG_THREADS 256
 #endif
 constexpr int kFlagThreads = ECC_FLAG_THREADS;  // 256: every slice's workgroup resident at once (8 per CU)
-constexpr int kFlagQuads = 8;  // 4-event quads a lane has in flight per batch
+#ifndef ECC_FLAG_QUADS
+#define ECC_FLAG_QUADS 8
+#endif
+constexpr int kFlagQuads = ECC_FLAG_QUADS;  // 4-event quads a lane has in flight per batch
 constexpr int kFlagBatch = kFlagQuads * kFlagThreads;  // quads per batch
 constexpr int kFlagCandMax = 16384;  // slices up to this many events take the candidate-list form
 
