@@ -587,7 +587,8 @@ def bench_ingest(ecc, ctx, args, xy_h, t_h, p_h, n):
 def bench_c3(ecc, ctx, args, rep_xy, uniq, c0, K, n_pts=50_000_000):
     """BASELINE C3: k-means k=16 on 50 M points (this step's C2-style representatives tiled to
     50 M), 10 Lloyd passes + final labels, three ways: packed-u16 points through the per-pixel
-    count path, and float points through the vector and the matrix-core assignment engines.
+    count path, and float points through the vector and the two matrix-core assignment engines
+    (4x4x1 per-lane form, 32x32x2 streaming form).
     Roofline per SURVEY §8d: 8 B/point/iteration (float2 read) + 1 B/point (labels)."""
     u = uniq.numpy()
     rx = rep_xy.numpy()
@@ -611,7 +612,8 @@ def bench_c3(ecc, ctx, args, rep_xy, uniq, c0, K, n_pts=50_000_000):
     for name, run in (
             ("xy16_count_image", lambda: ctx.kmeans_xy16_frame(d_pts, 1, n_pts, None, 346, 260, d_c, cfg, d_lab)),
             ("f32_vector", lambda: ctx.kmeans_f32_engine(d_f, n_pts, d_c, cfg, 1, d_lab)),
-            ("f32_mfma", lambda: ctx.kmeans_f32_engine(d_f, n_pts, d_c, cfg, 2, d_lab))):
+            ("f32_mfma", lambda: ctx.kmeans_f32_engine(d_f, n_pts, d_c, cfg, 2, d_lab)),
+            ("f32_mfma_32x32x2", lambda: ctx.kmeans_f32_engine(d_f, n_pts, d_c, cfg, 3, d_lab))):
         def full():
             ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, ctx.stream))
             run()
@@ -630,9 +632,9 @@ def bench_c3(ecc, ctx, args, rep_xy, uniq, c0, K, n_pts=50_000_000):
     # the three forms agree bit for bit (integer-valued points: exact fp64 / integer sums)
     out["centroids_agree"] = bool(all(np.array_equal(results[a].view(np.uint32), results["f32_vector"].view(np.uint32))
                                       for a in results))
-    f32 = {k: out[k]["ms"] for k in ("f32_vector", "f32_mfma")}
+    f32 = {k: out[k]["ms"] for k in ("f32_vector", "f32_mfma", "f32_mfma_32x32x2")}
     out["winner_f32"] = min(f32, key=f32.get)
-    out["winner"] = min(("xy16_count_image", "f32_vector", "f32_mfma"), key=lambda k: out[k]["ms"])
+    out["winner"] = min(("xy16_count_image", *f32), key=lambda k: out[k]["ms"])
     return out
 
 

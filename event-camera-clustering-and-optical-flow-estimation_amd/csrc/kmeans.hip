@@ -31,6 +31,9 @@
 #ifndef ECC_KM_LUT_UNROLL
 #define ECC_KM_LUT_UNROLL 4
 #endif
+#ifndef ECC_KM_MFMA_BLOCKS
+#define ECC_KM_MFMA_BLOCKS 2  // matrix engine: 64-pair blocks per trip
+#endif
 #ifndef ECC_KM_ACC_SUB
 #define ECC_KM_ACC_SUB 4
 #endif
@@ -343,8 +346,8 @@ kmeans_fast_kernel(const uint32_t *__restrict__ xy, Segs segs, const float *__re
     float cx[K], cy[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
-        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+        cx[i] = uniform_f32(i < k ? cent[2 * i] : __builtin_inff());
+        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : __builtin_inff());
     }
     if (kAccumulate) {
         for (int i = tid; i < 3 * K; i += kThreads) (&w_acc[0][0])[i] = 0ull;
@@ -460,8 +463,8 @@ kmeans_img_labels_kernel(const uint32_t *__restrict__ xy, Segs segs, const float
     __shared__ float s_cx[K], s_cy[K];
     const int tid = threadIdx.x;
     if (tid < K) {
-        s_cx[tid] = tid < k ? cent[2 * tid] : 1e30f;
-        s_cy[tid] = tid < k ? cent[2 * tid + 1] : 1e30f;
+        s_cx[tid] = tid < k ? cent[2 * tid] : __builtin_inff();
+        s_cy[tid] = tid < k ? cent[2 * tid + 1] : __builtin_inff();
     }
     __syncthreads();
     const uint32_t img_w = img_wh[0], img_h = img_wh[1];
@@ -528,8 +531,8 @@ kmeans_lds_labels_kernel(const uint32_t *__restrict__ xy, Segs segs, const float
     __shared__ float s_cx[K], s_cy[K];
     const int tid = threadIdx.x, sub = tid >> 8, t = tid & 255;
     if (tid < K) {
-        s_cx[tid] = tid < k ? cent[2 * tid] : 1e30f;
-        s_cy[tid] = tid < k ? cent[2 * tid + 1] : 1e30f;
+        s_cx[tid] = tid < k ? cent[2 * tid] : __builtin_inff();
+        s_cy[tid] = tid < k ? cent[2 * tid + 1] : __builtin_inff();
     }
     const uint32_t img_w = img_wh[0], img_h = img_wh[1];
     // rows copied as words (row pitch img_w rounded up to 4), eight loads in flight per lane
@@ -676,6 +679,45 @@ __device__ __forceinline__ uint32_t assign_mfma(float px, float py, const float 
     return ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy))) < thr ? (uint32_t)bi : 255u;
 }
 
+// Matrix engine, streaming form (k <= 16, 16-B aligned points): v_mfma_f32_32x32x2f32, a 32 x 32
+// x 2 product per instruction (4x the work of the 4x4x1 form above at twice its cycles).  A = 32
+// centre rows (k index 0: -2 cx, 1: -2 cy), row i holding centre (i & 3) | (i >> 3) << 2, so that
+// D register r of EVERY lane is centre r (rows (r&3) + 8 (r>>2) + 4 (lane>>5)); B = 32 point
+// columns (lanes 0-31: x, lanes 32-63: y of point lane & 31); C = |c_r|^2.  D is the same k-ordered
+// fma chain as assign_mfma's two 4x4x1 steps, fma(-2cy, py, fma(-2cx, px, |c|^2)).  Both halves of
+// the wave see the same 32 columns, so each pair of instructions (even and odd points of 32 pairs)
+// leaves lanes 0-31 the even points' 16 values and lanes 32-63 the odd points'.
+typedef float floatx16_t __attribute__((ext_vector_type(16)));
+
+// The argmin of one point from its 16 MFMA values s_r = |c_r|^2 - 2 c_r.p: the smallest s, and the
+// one index whose s lies below s + margin' (margin' = 1.0625 x assign_mfma's margin, which covers
+// the rounding of the sum, so every other s exceeds the winner by more than the margin).  More
+// than one such index (a close call, a tie), none (NaN input) or an infinite margin takes the exact
+// vector path; so does a non-finite point.  Same proof as assign_mfma.
+template <int K>
+__device__ __forceinline__ uint32_t pick_mfma(const float (&v)[K], float px, float py, float emul_c2, float emul_x,
+                                              float emul_y, const float2 *__restrict__ s_c, const float (&cx)[K],
+                                              const float (&cy)[K], float thr) {
+    float b = v[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) b = fminf(b, v[i]);
+    const float E = 0x1p-21f * (emul_c2 + 2.0f * (emul_x * fabsf(px) + emul_y * fabsf(py)));
+    const float P = px * px + py * py;
+    const float margin = 2.0f * E + 0x1p-19f * (fabsf(b) + P + E);
+    const float lim = b + 1.0625f * margin;
+    int cnt = 0, bi = 0;
+#pragma unroll
+    for (int i = K - 1; i >= 0; --i) {
+        const bool in = v[i] < lim;
+        cnt += in ? 1 : 0;
+        bi = in ? i : bi;
+    }
+    if (__builtin_expect(!(cnt == 1 && lim < __builtin_inff()), 0)) return assign_fast<K>(px, py, cx, cy, thr);
+    const float2 c = s_c[bi];
+    const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
+    return ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy))) < thr ? (uint32_t)bi : 255u;
+}
+
 constexpr int kF32Unroll = 4;  // 64-point blocks per wave per trip (loads in flight together)
 
 template <int K, bool kMfma, bool kAccumulate>
@@ -691,8 +733,8 @@ kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__
     float cx[K], cy[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
-        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+        cx[i] = uniform_f32(i < k ? cent[2 * i] : __builtin_inff());
+        cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : __builtin_inff());
     }
     // matrix-engine operands: A rows (lane & 3 = row i of every 4x4 block), |c|^2 per register
     float ax[K / 4], ay[K / 4], c2[K];
@@ -715,7 +757,7 @@ kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__
             }
         }
     }
-    if (tid < K) s_c[tid] = make_float2(tid < k ? cent[2 * tid] : 1e30f, tid < k ? cent[2 * tid + 1] : 1e30f);
+    if (tid < K) s_c[tid] = make_float2(tid < k ? cent[2 * tid] : __builtin_inff(), tid < k ? cent[2 * tid + 1] : __builtin_inff());
     if (kAccumulate && lane < K) {
         s_n[wave][lane] = 0u;
         s_sx[wave][lane] = 0.0;
@@ -1117,7 +1159,7 @@ __device__ __forceinline__ uint32_t lut_point(float px, float py, const LutView 
 // aligned); an odd last point is taken by lane 0 of workgroup 0.
 constexpr int kPairUnroll = 4;
 
-template <int K, bool kAccumulate, bool kLut>
+template <int K, bool kAccumulate, bool kLut, bool kMfma = false>
 __global__ void __launch_bounds__(kThreads)
 kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *__restrict__ cent, int k, float thr,
                        float thr2, double *__restrict__ acc, int n_copies, const KmState *__restrict__ st,
@@ -1162,11 +1204,28 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     if constexpr (!kLut) {
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            cx[i] = uniform_f32(i < k ? cent[2 * i] : 1e30f);
-            cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : 1e30f);
+            cx[i] = uniform_f32(i < k ? cent[2 * i] : __builtin_inff());
+            cy[i] = uniform_f32(i < k ? cent[2 * i + 1] : __builtin_inff());
         }
     }
-    if (tid < K) s_c[tid] = make_float2(tid < k ? cent[2 * tid] : 1e30f, tid < k ? cent[2 * tid + 1] : 1e30f);
+    // matrix-engine operands (kMfma): this lane's A element, |c_r|^2 as the C input, error scales
+    float a_op = 0.f, em_c2 = 0.f, em_x = 0.f, em_y = 0.f;
+    floatx16_t c2v{};
+    if constexpr (kMfma) {
+        static_assert(K == 16, "the 32x32x2 layout maps D register r to centre r < 16");
+        const int i = lane & 31, c = (i & 3) | ((i >> 3) << 2);
+        a_op = c < k ? -2.0f * cent[2 * c + (lane >> 5)] : 0.f;
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            c2v[r] = r < k ? __fadd_rn(__fmul_rn(cx[r], cx[r]), __fmul_rn(cy[r], cy[r])) : __builtin_inff();
+            if (r < k) {
+                em_c2 = fmaxf(em_c2, c2v[r]);
+                em_x = fmaxf(em_x, fabsf(cx[r]));
+                em_y = fmaxf(em_y, fabsf(cy[r]));
+            }
+        }
+    }
+    if (tid < K) s_c[tid] = make_float2(tid < k ? cent[2 * tid] : __builtin_inff(), tid < k ? cent[2 * tid + 1] : __builtin_inff());
     if (kAccumulate && lane < K) {
         for (int b = 0; b < kSub; ++b) {
             s_n[wave * kSub + b][lane] = 0u;
@@ -1187,8 +1246,11 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     const int64_t nblk = (npair + 63) / 64;  // 64 pairs per wave block
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     // table path: loads per trip (8 measured slower than 4: 117 vs 110 us per accumulate pass)
-    constexpr int kU = kLut ? ECC_KM_LUT_UNROLL : kPairUnroll;
-    const int64_t span = stride * kU;
+    // matrix engine: each lane loads the pairs of lanes (lane & 31) and (lane & 31) + 32 of a block
+    // (the two column sets of its two instruction pairs; the duplicate addresses coalesce)
+    constexpr int kBlk = kMfma ? ECC_KM_MFMA_BLOCKS : (kLut ? ECC_KM_LUT_UNROLL : kPairUnroll);  // blocks per trip
+    constexpr int kU = kMfma ? 2 * kBlk : kBlk;  // 16-B loads per lane per trip
+    const int64_t span = stride * kBlk;
     // a trip's loads through a buffer view based at its first pair: unconditional (0 past the
     // last pair), one VGPR of lane offset for all of them, the u part in the scalar offset
     auto load = [&](int64_t b0, float4 (&q)[kU]) __attribute__((always_inline)) {
@@ -1197,7 +1259,8 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
         const __amdgpu_buffer_rsrc_t v = ecc::buffer_view(xy4 + first, rem < 0xffffffffll ? (uint32_t)rem : 0xffffffffu);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const uint4 w = ecc::buffer_load_u128(v, (uint32_t)lane * 16u, (uint32_t)(u * stride * 64 * 16));
+            const uint32_t lo = kMfma ? (uint32_t)(lane & 31) * 16u + (uint32_t)(u & 1) * 512u : (uint32_t)lane * 16u;
+            const uint4 w = ecc::buffer_load_u128(v, lo, (uint32_t)((kMfma ? u >> 1 : u) * stride * 64 * 16));
             q[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
         }
     };
@@ -1243,9 +1306,32 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
     };
     auto test = [&](int64_t b0, const float4 (&q)[kU]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
+        for (int u = 0; u < kBlk; ++u) {
             const int64_t blk = b0 + u * stride;
             if (blk >= nblk) break;  // wave-uniform
+            if constexpr (kMfma) {
+                // set h = the pairs 32h..32h+31 of the block, in both halves of the wave
+                const bool low = lane < 32;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int src = (lane & 31) + 32 * h;
+                    const float4 qs = q[2 * u + h];
+                    const float sx = qs.x, sy = qs.y, sz = qs.z, sw = qs.w;
+                    const floatx16_t de = __builtin_amdgcn_mfma_f32_32x32x2f32(a_op, low ? sx : sy, c2v, 0, 0, 0);
+                    const floatx16_t dd = __builtin_amdgcn_mfma_f32_32x32x2f32(a_op, low ? sz : sw, c2v, 0, 0, 0);
+                    float v[K];
+#pragma unroll
+                    for (int r = 0; r < K; ++r) v[r] = low ? de[r] : dd[r];
+                    const float px = low ? sx : sz, py = low ? sy : sw;  // lanes 0-31: even, 32-63: odd point
+                    const uint32_t l = pick_mfma<K>(v, px, py, em_c2, em_x, em_y, s_c, cx, cy, thr);
+                    const int64_t pq = blk * 64 + src;
+                    if (pq < npair) {
+                        if (labels) labels[2 * pq + (low ? 0 : 1)] = (uint8_t)l;
+                        account(make_float2(px, py), l);
+                    }
+                }
+                continue;
+            }
             const int64_t pp = blk * 64 + lane;
             const float2 p0 = make_float2(q[u].x, q[u].y), p1 = make_float2(q[u].z, q[u].w);
             uint32_t l0, l1;
@@ -1334,7 +1420,12 @@ bool launch_f32_fast(int k, int method, dim3 grid, hipStream_t s, const float *x
 #define ECC_F32_LAUNCH(KK, MF)                                                                               \
     hipLaunchKernelGGL((kmeans_f32_fast_kernel<KK, MF, kAccumulate>), grid, dim3(kThreads), 0, s, p, n, cent, k, \
                        thr, thr2, acc, n_copies, st, labels)
-    if (method == 2) {
+    const bool pairs_ok = (reinterpret_cast<uintptr_t>(xy) & 15) == 0 && (reinterpret_cast<uintptr_t>(labels) & 1) == 0;
+    if (method == 3 && k <= 16 && pairs_ok) {  // matrix engine, 32x32x2 streaming form
+        hipLaunchKernelGGL((kmeans_f32_pair_kernel<16, kAccumulate, false, true>), grid, dim3(kThreads), 0, s,
+                           reinterpret_cast<const float4 *>(xy), n, cent, k, thr, thr2, acc, n_copies, st, labels,
+                           geom, lut);
+    } else if (method >= 2) {  // matrix engine, 4x4x1 form (also engine 3's k > 16 / unaligned case)
         if (k <= 16) ECC_F32_LAUNCH(16, true);
         else ECC_F32_LAUNCH(32, true);
     } else if ((reinterpret_cast<uintptr_t>(xy) & 15) == 0 && (reinterpret_cast<uintptr_t>(labels) & 1) == 0) {  // 16-B loads of point pairs
@@ -1736,8 +1827,8 @@ kmeans_step_kernel(StepArgs a, const uint32_t *__restrict__ ext, int n_ext, uint
     float cx[K], cy[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        cx[i] = uniform_f32(i < a.k ? s_c[0][i] : 1e30f);
-        cy[i] = uniform_f32(i < a.k ? s_c[1][i] : 1e30f);
+        cx[i] = uniform_f32(i < a.k ? s_c[0][i] : __builtin_inff());
+        cy[i] = uniform_f32(i < a.k ? s_c[1][i] : __builtin_inff());
     }
     const uint32_t w = s_wh[0][0], h = s_wh[1][0];
     const int64_t cells = (int64_t)w * h;
@@ -1993,7 +2084,7 @@ static int kmeans_run_f32_impl(ecc_ctx *ctx, const float *xy, int64_t n_points, 
                                int method, float *centroids, uint8_t *labels, int32_t *iters_out, ecc_stream_t stream) {
     int rc = kmeans_check(ctx, cfg, centroids);
     if (rc) return rc;
-    if (n_points < 0 || (n_points > 0 && !xy) || method < 0 || method > 2) return ECC_ERR_INVALID;
+    if (n_points < 0 || (n_points > 0 && !xy) || method < 0 || method > 3) return ECC_ERR_INVALID;
     if (method != 0 && cfg->k > kFastMaxK) return ECC_ERR_INVALID;  // the engines take k <= 32
     if ((reinterpret_cast<uintptr_t>(xy) & 7) != 0) return ECC_ERR_INVALID;  // float2 loads
     const bool fast = cfg->k <= kFastMaxK;
@@ -2016,7 +2107,7 @@ static int kmeans_run_f32_impl(ecc_ctx *ctx, const float *xy, int64_t n_points, 
     auto *geom = reinterpret_cast<LutGeom *>(ws + geom_off);
     auto *lut = reinterpret_cast<uint32_t *>(ws + lut_off);
     ECC_CHECK_HIP(ctx, hipMemsetAsync(ctx->ws, 0, box_off, s), "memset(kmeans acc)");
-    const char *name = eng == 2 ? "kmeans_f32_mfma_kernel" : "kmeans_f32_vec_kernel";
+    const char *name = eng == 3 ? "kmeans_f32_mfma32_kernel" : eng == 2 ? "kmeans_f32_mfma_kernel" : "kmeans_f32_vec_kernel";
     const int grid = fast ? (int)std::max<int64_t>(1, std::min<int64_t>((n_points + 255) / 256, 4096))
                           : grid_for((n_points + kThreads - 1) / kThreads);
     const float thr2 = sqrt_threshold(cfg->threshold);

@@ -366,7 +366,8 @@ class Context:
 
     def kmeans_f32_engine(self, xy: DeviceArray, n: int, centroids: DeviceArray, cfg: KmeansCfg, engine: int,
                           labels: DeviceArray | None = None, iters: DeviceArray | None = None):
-        """engine: 0 default, 1 vector (SGPR centres), 2 matrix cores (MFMA distance + exact fallback)."""
+        """engine: 0 default, 1 vector (SGPR centres), 2 matrix cores (4x4x1 MFMA distance + exact
+        fallback), 3 matrix cores in the streaming 32x32x2 form (k <= 16, 16-B aligned points)."""
         check(lib.ecc_kmeans_run_f32_engine(self.ctx, xy.ptr, n, C.byref(cfg), engine, centroids.ptr,
                                             _ptr(labels), _ptr(iters), self.stream), "ecc_kmeans_run_f32_engine")
 

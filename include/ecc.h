@@ -184,8 +184,10 @@ int ecc_kmeans_run_xy16_frame(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, 
 /* The same with an explicit assignment engine for k <= 32 (BASELINE config C3): 0 = default
  * (the vector engine), 1 = vector (centres in scalar registers, exact fp32 d^2 per centre),
  * 2 = matrix cores (d^2 - |p|^2 from v_mfma_f32_4x4x1f32, exact fallback near ties, the
- * winner's exact d^2 against the threshold).  Both return the reference's labels; sums are fp64
- * (exact for integer-valued coordinates).  xy must be 8-byte aligned. */
+ * winner's exact d^2 against the threshold), 3 = matrix cores in the streaming form (16 centres x
+ * 32 points per v_mfma_f32_32x32x2f32, same margin and fallback; k <= 16 with 16-byte aligned xy,
+ * otherwise engine 2).  All return the reference's labels; sums are fp64 (exact for
+ * integer-valued coordinates).  xy must be 8-byte aligned. */
 int ecc_kmeans_run_f32_engine(ecc_ctx *ctx, const float *xy, int64_t n_points, const ecc_kmeans_cfg *cfg,
                               int32_t engine, float *centroids, uint8_t *labels, int32_t *iters_out,
                               ecc_stream_t stream);

@@ -219,7 +219,7 @@ def test_kmeans_f32_matches_oracle(ecc, orc, gpu):
     assert (d_lab.numpy() != o_lab).mean() < 1e-4
 
 
-@pytest.mark.parametrize("engine", [1, 2])
+@pytest.mark.parametrize("engine", [1, 2, 3])
 @pytest.mark.parametrize("k,data", [(16, "float"), (5, "int"), (32, "int"), (16, "ties")])
 def test_kmeans_f32_engines_match_oracle(ecc, orc, gpu, engine, k, data):
     """Both assignment engines (vector / matrix cores): labels identical to the oracle's
@@ -271,7 +271,7 @@ def test_kmeans_assign_ties_and_threshold(ecc, orc, gpu):
     assert list(g[:7]) == [0, 0, 1, 1, 3, 255, 1]
 
 
-@pytest.mark.parametrize("engine", [1, 2])
+@pytest.mark.parametrize("engine", [1, 2, 3])
 def test_kmeans_f32_threshold_and_tie_boundaries_ulps(ecc, orc, gpu, engine):
     """The f32 engines' fast screens (the vector engine's 32-ulp buckets + d2 < thr2, the matrix
     engine's margin) against assign_to_centers' rule at its edges: points a few ulps either side
@@ -343,6 +343,34 @@ def test_kmeans_f32_candidate_table_edges(ecc, orc, gpu, case):
                           d_lab2)
     gpu.sync()
     assert (d_lab2.numpy() == orc.kmeans_assign_f32(bad.ravel(), d_c.numpy(), thr)).all()
+
+
+@pytest.mark.parametrize("engine", [2, 3])
+@pytest.mark.parametrize("k", [1, 3, 16])
+def test_kmeans_f32_matrix_engines_extreme_points(ecc, orc, gpu, engine, k):
+    """The matrix engines' margin screen on the points it must hand to the exact path: NaN, +-inf,
+    huge (|p| 1e19..1e30: infinite or NaN MFMA values), subnormal and negative coordinates, an odd
+    point count; labels-only pass against assign_to_centers.  (Found: the unused centre slots of
+    k < 16 were padded with 1e30, which a point at (1e30, 1e30) matched exactly; they are +inf now,
+    never within any threshold.)"""
+    rng = np.random.default_rng(40 + engine + k)
+    pts = rng.uniform(-50, 400, (20001, 2)).astype(np.float32)
+    pts[::11, 0] = np.nan
+    pts[1::11, 1] = np.inf
+    pts[2::11] = -np.inf
+    pts[3::11] = rng.choice([1e19, -1e19, 1e30, -3e30], (len(pts[3::11]), 2))
+    pts[4::11] = rng.choice([1e-40, -1e-41, 0.0, -0.0], (len(pts[4::11]), 2))
+    c = rng.uniform(-20, 380, (k, 2)).astype(np.float32)
+    c[0] = [0.0, 0.0]
+    flat = pts.ravel()
+    d_lab = ecc.DeviceArray(len(pts), np.uint8)
+    for thr in (50.0, 1e35):
+        gpu.kmeans_f32_engine(dev(ecc, flat), len(pts), dev(ecc, c.ravel()),
+                              ecc.kmeans_cfg(k=k, max_iters=0, tol=-1.0, threshold=thr), engine, d_lab)
+        gpu.sync()
+        g, o = d_lab.numpy(), orc.kmeans_assign_f32(flat, c.ravel(), thr)
+        bad = np.flatnonzero(g != o)
+        assert len(bad) == 0, (thr, len(bad), [(pts[i].tolist(), int(g[i]), int(o[i])) for i in bad[:6]], c.tolist())
 
 
 # ------------------------------------------------------------------------------ SAE + arc corners
@@ -1123,7 +1151,7 @@ def test_kmeans_frame_segments_match_oracle(ecc, orc, gpu, wh, frame, k):
     assert (g_dense == o_lab).all()
 
 
-@pytest.mark.parametrize("engine", [1, 2])
+@pytest.mark.parametrize("engine", [1, 2, 3])
 def test_kmeans_c3_f32_50m(ecc, gpu, c3_points, engine):
     pts, c0, o_c, o_lab, o_it = c3_points
     n = len(pts)
