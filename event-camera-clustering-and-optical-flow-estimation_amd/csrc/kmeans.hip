@@ -32,7 +32,10 @@
 #define ECC_KM_LUT_UNROLL 4
 #endif
 #ifndef ECC_KM_MFMA_BLOCKS
-#define ECC_KM_MFMA_BLOCKS 2  // matrix engine: 64-pair blocks per trip
+#define ECC_KM_MFMA_BLOCKS 1  // matrix engine: 64-pair blocks per trip
+#endif
+#ifndef ECC_KM_MFMA_WAVES
+#define ECC_KM_MFMA_WAVES 4  // matrix engine 3: waves/SIMD the register budget is held to
 #endif
 #ifndef ECC_KM_ACC_SUB
 #define ECC_KM_ACC_SUB 4
@@ -1160,7 +1163,7 @@ __device__ __forceinline__ uint32_t lut_point(float px, float py, const LutView 
 constexpr int kPairUnroll = 4;
 
 template <int K, bool kAccumulate, bool kLut, bool kMfma = false>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, kMfma ? ECC_KM_MFMA_WAVES : 1)
 kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *__restrict__ cent, int k, float thr,
                        float thr2, double *__restrict__ acc, int n_copies, const KmState *__restrict__ st,
                        uint8_t *__restrict__ labels, const LutGeom *__restrict__ geom,
