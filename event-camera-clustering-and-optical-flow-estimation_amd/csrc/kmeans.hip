@@ -1212,12 +1212,16 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
         }
     }
     // matrix-engine operands (kMfma): this lane's A element, |c_r|^2 as the C input, error scales
-    float a_op = 0.f, em_c2 = 0.f, em_x = 0.f, em_y = 0.f;
+    float a_ev = 0.f, a_od = 0.f, em_c2 = 0.f, em_x = 0.f, em_y = 0.f;
     floatx16_t c2v{};
     if constexpr (kMfma) {
         static_assert(K == 16, "the 32x32x2 layout maps D register r to centre r < 16");
         const int i = lane & 31, c = (i & 3) | ((i >> 3) << 2);
-        a_op = c < k ? -2.0f * cent[2 * c + (lane >> 5)] : 0.f;
+        const float a_op = c < k ? -2.0f * cent[2 * c + (lane >> 5)] : 0.f;
+        // rows (i & 4) == 0 are lanes 0-31's D rows, the others lanes 32-63's: the even points'
+        // instruction fills the first, the odd points' (chained on its output) the second
+        a_ev = (i & 4) ? 0.f : a_op;
+        a_od = (i & 4) ? a_op : 0.f;
 #pragma unroll
         for (int r = 0; r < K; ++r) {
             c2v[r] = r < k ? __fadd_rn(__fmul_rn(cx[r], cx[r]), __fmul_rn(cy[r], cy[r])) : __builtin_inff();
@@ -1320,11 +1324,14 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
                     const int src = (lane & 31) + 32 * h;
                     const float4 qs = q[2 * u + h];
                     const float sx = qs.x, sy = qs.y, sz = qs.z, sw = qs.w;
-                    const floatx16_t de = __builtin_amdgcn_mfma_f32_32x32x2f32(a_op, low ? sx : sy, c2v, 0, 0, 0);
-                    const floatx16_t dd = __builtin_amdgcn_mfma_f32_32x32x2f32(a_op, low ? sz : sw, c2v, 0, 0, 0);
+                    // even points into lanes 0-31's rows (lanes 32-63 keep C), then the odd points
+                    // into lanes 32-63's rows with the first result as C (lanes 0-31 add fma(0, b)
+                    // terms: unchanged, or NaN for a non-finite odd point -> the exact path)
+                    const floatx16_t de = __builtin_amdgcn_mfma_f32_32x32x2f32(a_ev, low ? sx : sy, c2v, 0, 0, 0);
+                    const floatx16_t dd = __builtin_amdgcn_mfma_f32_32x32x2f32(a_od, low ? sz : sw, de, 0, 0, 0);
                     float v[K];
 #pragma unroll
-                    for (int r = 0; r < K; ++r) v[r] = low ? de[r] : dd[r];
+                    for (int r = 0; r < K; ++r) v[r] = dd[r];
                     const float px = low ? sx : sz, py = low ? sy : sw;  // lanes 0-31: even, 32-63: odd point
                     const uint32_t l = pick_mfma<K>(v, px, py, em_c2, em_x, em_y, s_c, cx, cy, thr);
                     const int64_t pq = blk * 64 + src;
