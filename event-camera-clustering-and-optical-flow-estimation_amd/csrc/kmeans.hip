@@ -700,7 +700,7 @@ typedef float floatx16_t __attribute__((ext_vector_type(16)));
 template <int K>
 __device__ __forceinline__ uint32_t pick_mfma(const float (&v)[K], float px, float py, float emul_c2, float emul_x,
                                               float emul_y, const float2 *__restrict__ s_c, const float (&cx)[K],
-                                              const float (&cy)[K], float thr) {
+                                              const float (&cy)[K], float thr, float thr2) {
     float b = v[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) b = fminf(b, v[i]);
@@ -718,7 +718,7 @@ __device__ __forceinline__ uint32_t pick_mfma(const float (&v)[K], float px, flo
     if (__builtin_expect(!(cnt == 1 && lim < __builtin_inff()), 0)) return assign_fast<K>(px, py, cx, cy, thr);
     const float2 c = s_c[bi];
     const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
-    return ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy))) < thr ? (uint32_t)bi : 255u;
+    return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < thr2 ? (uint32_t)bi : 255u;  // sqrt_rn(d2) < thr
 }
 
 constexpr int kF32Unroll = 4;  // 64-point blocks per wave per trip (loads in flight together)
@@ -1333,7 +1333,7 @@ kmeans_f32_pair_kernel(const float4 *__restrict__ xy4, int64_t n, const float *_
 #pragma unroll
                     for (int r = 0; r < K; ++r) v[r] = dd[r];
                     const float px = low ? sx : sz, py = low ? sy : sw;  // lanes 0-31: even, 32-63: odd point
-                    const uint32_t l = pick_mfma<K>(v, px, py, em_c2, em_x, em_y, s_c, cx, cy, thr);
+                    const uint32_t l = pick_mfma<K>(v, px, py, em_c2, em_x, em_y, s_c, cx, cy, thr, thr2);
                     const int64_t pq = blk * 64 + src;
                     if (pq < npair) {
                         if (labels) labels[2 * pq + (low ? 0 : 1)] = (uint8_t)l;
