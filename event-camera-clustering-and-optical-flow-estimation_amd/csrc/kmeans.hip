@@ -655,7 +655,7 @@ template <int K>
 __device__ __forceinline__ uint32_t assign_mfma(float px, float py, const float (&ax)[K / 4], const float (&ay)[K / 4],
                                                 const float (&c2)[K], float emul_c2, float emul_x, float emul_y,
                                                 const float2 *__restrict__ s_c, const float (&cx)[K],
-                                                const float (&cy)[K], float thr) {
+                                                const float (&cy)[K], float thr, float thr2) {
     floatx4_t d[K / 4];
 #pragma unroll
     for (int g = 0; g < K / 4; ++g) {
@@ -679,7 +679,7 @@ __device__ __forceinline__ uint32_t assign_mfma(float px, float py, const float 
     if (__builtin_expect(!(b2 - b > margin), 0)) return assign_fast<K>(px, py, cx, cy, thr);  // close call / NaN
     const float2 c = s_c[bi];
     const float dx = __fsub_rn(c.x, px), dy = __fsub_rn(c.y, py);
-    return ecc::sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy))) < thr ? (uint32_t)bi : 255u;
+    return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < thr2 ? (uint32_t)bi : 255u;  // sqrt_rn(d2) < thr
 }
 
 // Matrix engine, streaming form (k <= 16, 16-B aligned points): v_mfma_f32_32x32x2f32, a 32 x 32
@@ -781,8 +781,8 @@ kmeans_f32_fast_kernel(const float2 *__restrict__ xy, int64_t n, const float *__
             if (b0 + u * stride >= nblk) break;  // wave-uniform
             uint32_t lab[2];
             if constexpr (kMfma) {
-                lab[0] = assign_mfma<K>(q[u].x, q[u].y, ax, ay, c2, em_c2, em_x, em_y, s_c, cx, cy, thr);
-                lab[1] = assign_mfma<K>(q[u + 1].x, q[u + 1].y, ax, ay, c2, em_c2, em_x, em_y, s_c, cx, cy, thr);
+                lab[0] = assign_mfma<K>(q[u].x, q[u].y, ax, ay, c2, em_c2, em_x, em_y, s_c, cx, cy, thr, thr2);
+                lab[1] = assign_mfma<K>(q[u + 1].x, q[u + 1].y, ax, ay, c2, em_c2, em_x, em_y, s_c, cx, cy, thr, thr2);
             } else {
                 assign_pair<K>(q[u], q[u + 1], cx, cy, s_c, thr, thr2, lab[0], lab[1]);
             }
