@@ -90,8 +90,44 @@ def parse():
     return a
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N` without an external launcher: run N ranks of this script under
+    `torch.distributed.run` as a CHILD process (nothing here has touched the GPU yet: no torch,
+    no libecc, no exec) and return its exit code; rank 0 of the child prints the JSON line.
+    Under a launcher (WORLD_SIZE set) the world size must equal --gpus."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != args.gpus and not (args.force_dist and args.gpus == 1 and int(world_env) == 1):
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env} (one rank per GPU: they must agree)",
+                  file=sys.stderr, flush=True)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["MASTER_ADDR"] = "127.0.0.1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -107,9 +143,13 @@ def main():
             os.environ.setdefault("WORLD_SIZE", "1")
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 2000))
+        if not args.same_device and local >= torch.cuda.device_count():
+            raise SystemExit(f"bench.py: rank {rank} needs device {local}, only {torch.cuda.device_count()} visible")
         torch.cuda.set_device(local)
         tdist.init_process_group(args.dist_backend)
         dist = tdist
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
     import eccpy as ecc
 
     W, H, n, K, I = args.width, args.height, args.events, args.k, args.iters
@@ -338,6 +378,13 @@ def main():
             traffic_src = tfiles[-1].name
         except (ValueError, KeyError, TypeError):
             traffic = None
+    # the same kernel's average launch time from the newest committed rocprofv3 --stats summary
+    # (a one-stream `bench.py --serial` trace, scripts/gpu_evidence.sh); the line's frac is the
+    # lower of the live HIP-event figure and the rocprof one
+    rp_ms, rp_src = rocprof_avg_ms(dominant)
+    achieved_live = achieved
+    if rp_ms:
+        achieved = min(achieved, bytes_per_launch / (rp_ms * 1e-3) / 1e9)
 
     # ---- tracker (sequential over slices, rank 0 of a 1-GPU run) ---------------------------------
     tracker = None
@@ -491,6 +538,8 @@ def main():
         "value": round(value, 2),
         "unit": "Mevents/s",
         "n_gpus": world,
+        "dist_world": dist.get_world_size() if dist else None,
+        "dist_backend": args.dist_backend if dist else None,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
@@ -511,7 +560,10 @@ def main():
         "roofline": {
             "kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "avg_launch_ms": round(avg_ms, 5), "algorithmic_bytes_per_launch": bytes_per_launch,
+            "avg_launch_ms": round(avg_ms, 5), "achieved_hip_events": round(achieved_live, 2),
+            "rocprof_avg_launch_ms": round(rp_ms, 5) if rp_ms else None, "rocprof_source": rp_src,
+            "frac_from": "min(HIP events, rocprof)" if rp_ms else "HIP events",
+            "algorithmic_bytes_per_launch": bytes_per_launch,
             "algorithmic_bytes": f"SURVEY §8d bytes of the kernel's stage ({dom_stage})",
             "traffic_source": traffic_src,
             "timing": f"HIP events around every launch in a second, eager, one-stream {args.steps}-step "
@@ -537,6 +589,24 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def rocprof_avg_ms(kernel):
+    """(average ms per launch, file) of `kernel` (libecc's timing name) in the newest
+    profiles/*_kernel_stats.csv that lists it, or (None, None)."""
+    import csv
+    import re
+    for f in sorted((ROOT / "profiles").glob("r*_kernel_stats.csv"), reverse=True):
+        if "kmeans_f32" in f.name:
+            continue
+        try:
+            for r in csv.DictReader(open(f)):
+                m = re.search(r"::([A-Za-z_0-9]+)(<[^>]*>)?\(", r["Name"])
+                if m and m.group(1) == kernel:
+                    return float(r["AverageNs"]) * 1e-6, f.name
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 def timed_kernels(ctx, run, reps):

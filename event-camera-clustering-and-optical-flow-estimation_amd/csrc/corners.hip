@@ -43,6 +43,10 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kBuildUnroll = 8;
+// ctx->flags[10]: unsorted-time verdict of the running call (flags[0]: the last finished call's)
+constexpr int kSortPendingWord = 10;
+// the flag pass's dynamic LDS limit: 160 KiB less its static LDS (ctot[kFlagQuads][4], 128 B)
+constexpr size_t kFlagDynLdsMax = 160 * 1024 - 256;
 constexpr int kArcThreads = 512;  // 8 waves: one lane per window pixel (484) when staging
 constexpr int kGroup = 32;         // slices per group (mask bits)
 constexpr int kTile = 14;          // tile edge (pixels): the 22x22 window fits one 8-wave workgroup
@@ -164,7 +168,7 @@ __device__ __forceinline__ void block_excl_scan_inplace(int32_t *a, int n, int32
 
 __global__ void __launch_bounds__(kSortThreads, 8)  // 8 waves/SIMD: two workgroups per CU
 slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g, Sorted so,
-                  int32_t *__restrict__ first_border, int32_t *__restrict__ err, int32_t err_val,
+                  int32_t *__restrict__ first_border, int32_t *__restrict__ err, int32_t *__restrict__ err_status,
                   uint32_t *__restrict__ zero0, int32_t *__restrict__ zero1) {
     extern __shared__ int32_t hist[];  // [nb]: counts, then offsets, then (long slices) cursors;
                                        // then [kSortChunk] staging of the sorted slice
@@ -173,9 +177,12 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
     const int64_t s = blockIdx.x;
     // the call's counters that later kernels of the call start from (a 4-B memset each was a
     // fill launch on the critical path): arc_kernel's overflow count, the NMS error word
+    // and the published sort verdict of the previous call (the pending word `err` is cleared by
+    // the previous call's sae_prefix_kernel, or is still set if that call stopped after prepare)
     if (s == 0 && tid == 0) {
         if (zero0) *zero0 = 0u;
         if (zero1) *zero1 = 0;
+        *err_status = 0;
     }
     const int64_t lo = s * g.S;
     const int len = (int)((lo + g.S < g.n ? lo + g.S : g.n) - lo);
@@ -219,7 +226,7 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
             br[u] |= (uint32_t)atomicAdd(&hist[br[u] >> 16], 1) & 0xffffu;
         }
     }
-    if (__any(bad) && lane == 0 && !g.any_order) *err = err_val;  // this call's tag: no reset needed
+    if (__any(bad) && lane == 0 && !g.any_order) *err = 1;  // pending: published by sae_prefix_kernel
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) fb = min(fb, __shfl_xor(fb, o));
     if (lane == 0) wsum[tid >> 6] = fb;
@@ -496,7 +503,14 @@ constexpr int kPrefixRound = kPrefixPer * (kThreads / 64);
 
 __global__ void __launch_bounds__(kThreads)
 sae_prefix_kernel(CornerGeom g, int64_t n_groups, const uint32_t *__restrict__ gmask, int64_t *__restrict__ gB,
-                  int64_t *__restrict__ sae) {
+                  int64_t *__restrict__ sae, int32_t *__restrict__ err_status, int32_t *__restrict__ err_pending) {
+    // the call's sort verdict: slice_sort (all of it finished before this kernel) left it in the
+    // pending word; publish it and clear the pending word for the next call.  Both words live in
+    // device memory and are rewritten by every call, so a captured graph replays them correctly.
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *err_status = *err_pending;
+        *err_pending = 0;
+    }
     __shared__ int64_t s_last[kThreads / 64][kPrefixPix];
     __shared__ uint8_t s_has[kThreads / 64][kPrefixPix];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1502,7 +1516,6 @@ sae_max_combine_kernel(const int64_t *__restrict__ images, int n_images, int64_t
 struct CornerState {
     void *evt = nullptr;
     size_t evt_bytes = 0;
-    int32_t epoch = 0;  // tag of the last sort phase: slice_sort writes it to ctx->flags[0] on error
     // diagnostics of the last detection (ecc_fast_detect_stats)
     const uint32_t *n_over = nullptr;
     int64_t n_items = 0, n_slices = 0, n_groups = 0;
@@ -1649,7 +1662,6 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     CornerState *st = state_of(ctx);
-    if (phases & 1) ++st->epoch;  // ecc_fast_detect_status: flags[0] == epoch <=> this call's sort failed
     if (n == 0) {
         if (local_last) ECC_CHECK_HIP(ctx, hipMemsetAsync(local_last, 0, (size_t)g.W * g.H * 8, s), "memset(local)");
         return ECC_OK;
@@ -1681,7 +1693,8 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         }
         ECC_TIMED(ctx, s, "slice_sort_kernel");
         hipLaunchKernelGGL(slice_sort_kernel, dim3((unsigned)g.n_slices), dim3(kSortThreads), lds, s, xy, t, g,
-                           so, first_border, ctx->flags, st->epoch, (phases & 2) ? gi.n_over : nullptr, zero_nms_err);
+                           so, first_border, ctx->flags + kSortPendingWord, ctx->flags,
+                           (phases & 2) ? gi.n_over : nullptr, zero_nms_err);
     }
     {
         ECC_TIMED(ctx, s, "pair_build_kernel");
@@ -1710,7 +1723,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         const int64_t HW = (int64_t)g.W * g.H;
         const unsigned blocks = (unsigned)((HW + kPrefixPix - 1) / kPrefixPix);
         hipLaunchKernelGGL(sae_prefix_kernel, dim3(blocks), dim3(kThreads), 0, s, g, n_groups,
-                           (const uint32_t *)gi.mask, gi.B, sae);
+                           (const uint32_t *)gi.mask, gi.B, sae, ctx->flags, ctx->flags + kSortPendingWord);
     }
     {
         ECC_TIMED(ctx, s, "arc_kernel");
@@ -1729,7 +1742,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     }
     {
         ECC_TIMED(ctx, s, "flags_kernel");
-        constexpr size_t kLdsMax = 160 * 1024;
+        constexpr size_t kLdsMax = kFlagDynLdsMax;
         const size_t lds = (size_t)g.n_tiles * kSegWords * sizeof(uint32_t);
         if (lds <= kLdsMax) {
             static bool lds_set[2] = {false, false};
@@ -1804,7 +1817,7 @@ ECC_API int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t 
     uint32_t *cand = nullptr;
     int32_t *n_cand = nullptr;
     if (n > 0 && cfg->slice_events % 4 == 0 && cfg->slice_events <= kFlagCandMax &&
-        tiles * kSegWords * 4 <= 160 * 1024) {
+        tiles * kSegWords * 4 <= (int64_t)kFlagDynLdsMax) {
         int rc = ecc::nms_candidates(ctx, n, cfg->slice_events, cfg->width, cfg->height, box_size, &cand, &n_cand);
         if (rc) return rc;
     }
@@ -1840,12 +1853,14 @@ ECC_API int ecc_fast_detect_finish(ecc_ctx *ctx, const uint32_t *xy, const int64
 
 ECC_API int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream) {
     if (!ctx) return ECC_ERR_INVALID;
-    int32_t f = 0;
+    // flags[0]: the last finished call's verdict; the pending word: a prepare-only call's
+    int32_t f = 0, pend = 0;
     ECC_CHECK_HIP(ctx, hipMemcpyAsync(&f, ctx->flags, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
                   "read err flag");
+    ECC_CHECK_HIP(ctx, hipMemcpyAsync(&pend, ctx->flags + kSortPendingWord, 4, hipMemcpyDeviceToHost,
+                                      ecc::as_stream(stream)), "read err flag");
     ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
-    const int32_t epoch = state_of(ctx)->epoch;
-    return (epoch != 0 && f == epoch) ? ECC_ERR_UNSORTED_TIME : ECC_OK;
+    return (f != 0 || pend != 0) ? ECC_ERR_UNSORTED_TIME : ECC_OK;
 }
 
 ECC_API int ecc_fast_detect_stats(ecc_ctx *ctx, int64_t *out, int32_t n_out, ecc_stream_t stream) {

@@ -104,12 +104,22 @@ __device__ __forceinline__ void for_points_by_wave(int m, int64_t base, const in
     }
 }
 
+// A list entry of point j of an m-point segment.  An entry outside [0, m) (a malformed list:
+// parent[] is sized by the stride) reads as j itself, which no phase acts on (self-unions are
+// no-ops; a non-core j has no component), and sets bit 4 of the status word.
+__device__ __forceinline__ int nbr_at(const int32_t *__restrict__ nbr, int64_t e, int m, int j, int32_t *err) {
+    const int q = nbr[e];
+    if ((unsigned)q < (unsigned)m) return q;
+    atomicOr(err, 4);
+    return j;
+}
+
 // Smallest component among the core neighbours of j's list, reduced over the wave (0x7fffffff: none).
 __device__ __forceinline__ int wave_first_comp(const int *parent, const int32_t *__restrict__ nbr, int64_t e0,
-                                               int64_t e1) {
+                                               int64_t e1, int m, int j, int32_t *err) {
     int first = 0x7fffffff;
     for (int64_t e = e0 + (threadIdx.x & 63); e < e1; e += 64) {
-        const int c = comp_of(parent, nbr[e]);
+        const int c = comp_of(parent, nbr_at(nbr, e, m, j, err));
         if (c >= 0 && c < first) first = c;
     }
 #pragma unroll
@@ -153,7 +163,7 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         for_points_by_wave(m, base, offsets, [&](int j, int64_t e0, int64_t e1) {
             if (parent[j] == -1) return;  // non-core stays -1 during the unions: uniform
             for (int64_t e = e0 + lane; e < e1; e += 64) {
-                const int q = nbr[e];
+                const int q = nbr_at(nbr, e, m, j, err);
                 if (q > j && parent[q] != -1) uf_union(parent, j, q);
             }
         });
@@ -219,14 +229,14 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         }
         for_points_by_wave(m, base, offsets, [&](int j, int64_t e0, int64_t e1) {
             if (parent[j] != -1) return;  // core: counted above (uniform)
-            const int first = wave_first_comp(parent, nbr, e0, e1);
+            const int first = wave_first_comp(parent, nbr, e0, e1, m, j, err);
             if (first == 0x7fffffff) return;  // noise
             if (lane == 0) {
                 atomicAdd(&c_size[first], 1);
                 atomicMin(&c_front[first], j);
             }
             for (int64_t e = e0 + lane; e < e1; e += 64) {  // later clusters seeded by a neighbour
-                const int v = parent[nbr[e]];
+                const int v = parent[nbr_at(nbr, e, m, j, err)];
                 if (v <= -2 && -v - 2 != first) {
                     atomicAdd(&c_size[-v - 2], 1);
                     atomicMin(&c_front[-v - 2], j);
@@ -260,11 +270,11 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         }
         for_points_by_wave(m, base, offsets, [&](int j, int64_t e0, int64_t e1) {
             if (parent[j] != -1) return;  // core: labelled above (uniform)
-            const int first = wave_first_comp(parent, nbr, e0, e1);
+            const int first = wave_first_comp(parent, nbr, e0, e1, m, j, err);
             if (lane == 0) labels[base + j] = first == 0x7fffffff ? -1 : c_rank[first];
             if (first == 0x7fffffff) return;
             for (int64_t e = e0 + lane; e < e1; e += 64) {
-                const int v = parent[nbr[e]];
+                const int v = parent[nbr_at(nbr, e, m, j, err)];
                 if (v <= -2 && -v - 2 != first && c_rank[-v - 2] >= 0) {
                     const unsigned long long at = atomicAdd(n_dups, 1ull);
                     if ((int64_t)at < dup_cap) {
@@ -612,16 +622,10 @@ ECC_API int ecc_dbscan_extract(ecc_ctx *ctx, int64_t n_segs, int64_t seg_stride,
     if (n_dups) ECC_CHECK_HIP(ctx, hipMemsetAsync(n_dups, 0, 8, s), "memset(n_dups)");
     if (n_segs == 0) return ECC_OK;
     const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 4096);
+    // parent[] (dynamic): seg_stride <= kMaxPts = 16384 entries, at most 64 KiB, with the static
+    // tables inside gfx950's 160 KiB
     const size_t lds = (size_t)seg_stride * sizeof(int);
-    if (lds > 65536) {
-        static bool lds_set = false;
-        if (!lds_set) {
-            ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&dbscan_extract_kernel),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kMaxPts * (int)sizeof(int)),
-                          "dbscan_extract LDS");
-            lds_set = true;
-        }
-    }
+    static_assert(kMaxPts * sizeof(int) <= 65536, "dynamic LDS of dbscan_extract_kernel");
     ECC_TIMED(ctx, s, "dbscan_extract_kernel");
     hipLaunchKernelGGL(dbscan_extract_kernel, dim3(grid), dim3(kThreads), lds, s, n_segs, seg_stride, seg_counts,
                        offsets, nbr, nbr_len, min_pts, min_cluster_size, max_cluster_size, labels, n_clusters, dups, dup_cap,
@@ -666,6 +670,7 @@ ECC_API int ecc_dbscan_status(ecc_ctx *ctx, ecc_stream_t stream) {
     ECC_CHECK_HIP(ctx, hipMemcpyAsync(&f, ctx->flags + kFlagWord, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
                   "read dbscan err");
     ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
+    if (f & 4) return ECC_ERR_INVALID;  // a neighbour index outside its segment (ecc_dbscan_extract)
     return (f & 2) ? ECC_ERR_CAPACITY : ECC_OK;
 }
 

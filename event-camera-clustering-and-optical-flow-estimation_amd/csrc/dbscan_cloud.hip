@@ -93,9 +93,13 @@ db_core_kernel(const Grid *__restrict__ gp, Cloud c, int32_t *__restrict__ paren
     T p[3];
 #pragma unroll
     for (int d = 0; d < D; ++d) p[d] = sc[(int64_t)d * c.n + k];
+    // the point itself counts unconditionally (radiusSearch pushes `index` first,
+    // DBSCAN_simple.h:124-125; DBSCAN_precomp.h:25-26): a non-finite point, whose distance to
+    // itself is NaN, still has one neighbour and is core when min_pts <= 1.  Its cell coordinates
+    // are the same in the count and the query (cell_coord), so the walk always reaches it.
     int cnt = 0;
     ecc::rgrid::for_runs<T, D>(g, c.cell_off, p, [&](int64_t lo, int64_t hi) {
-        for (int64_t j = lo; j < hi; ++j) cnt += ecc::rgrid::sq_dist<T, D>(sc, c.n, j, p) <= c.eps2 ? 1 : 0;
+        for (int64_t j = lo; j < hi; ++j) cnt += (j == k || ecc::rgrid::sq_dist<T, D>(sc, c.n, j, p) <= c.eps2) ? 1 : 0;
     });
     const bool core = cnt >= c.min_pts;
     const int32_t i = c.sidx[k];
@@ -391,8 +395,9 @@ ECC_API int ecc_dbscan_cloud_f64(ecc_ctx *ctx, const double *pts, int64_t n, int
 }
 
 // Only the duplicate-capacity bit of this path's own word (a radius call in between cannot change
-// it).  Non-finite points are not an error: as in the reference's radiusSearch they are nobody's
-// neighbour, so they come out as noise (label -1) and the other clusters are unaffected.
+// it).  Non-finite points are not an error: as in the reference's radiusSearch they are nobody
+// else's neighbour, so they come out as noise (label -1), or as singleton clusters when
+// min_pts <= 1 (the point itself always counts), and the other clusters are unaffected.
 ECC_API int ecc_dbscan_cloud_status(ecc_ctx *ctx, ecc_stream_t stream) {
     if (!ctx) return ECC_ERR_INVALID;
     int32_t f = 0;

@@ -51,7 +51,7 @@ downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, i
     __shared__ __attribute__((aligned(16))) uint32_t table[kBuckets];
     constexpr int kWaves = NT / 64, kChunk = NT * 4;  // events per chunk: 4 consecutive per lane
     __shared__ int wave_tot[MAXC][kWaves];
-    __shared__ int red[2][kWaves];
+    __shared__ int red[kWaves];
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -98,8 +98,11 @@ downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, i
     }
     __syncthreads();
 
-    // 4. representatives (bucket min == own index) and repeated marks (:65-75)
+    // 4. representatives (bucket min == own index) and repeated marks (:65-75); a bucket is
+    //    repeated (hit >= 2 times) iff some non-first event's ds_or finds bit 31 clear: exactly
+    //    one such ds_or per repeated bucket, so the returned old values count them
     uint32_t repmask[MAXC];
+    int rp = 0;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
         repmask[c] = 0;
@@ -111,7 +114,7 @@ downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, i
                     const int li = c * kChunk + 4 * tid + k;
                     const uint32_t first = table[h] & kEmpty;
                     if (first == (uint32_t)li) repmask[c] |= 1u << k;
-                    else atomicOr(&table[h], kRepeatBit);
+                    else rp += (atomicOr(&table[h], kRepeatBit) & kRepeatBit) ? 0 : 1;
                 }
             }
         }
@@ -132,23 +135,10 @@ downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, i
     }
     __syncthreads();
 
-    // 6. counts: unique = occupied buckets, repeated = buckets hit >= 2 times
-    {
-        int u = 0, rp = 0;
-        const uint4 *t4 = reinterpret_cast<const uint4 *>(table);
-        for (int i = tid; i < kBuckets / 4; i += NT) {
-            const uint4 q = t4[i];
-            u += (q.x != kEmpty) + (q.y != kEmpty) + (q.z != kEmpty) + (q.w != kEmpty);
-            rp += (q.x >> 31) + (q.y >> 31) + (q.z >> 31) + (q.w >> 31);
-        }
-        // note: a repeated bucket has bit31 set and a min < kEmpty, so it is != kEmpty
+    // 6. repeated count per wave (unique = occupied buckets = the representatives: step 7's total)
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            u += __shfl_xor(u, o);
-            rp += __shfl_xor(rp, o);
-        }
-        if (lane == 0) { red[0][wave] = u; red[1][wave] = rp; }
-    }
+    for (int o = 32; o > 0; o >>= 1) rp += __shfl_xor(rp, o);
+    if (lane == 0) red[wave] = rp;
 
     // 7. compacted write-out in ascending event order
     int base = 0;
@@ -174,10 +164,10 @@ downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, i
     }
     __syncthreads();
     if (tid == 0) {
-        int u = 0, rp = 0;
-        for (int ww = 0; ww < kWaves; ++ww) { u += red[0][ww]; rp += red[1][ww]; }
-        if (win_unique) win_unique[w] = u;
-        if (win_repeated) win_repeated[w] = rp;
+        int r = 0;
+        for (int ww = 0; ww < kWaves; ++ww) r += red[ww];
+        if (win_unique) win_unique[w] = base;  // every lane's `base` is the window's total
+        if (win_repeated) win_repeated[w] = r;
     }
 }
 

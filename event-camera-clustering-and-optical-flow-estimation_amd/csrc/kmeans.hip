@@ -646,10 +646,16 @@ kmeans_f32_kernel(const float *__restrict__ xy, int64_t n, const float *__restri
 // 2E + 2^-19 (|s_best| + |p|^2 + E) proves the best index is the unique d^2 minimum with no
 // earlier centre inside assign_fast's square-root tie band; the winner's exact d^2 then decides
 // the threshold.  Any closer call (and NaN input) takes the exact vector path.
+// The argument assumes only that each of the three roundings of s is bounded — not the order in
+// which the matrix core sums the products, nor how it treats subnormals: a relative bound does
+// not hold for subnormal or flushed results, so E also carries an absolute term (kAbsRound)
+// above three flushes to zero of a result below the smallest normal (3 x 2^-126).  Points whose
+// gaps are that small (coordinates around 1e-19 and below) always take the exact path.
 // Accumulation (both engines): per wave LDS slots, u32 count and fp64 sums (ds_add_f64: exact for
 // integer-valued coordinates, 1e-16 relative otherwise); per workgroup one fp64 global atomic per
 // (cluster, field) into one of n_copies replicas that the update kernel sums.
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
+constexpr float kAbsRound = 0x1p-124f;  // > 3 x 2^-126: the absolute part of E (see above)
 
 template <int K>
 __device__ __forceinline__ uint32_t assign_mfma(float px, float py, const float (&ax)[K / 4], const float (&ay)[K / 4],
@@ -673,7 +679,7 @@ __device__ __forceinline__ uint32_t assign_mfma(float px, float py, const float 
         bi = lt ? i : bi;
         b = lt ? v : b;
     }
-    const float E = 0x1p-21f * (emul_c2 + 2.0f * (emul_x * fabsf(px) + emul_y * fabsf(py)));
+    const float E = 0x1p-21f * (emul_c2 + 2.0f * (emul_x * fabsf(px) + emul_y * fabsf(py))) + kAbsRound;
     const float P = px * px + py * py;
     const float margin = 2.0f * E + 0x1p-19f * (fabsf(b) + P + E);
     if (__builtin_expect(!(b2 - b > margin), 0)) return assign_fast<K>(px, py, cx, cy, thr);  // close call / NaN
@@ -704,7 +710,7 @@ __device__ __forceinline__ uint32_t pick_mfma(const float (&v)[K], float px, flo
     float b = v[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) b = fminf(b, v[i]);
-    const float E = 0x1p-21f * (emul_c2 + 2.0f * (emul_x * fabsf(px) + emul_y * fabsf(py)));
+    const float E = 0x1p-21f * (emul_c2 + 2.0f * (emul_x * fabsf(px) + emul_y * fabsf(py))) + kAbsRound;
     const float P = px * px + py * py;
     const float margin = 2.0f * E + 0x1p-19f * (fabsf(b) + P + E);
     const float lim = b + 1.0625f * margin;

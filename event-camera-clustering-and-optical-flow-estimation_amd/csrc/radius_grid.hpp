@@ -60,8 +60,10 @@ bbox_kernel(const T *__restrict__ pts, int64_t n, int dim, int64_t *keys, int32_
     bool fin = true;
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
         // a point with a non-finite coordinate is left out of the box: its distance to every
-        // point, itself included, is NaN or inf, never <= eps^2 (the reference's `d2 <= r2`), so
-        // whatever cell it lands in it is nobody's neighbour
+        // other point is NaN or inf, never <= eps^2 (the reference's `d2 <= r2`), so whatever
+        // cell it lands in it is nobody else's neighbour (the DBSCAN cloud counts the query point
+        // itself unconditionally, as radiusSearch does; the radius entry points report such
+        // input through `bad` instead)
         double v[3] = {0.0, 0.0, 0.0};
         bool pf = true;
 #pragma unroll

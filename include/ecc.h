@@ -480,7 +480,8 @@ int ecc_optics_f64(ecc_ctx *ctx, const double *pts, int64_t n, int32_t dim, int3
  * nbr_len = entries of nbr (a segment whose offsets run past it is rejected, not read).
  * ecc_dbscan_status: ECC_ERR_CAPACITY if dups overflowed, a segment had more than 4096
  * core-connected components, or its lists exceed nbr_len (that segment's labels are then
- * all -1 and n_clusters 0). */
+ * all -1 and n_clusters 0); ECC_ERR_INVALID if a list entry lies outside [0, seg_counts[s])
+ * (the entry is ignored; the segment's result is then unspecified). */
 int ecc_dbscan_extract(ecc_ctx *ctx, int64_t n_segs, int64_t seg_stride, const int32_t *seg_counts,
                        const int64_t *offsets, const int32_t *nbr, int64_t nbr_len, int32_t min_pts,
                        int32_t min_cluster_size, int32_t max_cluster_size, int32_t *labels,

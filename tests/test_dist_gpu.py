@@ -64,11 +64,12 @@ def test_rccl_one_rank_sharded_step_matches_oracle():
 
 @pytest.mark.gpu
 def test_gloo_two_ranks_overlapped_schedule_matches_oracle():
-    port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+    """`bench.py --gpus 2` with NO external launcher: bench.py itself starts the two ranks (a
+    torch.distributed.run child), and the line says so (n_gpus, dist_world)."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2",
            "--events", str(16384 * 24), "--dist-backend", "gloo", "--same-device", "--overlap"] + COMMON
     res = _run(cmd, timeout=300)
+    assert res["n_gpus"] == 2 and res["dist_world"] == 2 and res["dist_backend"] == "gloo", res
     par = res["dist_parity"]
     assert par is not None and par["mismatches"] == 0, par
     assert par["events_total"] == 2 * 16384 * 24

@@ -148,11 +148,14 @@ def test_dbscan_cloud_duplicate_capacity_and_edge_cases(ecc, orc, gpu):
     assert len(got) == 1 and len(got[0]) == 500
 
 
-def test_dbscan_cloud_non_finite_points_are_noise(ecc, orc, gpu):
+@pytest.mark.parametrize("min_pts", [1, 5])
+def test_dbscan_cloud_non_finite_points_are_noise(ecc, orc, gpu, min_pts):
     """A point with a NaN or inf coordinate: `d2 <= r2` (DBSCAN_simple.h:132-136) is false for
-    every pair it is in, itself included, so the reference makes it noise and clusters the rest
-    as without it (a non-dense PCL cloud).  Same here, with no error status — and a radius call
-    in between does not change the status of the DBSCAN call before it."""
+    every pair with another point, but radiusSearch pushes the point itself unconditionally
+    (:124-125), so it has one neighbour: noise for min_pts > 1, a singleton cluster for
+    min_pts <= 1 (min size 1).  The rest is clustered as without it (a non-dense PCL cloud).
+    Same here, with no error status, compared with the oracle's literal queue in every case — and
+    a radius call in between does not change the status of the DBSCAN call before it."""
     pts = event_cloud(ecc, 8000, 31, 0.3, 0.45)
     rng = np.random.default_rng(3)
     bad = rng.choice(len(pts), 40, replace=False)
@@ -160,15 +163,24 @@ def test_dbscan_cloud_non_finite_points_are_noise(ecc, orc, gpu):
     for k, i in enumerate(bad):
         pts[i, k % 3] = vals[k % 3]
     pts[bad[0]] = np.nan  # all coordinates
-    _, ref = orc.dbscan_cloud(pts, 6.0, 5, 1, 1 << 30)
-    st, _, lab, got = gpu_dbscan_cloud(ecc, gpu, pts, 6.0, 5, 1, 1 << 30)
-    assert st == 0 and (lab[bad] == -1).all()
+    _, ref = orc.dbscan_cloud(pts, 6.0, min_pts, 1, 1 << 30)
+    st, _, lab, got = gpu_dbscan_cloud(ecc, gpu, pts, 6.0, min_pts, 1, 1 << 30)
+    assert st == 0
     assert_same_clusters(got, ref)
     assert len(got) > 5
-    # an all-non-finite cloud: all noise
+    if min_pts > 1:
+        assert (lab[bad] == -1).all()
+    else:  # each non-finite point is a cluster of its own
+        assert all(sum(1 for c in got if len(c) == 1 and c[0] == i) == 1 for i in bad)
+    # an all-non-finite cloud: all noise, or all singletons at min_pts 1
     allbad = np.full((50, 3), np.nan, np.float32)
-    st, _, lab, got = gpu_dbscan_cloud(ecc, gpu, allbad, 1.0, 1, 1, 10)
-    assert st == 0 and got == [] and (lab == -1).all()
+    allbad[::3, 1] = np.inf
+    for mp, ms in ((1, 1), (5, 1), (1, 2)):
+        _, ref = orc.dbscan_cloud(allbad, 1.0, mp, ms, 10)
+        st, _, lab, got = gpu_dbscan_cloud(ecc, gpu, allbad, 1.0, mp, ms, 10)
+        assert st == 0
+        assert_same_clusters(got, ref)
+        assert len(got) == (50 if (mp, ms) == (1, 1) else 0)
     # the radius path still reports non-finite input; DBSCAN's own status is its own word
     d_p = dev(ecc, pts.ravel())
     d_lab, d_nc, d_nd = ecc.DeviceArray(len(pts), np.int32), ecc.DeviceArray(1, np.int32), ecc.DeviceArray(1, np.int64)

@@ -373,6 +373,31 @@ def test_kmeans_f32_matrix_engines_extreme_points(ecc, orc, gpu, engine, k):
         assert len(bad) == 0, (thr, len(bad), [(pts[i].tolist(), int(g[i]), int(o[i])) for i in bad[:6]], c.tolist())
 
 
+@pytest.mark.parametrize("engine", [1, 2, 3])
+def test_kmeans_f32_engines_subnormal_squares(ecc, orc, gpu, engine):
+    """Points and centres around 1e-20: every |c|^2, |p|^2 and d^2 is subnormal in fp32, so a
+    flush-to-zero anywhere in the screen (the matrix engines' |c|^2 - 2 c.p products, the vector
+    engine's table) would tie centres the reference (`length()` with IEEE subnormals,
+    assign_to_centers.cl:15-25) tells apart.  The engines' margin argument assumes only that each
+    rounding is bounded, not the order in which the matrix core sums the products; the exact
+    fallback must catch every point the screen cannot decide.  Labels-only passes at three
+    thresholds against the oracle's assignment."""
+    rng = np.random.default_rng(90 + engine)
+    pts = (rng.uniform(-3.0, 3.0, (30001, 2)) * 1e-20).astype(np.float32)
+    pts[::13] = (rng.integers(-3, 4, (len(pts[::13]), 2)) * 1e-20).astype(np.float32)  # ties
+    c = (rng.uniform(-2.5, 2.5, (16, 2)) * 1e-20).astype(np.float32)
+    flat = pts.ravel()
+    d_lab = ecc.DeviceArray(len(pts), np.uint8)
+    for thr in (50.0, 2e-20, 7e-21):
+        gpu.kmeans_f32_engine(dev(ecc, flat), len(pts), dev(ecc, c.ravel()),
+                              ecc.kmeans_cfg(k=16, max_iters=0, tol=-1.0, threshold=thr), engine, d_lab)
+        gpu.sync()
+        g, o = d_lab.numpy(), orc.kmeans_assign_f32(flat, c.ravel(), thr)
+        bad = np.flatnonzero(g != o)
+        assert len(bad) == 0, (thr, len(bad), [(pts[i].tolist(), int(g[i]), int(o[i])) for i in bad[:6]])
+        assert len(set(o.tolist())) > 8  # the case really separates many centres
+
+
 # ------------------------------------------------------------------------------ SAE + arc corners
 def _fast_gpu(ecc, gpu, xy, t, W, H, border_mode=0, first_detect=1, sae0=None, slice_events=16384):
     cfg = ecc.corner_cfg(width=W, height=H, border_mode=border_mode, first_detect_slice=first_detect,
@@ -1326,6 +1351,32 @@ def test_dbscan_extract_rejects_short_lists(ecc, gpu):
     assert (d_lab.numpy() == -1).all() and int(d_nc.numpy()[0]) == 0
 
 
+def test_dbscan_extract_rejects_out_of_segment_neighbours(ecc, gpu):
+    """A list entry outside [0, m) is never used as an LDS index: status INVALID; a good call
+    afterwards is OK again."""
+    m, stride = 40, 64
+    lists = [[j, (j + 1) % m] for j in range(m)]
+    lists[7].append(m + 3)       # past the segment's points, inside the stride
+    lists[9].append(100000)      # far outside
+    lists[11].append(-5)
+    off = np.zeros(stride + 1, np.int64)
+    off[1:m + 1] = np.cumsum([len(l) for l in lists])
+    off[m + 1:] = off[m]
+    nbr = np.concatenate([np.array(l, np.int32) for l in lists])
+    d_off, d_nbr = dev(ecc, off), dev(ecc, nbr)
+    d_cnt = dev(ecc, np.array([m], np.int32))
+    d_lab, d_nc, d_nd = ecc.DeviceArray(stride, np.int32), ecc.DeviceArray(1, np.int32), ecc.DeviceArray(1, np.int64)
+    gpu.dbscan_extract(1, stride, d_cnt, d_off, d_nbr, 2, 1, 1 << 30, d_lab, d_nc, None, 0, d_nd)
+    assert gpu.dbscan_status() == ecc.ERR_INVALID
+    good = np.concatenate([np.array(l[:2], np.int32) for l in lists])
+    off[1:m + 1] = np.arange(1, m + 1) * 2
+    off[m + 1:] = off[m]
+    d_off, d_nbr = dev(ecc, off), dev(ecc, good)
+    gpu.dbscan_extract(1, stride, d_cnt, d_off, d_nbr, 2, 1, 1 << 30, d_lab, d_nc, None, 0, d_nd)
+    assert gpu.dbscan_status() == 0
+    assert int(d_nc.numpy()[0]) == 1 and (d_lab.numpy()[:m] == 0).all()  # one ring of 40 core points
+
+
 # ------------------------------------------------------------------------------ HIP graph replay
 def test_graph_replay_matches_eager(ecc, orc, gpu):
     """ecc_graph_begin/end/launch: a captured downsample -> k-means -> corners -> NMS step replays
@@ -1377,6 +1428,64 @@ def test_graph_replay_matches_eager(ecc, orc, gpu):
     for e, a, windowed in zip(eager, (rep_xy, d_c, labels, sae, flags, nms_cnt), (1, 0, 1, 0, 0, 0)):
         got = a.numpy()
         assert (got[valid] == e[valid]).all() if windowed else (got == e).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_nms", [False, True])
+def test_graph_replay_reports_unsorted_time_per_replay(ecc, gpu, with_nms):
+    """The unsorted-time verdict is produced inside the captured work: a replay over unsorted
+    timestamps reports ECC_ERR_UNSORTED_TIME, the next replay over sorted ones reports OK, and an
+    eager call between replays does not leak its verdict into them."""
+    W, H = 346, 260
+    n = 16384 * 6
+    xy, t, _ = ecc.gen_events(n, seed=5, width=W, height=H)
+    bad_t = t.copy()
+    bad_t[n // 2], bad_t[n // 2 + 1] = t[n // 2 + 1] + 5, t[n // 2]
+    d_xy, d_t = dev(ecc, xy), dev(ecc, t)
+    d_tbad, d_tok = dev(ecc, bad_t), dev(ecc, t)
+    ccfg = ecc.corner_cfg(width=W, height=H)
+    sae, flags = ecc.DeviceArray(W * H, np.int64), ecc.DeviceArray(n, np.uint8)
+    ns, cap = n // 16384, 1024
+    out, cnt = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE), ecc.DeviceArray(ns, np.int32)
+    lib = ecc.lib
+
+    def detect(tt):
+        if with_nms:
+            gpu.fast_detect_nms(d_xy, tt, n, ccfg, sae, flags, 15, cap, out, cnt)
+        else:
+            gpu.fast_detect(d_xy, tt, n, ccfg, sae, flags)
+
+    detect(d_t)
+    gpu.sync()
+    assert gpu.fast_detect_status() == 0
+    gp = ecc.P()
+    ecc.check(lib.ecc_graph_begin(gpu.stream))
+    detect(d_t)
+    ecc.check(lib.ecc_graph_end(gpu.stream, ecc.C.byref(gp)))
+    unsorted = ecc.ERR_UNSORTED_TIME
+    try:
+        for t_src, want in ((bad_t, unsorted), (t, 0), (bad_t, unsorted), (bad_t, unsorted), (t, 0)):
+            ecc.check(lib.ecc_memcpy_h2d(d_t.ptr, t_src.ctypes.data, t_src.nbytes, gpu.stream))
+            ecc.check(lib.ecc_graph_launch(gp.value, gpu.stream))
+            gpu.sync()
+            assert gpu.fast_detect_status() == want, (want, t_src is bad_t)
+        # an eager unsorted call, then a sorted replay: OK; an eager sorted call, then an
+        # unsorted replay: the error
+        detect(d_tbad)
+        gpu.sync()
+        assert gpu.fast_detect_status() == unsorted
+        ecc.check(lib.ecc_graph_launch(gp.value, gpu.stream))  # d_t holds the sorted t
+        gpu.sync()
+        assert gpu.fast_detect_status() == 0
+        ecc.check(lib.ecc_memcpy_h2d(d_t.ptr, bad_t.ctypes.data, bad_t.nbytes, gpu.stream))
+        detect(d_tok)
+        gpu.sync()
+        assert gpu.fast_detect_status() == 0
+        ecc.check(lib.ecc_graph_launch(gp.value, gpu.stream))
+        gpu.sync()
+        assert gpu.fast_detect_status() == unsorted
+    finally:
+        ecc.check(lib.ecc_graph_destroy(gp.value))
 
 
 # ------------------------------------------------------------------------------ multi-GPU forms
