@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--no-ingest", action="store_true", help="skip the RAW (EVT 3.0 / 2.0) decode measurement")
     ap.add_argument("--no-eps", action="store_true", help="skip the eps-neighbourhood (DBSCAN / OPTICS) measurement")
     ap.add_argument("--no-c3", action="store_true", help="skip the BASELINE C3 k-means (k=16, 50 M points) measurement")
+    ap.add_argument("--corner-shards", type=int, default=1,
+                    help="one GPU: run the corner chain as this many time-window shards on their own contexts "
+                         "and streams (the multi-GPU SAE hand-off inside the device)")
     ap.add_argument("--serial", action="store_true",
                     help="one stream for the whole step (isolated per-kernel times for profiling)")
     ap.add_argument("--graph", action="store_true",
@@ -232,6 +235,51 @@ def main():
         ecc.check(lib.ecc_event_create(ecc.C.byref(ev_fork)), "event")
         ecc.check(lib.ecc_event_create(ecc.C.byref(ev_join)), "event")
 
+    # --corner-shards P (one GPU): the corner chain as P time-window shards of the batch on P
+    # contexts and streams — the multi-GPU SAE hand-off inside one device (prepare every shard,
+    # shard p starts from the max of the lower shards' own last-timestamp images, finish + NMS),
+    # so the shards' kernels overlap each other's tails and low-occupancy phases
+    P = max(1, args.corner_shards) if not dist else 1
+    cshards = []
+    if P > 1:
+        HW = W * H
+        cuts = [round(p * ns / P) * SLICE for p in range(P + 1)]
+        c_last = ecc.DeviceArray(P * HW, np.int64)
+        for p in range(P):
+            cx = ctx if p == 0 else ecc.Context(local)
+            cfg_p = ecc.corner_cfg(width=W, height=H, first_detect_slice=1 if p == 0 else 0)
+            sae_p = sae if p == P - 1 else ecc.DeviceArray(HW, np.int64)
+            evs = [ecc.P(), ecc.P()]
+            for e in evs:
+                ecc.check(lib.ecc_event_create(ecc.C.byref(e)), "event")
+            cshards.append(dict(ctx=cx, lo=cuts[p], n=cuts[p + 1] - cuts[p], cfg=cfg_p, sae=sae_p,
+                                ev_prep=evs[0], ev_done=evs[1]))
+
+    def corner_chain_shards(nb):
+        main = ctx.stream
+        for p, c in enumerate(cshards):
+            S = c["ctx"].stream
+            if p > 0:
+                ecc.check(lib.ecc_stream_wait_event(S, ev_fork))
+            ecc.check(lib.ecc_fast_detect_prepare(c["ctx"].ctx, d_xy.ptr + 4 * c["lo"], d_t.ptr + 8 * c["lo"], c["n"],
+                                                  ecc.C.byref(c["cfg"]), c_last.ptr + 8 * p * W * H, S), "prepare")
+            ecc.check(lib.ecc_event_record(c["ev_prep"], S))
+        for p, c in enumerate(cshards):
+            S, cx = c["ctx"].stream, c["ctx"].ctx
+            for q in range(p):
+                ecc.check(lib.ecc_stream_wait_event(S, cshards[q]["ev_prep"]))
+            # the SAE at the shard's start: the step's initial SAE is zero (memset), so the max
+            # of the lower shards' own last images
+            ecc.check(lib.ecc_sae_max_combine(cx, c_last.ptr, p, W * H, c["sae"].ptr, S), "sae combine")
+            s0 = c["lo"] // SLICE
+            ecc.check(lib.ecc_fast_detect_finish_nms(cx, d_xy.ptr + 4 * c["lo"], d_t.ptr + 8 * c["lo"], c["n"],
+                                                     ecc.C.byref(c["cfg"]), c["sae"].ptr, flags.ptr + c["lo"], 15,
+                                                     cap, nms_out[nb].ptr + s0 * cap * ecc.CORNER_DTYPE.itemsize,
+                                                     nms_cnt[nb].ptr + 4 * s0, S), "finish_nms")
+            if p > 0:
+                ecc.check(lib.ecc_event_record(c["ev_done"], S))
+                ecc.check(lib.ecc_stream_wait_event(main, c["ev_done"]))
+
     def step(serial=args.serial, nb=0):
         if dist:
             # gloo collectives block the host, so its timing runs keep one stream (measured faster);
@@ -246,18 +294,23 @@ def main():
         ecc.check(lib.ecc_kmeans_run_xy16_frame(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, W, H, ecc.C.byref(kcfg),
                                                 d_c.ptr, labels.ptr, None, ks), "kmeans")
         ecc.check(lib.ecc_event_record(ev_join, ks))
-        ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
-        # detect + per-slice NMS in one call: the flag pass writes the NMS candidate lists
-        ctx.fast_detect_nms(d_xy, d_t, n, ccfg, sae, flags, 15, cap, nms_out[nb], nms_cnt[nb])
+        if cshards and not serial:
+            corner_chain_shards(nb)  # every shard's SAE is derived from zero (the memset below)
+        else:
+            ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
+            # detect + per-slice NMS in one call: the flag pass writes the NMS candidate lists
+            ctx.fast_detect_nms(d_xy, d_t, n, ccfg, sae, flags, 15, cap, nms_out[nb], nms_cnt[nb])
         ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_join))
 
     for _ in range(args.warmup):
         step()
     ctx.sync()
-    if ctx.fast_detect_status() != 0:
-        raise RuntimeError("fast_detect reported a status error")
-    if ctx.corner_nms_status() != 0:
-        raise RuntimeError("corner_nms reported a status error")
+    for cx in [ctx] + [c["ctx"] for c in cshards[1:]]:
+        cx.sync()
+        if cx.fast_detect_status() != 0:
+            raise RuntimeError("fast_detect reported a status error")
+        if cx.corner_nms_status() != 0:
+            raise RuntimeError("corner_nms reported a status error")
     if dist and lib.ecc_kmeans_counts_status(ctx.ctx, ctx.stream) != 0:
         raise RuntimeError("a representative lies outside the k-means count frame")
     n_reps = int(uniq.numpy().sum())
@@ -556,6 +609,7 @@ def main():
             "kmeans_iters": I, "parallelism": f"time-window shards x{world}",
             "launch": "hipGraph replay of the captured step" if graph is not None else "eager launches",
             "streams": "two streams sharing all CUs" if not (dist or args.serial) else "see parallelism",
+            "corner_shards": P,
         },
         "roofline": {
             "kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -778,14 +832,16 @@ def bench_eps(ecc, ctx, args, rep_xy, uniq, n_win, n_reps):
     dups_g = d_dups.numpy()[:2 * min(nd_g, dup_cap)].reshape(-1, 2)
     same = (np.array_equal(g_lab.numpy()[valid], lab_chain[valid]) and np.array_equal(g_nc.numpy(), nc)
             and nd_g == nd_chain and set(map(tuple, dups_g.tolist())) == set(map(tuple, dups_chain.tolist())))
-    gk = kern.get("dbscan_grid_kernel", float("nan"))
+    # the row-run kernel (distinct-pixel windows) + the cell-grid kernel over what it leaves
+    gks = [k for k in ("dbscan_run_kernel", "dbscan_grid_left_kernel", "dbscan_grid_kernel") if k in kern]
+    gk = sum(kern[k] for k in gks) if gks else float("nan")
     res["dbscan_grid_eps20_minpts20"] = {
         "reps": n_reps, "windows": n_win, "ms_per_call": round(grid_ms, 4),
         "us_per_window": round(grid_ms * 1e3 / n_win, 3), "mreps_s": round(n_reps / (grid_ms * 1e-3) / 1e6, 1),
         "clusters": int(g_nc.numpy().sum()), "dup_memberships": nd_g, "status": st_g,
         "equals_chain": bool(same),
         "kernels_us": {k: round(v * 1e3, 2) for k, v in sorted(kern.items())},
-        "roofline": {"kernel": "dbscan_grid_kernel", "bound": "hbm",
+        "roofline": {"kernel": "+".join(gks), "bound": "hbm",
                      "achieved": round(n_reps * 8 / (gk * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(n_reps * 8 / (gk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "algorithmic_bytes": "4 B/rep in + 4 B/rep label out"},

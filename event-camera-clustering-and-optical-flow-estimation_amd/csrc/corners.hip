@@ -503,13 +503,18 @@ constexpr int kPrefixRound = kPrefixPer * (kThreads / 64);
 
 __global__ void __launch_bounds__(kThreads)
 sae_prefix_kernel(CornerGeom g, int64_t n_groups, const uint32_t *__restrict__ gmask, int64_t *__restrict__ gB,
-                  int64_t *__restrict__ sae, int32_t *__restrict__ err_status, int32_t *__restrict__ err_pending) {
+                  int64_t *__restrict__ sae, int32_t *__restrict__ err_status, int32_t *__restrict__ err_pending,
+                  uint32_t *__restrict__ zero0, int32_t *__restrict__ zero1) {
     // the call's sort verdict: slice_sort (all of it finished before this kernel) left it in the
     // pending word; publish it and clear the pending word for the next call.  Both words live in
     // device memory and are rewritten by every call, so a captured graph replays them correctly.
+    // A finish-only call also zeroes the counters of its later kernels here (the arc kernels'
+    // overflow count, the NMS error word), as slice_sort does in a one-call detection.
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *err_status = *err_pending;
         *err_pending = 0;
+        if (zero0) *zero0 = 0u;
+        if (zero1) *zero1 = 0;
     }
     __shared__ int64_t s_last[kThreads / 64][kPrefixPix];
     __shared__ uint8_t s_has[kThreads / 64][kPrefixPix];
@@ -1713,7 +1718,6 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         ECC_CHECK_LAUNCH(ctx, "fast_detect_prepare");
         return ECC_OK;
     }
-    if (!(phases & 1)) ECC_CHECK_HIP(ctx, hipMemsetAsync(gi.n_over, 0, 4, s), "memset(overflow count)");
     st->n_over = gi.n_over;
     st->n_items = n_items;
     st->n_slices = g.n_slices;
@@ -1723,7 +1727,8 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         const int64_t HW = (int64_t)g.W * g.H;
         const unsigned blocks = (unsigned)((HW + kPrefixPix - 1) / kPrefixPix);
         hipLaunchKernelGGL(sae_prefix_kernel, dim3(blocks), dim3(kThreads), 0, s, g, n_groups,
-                           (const uint32_t *)gi.mask, gi.B, sae, ctx->flags, ctx->flags + kSortPendingWord);
+                           (const uint32_t *)gi.mask, gi.B, sae, ctx->flags, ctx->flags + kSortPendingWord,
+                           (phases & 1) ? nullptr : gi.n_over, (phases & 1) ? nullptr : zero_nms_err);
     }
     {
         ECC_TIMED(ctx, s, "arc_kernel");
@@ -1807,9 +1812,10 @@ ECC_API int ecc_fast_detect(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
     return fast_detect_phases(ctx, xy, t, n, cfg, sae, corner_flags, nullptr, 3, stream);
 }
 
-ECC_API int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
-                                const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags, int32_t box_size,
-                                int32_t cap, ecc_corner *out, int32_t *out_count, ecc_stream_t stream) {
+// detection (phases 3: sort + tests; 2: the finish half) followed by the per-slice NMS
+static int fast_detect_nms_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                                  const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags, int32_t box_size,
+                                  int32_t cap, ecc_corner *out, int32_t *out_count, int phases, ecc_stream_t stream) {
     if (!ctx || !cfg) return ECC_ERR_INVALID;
     if (ecc::nms_check_args(n, cfg->slice_events, cfg->width, cfg->height, box_size, cap)) return ECC_ERR_INVALID;
     if (n > 0 && (!out_count || (cap > 0 && !out))) return ECC_ERR_INVALID;
@@ -1822,15 +1828,17 @@ ECC_API int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t 
         if (rc) return rc;
     }
     if (!cand) {  // the two calls
-        int rc = ecc_fast_detect(ctx, xy, t, n, cfg, sae, corner_flags, stream);
+        int rc = phases == 3 ? ecc_fast_detect(ctx, xy, t, n, cfg, sae, corner_flags, stream)
+                             : ecc_fast_detect_finish(ctx, xy, t, n, cfg, sae, corner_flags, stream);
         if (rc) return rc;
         return ecc_corner_nms(ctx, xy, corner_flags, n, cfg->slice_events, cfg->width, cfg->height, box_size, cap, out,
                               out_count, stream);
     }
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
-    // the NMS error word is zeroed by the sort kernel (n > 0 here: nms_candidates gave a buffer)
-    int rc = fast_detect_phases(ctx, xy, t, n, cfg, sae, corner_flags, nullptr, 3, stream, cand, n_cand,
+    // the NMS error word is zeroed by the call's first kernel (n > 0 here: nms_candidates gave a
+    // buffer): the sort kernel, or in a finish-only call the SAE prefix
+    int rc = fast_detect_phases(ctx, xy, t, n, cfg, sae, corner_flags, nullptr, phases, stream, cand, n_cand,
                                 ctx->flags + 1);
     if (rc) return rc;
     rc = ecc::nms_greedy(ctx, cand, n_cand, n, cfg->slice_events, cfg->width, cfg->height, box_size, cap, out,
@@ -1838,6 +1846,19 @@ ECC_API int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t 
     if (rc) return rc;
     ECC_CHECK_LAUNCH(ctx, "fast_detect_nms");
     return ECC_OK;
+}
+
+ECC_API int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                                const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags, int32_t box_size,
+                                int32_t cap, ecc_corner *out, int32_t *out_count, ecc_stream_t stream) {
+    return fast_detect_nms_phases(ctx, xy, t, n, cfg, sae, corner_flags, box_size, cap, out, out_count, 3, stream);
+}
+
+ECC_API int ecc_fast_detect_finish_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                                       const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
+                                       int32_t box_size, int32_t cap, ecc_corner *out, int32_t *out_count,
+                                       ecc_stream_t stream) {
+    return fast_detect_nms_phases(ctx, xy, t, n, cfg, sae, corner_flags, box_size, cap, out, out_count, 2, stream);
 }
 
 ECC_API int ecc_fast_detect_prepare(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,

@@ -29,6 +29,7 @@
 #include "eps_grid.hpp"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace {
 
@@ -36,6 +37,12 @@ constexpr int kThreads = 1024;
 constexpr int kMaxPts = 16384;
 constexpr int kMaxComp = 4096;
 constexpr int kFlagWord = 4;  // ctx->flags[4]: bit 1 capacity
+constexpr int kLeftWord = 11;  // ctx->flags[11]: segments dbscan_run_kernel left to dbscan_grid_kernel
+
+bool getenv_flag(const char *name) {
+    const char *v = std::getenv(name);
+    return v && v[0] && v[0] != '0';
+}
 
 __device__ __forceinline__ int uf_find(int *parent, int x) {
     int p = parent[x];
@@ -106,20 +113,21 @@ __device__ __forceinline__ void for_points_by_wave(int m, int64_t base, const in
 
 // A list entry of point j of an m-point segment.  An entry outside [0, m) (a malformed list:
 // parent[] is sized by the stride) reads as j itself, which no phase acts on (self-unions are
-// no-ops; a non-core j has no component), and sets bit 4 of the status word.
-__device__ __forceinline__ int nbr_at(const int32_t *__restrict__ nbr, int64_t e, int m, int j, int32_t *err) {
+// no-ops; a non-core j has no component), and sets the segment's LDS flag (bit 4 of the status
+// word; an LDS store on the rare path, so no register is carried through the list walks).
+__device__ __forceinline__ int nbr_at(const int32_t *__restrict__ nbr, int64_t e, int m, int j, int *bad) {
     const int q = nbr[e];
     if ((unsigned)q < (unsigned)m) return q;
-    atomicOr(err, 4);
+    *bad = 1;
     return j;
 }
 
 // Smallest component among the core neighbours of j's list, reduced over the wave (0x7fffffff: none).
 __device__ __forceinline__ int wave_first_comp(const int *parent, const int32_t *__restrict__ nbr, int64_t e0,
-                                               int64_t e1, int m, int j, int32_t *err) {
+                                               int64_t e1, int m, int j, int *bad) {
     int first = 0x7fffffff;
     for (int64_t e = e0 + (threadIdx.x & 63); e < e1; e += 64) {
-        const int c = comp_of(parent, nbr_at(nbr, e, m, j, err));
+        const int c = comp_of(parent, nbr_at(nbr, e, m, j, bad));
         if (c >= 0 && c < first) first = c;
     }
 #pragma unroll
@@ -139,7 +147,7 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
     __shared__ int c_size[kMaxComp], c_front[kMaxComp];
     __shared__ int16_t c_rank[kMaxComp];
     __shared__ int wsum[kThreads / 64];
-    __shared__ int s_kept;
+    __shared__ int s_kept, s_bad;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int64_t s = blockIdx.x; s < n_segs; s += gridDim.x) {
         const int m = seg_counts ? min(seg_counts[s], (int)stride) : (int)stride;
@@ -153,6 +161,7 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
             __syncthreads();
             continue;
         }
+        if (tid == 0) s_bad = 0;  // a list entry outside [0, m); read after the segment's last barrier
         // 1. core flags: |N_eps| >= min_pts (self included)
         for (int j = tid; j < m; j += kThreads) {
             const int64_t c = offsets[base + j + 1] - offsets[base + j];
@@ -163,7 +172,7 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         for_points_by_wave(m, base, offsets, [&](int j, int64_t e0, int64_t e1) {
             if (parent[j] == -1) return;  // non-core stays -1 during the unions: uniform
             for (int64_t e = e0 + lane; e < e1; e += 64) {
-                const int q = nbr_at(nbr, e, m, j, err);
+                const int q = nbr_at(nbr, e, m, j, &s_bad);
                 if (q > j && parent[q] != -1) uf_union(parent, j, q);
             }
         });
@@ -229,14 +238,14 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         }
         for_points_by_wave(m, base, offsets, [&](int j, int64_t e0, int64_t e1) {
             if (parent[j] != -1) return;  // core: counted above (uniform)
-            const int first = wave_first_comp(parent, nbr, e0, e1, m, j, err);
+            const int first = wave_first_comp(parent, nbr, e0, e1, m, j, &s_bad);
             if (first == 0x7fffffff) return;  // noise
             if (lane == 0) {
                 atomicAdd(&c_size[first], 1);
                 atomicMin(&c_front[first], j);
             }
             for (int64_t e = e0 + lane; e < e1; e += 64) {  // later clusters seeded by a neighbour
-                const int v = parent[nbr_at(nbr, e, m, j, err)];
+                const int v = parent[nbr_at(nbr, e, m, j, &s_bad)];
                 if (v <= -2 && -v - 2 != first) {
                     atomicAdd(&c_size[-v - 2], 1);
                     atomicMin(&c_front[-v - 2], j);
@@ -270,11 +279,11 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
         }
         for_points_by_wave(m, base, offsets, [&](int j, int64_t e0, int64_t e1) {
             if (parent[j] != -1) return;  // core: labelled above (uniform)
-            const int first = wave_first_comp(parent, nbr, e0, e1, m, j, err);
+            const int first = wave_first_comp(parent, nbr, e0, e1, m, j, &s_bad);
             if (lane == 0) labels[base + j] = first == 0x7fffffff ? -1 : c_rank[first];
             if (first == 0x7fffffff) return;
             for (int64_t e = e0 + lane; e < e1; e += 64) {
-                const int v = parent[nbr_at(nbr, e, m, j, err)];
+                const int v = parent[nbr_at(nbr, e, m, j, &s_bad)];
                 if (v <= -2 && -v - 2 != first && c_rank[-v - 2] >= 0) {
                     const unsigned long long at = atomicAdd(n_dups, 1ull);
                     if ((int64_t)at < dup_cap) {
@@ -287,6 +296,7 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
             }
         });
         __syncthreads();
+        if (tid == 0 && s_bad) atomicOr(err, 4);
     }
 }
 
@@ -325,7 +335,9 @@ __global__ void __launch_bounds__(kThreads)
 dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stride, const int32_t *__restrict__ seg_counts,
                    int e_int, uint32_t r2i, int min_pts, int min_size, int max_size, int32_t *__restrict__ labels,
                    int32_t *__restrict__ n_clusters, int64_t *__restrict__ dups, int64_t dup_cap,
-                   unsigned long long *n_dups, int32_t *err) {
+                   unsigned long long *n_dups, int32_t *err, const int32_t *__restrict__ left) {
+    // left != null: only the segments dbscan_run_kernel left (n_clusters[s] == -1)
+    if (left && *left == 0) return;  // uniform
     extern __shared__ uint32_t lds_d[];
     uint32_t *cend = lds_d;
     uint32_t *spt = cend + ecc::epsg::kCells + 1;
@@ -337,6 +349,7 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
     __shared__ int s_kept;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int64_t s = blockIdx.x; s < n_segs; s += gridDim.x) {
+        if (left && n_clusters[s] != -1) continue;  // uniform: done by the row-run kernel
         int m = seg_counts ? seg_counts[s] : (int)stride;
         m = m < 0 ? 0 : (m > (int)stride ? (int)stride : m);
         const int64_t base = s * stride;
@@ -604,6 +617,381 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
     }
 }
 
+// ---- row-run DBSCAN (distinct-pixel segments: downsample windows) -------------------------------
+// A downsample window's representatives are distinct pixels, so the segment is an occupancy
+// bitmap over its bounding box (eps.hip's row-run form): word w of row y holds 32 pixels and the
+// number of points in the words before it, so a pixel's raster rank is one word read + popc, and
+// rk2idx[rank] is its segment index.  A second bitmap marks the core points.
+//   counts:  the disk's rows as prefix differences (eps_run_counts_kernel's count, self included);
+//   unions:  the core points within eps of core point p in a row are a chord [x - w, x + w] of
+//            that row.  Consecutive core points of one row within eps of each other (gap <= e)
+//            are united left to right (a chain); a chord is at most 2e + 1 wide, so its core
+//            points lie in at most two chains — the one holding its leftmost core point and the
+//            one holding its rightmost.  Uniting p with those two (rows below p only: the pair is
+//            symmetric, and the chord of q in p's row holds p) makes p core-connected to every
+//            core point within eps, with no distance test and no candidate walk;
+//   members: a non-core point walks the core bits of its disk's chords (fewer than min_pts);
+// the rest (component ids in seed order, sizes, output order, labels, duplicate memberships) is
+// dbscan_grid_kernel's closed form.  Segments that repeat a pixel, whose bitmap exceeds kDrWords,
+// or with eps >= kDrHw are marked (n_clusters[s] = -1, counted in *left) for dbscan_grid_kernel.
+constexpr int kDrWords = 4864;  // (bits, prefix) pairs: 346x260 needs 2860
+constexpr int kDrHw = 512;      // disk half-width table: eps < 512
+constexpr int kDrPer = kGridMaxPts / kThreads;
+
+__global__ void __launch_bounds__(kThreads)
+dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stride, const int32_t *__restrict__ seg_counts,
+                  int e_int, uint32_t r2i, int min_pts, int min_size, int max_size, int32_t *__restrict__ labels,
+                  int32_t *__restrict__ n_clusters, int64_t *__restrict__ dups, int64_t dup_cap,
+                  unsigned long long *n_dups, int32_t *err, int32_t *left) {
+    __shared__ uint2 wd[kDrWords + 1];     // occupancy bits | points before the word; [kDrWords] = 0
+    __shared__ uint32_t cw[kDrWords + 1];  // core bits
+    __shared__ uint16_t rk2idx[kGridMaxPts];
+    __shared__ int parent[kGridMaxPts];
+    __shared__ int c_size[kMaxComp], c_front[kMaxComp];
+    __shared__ int16_t c_rank[kMaxComp];
+    __shared__ uint16_t hwt[kDrHw];
+    __shared__ int box[kThreads / 64][4];
+    __shared__ int wsum[kThreads / 64];
+    __shared__ int s_dup, s_kept;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kW = kThreads / 64;
+    if (tid == 0) {
+        wd[kDrWords] = make_uint2(0u, 0u);
+        cw[kDrWords] = 0u;
+    }
+    for (int a = tid; a < kDrHw && a <= e_int; a += kThreads) {  // exact integer square roots
+        const uint32_t v = r2i - (uint32_t)(a * a);
+        uint32_t h = (uint32_t)sqrtf((float)v);
+        while (h * h > v) --h;
+        while ((h + 1) * (h + 1) <= v) ++h;
+        hwt[a] = (uint16_t)h;
+    }
+    for (int64_t s = blockIdx.x; s < n_segs; s += gridDim.x) {
+        int m = seg_counts ? seg_counts[s] : (int)stride;
+        m = m < 0 ? 0 : (m > (int)stride ? (int)stride : m);
+        const int64_t base = s * stride;
+#if ECC_DBSCAN_PROFILE
+        unsigned long long db_t_ = wall_clock64();
+#endif
+        // points: lane tid holds j = u * kThreads + tid
+        uint32_t v[kDrPer];
+        int xmn = 0x7fffffff, ymn = 0x7fffffff, xmx = -1, ymx = -1;
+#pragma unroll
+        for (int u = 0; u < kDrPer; ++u) {
+            const int j = u * kThreads + tid;
+            v[u] = j < m ? xy[base + j] : 0u;
+            if (j < m) {
+                xmn = min(xmn, ecc::xy_x(v[u])); ymn = min(ymn, ecc::xy_y(v[u]));
+                xmx = max(xmx, ecc::xy_x(v[u])); ymx = max(ymx, ecc::xy_y(v[u]));
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            xmn = min(xmn, __shfl_xor(xmn, o)); ymn = min(ymn, __shfl_xor(ymn, o));
+            xmx = max(xmx, __shfl_xor(xmx, o)); ymx = max(ymx, __shfl_xor(ymx, o));
+        }
+        if (lane == 0) {
+            box[wave][0] = xmn; box[wave][1] = ymn;
+            box[wave][2] = xmx; box[wave][3] = ymx;
+        }
+        if (tid == 0) s_dup = 0;
+        __syncthreads();
+        xmn = box[0][0]; ymn = box[0][1]; xmx = box[0][2]; ymx = box[0][3];
+#pragma unroll
+        for (int w = 1; w < kW; ++w) {
+            xmn = min(xmn, box[w][0]); ymn = min(ymn, box[w][1]);
+            xmx = max(xmx, box[w][2]); ymx = max(ymx, box[w][3]);
+        }
+        const int Wb = m ? xmx - xmn + 1 : 1, H = m ? ymx - ymn + 1 : 1;
+        const int WW = (Wb >> 5) + 1;
+        const int64_t words64 = (int64_t)H * WW;
+        bool leftover = words64 > kDrWords || e_int >= kDrHw;  // uniform
+        const int words = leftover ? 0 : (int)words64;
+        for (int w = tid; w < words; w += kThreads) {
+            wd[w] = make_uint2(0u, 0u);
+            cw[w] = 0u;
+        }
+        __syncthreads();
+        if (!leftover) {
+#pragma unroll
+            for (int u = 0; u < kDrPer; ++u) {
+                if (u * kThreads + tid >= m) break;
+                const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
+                const uint32_t bit = 1u << (x & 31);
+                if (atomicOr(&wd[y * WW + (x >> 5)].x, bit) & bit) s_dup = 1;
+            }
+        }
+        __syncthreads();
+        leftover = leftover || s_dup;  // uniform
+        if (leftover) {
+            if (tid == 0 && m > 0) {
+                n_clusters[s] = -1;
+                atomicAdd(left, 1);
+            }
+            __syncthreads();
+            continue;
+        }
+        {  // points before each word (thread t: words [t * per, t * per + per))
+            const int per = (words + kThreads - 1) / kThreads;
+            const int w0 = tid * per, w1 = min(w0 + per, words);
+            int loc = 0;
+            for (int w = w0; w < w1; ++w) loc += __popc(wd[w].x);
+            const int inc = ecc::wave_incl_scan(loc);
+            if (lane == 63) wsum[wave] = inc;
+            __syncthreads();
+            int off = inc - loc;
+            for (int w = 0; w < wave; ++w) off += wsum[w];
+            for (int w = w0; w < w1; ++w) {
+                wd[w].y = (uint32_t)off;
+                off += __popc(wd[w].x);
+            }
+        }
+        __syncthreads();
+        // raster rank of the pixel at (x, y) of the box (a set bit)
+        auto rank_at = [&](int x, int y) -> int {
+            const uint2 q = wd[y * WW + (x >> 5)];
+            return (int)q.y + __popc(q.x & ((1u << (x & 31)) - 1u));
+        };
+        const int amax = min(e_int, H - 1);
+        // counts -> core flags and bits; rank -> index
+#pragma unroll
+        for (int u = 0; u < kDrPer; ++u) {
+            const int j = u * kThreads + tid;
+            if (j >= m) break;
+            const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
+            rk2idx[rank_at(x, y)] = (uint16_t)j;
+            int cnt = 0;
+            for (int a = 0; a <= amax; ++a) {
+                const int hw = hwt[a];
+                const int xl = max(x - hw, 0), xh = min(x + hw + 1, Wb);
+                const uint32_t ml = (1u << (xl & 31)) - 1u, mh = (1u << (xh & 31)) - 1u;
+                const int cl = xl >> 5, ch = xh >> 5;
+#pragma unroll
+                for (int sgn = 0; sgn < 2; ++sgn) {
+                    if (sgn && a == 0) break;
+                    const int yy = sgn ? y - a : y + a;
+                    const bool ok = (unsigned)yy < (unsigned)H;
+                    const int rb = yy * WW;
+                    const uint2 lo = wd[ok ? rb + cl : kDrWords], hi = wd[ok ? rb + ch : kDrWords];
+                    cnt += (int)(hi.y - lo.y) + __popc(hi.x & mh) - __popc(lo.x & ml);
+                }
+            }
+            const bool core = cnt >= min_pts;
+            parent[j] = core ? j : -1;
+            if (core) atomicOr(&cw[y * WW + (x >> 5)], 1u << (x & 31));
+        }
+        __syncthreads();
+        DB_MARK(0);  // bitmap + counts
+        // lowest / highest core bit of row yy in columns [lo, hi] (-1: none)
+        auto first_core = [&](int rb, int lo, int hi) -> int {
+            for (int w = lo >> 5; w <= (hi >> 5); ++w) {
+                uint32_t b = cw[rb + w];
+                if (w == (lo >> 5)) b &= ~((1u << (lo & 31)) - 1u);
+                if (w == (hi >> 5)) b &= (hi & 31) == 31 ? 0xffffffffu : ((2u << (hi & 31)) - 1u);
+                if (b) return (w << 5) + __ffs(b) - 1;
+            }
+            return -1;
+        };
+        auto last_core = [&](int rb, int lo, int hi) -> int {
+            for (int w = hi >> 5; w >= (lo >> 5); --w) {
+                uint32_t b = cw[rb + w];
+                if (w == (lo >> 5)) b &= ~((1u << (lo & 31)) - 1u);
+                if (w == (hi >> 5)) b &= (hi & 31) == 31 ? 0xffffffffu : ((2u << (hi & 31)) - 1u);
+                if (b) return (w << 5) + 31 - __clz(b);
+            }
+            return -1;
+        };
+        // unions: the row chain link to the right, then the two chains of every chord below
+#pragma unroll
+        for (int u = 0; u < kDrPer; ++u) {
+            const int j = u * kThreads + tid;
+            if (j >= m) break;
+            if (parent[j] == -1) continue;
+            const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
+            if (x + 1 < Wb && e_int > 0) {
+                const int c = first_core(y * WW, x + 1, min(x + e_int, Wb - 1));
+                if (c >= 0) uf_union(parent, j, rk2idx[rank_at(c, y)]);
+            }
+            for (int a = 1; a <= amax && y + a < H; ++a) {
+                const int hw = hwt[a];
+                const int lo = max(x - hw, 0), hi = min(x + hw, Wb - 1);
+                const int rb = (y + a) * WW;
+                const int cl = first_core(rb, lo, hi);
+                if (cl < 0) continue;
+                uf_union(parent, j, rk2idx[rank_at(cl, y + a)]);
+                const int cr = last_core(rb, cl, hi);
+                if (cr > cl) uf_union(parent, j, rk2idx[rank_at(cr, y + a)]);
+            }
+        }
+        __syncthreads();
+        DB_MARK(1);  // unions
+        // compress; roots -> component ids in ascending root (= seed) order
+        int roots[kGridPer], nr = 0;
+        const int j0 = tid * kGridPer;
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u) {
+            const int j = j0 + u;
+            roots[u] = 0;
+            if (j < m && parent[j] != -1) {
+                const int r = uf_find(parent, j);
+                roots[u] = r == j;
+                nr += roots[u];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u) {
+            const int j = j0 + u;
+            if (j < m && parent[j] != -1 && !roots[u]) parent[j] = uf_root(parent, j);
+        }
+        int xs = nr;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(xs, d);
+            if (lane >= d) xs += o;
+        }
+        if (lane == 63) wsum[wave] = xs;
+        __syncthreads();
+        int pre = 0, nc = 0;
+        for (int w = 0; w < kW; ++w) {
+            if (w < wave) pre += wsum[w];
+            nc += wsum[w];
+        }
+        int cid = pre + xs - nr;
+        if (nc <= kMaxComp) {
+#pragma unroll
+            for (int u = 0; u < kGridPer; ++u)
+                if (roots[u]) parent[j0 + u] = -(cid++) - 2;
+        }
+        __syncthreads();
+        if (nc > kMaxComp) {  // too many components for the LDS tables
+            if (tid == 0) {
+                atomicOr(err, 2);
+                n_clusters[s] = 0;
+            }
+            for (int j = tid; j < m; j += kThreads) labels[base + j] = -1;
+            __syncthreads();
+            continue;
+        }
+        for (int c = tid; c < nc; c += kThreads) {
+            c_size[c] = 0;
+            c_front[c] = 0x7fffffff;
+        }
+        __syncthreads();
+        DB_MARK(2);  // compress + ids
+        // the core neighbours of a non-core point: f(q) for the index q of every core bit of the
+        // chords of its disk (all rows: the relation is walked from the non-core side only)
+        auto for_core_nbrs = [&](int x, int y, auto &&f) {
+            for (int a = -amax; a <= amax; ++a) {
+                const int yy = y + a;
+                if ((unsigned)yy >= (unsigned)H) continue;
+                const int hw = hwt[a < 0 ? -a : a];
+                const int lo = max(x - hw, 0), hi = min(x + hw, Wb - 1);
+                const int rb = yy * WW;
+                for (int w = lo >> 5; w <= (hi >> 5); ++w) {
+                    uint32_t b = cw[rb + w];
+                    if (w == (lo >> 5)) b &= ~((1u << (lo & 31)) - 1u);
+                    if (w == (hi >> 5)) b &= (hi & 31) == 31 ? 0xffffffffu : ((2u << (hi & 31)) - 1u);
+                    const uint2 q = wd[rb + w];
+                    while (b) {
+                        const int bit = __ffs(b) - 1;
+                        b &= b - 1u;
+                        f((int)rk2idx[q.y + __popc(q.x & ((1u << bit) - 1u))]);
+                    }
+                }
+            }
+        };
+        // memberships -> sizes and first members (first claim + later seeds, as the grid kernel)
+        int claim[kDrPer];
+        uint32_t more = 0u;
+#pragma unroll
+        for (int u = 0; u < kDrPer; ++u) {
+            const int j = u * kThreads + tid;
+            claim[u] = -1;
+            if (j >= m) continue;
+            const int cj = comp_of(parent, j);
+            if (cj >= 0) {
+                claim[u] = cj;
+                atomicAdd(&c_size[cj], 1);
+                atomicMin(&c_front[cj], j);
+                continue;
+            }
+            const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
+            int first = 0x7fffffff, n_seed = 0, seed_c = -1;
+            for_core_nbrs(x, y, [&](int q) {
+                const int pv = parent[q];
+                const int c = pv <= -2 ? -pv - 2 : -parent[pv] - 2;
+                first = c < first ? c : first;
+                n_seed += pv <= -2 ? 1 : 0;
+                seed_c = pv <= -2 ? c : seed_c;
+            });
+            if (first == 0x7fffffff) continue;  // noise
+            claim[u] = first;
+            atomicAdd(&c_size[first], 1);
+            atomicMin(&c_front[first], j);
+            if (n_seed == 0 || (n_seed == 1 && seed_c == first)) continue;
+            more |= 1u << u;
+            for_core_nbrs(x, y, [&](int q) {  // later clusters seeded by a neighbour
+                const int pv = parent[q];
+                if (pv <= -2 && -pv - 2 != first) {
+                    atomicAdd(&c_size[-pv - 2], 1);
+                    atomicMin(&c_front[-pv - 2], j);
+                }
+            });
+        }
+        __syncthreads();
+        DB_MARK(3);  // memberships
+        // output order: kept clusters by (size desc, front asc, creation asc)
+        if (tid == 0) s_kept = 0;
+        __syncthreads();
+        for (int c = tid; c < nc; c += kThreads) {
+            const int sz = c_size[c], fr = c_front[c];
+            int r = -1;
+            if (sz >= min_size && sz <= max_size) {
+                r = 0;
+                for (int o = 0; o < nc; ++o) {
+                    const int so = c_size[o];
+                    if (so < min_size || so > max_size) continue;
+                    r += so > sz || (so == sz && (c_front[o] < fr || (c_front[o] == fr && o < c)));
+                }
+                atomicAdd(&s_kept, 1);
+            }
+            c_rank[c] = (int16_t)r;
+        }
+        __syncthreads();
+        if (tid == 0) n_clusters[s] = s_kept;
+        DB_MARK(4);  // ranks
+        // labels (first claim, coalesced: lane tid holds j = u * kThreads + tid) and the further
+        // memberships
+#pragma unroll
+        for (int u = 0; u < kDrPer; ++u) {
+            const int j = u * kThreads + tid;
+            if (j >= m) break;
+            labels[base + j] = claim[u] >= 0 ? c_rank[claim[u]] : -1;
+            if (!((more >> u) & 1u)) continue;
+            const int first = claim[u];
+            const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
+            for_core_nbrs(x, y, [&](int q) {
+                const int pv = parent[q];
+                if (pv <= -2 && -pv - 2 != first && c_rank[-pv - 2] >= 0) {
+                    const unsigned long long at = atomicAdd(n_dups, 1ull);
+                    if ((int64_t)at < dup_cap) {
+                        dups[2 * at] = base + j;
+                        dups[2 * at + 1] = c_rank[-pv - 2];
+                    } else {
+                        atomicOr(err, 2);
+                    }
+                }
+            });
+        }
+        __syncthreads();
+        DB_MARK(5);  // labels + dups
+#if ECC_DBSCAN_PROFILE
+        if (tid == 0) atomicAdd(&g_db_prof[7], 1ull);
+#endif
+    }
+}
+
 }  // namespace
 
 ECC_API int ecc_dbscan_extract(ecc_ctx *ctx, int64_t n_segs, int64_t seg_stride, const int32_t *seg_counts,
@@ -655,11 +1043,26 @@ ECC_API int ecc_dbscan_grid(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, in
     ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(dbscan_grid_kernel),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                   "dbscan_grid lds");
-    const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 2048);
-    ECC_TIMED(ctx, s, "dbscan_grid_kernel");
-    hipLaunchKernelGGL(dbscan_grid_kernel, dim3(grid), dim3(kThreads), lds, s, xy, n_segs, seg_stride, seg_counts,
-                       e_int, (uint32_t)r2i, min_pts, min_cluster_size, max_cluster_size, labels, n_clusters, dups,
-                       dup_cap, reinterpret_cast<unsigned long long *>(n_dups), err);
+    // the row-run kernel first (distinct-pixel segments whose bitmap fits its LDS); the grid kernel
+    // takes what it leaves, and exits at once when it leaves nothing
+    const bool run = e_int < kDrHw && !getenv_flag("ECC_DBSCAN_GRID_ONLY");
+    int32_t *left = ctx->flags + kLeftWord;
+    if (run) {
+        ECC_CHECK_HIP(ctx, hipMemsetAsync(left, 0, 4, s), "memset(dbscan leftovers)");
+        ECC_TIMED(ctx, s, "dbscan_run_kernel");
+        const unsigned grid = (unsigned)std::min<int64_t>(n_segs, 1 << 20);
+        hipLaunchKernelGGL(dbscan_run_kernel, dim3(grid), dim3(kThreads), 0, s, xy, n_segs, seg_stride, seg_counts,
+                           e_int, (uint32_t)r2i, min_pts, min_cluster_size, max_cluster_size, labels, n_clusters, dups,
+                           dup_cap, reinterpret_cast<unsigned long long *>(n_dups), err, left);
+    }
+    const unsigned grid = (unsigned)std::min<int64_t>(n_segs, run ? (int64_t)ctx->n_cu : 2048);
+    {
+        ECC_TIMED(ctx, s, run ? "dbscan_grid_left_kernel" : "dbscan_grid_kernel");
+        hipLaunchKernelGGL(dbscan_grid_kernel, dim3(grid), dim3(kThreads), lds, s, xy, n_segs, seg_stride, seg_counts,
+                           e_int, (uint32_t)r2i, min_pts, min_cluster_size, max_cluster_size, labels, n_clusters, dups,
+                           dup_cap, reinterpret_cast<unsigned long long *>(n_dups), err,
+                           run ? (const int32_t *)left : nullptr);
+    }
     ECC_CHECK_LAUNCH(ctx, "dbscan_grid");
     return ECC_OK;
 }

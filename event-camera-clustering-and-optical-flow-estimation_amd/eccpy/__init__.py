@@ -149,6 +149,7 @@ _sigs = {
     "ecc_fast_detect_nms": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, i32, i32, P, P, P]),
     "ecc_fast_detect_prepare": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P]),
     "ecc_fast_detect_finish": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, P]),
+    "ecc_fast_detect_finish_nms": (C.c_int, [P, P, P, i64, C.POINTER(CornerCfg), P, P, i32, i32, P, P, P]),
     "ecc_fast_detect_status": (C.c_int, [P, P]),
     "ecc_fast_detect_stats": (C.c_int, [P, P, i32, P]),
     "ecc_sae_scatter": (C.c_int, [P, P, P, i64, i32, i32, P, P]),

@@ -7,6 +7,7 @@
 //   * merge_clusters_ returns before the emptied clusters are erased (AEClustering.cpp:107-110);
 //   * kappa = 0 (the default) makes the sampled distance DBL_MAX, so it never assigns (Q19);
 //   * forget() on an empty cluster is guarded (the reference reads datT_[0] first, Q18).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
@@ -61,21 +62,17 @@ double MyCluster::manhattanDistance(const Vec2d &x) const {
 }
 
 double MyCluster::manhattanDistanceWithSampling(const Vec2d &x) const {
-    double ma = std::numeric_limits<double>::max();
+    // nearest member by truncating Manhattan distance: all members while the cluster holds fewer
+    // than kappa, else kappa members drawn with std::rand() (MyCluster.cpp:72-99; kappa 0 by
+    // default, so the draw never happens and the result is DBL_MAX, Q19)
+    auto l1 = [&x](const Vec2d &y) -> double { return iabs_trunc(x[0] - y[0]) + iabs_trunc(x[1] - y[1]); };
+    double nearest = std::numeric_limits<double>::max();
     if (kappa_ > n_) {
-        for (const auto &y : dat_) {
-            const double foo = iabs_trunc(x[0] - y[0]) + iabs_trunc(x[1] - y[1]);
-            if (foo < ma) ma = foo;
-        }
-    } else {
-        for (int ii = 0; ii < kappa_; ++ii) {
-            const int idx = std::rand() % (int)dat_.size();
-            const Vec2d &y = dat_[idx];
-            const double foo = iabs_trunc(x[0] - y[0]) + iabs_trunc(x[1] - y[1]);
-            if (foo < ma) ma = foo;
-        }
+        for (const auto &y : dat_) nearest = std::min(nearest, l1(y));
+        return nearest;
     }
-    return ma;
+    for (int draw = 0; draw < kappa_; ++draw) nearest = std::min(nearest, l1(dat_[std::rand() % (int)dat_.size()]));
+    return nearest;
 }
 
 Vec2d MyCluster::getClusterCentroid() const {

@@ -311,6 +311,14 @@ int ecc_corner_nms_status(ecc_ctx *ctx, ecc_stream_t stream);
 int ecc_fast_detect_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
                         const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags, int32_t box_size,
                         int32_t cap, ecc_corner *out, int32_t *out_count, ecc_stream_t stream);
+/* The finish half of ecc_fast_detect_nms after ecc_fast_detect_prepare on the same context:
+ * prepare + finish_nms == ecc_fast_detect_nms.  Time-window shards of one stream (several
+ * GPUs, or several contexts and streams on one GPU) each prepare their shard, take their
+ * initial SAE as the ecc_sae_max_combine of the lower shards' local_last images, and finish. */
+int ecc_fast_detect_finish_nms(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
+                               const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
+                               int32_t box_size, int32_t cap, ecc_corner *out, int32_t *out_count,
+                               ecc_stream_t stream);
 /* Dense form of ecc_corner_nms' per-slice lists (multi-GPU corner gather): with
  * counts[s] <= cap as ecc_corner_nms writes them, offsets[0..n_slices] (DEVICE int64) = the
  * exclusive scan of counts (offsets[n_slices] = total) and out[offsets[s] + d] = in[s*cap + d]. */

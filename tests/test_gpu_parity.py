@@ -1338,6 +1338,65 @@ def test_dbscan_extract_border_duplicates(ecc, orc, gpu, fused):
     assert n_dup > 0  # the case really exercises duplicate memberships
 
 
+@pytest.mark.parametrize("eps,min_pts", [(1.0, 2), (1.5, 3), (2.0, 4), (3.7, 6), (6.0, 12), (12.5, 30), (40.0, 50)])
+@pytest.mark.parametrize("path", ["run", "grid_only"])
+def test_dbscan_grid_distinct_pixel_segments(ecc, orc, gpu, monkeypatch, eps, min_pts, path):
+    """Segments of DISTINCT pixels (the downsample windows' case: ecc_dbscan_grid's row-run kernel)
+    mixed with segments that repeat a pixel (left to the cell-grid kernel) in one call: dense
+    random patches with holes (chains broken inside chords, border points reached by several
+    seeds), sparse scatter, a full square, a single row and column, one and zero points — against
+    the oracle's literal seed queue.  `grid_only` forces the cell-grid kernel for every segment."""
+    if path == "grid_only":
+        monkeypatch.setenv("ECC_DBSCAN_GRID_ONLY", "1")
+    rng = np.random.default_rng(int(eps * 10) + min_pts)
+    stride = 2048
+    segs = []
+    for k in range(40):
+        kind = k % 8
+        if kind == 0:    # dense patch with holes
+            side = int(rng.integers(20, 60))
+            cells = rng.choice(side * side, int(side * side * rng.uniform(0.2, 0.7)), replace=False)
+            pts = np.stack([cells % side, cells // side], 1) + rng.integers(0, 200, 2)
+        elif kind == 1:  # sparse scatter over a large box
+            cells = rng.choice(300 * 250, int(rng.integers(50, 2000)), replace=False)
+            pts = np.stack([cells % 300, cells // 300], 1)
+        elif kind == 2:  # a full square
+            side = int(rng.integers(3, 40))
+            g = np.arange(side * side)
+            pts = np.stack([g % side, g // side], 1) + 5
+        elif kind == 3:  # one row and one column with gaps
+            xs = np.unique(rng.integers(0, 340, 300))
+            pts = np.concatenate([np.stack([xs, np.full_like(xs, 7)], 1), np.stack([np.full_like(xs[:200], 11), xs[:200] % 250], 1)])
+            pts = np.unique(pts, axis=0)
+        elif kind == 4:  # repeats a pixel: the cell-grid kernel's segment
+            pts = rng.integers(0, 30, (int(rng.integers(10, 800)), 2))
+        elif kind == 5:
+            pts = rng.integers(0, 346, (1, 2))
+        elif kind == 6:
+            pts = np.zeros((0, 2), np.int64)
+        else:            # clustered blobs of distinct pixels
+            c = rng.integers(20, 300, (6, 2))
+            raw = (c[rng.integers(0, 6, 3000)] + rng.normal(0, eps * 1.5, (3000, 2))).round().astype(np.int64)
+            raw = np.clip(raw, 0, 345)
+            pts = np.unique(raw, axis=0)
+            pts = pts[rng.permutation(len(pts))]
+        pts = pts[:stride]
+        if kind not in (4,):
+            pts = pts[rng.permutation(len(pts))]
+        segs.append(pts.astype(np.int64))
+    counts = np.array([len(p) for p in segs], np.int32)
+    xy = np.zeros(len(segs) * stride, np.uint32)
+    for s, p in enumerate(segs):
+        if len(p):
+            xy[s * stride: s * stride + len(p)] = ecc.pack_xy(p[:, 0], p[:, 1])
+    got = _dbscan_gpu(ecc, gpu, xy, len(segs), stride, counts, eps, min_pts, 1, 1 << 30, True)
+    for s, p in enumerate(segs):
+        ref = orc.dbscan_lists(p.reshape(-1, 2), eps, min_pts) if len(p) else []
+        assert len(got[s]) == len(ref), (s, len(got[s]), len(ref))
+        for a, b in zip(got[s], ref):
+            assert np.array_equal(a, b), s
+
+
 def test_dbscan_extract_rejects_short_lists(ecc, gpu):
     """offsets that run past nbr_len: the segment is rejected (status CAPACITY), never read."""
     n = 64
@@ -1428,6 +1487,70 @@ def test_graph_replay_matches_eager(ecc, orc, gpu):
     for e, a, windowed in zip(eager, (rep_xy, d_c, labels, sae, flags, nms_cnt), (1, 0, 1, 0, 0, 0)):
         got = a.numpy()
         assert (got[valid] == e[valid]).all() if windowed else (got == e).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [2, 3, 5])
+def test_corner_shards_in_one_device_equal_one_call(ecc, orc, gpu, parts):
+    """Time-window shards on separate contexts and streams of ONE device (bench.py
+    --corner-shards): prepare each shard, start shard p from ecc_sae_max_combine of the lower
+    shards' own last images, ecc_fast_detect_finish_nms — flags, final SAE and NMS lists equal the
+    one-call ecc_fast_detect_nms and the oracle (Q15 only on the first shard)."""
+    W, H = 346, 260
+    ns = 67  # slices; uneven cuts, shards of different group alignment
+    n = ns * 16384
+    xy, t, _ = ecc.gen_events(n, seed=17, width=W, height=H)
+    d_xy, d_t = dev(ecc, xy), dev(ecc, t)
+    cap, HW = 2048, W * H
+    flags, sae = ecc.DeviceArray(n, np.uint8), ecc.DeviceArray(HW, np.int64)
+    out, cnt = ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE), ecc.DeviceArray(ns, np.int32)
+    sae.fill_bytes(0, gpu.stream)
+    gpu.fast_detect_nms(d_xy, d_t, n, ecc.corner_cfg(width=W, height=H), sae, flags, 15, cap, out, cnt)
+    gpu.sync()
+    ref = [a.numpy() for a in (flags, sae, out, cnt)]
+    o_flags, o_sae = orc.fast_detect(xy, t, W, H)
+    assert (ref[0] == o_flags).all() and (ref[1] == o_sae).all()
+    lib = ecc.lib
+    cuts = [round(p * ns / parts) * 16384 for p in range(parts + 1)]
+    ctxs = [gpu] + [ecc.Context(0) for _ in range(parts - 1)]
+    last = ecc.DeviceArray(parts * HW, np.int64)
+    saes = [ecc.DeviceArray(HW, np.int64) for _ in range(parts)]
+    f2, o2, c2 = ecc.DeviceArray(n, np.uint8), ecc.DeviceArray(ns * cap, ecc.CORNER_DTYPE), ecc.DeviceArray(ns, np.int32)
+    f2.fill_bytes(0xA5, gpu.stream)
+    cfgs = [ecc.corner_cfg(width=W, height=H, first_detect_slice=1 if p == 0 else 0) for p in range(parts)]
+    evs = []
+    for p in range(parts):
+        e = ecc.P()
+        ecc.check(lib.ecc_event_create(ecc.C.byref(e)))
+        evs.append(e)
+    gpu.sync()
+    for p, cx in enumerate(ctxs):
+        lo, m = cuts[p], cuts[p + 1] - cuts[p]
+        ecc.check(lib.ecc_fast_detect_prepare(cx.ctx, d_xy.ptr + 4 * lo, d_t.ptr + 8 * lo, m, ecc.C.byref(cfgs[p]),
+                                              last.ptr + 8 * p * HW, cx.stream))
+        ecc.check(lib.ecc_event_record(evs[p], cx.stream))
+    for p, cx in enumerate(ctxs):
+        lo, m = cuts[p], cuts[p + 1] - cuts[p]
+        for q in range(p):
+            ecc.check(lib.ecc_stream_wait_event(cx.stream, evs[q]))
+        ecc.check(lib.ecc_sae_max_combine(cx.ctx, last.ptr, p, HW, saes[p].ptr, cx.stream))
+        s0 = lo // 16384
+        ecc.check(lib.ecc_fast_detect_finish_nms(cx.ctx, d_xy.ptr + 4 * lo, d_t.ptr + 8 * lo, m, ecc.C.byref(cfgs[p]),
+                                                 saes[p].ptr, f2.ptr + lo, 15, cap,
+                                                 o2.ptr + s0 * cap * ecc.CORNER_DTYPE.itemsize, c2.ptr + 4 * s0,
+                                                 cx.stream))
+    for cx in ctxs:
+        cx.sync()
+        assert cx.fast_detect_status() == 0 and cx.corner_nms_status() == 0
+    assert (f2.numpy() == ref[0]).all()
+    assert (saes[-1].numpy() == ref[1]).all()
+    c = c2.numpy()
+    assert (c == ref[3]).all()
+    got, want = o2.numpy(), ref[2]
+    for s in range(ns):
+        assert (got[s * cap: s * cap + c[s]] == want[s * cap: s * cap + c[s]]).all(), s
+    for cx in ctxs[1:]:
+        cx.close()
 
 
 @pytest.mark.gpu
