@@ -149,12 +149,7 @@ __device__ __forceinline__ void block_excl_scan_inplace(int32_t *a, int n, int32
     const int b0 = min(n, tid * per), b1 = min(n, b0 + per);
     int sum = 0;
     for (int i = b0; i < b1; ++i) sum += a[i];
-    int incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
+    const int incl = ecc::wave_incl_scan(sum);  // DPP
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     int run = incl - sum;
@@ -227,8 +222,7 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
         }
     }
     if (__any(bad) && lane == 0 && !g.any_order) *err = 1;  // pending: published by sae_prefix_kernel
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) fb = min(fb, __shfl_xor(fb, o));
+    fb = ecc::wave_min_i32(fb);  // DPP
     if (lane == 0) wsum[tid >> 6] = fb;
     __syncthreads();
     if (tid == 0) {
@@ -294,14 +288,8 @@ __device__ __forceinline__ void tile_segs(const CornerGeom &g, const Sorted &so,
         a = row[tile];
         len = row[tile + 1] - a;
     }
-    int incl = len;
-    int64_t asum = a;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o);
-        if (tid >= o) incl += v;
-        asum += __shfl_xor(asum, o);
-    }
+    const int incl = ecc::wave_incl_scan(len);         // DPP (wave 0: all 64 lanes)
+    const int64_t asum = ecc::wave_sum_i64((int64_t)a);
     if (tid < kGroup) {
         T.start[tid] = s * g.S + a;
         T.pref[tid + 1] = incl;
@@ -457,12 +445,7 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
     // the pixel's 32 table words instead cost 32 LDS reads per pixel lane: 107 -> 100 us)
     const uint32_t m = tid < kTilePix ? pmask[lp] : 0u;
     const int cnt = __popc(m);
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
+    const int incl = ecc::wave_incl_scan(cnt);  // DPP (all lanes active)
     if (lane == 63) wtot[wave] = incl;
     __syncthreads();
     int off = incl - cnt;
@@ -866,20 +849,17 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         L.q4n = 0;
         L.n_exact = 0;
     }
-    if (tid < kMaxSeg) {
-        int64_t b0;
-        int len;
-        window_segment(g, grp, tile, tid, item_base, sub_end, b0, len);
-        int incl = len;  // prefix over lanes 0..12 of wave 0
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            const int v = __shfl_up(incl, o, 16);
-            if (tid >= o) incl += v;
+    if (wave == 0) {  // the segment table: lanes 0..12 of wave 0, prefix by DPP over the wave
+        int64_t b0 = 0;
+        int len = 0;
+        if (tid < kMaxSeg) window_segment(g, grp, tile, tid, item_base, sub_end, b0, len);
+        const int incl = ecc::wave_incl_scan(len);
+        if (tid < kMaxSeg) {
+            L.seg_lo[tid] = b0;
+            L.seg_pref[tid + 1] = incl;
+            L.seg_off[tid] = window_segment_offset(tid);
+            if (tid == 0) L.seg_pref[0] = 0;
         }
-        L.seg_lo[tid] = b0;
-        L.seg_pref[tid + 1] = incl;
-        L.seg_off[tid] = window_segment_offset(tid);
-        if (tid == 0) L.seg_pref[0] = 0;
     }
     __syncthreads();
     DENSE_MARK(0);  // (a) segment table + B_g window
@@ -922,12 +902,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
                 L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)(j * kTilePix + lp);
         }
     }
-    int64_t bmin = bq;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int64_t x = __shfl_xor(bmin, o);
-        bmin = x < bmin ? x : bmin;
-    }
+    const int64_t bmin = ecc::wave_min_i64(bq);  // DPP
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
     DENSE_MARK(1);  // (b) staging
@@ -1150,32 +1125,21 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         L.q4n = 0;
         L.redo = 0;
     }
-    if (tid < kMaxSeg) {
-        int incl = pre.len;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            const int v = __shfl_up(incl, o, 16);
-            if (tid >= o) incl += v;
+    if (wave == 0) {  // segment table: lanes 0..12 (pre.len is 0 above), prefix by DPP
+        const int incl = ecc::wave_incl_scan(pre.len);
+        if (tid < kMaxSeg) {
+            L.seg_lo[tid] = pre.b0;
+            L.seg_pref[tid + 1] = incl;
+            L.seg_off[tid] = window_segment_offset(tid);
+            if (tid == 0) L.seg_pref[0] = 0;
         }
-        L.seg_lo[tid] = pre.b0;
-        L.seg_pref[tid + 1] = incl;
-        L.seg_off[tid] = window_segment_offset(tid);
-        if (tid == 0) L.seg_pref[0] = 0;
     }
     const int cnt = win_lane ? __popc(mk_w) + 1 : 0;  // the pixel's values + its B_g slot
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
+    // wave scan of the counts and wave minimum of B_g by DPP moves (the lane-shuffle forms were
+    // 18 LDS permutes per wave, a fifth of the kernel's LDS instructions)
+    const int incl = ecc::wave_incl_scan(cnt);
     if (lane == 63) L.wave_tot[wave] = incl;
-    int64_t bmin = bq;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int64_t x = __shfl_xor(bmin, o);
-        bmin = x < bmin ? x : bmin;
-    }
+    const int64_t bmin = ecc::wave_min_i64(bq);
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();  // 1
     ARC_MARK(0);  // A

@@ -106,7 +106,7 @@ __device__ __forceinline__ void for_points_by_wave(int m, int64_t base, const in
         for (int tt = 0; tt < 64; ++tt) {
             const int j = wave + kW * (t0 + tt);
             if (j >= m) break;  // wave-uniform
-            body(j, (int64_t)__shfl(pe0, tt), (int64_t)__shfl(pe1, tt));
+            body(j, ecc::lane_value64(pe0, tt), ecc::lane_value64(pe1, tt));  // readlane: tt is uniform
         }
     }
 }
@@ -130,9 +130,7 @@ __device__ __forceinline__ int wave_first_comp(const int *parent, const int32_t 
         const int c = comp_of(parent, nbr_at(nbr, e, m, j, bad));
         if (c >= 0 && c < first) first = c;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) first = min(first, __shfl_xor(first, o));
-    return first;
+    return ecc::wave_min_i32(first);  // DPP
 }
 
 __global__ void __launch_bounds__(kThreads, 8)  // 64 VGPRs: two 16-wave workgroups per CU
@@ -194,12 +192,7 @@ dbscan_extract_kernel(int64_t n_segs, int64_t stride, const int32_t *__restrict_
             const int j = j0 + u;
             if (j < m && parent[j] != -1 && !((roots >> u) & 1u)) parent[j] = uf_root(parent, j);
         }
-        int x = nr;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int o = __shfl_up(x, d);
-            if (lane >= d) x += o;
-        }
+        const int x = ecc::wave_incl_scan(nr);  // DPP
         if (lane == 63) wsum[wave] = x;
         __syncthreads();
         int pre = 0, nc = 0;
@@ -476,12 +469,7 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
             const int j = j0 + u;
             if (j < m && parent[j] != -1 && !roots[u]) parent[j] = uf_root(parent, j);
         }
-        int x = nr;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int o = __shfl_up(x, d);
-            if (lane >= d) x += o;
-        }
+        const int x = ecc::wave_incl_scan(nr);  // DPP
         if (lane == 63) wsum[wave] = x;
         __syncthreads();
         int pre = 0, nc = 0;
@@ -685,11 +673,8 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                 xmx = max(xmx, ecc::xy_x(v[u])); ymx = max(ymx, ecc::xy_y(v[u]));
             }
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            xmn = min(xmn, __shfl_xor(xmn, o)); ymn = min(ymn, __shfl_xor(ymn, o));
-            xmx = max(xmx, __shfl_xor(xmx, o)); ymx = max(ymx, __shfl_xor(ymx, o));
-        }
+        xmn = ecc::wave_min_i32(xmn); ymn = ecc::wave_min_i32(ymn);  // DPP
+        xmx = ecc::wave_max_i32(xmx); ymx = ecc::wave_max_i32(ymx);
         if (lane == 0) {
             box[wave][0] = xmn; box[wave][1] = ymn;
             box[wave][2] = xmx; box[wave][3] = ymx;
@@ -801,16 +786,32 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             }
             return -1;
         };
-        // unions: the row chain link to the right, then the two chains of every chord below
+        // unions: the row chain link to the right, then the two chains of every chord below.  The
+        // point's own root is found once and carried (ra): a root that another lane hooks
+        // meanwhile still lies in the component, and the hook itself only ever moves a root
+        // that is still a root (the CAS), so a stale ra costs at most a retry of the full union.
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
             const int j = u * kThreads + tid;
             if (j >= m) break;
             if (parent[j] == -1) continue;
             const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
+            int ra = uf_find(parent, j);
+            auto unite = [&](int q) {
+                const int rb = uf_find(parent, q);
+                if (rb == ra) return;
+                if (rb > ra) {
+                    if (atomicCAS(&parent[rb], rb, ra) == rb) return;  // rb hooked under ra
+                } else if (atomicCAS(&parent[ra], ra, rb) == ra) {
+                    ra = rb;  // ra hooked under rb: rb is the root now
+                    return;
+                }
+                uf_union(parent, j, q);  // lost a race: the general loop
+                ra = uf_find(parent, j);
+            };
             if (x + 1 < Wb && e_int > 0) {
                 const int c = first_core(y * WW, x + 1, min(x + e_int, Wb - 1));
-                if (c >= 0) uf_union(parent, j, rk2idx[rank_at(c, y)]);
+                if (c >= 0) unite(rk2idx[rank_at(c, y)]);
             }
             for (int a = 1; a <= amax && y + a < H; ++a) {
                 const int hw = hwt[a];
@@ -818,9 +819,9 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                 const int rb = (y + a) * WW;
                 const int cl = first_core(rb, lo, hi);
                 if (cl < 0) continue;
-                uf_union(parent, j, rk2idx[rank_at(cl, y + a)]);
+                unite(rk2idx[rank_at(cl, y + a)]);
                 const int cr = last_core(rb, cl, hi);
-                if (cr > cl) uf_union(parent, j, rk2idx[rank_at(cr, y + a)]);
+                if (cr > cl) unite(rk2idx[rank_at(cr, y + a)]);
             }
         }
         __syncthreads();
@@ -844,12 +845,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             const int j = j0 + u;
             if (j < m && parent[j] != -1 && !roots[u]) parent[j] = uf_root(parent, j);
         }
-        int xs = nr;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int o = __shfl_up(xs, d);
-            if (lane >= d) xs += o;
-        }
+        const int xs = ecc::wave_incl_scan(nr);  // DPP
         if (lane == 63) wsum[wave] = xs;
         __syncthreads();
         int pre = 0, nc = 0;
@@ -892,6 +888,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                     uint32_t b = cw[rb + w];
                     if (w == (lo >> 5)) b &= ~((1u << (lo & 31)) - 1u);
                     if (w == (hi >> 5)) b &= (hi & 31) == 31 ? 0xffffffffu : ((2u << (hi & 31)) - 1u);
+                    if (!b) continue;
                     const uint2 q = wd[rb + w];
                     while (b) {
                         const int bit = __ffs(b) - 1;

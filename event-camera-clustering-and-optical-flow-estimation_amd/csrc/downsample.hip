@@ -136,8 +136,7 @@ downsample_hash_kernel(const uint32_t *__restrict__ xy, int64_t n, int window, i
     __syncthreads();
 
     // 6. repeated count per wave (unique = occupied buckets = the representatives: step 7's total)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) rp += __shfl_xor(rp, o);
+    rp = ecc::wave_sum_i32(rp);  // DPP
     if (lane == 0) red[wave] = rp;
 
     // 7. compacted write-out in ascending event order

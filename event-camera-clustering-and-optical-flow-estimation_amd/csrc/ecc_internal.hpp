@@ -141,6 +141,80 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
+// Wave reductions by DPP moves (VALU only: the __shfl_xor butterflies are LDS permutes, which
+// competed with the kernels' own LDS traffic — the arc kernel's scans and minimum were a fifth of
+// its LDS instructions).  Row rotations 8/4/2/1 leave every lane its row's result, row_bcast:15
+// folds rows 0 -> 1 and 2 -> 3, row_bcast:31 folds rows 0-1 into 2-3, so lane 63 holds the
+// wave's result, which is returned to every lane (readlane: wave-uniform).  Rows a broadcast
+// step does not write keep `identity`'s contribution.  All 64 lanes must be active.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t identity, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, kCtrl, kRowMask, 0xf, false);
+}
+template <class Op>
+__device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t v, uint32_t identity, Op op) {
+    v = op(v, dpp_u32<0x128, 0xf>(identity, v));  // row_ror:8
+    v = op(v, dpp_u32<0x124, 0xf>(identity, v));  // row_ror:4
+    v = op(v, dpp_u32<0x122, 0xf>(identity, v));  // row_ror:2
+    v = op(v, dpp_u32<0x121, 0xf>(identity, v));  // row_ror:1
+    v = op(v, dpp_u32<0x142, 0xa>(identity, v));  // row_bcast:15 into rows 1, 3
+    v = op(v, dpp_u32<0x143, 0xc>(identity, v));  // row_bcast:31 into rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int wave_min_i32(int v) {
+    return (int)wave_reduce_u32((uint32_t)v, 0x7fffffffu, [](uint32_t a, uint32_t b) { return (uint32_t)min((int)a, (int)b); });
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+    return (int)wave_reduce_u32((uint32_t)v, 0x80000000u, [](uint32_t a, uint32_t b) { return (uint32_t)max((int)a, (int)b); });
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    return wave_reduce_u32(v, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+}
+__device__ __forceinline__ int wave_sum_i32(int v) {
+    return (int)wave_reduce_u32((uint32_t)v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int64_t dpp_i64(int64_t identity, int64_t v) {
+    const uint32_t lo = dpp_u32<kCtrl, kRowMask>((uint32_t)identity, (uint32_t)v);
+    const uint32_t hi = dpp_u32<kCtrl, kRowMask>((uint32_t)((uint64_t)identity >> 32), (uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <class Op>
+__device__ __forceinline__ int64_t wave_reduce_i64(int64_t v, int64_t identity, Op op) {
+    v = op(v, dpp_i64<0x128, 0xf>(identity, v));
+    v = op(v, dpp_i64<0x124, 0xf>(identity, v));
+    v = op(v, dpp_i64<0x122, 0xf>(identity, v));
+    v = op(v, dpp_i64<0x121, 0xf>(identity, v));
+    v = op(v, dpp_i64<0x142, 0xa>(identity, v));
+    v = op(v, dpp_i64<0x143, 0xc>(identity, v));
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 63);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), 63);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+    return wave_reduce_i64(v, INT64_MAX, [](int64_t a, int64_t b) { return a < b ? a : b; });
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+    return wave_reduce_i64(v, 0, [](int64_t a, int64_t b) { return a + b; });
+}
+// Inclusive prefix sum of an int64 over the wave (wave_incl_scan's pattern on both halves).
+__device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t x) {
+    x += dpp_i64<0x111, 0xf>(0, x);
+    x += dpp_i64<0x112, 0xf>(0, x);
+    x += dpp_i64<0x114, 0xf>(0, x);
+    x += dpp_i64<0x118, 0xf>(0, x);
+    x += dpp_i64<0x142, 0xa>(0, x);
+    x += dpp_i64<0x143, 0xc>(0, x);
+    return x;
+}
+// The value of a wave-uniform lane index (readlane: scalar, no LDS permute).
+__device__ __forceinline__ int lane_value(int v, int lane_idx) { return __builtin_amdgcn_readlane(v, lane_idx); }
+__device__ __forceinline__ int64_t lane_value64(int64_t v, int lane_idx) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane_idx);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), lane_idx);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // Correctly rounded fp32 square root.  On gfx950 `__fsqrt_rn` may lower to the bare
 // v_sqrt_f32 (<= 1 ulp), which breaks bit-exactness against IEEE sqrtf on the host.  This is
 // the hardware approximation followed by the exact one-ulp correction with FMA residuals

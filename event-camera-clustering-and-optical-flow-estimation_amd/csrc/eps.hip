@@ -174,11 +174,8 @@ eps_run_counts_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, ui
             xmn = min(xmn, xy_x(v)); ymn = min(ymn, xy_y(v));
             xmx = max(xmx, xy_x(v)); ymx = max(ymx, xy_y(v));
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            xmn = min(xmn, __shfl_xor(xmn, o)); ymn = min(ymn, __shfl_xor(ymn, o));
-            xmx = max(xmx, __shfl_xor(xmx, o)); ymx = max(ymx, __shfl_xor(ymx, o));
-        }
+        xmn = ecc::wave_min_i32(xmn); ymn = ecc::wave_min_i32(ymn);  // DPP
+        xmx = ecc::wave_max_i32(xmx); ymx = ecc::wave_max_i32(ymx);
         if (lane == 0) {
             box[wave][0] = xmn; box[wave][1] = ymn;
             box[wave][2] = xmx; box[wave][3] = ymx;
@@ -386,7 +383,7 @@ __device__ __forceinline__ void emit_list(const CellGrid &g, const uint32_t *cen
         if (mine) bits[w] = 0ull;
     }
     const int inc = ecc::wave_incl_scan(cnt);
-    const int total = __shfl(inc, 63);
+    const int total = __builtin_amdgcn_readlane(inc, 63);
     if (lane == 0 && out0 + total != end) *err = 1;  // counts disagree with the lists
     int64_t out = out0 + (inc - cnt);
 #pragma unroll
@@ -443,8 +440,9 @@ eps_lists_kernel(const uint32_t *__restrict__ xy, SegView sv, int e_int, uint32_
                 const int64_t po0 = ql < m ? offsets[base + ql] : 0, po1 = ql < m ? offsets[base + ql + 1] : 0;
                 for (int tt = 0; tt < 64; ++tt) {
                     if (wave + kW * (t0 + tt) >= m) break;  // wave-uniform
-                    const uint32_t v = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)pv, tt));
-                    const int64_t out0 = __shfl(po0, tt), end = __shfl(po1, tt);
+                    // the query's point and list range: readlane of a wave-uniform lane (no permute)
+                    const uint32_t v = (uint32_t)ecc::lane_value((int)pv, tt);
+                    const int64_t out0 = ecc::lane_value64(po0, tt), end = ecc::lane_value64(po1, tt);
                     emit_list<kN>(g, cend, spt, sidx, bits, v, e_int, r2i, words, wpl, out0, end, nbr, nbr_cap, err);
                 }
             }

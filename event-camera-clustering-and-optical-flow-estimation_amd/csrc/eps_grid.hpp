@@ -89,11 +89,8 @@ __device__ __forceinline__ CellGrid bin_cells(const uint32_t *__restrict__ xy, i
             xmx = max(xmx, xy_x(pv[u])); ymx = max(ymx, xy_y(pv[u]));
         }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        xmn = min(xmn, __shfl_xor(xmn, o)); ymn = min(ymn, __shfl_xor(ymn, o));
-        xmx = max(xmx, __shfl_xor(xmx, o)); ymx = max(ymx, __shfl_xor(ymx, o));
-    }
+    xmn = wave_min_i32(xmn); ymn = wave_min_i32(ymn);  // DPP
+    xmx = wave_max_i32(xmx); ymx = wave_max_i32(ymx);
     if (lane == 0) {
         red[4 * wave + 0] = xmn; red[4 * wave + 1] = ymn;
         red[4 * wave + 2] = xmx; red[4 * wave + 3] = ymx;
@@ -138,12 +135,7 @@ __device__ __forceinline__ CellGrid bin_cells(const uint32_t *__restrict__ xy, i
         uint32_t loc[per], sum = 0;
 #pragma unroll
         for (int k = 0; k < per; ++k) { loc[k] = cend[tid * per + k]; sum += loc[k]; }
-        uint32_t inc = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o);
-            if (lane >= o) inc += y;
-        }
+        const uint32_t inc = (uint32_t)wave_incl_scan((int)sum);  // DPP
         if (lane == 63) red[wave] = (int)inc;
         __syncthreads();
         uint32_t off = inc - sum;

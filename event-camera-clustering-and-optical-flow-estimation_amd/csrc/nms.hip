@@ -77,12 +77,7 @@ nms_kernel(const uint32_t *__restrict__ xy, const uint8_t *__restrict__ flags, i
         }
         const int cntv = __popc(bits);
         // wave inclusive scan of cntv
-        int incl = cntv;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
+        const int incl = ecc::wave_incl_scan(cntv);  // DPP
         if (lane == 63) wave_tot[wave] = incl;
         __syncthreads();
         int off = n_cand + incl - cntv, tot = 0;

@@ -16,8 +16,7 @@ scan_block_sums(const int32_t *__restrict__ in, int64_t n, int64_t *__restrict__
         const int64_t i = b0 + threadIdx.x * 4 + k;
         if (i < n) s += in[i];
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = ecc::wave_sum_i64(s);  // DPP
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
     if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
@@ -32,12 +31,7 @@ scan_sums(int64_t *__restrict__ bsum, int64_t nb) {
     for (int64_t c0 = 0; c0 < nb; c0 += kThreads) {
         const int64_t i = c0 + threadIdx.x;
         const int64_t v = i < nb ? bsum[i] : 0;
-        int64_t inc = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int64_t y = __shfl_up(inc, o);
-            if (lane >= o) inc += y;
-        }
+        const int64_t inc = ecc::wave_incl_scan_i64(v);  // DPP
         if (lane == 63) wtot[wave] = inc;
         __syncthreads();
         int64_t off = carry + inc - v, tot = 0;
@@ -63,12 +57,7 @@ scan_finish(const int32_t *__restrict__ in, int64_t n, const int64_t *__restrict
         v[k] = i < n ? in[i] : 0;
         s += v[k];
     }
-    int64_t inc = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int64_t y = __shfl_up(inc, o);
-        if (lane >= o) inc += y;
-    }
+    const int64_t inc = ecc::wave_incl_scan_i64(s);  // DPP
     if (lane == 63) wtot[wave] = inc;
     __syncthreads();
     int64_t off = bsum[blockIdx.x] + inc - s;

@@ -942,6 +942,12 @@ tracker_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__restr
 // helpers, same operation order), so the state is bit-identical.  A slice with T + C > 256
 // (tracks + detections) hands the rest of the launch to tracker_kernel: the list is written to
 // the current buffer and ctr->resume = that slice.
+// Quad permutes by DPP (quad_perm: lane i of each quad reads lane sel[i] of it).
+template <int kCtrl>
+__device__ __forceinline__ int qperm(int v) { return __builtin_amdgcn_mov_dpp(v, kCtrl, 0xf, 0xf, false); }
+template <int kCtrl>
+__device__ __forceinline__ float qperm_f(float v) { return __int_as_float(qperm<kCtrl>(__float_as_int(v))); }
+
 constexpr int kFT = 256;    // the largest T + C of a slice handled here (LDS arrays)
 constexpr int kFThreads = 512;  // 8 waves: the round-0 scan runs 2-4 lanes per track
 constexpr int kFW = kFThreads / 64;
@@ -1206,15 +1212,28 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
                     scan(std::integral_constant<int, 32>{});
             }
             // the track's lanes: minimum, list sizes -> merged list offsets
+            // (quad DPP permutes: L = 2 or 4 lanes of a track lie in one quad; the lane shuffles
+            // were LDS permutes on the slice's serial chain.  Every permute runs in all lanes:
+            // one under a lane condition would read a disabled source lane.)
             int cnt = l_ovf ? kFList + 1 : l_n, incl = cnt;
-            for (int o = 1; o < L; o <<= 1) {
-                const float od = __shfl_xor(bd, o);
-                const int oi = __shfl_xor(bi, o);
+            auto take = [&](float od, int oi) {
                 if (oi >= 0 && (bi < 0 || od < bd || (od == bd && oi < bi))) { bd = od; bi = oi; }
-                const int v = __shfl_up(incl, o, L);
-                if (tj >= o) incl += v;
+            };
+            int total;
+            if (L == 4) {  // uniform
+                take(qperm_f<0xB1>(bd), qperm<0xB1>(bi));  // lane ^ 1
+                const int u1 = qperm<0x90>(incl);             // lane - 1
+                incl += tj >= 1 ? u1 : 0;
+                take(qperm_f<0x4E>(bd), qperm<0x4E>(bi));  // lane ^ 2
+                const int u2 = qperm<0x44>(incl);             // lane - 2
+                incl += tj >= 2 ? u2 : 0;
+                total = qperm<0xFF>(incl);                   // lane 3 of the quad
+            } else {
+                take(qperm_f<0xB1>(bd), qperm<0xB1>(bi));  // lane ^ 1
+                const int u1 = qperm<0xA0>(incl);             // lane - 1 within the pair
+                incl += tj >= 1 ? u1 : 0;
+                total = qperm<0xF5>(incl);                   // lane 1 of the pair
             }
-            const int total = __shfl(incl, (lane & ~(L - 1)) + L - 1);
             if (act && total <= kFList) {
                 const int off = incl - cnt;
                 for (int k = 0; k < l_n; ++k) {
