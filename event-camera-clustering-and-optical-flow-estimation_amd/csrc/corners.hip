@@ -60,6 +60,7 @@ constexpr int kMaxSlice = 1 << 19;       // group-local event index must fit 24 
 struct CornerGeom {
     int W, H, S, margin, border_mode, first_detect;
     int any_order;         // timestamps in any order: every group wide (index values, exact tests)
+    int dedup_words;       // slice_sort's dedup bitmap: n_tiles * 196 bits (0: off, too large)
     int tiles_x, n_tiles;  // bin n_tiles of each group holds the events outside the sensor
     int seg_stride;        // words per slice of the slice-major corner pairs: n_tiles * 7, to 16 B
     float inv_S;
@@ -141,9 +142,23 @@ constexpr int kSortThreads = 1024;
 constexpr int kSortEPT = 16;
 constexpr int kSortFence = 4;  // events whose loads may be in flight together
 constexpr int kSortChunk = kSortThreads * kSortEPT;
+constexpr int kSortWaves = kSortThreads / 64;
 
-// Block-wide exclusive scan in place of a[0, n) (kSortThreads threads, each a contiguous run).
-__device__ __forceinline__ void block_excl_scan_inplace(int32_t *a, int n, int32_t *wsum) {
+// Per-slice (slice, pixel) dedup of the keys (groups with 4-byte keys, slices in one chunk, time
+// order intact): an arc test reads, per (slice, pixel), only the largest timestamp, i.e. the key
+// of the pixel's LAST event in the slice; pair_build takes the maximum of what it receives.  The
+// slice's events are taken in kSortEPT rounds from the last (round u = events [1024 u, 1024 u +
+// 1024)): an event is dropped when a LATER round already set its tile pixel's bit in an LDS
+// bitmap (the staging area, not yet in use).  Events of one round at one pixel all stay (no
+// ordering inside a round), so the maximum always survives.  ~46 % of the events remain on the
+// bench's stream (40 % are distinct (slice, pixel) pairs), and pair_build reads only those.
+#ifndef ECC_SORT_DEDUP
+#define ECC_SORT_DEDUP 1
+#endif
+
+// Block-wide exclusive scan in place of a[0, n) (kSortThreads threads, each a contiguous run);
+// returns the total to every thread.
+__device__ __forceinline__ int block_excl_scan_inplace(int32_t *a, int n, int32_t *wsum) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int per = (n + kSortThreads - 1) / kSortThreads;
     const int b0 = min(n, tid * per), b1 = min(n, b0 + per);
@@ -152,13 +167,17 @@ __device__ __forceinline__ void block_excl_scan_inplace(int32_t *a, int n, int32
     const int incl = ecc::wave_incl_scan(sum);  // DPP
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
-    int run = incl - sum;
-    for (int w = 0; w < wave; ++w) run += wsum[w];
+    int run = incl - sum, total = 0;
+    for (int w = 0; w < kSortThreads / 64; ++w) {
+        run += w < wave ? wsum[w] : 0;
+        total += wsum[w];
+    }
     for (int i = b0; i < b1; ++i) {
         const int c = a[i];
         a[i] = run;
         run += c;
     }
+    return total;
 }
 
 __global__ void __launch_bounds__(kSortThreads, 8)  // 8 waves/SIMD: two workgroups per CU
@@ -166,7 +185,8 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
                   int32_t *__restrict__ first_border, int32_t *__restrict__ err, int32_t *__restrict__ err_status,
                   uint32_t *__restrict__ zero0, int32_t *__restrict__ zero1) {
     extern __shared__ int32_t hist[];  // [nb]: counts, then offsets, then (long slices) cursors;
-                                       // then [kSortChunk] staging of the sorted slice
+                                       // then [kSortChunk] staging (single slices: the keys in
+                                       // event order, then in tile order); then the dedup bitmap
     __shared__ int32_t wsum[kSortThreads / 64];
     const int tid = threadIdx.x, lane = tid & 63;
     const int64_t s = blockIdx.x;
@@ -187,14 +207,20 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
     const bool narrow = group_narrow(t, g, grp, &t_first);  // uniform
     const bool fmt4 = group_fmt4(t, g, grp);                // uniform
     const int nb = g.n_tiles + 1;
+    const bool single = len <= kSortChunk;
+    const bool dedup = ECC_SORT_DEDUP && single && fmt4 && g.dedup_words > 0;  // uniform
+    uint32_t *stage = reinterpret_cast<uint32_t *>(hist + nb);
+    uint32_t *bm = stage + kSortChunk;  // the dedup bitmap
     for (int b = tid; b < nb; b += kSortThreads) hist[b] = 0;
+    if (dedup)
+        for (int w = tid; w < g.dedup_words; w += kSortThreads) bm[w] = 0u;
     __syncthreads();
     bool bad = false;
     int fb = 0x7fffffff;
-    const bool single = len <= kSortChunk;
-    // per event only its final key and tile << 16 | rank stay in registers (single slices:
-    // rank < 2^14); the key is formed at load time
-    uint32_t kv[kSortEPT], br[kSortEPT];
+    // per event only tile << 16 | rank stays in registers (single slices: rank < 2^14); the key,
+    // formed at load time, waits in the staging area in event order (in registers, it held 16
+    // VGPRs through the load phase)
+    uint32_t br[kSortEPT];
     const uint32_t *__restrict__ xs = xy + lo;
     const int64_t *__restrict__ ts = t + lo;
     for (int c0 = 0; c0 < len; c0 += kSortChunk) {  // one iteration for single slices
@@ -211,9 +237,25 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
             // the previous event's t: a coalesced load of the neighbouring element (cache hit)
             const int64_t tp = (ic > 0 || lo > 0) ? ts[ic - 1] : INT64_MIN;
             bad |= ok && tp > tc;
-            kv[u] = tile_key(v, fmt4 ? (uint32_t)(tc - t_first) : (uint32_t)(lo + i - grp_first));
+            if (single) stage[u * kSortThreads + tid] = tile_key(v, fmt4 ? (uint32_t)(tc - t_first) : (uint32_t)(lo + i - grp_first));
             br[u] = ok ? (uint32_t)tile_of(v, g) << 16 : 0xffffffffu;
             if (ok && is_border(ecc::xy_x(v), ecc::xy_y(v), g)) fb = min(fb, i);
+        }
+        if (dedup && !__syncthreads_or(bad)) {  // uniform (single slices: one pass of this loop)
+#pragma unroll
+            for (int u = kSortEPT - 1; u >= 0; --u) {
+                const uint32_t b = br[u] >> 16;  // 0xffff: no event; n_tiles: outside the sensor (kept)
+                const bool cand = b < (uint32_t)g.n_tiles;
+                const uint32_t tp = b * kTilePix + (stage[u * kSortThreads + tid] & 255u);  // own key
+                bool drop = false;
+                if (u < kSortEPT - 1) {
+                    drop = cand && ((bm[tp >> 5] >> (tp & 31u)) & 1u);
+                    __syncthreads();  // every check of round u before its bits are set
+                }
+                if (drop) br[u] = 0xffffffffu;
+                else if (cand) atomicOr(&bm[tp >> 5], 1u << (tp & 31u));
+                if (u > 0) __syncthreads();  // round u's bits before round u-1's checks
+            }
         }
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u) {
@@ -231,20 +273,22 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
         first_border[s] = m;
     }
     __syncthreads();
-    block_excl_scan_inplace(hist, nb, wsum);
+    const int kept = block_excl_scan_inplace(hist, nb, wsum);  // len, less the dropped events
     __syncthreads();
     int32_t *row = so.toff + s * (int64_t)(nb + 1);
     for (int b = tid; b < nb; b += kSortThreads) row[b] = hist[b];
-    if (tid == 0) row[nb] = len;
+    if (tid == 0) row[nb] = kept;
     if (single) {  // place keys, then timestamps, in tile order in LDS; write both out contiguously
-        uint32_t *stage = reinterpret_cast<uint32_t *>(hist + nb);
-        __syncthreads();
+        uint32_t kv[kSortEPT];
+#pragma unroll
+        for (int u = 0; u < kSortEPT; ++u) kv[u] = stage[u * kSortThreads + tid];  // own keys
+        __syncthreads();  // every key read before the stage is permuted
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u)
             if (br[u] != 0xffffffffu) stage[hist[br[u] >> 16] + (br[u] & 0xffffu)] = kv[u];
         __syncthreads();
-        for (int i = tid; i < len; i += kSortThreads) so.key[lo + i] = stage[i];
-        if (fmt4 || !narrow) return;
+        for (int i = tid; i < kept; i += kSortThreads) so.key[lo + i] = stage[i];
+        if (fmt4 || !narrow) return;  // (no dedup below: kept == len)
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kSortEPT; ++u)  // rare (groups spanning >= 2^24 ticks): t read again
@@ -1625,6 +1669,10 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     g.n_tiles = g.tiles_x * ((g.H + kTile - 1) / kTile);
     g.seg_stride = (g.n_tiles * kSegWords + 3) & ~3;
     if (g.n_tiles > kMaxTiles) return ECC_ERR_INVALID;  // > 8191 16x16 tiles (~2.1 Mpixel)
+    // slice_sort's dedup bitmap (one bit per tile pixel), kept only while two of its workgroups
+    // still fit a CU's LDS (sensors up to ~400 tiles of 14x14 pixels, e.g. 346x260)
+    g.dedup_words = (int)(((int64_t)g.n_tiles * kTilePix + 31) / 32);
+    if (((size_t)g.n_tiles + 1 + kSortChunk + g.dedup_words) * 4 + 256 > 80 * 1024) g.dedup_words = 0;
     g.n = n;
     g.n_slices = (n + g.S - 1) / g.S;
     if (g.n_slices > INT32_MAX) return ECC_ERR_INVALID;
@@ -1651,7 +1699,8 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
 
     if (phases & 1) {
     {
-        const size_t lds = (size_t)nb * 4 + kSortChunk * 4;  // > 64 KiB: opt in (gfx950 has 160 KiB)
+        // > 64 KiB: opt in (gfx950 has 160 KiB); the dedup bitmap only while two workgroups fit a CU
+        const size_t lds = ((size_t)nb + kSortChunk + g.dedup_words) * 4;
         static int lds_set = 0;
         if ((int)lds > lds_set) {
             ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&slice_sort_kernel),
