@@ -140,7 +140,10 @@ __device__ __forceinline__ int slice_in_group(uint32_t el, const CornerGeom &g) 
 // the CU idle outside its load phase).
 constexpr int kSortThreads = 1024;
 constexpr int kSortEPT = 16;
-constexpr int kSortFence = 4;  // events whose loads may be in flight together
+#ifndef ECC_SORT_FENCE
+#define ECC_SORT_FENCE 4
+#endif
+constexpr int kSortFence = ECC_SORT_FENCE;  // events whose loads may be in flight together
 constexpr int kSortChunk = kSortThreads * kSortEPT;
 constexpr int kSortWaves = kSortThreads / 64;
 

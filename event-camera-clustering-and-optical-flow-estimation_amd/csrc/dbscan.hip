@@ -625,6 +625,8 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
 constexpr int kDrWords = 4864;  // (bits, prefix) pairs: 346x260 needs 2860
 constexpr int kDrHw = 512;      // disk half-width table: eps < 512
 constexpr int kDrPer = kGridMaxPts / kThreads;
+constexpr int kDrNarrow = 32;  // eps up to which a chord (2 eps + 1 pixels) spans at most 3 words
+constexpr int kDrRows = 4;     // chord rows per union batch
 
 __global__ void __launch_bounds__(kThreads)
 dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stride, const int32_t *__restrict__ seg_counts,
@@ -746,7 +748,8 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
             rk2idx[rank_at(x, y)] = (uint16_t)j;
             int cnt = 0;
-            for (int a = 0; a <= amax; ++a) {
+#pragma unroll 4
+            for (int a = 0; a <= amax; ++a) {  // (unrolled: four rows' word loads in flight)
                 const int hw = hwt[a];
                 const int xl = max(x - hw, 0), xh = min(x + hw + 1, Wb);
                 const uint32_t ml = (1u << (xl & 31)) - 1u, mh = (1u << (xh & 31)) - 1u;
@@ -786,10 +789,68 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             }
             return -1;
         };
+        // Rows y + s*a0 .. y + s*(a0 + kDrRows - 1) (s = +1 or -1; rows past amax or the box give
+        // -1): per row, the segment indices of the first and last core point of the point's chord
+        // there (eps <= kDrNarrow: a chord spans at most 3 words), -1 if none or the same point.
+        auto chord_ends_batch = [&](int a0, int x, int y, int sgn, int (&cand)[2 * kDrRows]) {
+            int pos[2 * kDrRows], row[kDrRows];
+            uint32_t b[kDrRows][3];
+            int lo[kDrRows], hi[kDrRows];
+#pragma unroll
+            for (int r = 0; r < kDrRows; ++r) {
+                const int a = a0 + r, yy = y + sgn * a;
+                const bool ok = a <= amax && (unsigned)yy < (unsigned)H;
+                const int hw = hwt[ok ? a : 0];
+                lo[r] = max(x - hw, 0);
+                hi[r] = min(x + hw, Wb - 1);
+                row[r] = ok ? yy : -1;
+                const int w0 = lo[r] >> 5, w1 = hi[r] >> 5, rb = yy * WW;
+                b[r][0] = cw[ok ? rb + w0 : kDrWords];
+                b[r][1] = cw[ok && w1 > w0 ? rb + w0 + 1 : kDrWords];
+                b[r][2] = cw[ok && w1 > w0 + 1 ? rb + w0 + 2 : kDrWords];
+            }
+#pragma unroll
+            for (int r = 0; r < kDrRows; ++r) {
+                const int w0 = lo[r] >> 5, nw = (hi[r] >> 5) - w0;  // last word: 0..2
+                const uint32_t hm = (hi[r] & 31) == 31 ? 0xffffffffu : ((2u << (hi[r] & 31)) - 1u);
+                uint32_t b0 = b[r][0] & ~((1u << (lo[r] & 31)) - 1u), b1 = b[r][1], b2 = b[r][2];
+                if (nw == 0) b0 &= hm;
+                else if (nw == 1) b1 &= hm;
+                else b2 &= hm;
+                const uint64_t lw = (uint64_t)b0 | ((uint64_t)b1 << 32);
+                const int base = w0 << 5;
+                const int cl = lw ? base + __builtin_ctzll(lw) : (b2 ? base + 64 + __builtin_ctz(b2) : -1);
+                const int cr = b2 ? base + 95 - __builtin_clz(b2) : (lw ? base + 63 - __builtin_clzll(lw) : -1);
+                pos[2 * r] = row[r] >= 0 && cl >= 0 ? rank_at(cl, row[r]) : -1;
+                pos[2 * r + 1] = row[r] >= 0 && cr > cl ? rank_at(cr, row[r]) : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < 2 * kDrRows; ++k) cand[k] = pos[k] >= 0 ? (int)rk2idx[pos[k]] : -1;
+        };
+        // the roots of cand[] (-1 stays -1), the chains walked in lockstep
+        auto roots_batch = [&](const int (&cand)[2 * kDrRows], int (&rt)[2 * kDrRows]) {
+#pragma unroll
+            for (int k = 0; k < 2 * kDrRows; ++k) rt[k] = cand[k];
+            for (;;) {
+                int nxt[2 * kDrRows];
+                bool more = false;
+#pragma unroll
+                for (int k = 0; k < 2 * kDrRows; ++k) nxt[k] = rt[k] >= 0 ? parent[rt[k]] : -1;
+#pragma unroll
+                for (int k = 0; k < 2 * kDrRows; ++k) {
+                    more |= rt[k] >= 0 && nxt[k] != rt[k];
+                    rt[k] = rt[k] >= 0 ? nxt[k] : -1;
+                }
+                if (!more) break;
+            }
+        };
         // unions: the row chain link to the right, then the two chains of every chord below.  The
         // point's own root is found once and carried (ra): a root that another lane hooks
         // meanwhile still lies in the component, and the hook itself only ever moves a root
         // that is still a root (the CAS), so a stale ra costs at most a retry of the full union.
+        // Chords of at most 3 words (eps <= kDrNarrow) go kDrRows rows at a time: their core
+        // words, ranks, indices and roots are loaded for all rows of the batch together (one
+        // dependent LDS round trip per step instead of one per row and step).
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
             const int j = u * kThreads + tid;
@@ -797,8 +858,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             if (parent[j] == -1) continue;
             const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
             int ra = uf_find(parent, j);
-            auto unite = [&](int q) {
-                const int rb = uf_find(parent, q);
+            auto unite_root = [&](int q, int rb) {  // rb: q's root when looked up (may be stale)
                 if (rb == ra) return;
                 if (rb > ra) {
                     if (atomicCAS(&parent[rb], rb, ra) == rb) return;  // rb hooked under ra
@@ -811,17 +871,36 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             };
             if (x + 1 < Wb && e_int > 0) {
                 const int c = first_core(y * WW, x + 1, min(x + e_int, Wb - 1));
-                if (c >= 0) unite(rk2idx[rank_at(c, y)]);
+                if (c >= 0) {
+                    const int q = rk2idx[rank_at(c, y)];
+                    unite_root(q, uf_find(parent, q));
+                }
             }
-            for (int a = 1; a <= amax && y + a < H; ++a) {
-                const int hw = hwt[a];
-                const int lo = max(x - hw, 0), hi = min(x + hw, Wb - 1);
-                const int rb = (y + a) * WW;
-                const int cl = first_core(rb, lo, hi);
-                if (cl < 0) continue;
-                unite(rk2idx[rank_at(cl, y + a)]);
-                const int cr = last_core(rb, cl, hi);
-                if (cr > cl) unite(rk2idx[rank_at(cr, y + a)]);
+            if (e_int <= kDrNarrow) {  // uniform
+                for (int a0 = 1; a0 <= amax && y + a0 < H; a0 += kDrRows) {
+                    int cand[2 * kDrRows];
+                    chord_ends_batch(a0, x, y, +1, cand);
+                    int rt[2 * kDrRows];
+                    roots_batch(cand, rt);
+#pragma unroll
+                    for (int k = 0; k < 2 * kDrRows; ++k)
+                        if (cand[k] >= 0) unite_root(cand[k], rt[k]);
+                }
+            } else {
+                for (int a = 1; a <= amax && y + a < H; ++a) {
+                    const int hw = hwt[a];
+                    const int lo = max(x - hw, 0), hi = min(x + hw, Wb - 1);
+                    const int rb = (y + a) * WW;
+                    const int cl = first_core(rb, lo, hi);
+                    if (cl < 0) continue;
+                    int q = rk2idx[rank_at(cl, y + a)];
+                    unite_root(q, uf_find(parent, q));
+                    const int cr = last_core(rb, cl, hi);
+                    if (cr > cl) {
+                        q = rk2idx[rank_at(cr, y + a)];
+                        unite_root(q, uf_find(parent, q));
+                    }
+                }
             }
         }
         __syncthreads();
