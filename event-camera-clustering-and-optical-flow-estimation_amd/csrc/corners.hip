@@ -379,54 +379,27 @@ __device__ __forceinline__ GroupRef group_ref(const int64_t *__restrict__ t, con
     return r;
 }
 
-// Sub-regions of a tile: rows/cols {0-3, 4-9, 10-13} -> r = ry * 3 + rx.  A neighbouring tile's
-// window reaches only the 4-pixel strips facing it, so the entries of each tile are stored in
-// sub-region order and a window reads exactly the sub-regions it covers.
-constexpr int kSub = 9;
-__host__ __device__ constexpr int sub_band(int c) { return c < kHalo ? 0 : (c < kTile - kHalo ? 1 : 2); }
-__host__ __device__ constexpr int sub_of(int lp) { return sub_band(lp / kTile) * 3 + sub_band(lp % kTile); }
-// The arc kernels stage a window's values from exactly these sub-regions and read each window
-// pixel's slice mask from pair_build's mask image: a mask bit without a staged value would read
-// stale LDS.  That holds only while a neighbour tile's facing band is the window's halo.
 static_assert(kWin == kTile + 2 * kHalo, "window = tile + halo on both sides");
 static_assert(kHalo >= 4, "the circles reach 4 px from the pixel under test");
-static_assert(kTile >= 2 * kHalo, "the two border bands of a tile must not overlap");
-static_assert(sub_band(kHalo - 1) == 0 && sub_band(kHalo) == 1 && sub_band(kTile - kHalo - 1) == 1 &&
-                  sub_band(kTile - kHalo) == 2 && sub_band(kTile - 1) == 2,
-              "a tile's border bands are exactly kHalo pixels wide (the neighbours' halo)");
-
-// Tile pixels in (sub-region, pixel) order.
-struct SubOrder {
-    uint8_t pix[kTilePix];
-    uint8_t end[kSub];  // exclusive end of each sub-region in pix[]
-};
-constexpr SubOrder make_sub_order() {
-    SubOrder o{};
-    int k = 0;
-    for (int r = 0; r < kSub; ++r) {
-        for (int lp = 0; lp < kTilePix; ++lp)
-            if (sub_of(lp) == r) o.pix[k++] = (uint8_t)lp;
-        o.end[r] = (uint8_t)k;
-    }
-    return o;
-}
-__constant__ SubOrder c_sub = make_sub_order();
 
 // 3. Per (group, tile): the distinct (slice, pixel) pairs the tile's events touch, each with the
 // value an arc test reads there (max over the slice's events at the pixel: v' or index + 1),
-// written as entries {j << 8 | pixel, value} in sub-region order at item_base[item] = the item's
-// place in its group's range with the group's items in tile order (an item has at least as many
-// events as pairs), with the sub-region ends in sub_end[item][9].
-// Also the slices that touched each pixel (gmask) and its last timestamp (glast).
-struct PairEntry {
-    uint32_t meta;  // j << 8 | pixel in tile
-    uint32_t v;
-};
+// stored PER PIXEL so that an arc workgroup stages a window pixel from its own fixed addresses,
+// with no per-item offset table between its loads:
+//   gmask[grp][q]  the slices that touched the pixel (bit j = slice j of the group),
+//   pv[grp][q]     its values in ascending j: {v0, v1, v2, v3} when it has <= 4 of them, else
+//                  {v0, v1, v2, x} with v3, v4, ... at ovf[4x], ovf[4x + 1], ... (16-B aligned, so
+//                  an arc workgroup reads them as whole uint4s),
+//   glast[grp][q]  its last timestamp.
+// Item i's overflow values go to its own part of ovf: from (its place in the group's range with
+// the group's items in tile order) + 4i, rounded up to 16 B.  A pixel with p > 4 values takes
+// p - 3 rounded up to 4 words, at most p, and an item has at least as many events as pairs, so
+// the 4 words per item cover the rounding and ovf needs n + 4 * n_items words.
+constexpr int kRecVals = 4;  // values a pixel record holds inline
 
 __global__ void __launch_bounds__(kThreads)
-pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEntry *__restrict__ entries,
-                  int64_t *__restrict__ item_base, int32_t *__restrict__ sub_end, uint32_t *__restrict__ gmask,
-                  int64_t *__restrict__ glast) {
+pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, uint32_t *__restrict__ ovf,
+                  uint4 *__restrict__ pv, uint32_t *__restrict__ gmask, int64_t *__restrict__ glast) {
     __shared__ uint32_t tab[kGroup][kTilePix];  // 24.5 KiB
     __shared__ uint32_t pmask[kTilePix];        // slices that touched each tile pixel
     __shared__ int32_t wtot[kThreads / 64];
@@ -435,9 +408,7 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
     const int64_t item = blockIdx.x;
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
-    // this lane's pixel in sub-region order: a per-lane constant-memory read is a vector load,
-    // issued here so that it completes during the setup
-    const int lp = tid < kTilePix ? c_sub.pix[tid] : 0;
+    const int lp = tid < kTilePix ? tid : 0;  // this lane's tile pixel
     {
         uint4 *z = reinterpret_cast<uint4 *>(&tab[0][0]);
         for (int i = tid; i < (int)(sizeof(tab) / 16); i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -487,36 +458,41 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, PairEn
         }
     }
     __syncthreads();
-    // lane k owns pixel c_sub.pix[k]: slice mask, entry count, exclusive prefix in sub-region order
-    // the pixel's slice mask, kept by one LDS atomicOr per event beside its atomicMax (reading
-    // the pixel's 32 table words instead cost 32 LDS reads per pixel lane: 107 -> 100 us)
+    // lane lp owns tile pixel lp: its slice mask, kept by one LDS atomicOr per event beside its
+    // atomicMax (reading the pixel's 32 table words instead cost 32 LDS reads per pixel lane)
     const uint32_t m = tid < kTilePix ? pmask[lp] : 0u;
     const int cnt = __popc(m);
-    const int incl = ecc::wave_incl_scan(cnt);  // DPP (all lanes active)
+    const int nov = cnt > kRecVals ? (cnt - (kRecVals - 1) + 3) & ~3 : 0;  // past the first three, to 16 B
+    const int incl = ecc::wave_incl_scan(nov);                  // DPP (all lanes active)
     if (lane == 63) wtot[wave] = incl;
     __syncthreads();
-    int off = incl - cnt;
+    int off = incl - nov;
     for (int w = 0; w < wave; ++w) off += wtot[w];
     if (tid >= kTilePix) return;
-    const int64_t base = gr.first + segs.base;  // the item's events range = room for its pairs
-    if (tid == 0) item_base[item] = base;
-    for (int r = 0; r < kSub; ++r)
-        if (tid + 1 == c_sub.end[r]) sub_end[item * kSub + r] = off + cnt;
-    PairEntry *out = entries + base + off;
-    for (uint32_t mm = m; mm; mm &= mm - 1u) {
-        const int j = __ffs(mm) - 1;
-        *out++ = PairEntry{(uint32_t)(j << 8 | lp), tab[j][lp]};
-    }
     int x0, y0;
     tile_origin(g, tile, x0, y0);
     const int px = x0 + lp % kTile, py = y0 + lp / kTile;
     if (px >= g.W || py >= g.H) return;
     const int64_t q = grp * (int64_t)g.H * g.W + (int64_t)py * g.W + px;
     gmask[q] = m;
-    if (m) {
-        const uint32_t v = tab[31 - __clz(m)][lp];
-        glast[q] = gr.narrow ? gr.Lt + (int64_t)v : t[gr.first + v - 1u];
+    if (!m) return;  // no slice touched it: arc workgroups never read its record
+    // the pixel's overflow values at 16-B index x4 (off is a multiple of 4)
+    const uint32_t x4 = (uint32_t)(((gr.first + segs.base + 4 * item + 3) >> 2) + (off >> 2));
+    uint32_t *xo = ovf + 4 * (int64_t)x4 - (kRecVals - 1);
+    static_assert(kRecVals == 4, "the record is one uint4");
+    uint32_t r0 = 0u, r1 = 0u, r2 = 0u, r3 = x4;  // selects, not a register array indexed by k
+    uint32_t v = 0u;
+    int k = 0;
+    for (uint32_t mm = m; mm; mm &= mm - 1u, ++k) {
+        v = tab[__ffs(mm) - 1][lp];
+        if (k == 0) r0 = v;
+        else if (k == 1) r1 = v;
+        else if (k == 2) r2 = v;
+        else if (cnt == kRecVals) r3 = v;
+        else xo[k] = v;
     }
+    pv[q] = make_uint4(r0, r1, r2, r3);
+    glast[q] = gr.narrow ? gr.Lt + (int64_t)v : t[gr.first + v - 1u];  // v: the newest slice's value
 }
 
 // 4. Per pixel, in place over the groups: gB[g] := B_g, the SAE before group g (the caller's
@@ -729,9 +705,7 @@ struct ArcLds {
     int32_t n_tasks;
     int32_t q4n;
     int32_t n_exact;      // some task needs the exact int64 test
-    int64_t seg_lo[16];   // window segments: first entry (absolute) ...
-    int32_t seg_pref[16]; // ... exclusive prefix of their lengths ...
-    int32_t seg_off[16];  // ... and the window offset of the neighbour tile's origin
+    int32_t wave_own[kWaves];  // the wave's own-tile pixels have pairs
 };
 
 __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, int32_t *exact_flag,
@@ -801,42 +775,34 @@ __device__ __noinline__ bool exact_pair_test(const ArcLds *L, int wp0, int64_t q
 
 // 5. Arc test of one (group, tile) item, all items of all groups in one launch.  The item's
 // corner pairs go to res (slice-major, store_res_slice_major); flags_event_kernel applies them.
-constexpr int kStageUnroll = 4;
+//
+// Staging: window pixel wp of the item (lane wp < 484) reads its slice mask, its value record and
+// its B_g from fixed per-pixel addresses (pair_build's gmask / pv images, sae_prefix's B), three
+// independent loads in flight together; only a pixel with more than four values reads the rest
+// of them from the overflow array, at the address its record names.
 
-// Window segment c (< 13) of item (grp, tile): the sub-regions of the 3x3 tiles around the tile
-// that its window covers (own tile: all; edge neighbours: the 3 facing sub-regions; corners: 1),
-// as (first entry, entries).  The geometry is packed into integer constants (a per-lane table
-// read would be a load): dx, dy in {-1,0,1} (2 bits + 1), first/last sub-region (4 bits).  The
-// three loads are unconditional and independent (clamped to the own item when the neighbour is
-// off the sensor), so they are in flight together: a load under a per-lane condition, or one
-// whose address waits on another, made them one round trip each.
-__device__ __forceinline__ void window_segment(const CornerGeom &g, int64_t grp, int tile, int c,
-                                               const int64_t *__restrict__ item_base,
-                                               const int32_t *__restrict__ sub_end, int64_t &b0, int &len) {
-    const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
-    const int sxt = (int)((0x2222215u >> (2 * c)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * c)) & 3u) - 1;
-    const int r0t = (int)((0x6835020268060ull >> (4 * c)) & 15u), r1t = (int)((0x6835020268288ull >> (4 * c)) & 15u);
-    const int nx = tx + sxt, ny = ty + syt;
-    const bool ok = nx >= 0 && ny >= 0 && nx < g.tiles_x && ny < g.n_tiles / g.tiles_x;
-    const int64_t bi = grp * g.n_tiles + (ok ? (int64_t)ny * g.tiles_x + nx : (int64_t)tile);
-    const int s0r = sub_end[bi * kSub + (r0t ? r0t - 1 : 0)];
-    const int s1 = sub_end[bi * kSub + r1t];
-    const int64_t ib = item_base[bi];
-    asm volatile("" ::"v"(s0r), "v"(s1), "v"(ib));  // keeps the loads out of an exec-mask branch
-    const int s0 = r0t ? s0r : 0;
-    b0 = ok ? ib + s0 : 0;
-    len = ok ? s1 - s0 : 0;
+// The slices of group grp whose pairs are tested (Q15: slices before first_detect are not).
+__device__ __forceinline__ uint32_t eligible_slices(const CornerGeom &g, int64_t grp) {
+    const int64_t j0 = (int64_t)g.first_detect - grp * kGroup;
+    return j0 <= 0 ? 0xffffffffu : (j0 >= kGroup ? 0u : (0xffffffffu << (int)j0));
 }
 
-// window offset of segment c's tile origin
-__device__ __forceinline__ int window_segment_offset(int c) {
-    const int sxt = (int)((0x2222215u >> (2 * c)) & 3u) - 1, syt = (int)((0x1556821u >> (2 * c)) & 3u) - 1;
-    return (syt * kTile) * kWin + sxt * kTile + kHalo * kWin + kHalo;
+// Values k0 .. p-1 (p > 4, k0 >= 3) of a pixel whose record is r: v_k at ovf[4 r.w + k - 3],
+// four loads in flight at a time (clamped indices), handed to put(k, v).
+__device__ __forceinline__ const uint32_t *overflow_base(const uint32_t *__restrict__ ovf, const uint4 &r) {
+    return ovf + 4 * (int64_t)r.w - (kRecVals - 1);
 }
-
-// Window segments: the sub-regions of the 3x3 tiles around the item's tile that its window
-// covers (own tile: all; edge neighbours: the 3 facing sub-regions; corners: 1) — 13 at most.
-constexpr int kMaxSeg = 13;
+template <class Put>
+__device__ __forceinline__ void overflow_values(const uint32_t *__restrict__ xo, int k0, int p, Put put) {
+    for (; k0 < p; k0 += 4) {
+        uint32_t a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = xo[min(k0 + u, p - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k0 + u < p) put(k0 + u, a[u]);
+    }
+}
 
 #ifndef ECC_ARC_PROFILE
 #define ECC_ARC_PROFILE 0
@@ -858,8 +824,7 @@ __device__ unsigned long long g_dense_prof[8];
 #endif
 
 __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const int64_t *__restrict__ t, const CornerGeom &g,
-                                               const int64_t *__restrict__ item_base,
-                                               const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
+                                               const uint32_t *__restrict__ ovf, const uint4 *__restrict__ pv,
                                                const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask,
                                                uint32_t *__restrict__ res) {
     const int64_t grp = item / g.n_tiles;
@@ -874,20 +839,30 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     int tx, ty;
     tile_origin_xy(g, tile, tx, ty);
     const int x0 = tx * kTile, y0 = ty * kTile;
-    const int wx0 = x0 - kHalo, wy0 = y0 - kHalo;
     const GroupRef gr = group_ref(t, g, grp);
     const int64_t grp_first = gr.first, Lt = gr.Lt;
     const bool narrow = gr.narrow;
     const int64_t *Bg = gB + grp * HW;
 
-    // (a) the window pixel's B_g (lane wp < 484), the segment table (lanes 0..12), cleared masks
+    // (a) window pixel wp (lane wp < 484): its B_g, slice mask and value record, three loads in
+    //     flight together; its values go to the dense planes T[j][wp], the own tile's eligible
+    //     pairs (slice and pixel; the per-event cut of border mode 1 is applied when flagging)
+    //     are the test tasks
     static_assert(kArcThreads >= kWinPix, "one lane per window pixel");
     const int wp = tid;
     const bool win_lane = wp < kWinPix;
-    const int wx = wx0 + wp % kWin, wy = wy0 + wp / kWin;
+    const int ox = wp % kWin - kHalo, oy = wp / kWin - kHalo;  // pixel relative to the tile origin
+    const int wx = x0 + ox, wy = y0 + oy;
     const bool in = win_lane && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H;
-    const int64_t bq = in ? Bg[(int64_t)wy * g.W + wx] : INT64_MAX;  // INT64_MAX: outside (never read)
-    if (win_lane) L.mb[wp].mask = in ? gmask[grp * HW + (int64_t)wy * g.W + wx] : 0u;  // as in arc_kernel
+    const int64_t q = grp * HW + (int64_t)wy * g.W + wx;
+    int64_t bq = INT64_MAX;  // INT64_MAX: outside (never read)
+    uint32_t mk = 0u;
+    uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+    if (in) {
+        bq = gB[q];
+        mk = gmask[q];
+        rec = pv[q];
+    }
     for (int w = tid; w < kPairWords; w += kArcThreads) L.res[w] = 0u;
     if (tid == 0) {
         L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
@@ -896,63 +871,41 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         L.q4n = 0;
         L.n_exact = 0;
     }
-    if (wave == 0) {  // the segment table: lanes 0..12 of wave 0, prefix by DPP over the wave
-        int64_t b0 = 0;
-        int len = 0;
-        if (tid < kMaxSeg) window_segment(g, grp, tile, tid, item_base, sub_end, b0, len);
-        const int incl = ecc::wave_incl_scan(len);
-        if (tid < kMaxSeg) {
-            L.seg_lo[tid] = b0;
-            L.seg_pref[tid + 1] = incl;
-            L.seg_off[tid] = window_segment_offset(tid);
-            if (tid == 0) L.seg_pref[0] = 0;
+    const bool own = win_lane && ox >= 0 && oy >= 0 && ox < kTile && oy < kTile;
+    const uint64_t own_pairs = __ballot(own && mk != 0u);
+    if (lane == 0) L.wave_own[wave] = own_pairs != 0ull;
+    __syncthreads();  // the task counter is zeroed
+    if (win_lane) {
+        L.mb[wp].mask = mk;
+        const int p = __popc(mk);
+        uint32_t mm = mk;
+        for (int k = 0; mm && k < kRecVals - 1; ++k, mm &= mm - 1u)
+            L.T[__ffs(mm) - 1][wp] = k == 0 ? rec.x : (k == 1 ? rec.y : rec.z);
+        if (mm && p == kRecVals) {
+            L.T[__ffs(mm) - 1][wp] = rec.w;
+        } else if (mm) {  // v3.. from the overflow array, ascending j as the bits
+            overflow_values(overflow_base(ovf, rec), kRecVals - 1, p, [&](int, uint32_t v) {
+                L.T[__ffs(mm) - 1][wp] = v;
+                mm &= mm - 1u;
+            });
         }
-    }
-    __syncthreads();
-    DENSE_MARK(0);  // (a) segment table + B_g window
-    if (L.seg_pref[1] == 0) return;  // no events in the tile: nothing to flag
-    const int total = L.seg_pref[kMaxSeg];
-    int pref[kMaxSeg + 1];
-#pragma unroll
-    for (int c = 0; c <= kMaxSeg; ++c) pref[c] = L.seg_pref[c];  // uniform (SGPRs)
-
-    // (b) each entry is a distinct (slice, pixel) pair of one tile: its value goes to T, its slice
-    //     bit to the pixel's mask; the own tile's pairs (segment 0) with an eligible slice and
-    //     pixel are the test tasks (the per-event cut of border mode 1 is applied when flagging)
-    for (int i0 = 0; i0 < total; i0 += kStageUnroll * kArcThreads) {
-        PairEntry ent[kStageUnroll];
-        int sg[kStageUnroll];
-        int64_t ea[kStageUnroll];
-        // segment starts first, then the loads unconditional on clamped indices (in flight together)
-#pragma unroll
-        for (int u = 0; u < kStageUnroll; ++u) {
-            const int i = min(i0 + u * kArcThreads + tid, total - 1);
-            int r = 0;
-#pragma unroll
-            for (int c = 1; c < kMaxSeg; ++c) r += (i >= pref[c]) ? 1 : 0;
-            int pr = 0;
-#pragma unroll
-            for (int c = 1; c < kMaxSeg; ++c) pr = (r == c) ? pref[c] : pr;
-            sg[u] = (i0 + u * kArcThreads + tid < total) ? r : -1;
-            ea[u] = L.seg_lo[r] + (i - pr);
-        }
-#pragma unroll
-        for (int u = 0; u < kStageUnroll; ++u) ent[u] = entries[ea[u]];
-#pragma unroll
-        for (int u = 0; u < kStageUnroll; ++u) {
-            if (sg[u] < 0) continue;
-            const int lp = (int)(ent[u].meta & 255u), j = (int)(ent[u].meta >> 8);
-            const int ewp = L.seg_off[sg[u]] + (lp / kTile) * kWin + lp % kTile;
-            L.T[j][ewp] = ent[u].v;
-            if (sg[u] == 0 && (int64_t)grp * kGroup + j >= g.first_detect &&
-                !is_border(x0 + lp % kTile, y0 + lp / kTile, g))
-                L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)(j * kTilePix + lp);
+        if (own && !is_border(wx, wy, g)) {
+            const int lp = oy * kTile + ox;
+            for (uint32_t tm = mk & eligible_slices(g, grp); tm; tm &= tm - 1u)
+                L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)((__ffs(tm) - 1) * kTilePix + lp);
         }
     }
     const int64_t bmin = ecc::wave_min_i64(bq);  // DPP
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
-    DENSE_MARK(1);  // (b) staging
+    DENSE_MARK(0);  // (a) staging
+    {
+        int any = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) any |= L.wave_own[w];
+        if (!any) return;  // uniform: no events in the tile, nothing to flag
+    }
+    DENSE_MARK(1);
 
     // (c) clamped B_g per window pixel
     if (win_lane) {
@@ -1059,14 +1012,14 @@ struct SparseLds {
     uint32_t vals[kValCap + kWinPix];   // 17.9 KiB: the pairs + one B_g slot per window pixel
     PixInfo pix[kWinPix];               // 3.8 KiB
     uint32_t res[kPairWords];
-    uint16_t tasks[kGroup * kTilePix];  // the tile's eligible pairs (j * 196 + pixel)
+    uint16_t tasks[kValCap];  // the tile's eligible pairs (j * 196 + pixel): at most the window's pairs
     uint16_t q4[kQ4Cap];
     int64_t wave_min[kWaves];
+    int64_t wave_cmax[kWaves];  // the largest B_g at or below L (clamped to 0)
     int32_t wave_tot[kWaves];
-    int32_t exact_only, mixed, n_tasks, q4n, redo;
-    int64_t seg_lo[16];
-    int32_t seg_pref[16];
-    int32_t seg_off[16];
+    int32_t task_tot[kWaves];
+    int32_t wave_own[kWaves];  // the wave's own-tile pixels have pairs
+    int32_t exact_only, mixed, q4n, redo;
 };
 
 // Branch-free by layout: one 8-B pixel read and one value read (a conditional read compiles to
@@ -1080,7 +1033,6 @@ __device__ __forceinline__ uint32_t sparse_value(const SparseLds &L, int wp, uin
 #ifndef ECC_ARC_WAVES
 #define ECC_ARC_WAVES 8
 #endif
-constexpr int kSparseHold = kValCap / kArcThreads;  // entries per lane, held between the two passes
 
 #if ECC_ARC_PROFILE
 // profiling builds: per-workgroup wall-clock of arc_kernel's phases, summed (thread 0); [7] = items
@@ -1100,52 +1052,43 @@ __device__ unsigned long long g_arc_items[kProfItems][8];
 #define ARC_MARK(k) do { } while (0)
 #endif
 
-// One item's phase-A loads (B_g and slice mask of window pixel `tid`, the segment `tid` < 13 of the
-// window), issued by arc_prefetch ahead of their use: the persistent arc kernel issues the next
-// item's while the current item's tests run.
+// One item's phase-A loads: window pixel `tid`'s B_g, slice mask and value record, from fixed
+// per-pixel addresses (no offset table in between), so the three are in flight together.
 struct ArcPre {
     int64_t bq;   // B_g (INT64_MAX outside the sensor / past the window)
     uint32_t mk;  // slices of the group that touched the pixel
-    int64_t b0;   // segment: first entry
-    int len;      // segment: entries
+    uint4 rec;    // its values (pair_build's record)
 };
 
-__device__ __forceinline__ void arc_prefetch(ArcPre &p, int64_t item, const CornerGeom &g,
-                                             const int64_t *__restrict__ item_base, const int32_t *__restrict__ sub_end,
+__device__ __forceinline__ void arc_prefetch(ArcPre &p, int64_t item, const CornerGeom &g, const uint4 *__restrict__ pv,
                                              const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask) {
     const int tid = threadIdx.x;
     p.bq = INT64_MAX;
     p.mk = 0u;
-    p.b0 = 0;
-    p.len = 0;
-    if (item < 0) return;  // uniform
+    p.rec = make_uint4(0u, 0u, 0u, 0u);
     const int64_t HW = (int64_t)g.H * g.W;
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
     const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
     const int wx = tx * kTile - kHalo + tid % kWin, wy = ty * kTile - kHalo + tid / kWin;
     if (tid < kWinPix && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
-        const int64_t q = (int64_t)wy * g.W + wx;
-        p.bq = gB[grp * HW + q];
-        p.mk = gmask[grp * HW + q];
+        const int64_t q = grp * HW + (int64_t)wy * g.W + wx;
+        p.bq = gB[q];
+        p.mk = gmask[q];
+        p.rec = pv[q];
     }
-    if (tid < kMaxSeg) window_segment(g, grp, tile, tid, item_base, sub_end, p.b0, p.len);
 }
 
 // The arc tests of one (group, tile) item from its phase-A loads `pre`.
-//   A: segment table, wave scans of the value counts and of min B_g     -> barrier 1
-//   B: entry loads issued; pixel records, B_g slots, clamp               -> barrier 2
-//   C: tasks, value scatter                                              -> barrier 3
-//   circle 3 -> barrier 4 -> circle 4 -> barrier 5
-// The slice mask of every window pixel comes from pair_build's mask image, so its value count,
-// the wave prefix of the counts and the window minimum of B_g are all known before the first
-// barrier; the entries are loaded right after it, while the pixel records and B_g slots are
-// written, and scattered after the second.
+//   A: wave scans of the value counts and task counts, wave minimum of B_g    -> barrier 1
+//   B: pixel records, clamped B_g slots, values (overflow loads), tasks       -> barrier 2
+//   circle 3 -> barrier 3 -> circle 4 -> barrier 4
+// Every lane knows its own pixel's values, so the list offsets, the task offsets and the window
+// minimum of B_g are all wave scans before the first barrier, and each lane writes its pixel's
+// list and tasks itself (no scatter, no LDS atomics).
 __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPre &pre,
                                          const int64_t *__restrict__ t, const CornerGeom &g,
-                                         const int64_t *__restrict__ item_base, const PairEntry *__restrict__ entries,
-                                         const int32_t *__restrict__ sub_end, const int64_t *__restrict__ gB,
-                                         const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
+                                         const uint32_t *__restrict__ ovf, uint32_t *__restrict__ res,
                                          int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
     const int64_t grp = item / g.n_tiles;
     const int tile = (int)(item % g.n_tiles);
@@ -1164,68 +1107,105 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     const bool win_lane = wp < kWinPix;
     const int64_t bq = pre.bq;
     const uint32_t mk_w = pre.mk;
+    const int ox = wp % kWin - kHalo, oy = wp / kWin - kHalo;  // pixel relative to the tile origin
+    const bool own = win_lane && ox >= 0 && oy >= 0 && ox < kTile && oy < kTile;
     for (int w = tid; w < kPairWords; w += kArcThreads) L.res[w] = 0u;
     if (tid == 0) {
         L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
-        L.mixed = 0;
-        L.n_tasks = 0;
         L.q4n = 0;
         L.redo = 0;
     }
-    if (wave == 0) {  // segment table: lanes 0..12 (pre.len is 0 above), prefix by DPP
-        const int incl = ecc::wave_incl_scan(pre.len);
-        if (tid < kMaxSeg) {
-            L.seg_lo[tid] = pre.b0;
-            L.seg_pref[tid + 1] = incl;
-            L.seg_off[tid] = window_segment_offset(tid);
-            if (tid == 0) L.seg_pref[0] = 0;
-        }
-    }
+    // the own tile's eligible pairs of this pixel (Q15 slices; border pixels are never corners)
+    const uint32_t tm = (own && !is_border(x0 + ox, y0 + oy, g)) ? (mk_w & eligible_slices(g, grp)) : 0u;
     const int cnt = win_lane ? __popc(mk_w) + 1 : 0;  // the pixel's values + its B_g slot
-    // wave scan of the counts and wave minimum of B_g by DPP moves (the lane-shuffle forms were
-    // 18 LDS permutes per wave, a fifth of the kernel's LDS instructions)
+    const int tcnt = __popc(tm);
+    // wave scans and the wave minimum of B_g by DPP moves
     const int incl = ecc::wave_incl_scan(cnt);
-    if (lane == 63) L.wave_tot[wave] = incl;
+    const int tincl = ecc::wave_incl_scan(tcnt);
+    const uint64_t own_pairs = __ballot(own && mk_w != 0u);
+    // the clamped B_g values are not all equal ("mixed", so ties among them may be artefacts) iff
+    // the largest of them exceeds the window minimum: per-wave minimum and largest clamped value
     const int64_t bmin = ecc::wave_min_i64(bq);
-    if (lane == 0) L.wave_min[wave] = bmin;
+    const int64_t cmax = ecc::wave_max_i64(bq <= Lt ? bq : INT64_MIN);  // bq: INT64_MAX outside
+    // a pixel with more than 4 values: v3 .. v6 as one 16-B load, issued now (its address is in
+    // the record) so that it flies during the scans and the barrier; the other lanes of the wave
+    // load the first line of ovf (no per-lane branch around the load)
+    const int p = cnt - 1;
+    uint4 xa = make_uint4(0u, 0u, 0u, 0u), xb = xa;
+#ifndef ECC_ARC_XPF
+#define ECC_ARC_XPF 1  // 16-B overflow lines loaded before barrier 1 (0: none, after it)
+#endif
+    if (ECC_ARC_XPF && __ballot(p > kRecVals)) {  // uniform
+        const uint4 *x4 = reinterpret_cast<const uint4 *>(ovf) + (p > kRecVals ? pre.rec.w : 0u);
+        xa = x4[0];
+        if (ECC_ARC_XPF > 1) xb = x4[1];
+    }
+    if (lane == 63) {
+        L.wave_tot[wave] = incl;
+        L.task_tot[wave] = tincl;
+    }
+    if (lane == 0) {
+        L.wave_min[wave] = bmin;
+        L.wave_cmax[wave] = cmax;
+        L.wave_own[wave] = own_pairs != 0ull;
+    }
     __syncthreads();  // 1
     ARC_MARK(0);  // A
-    const int total = L.seg_pref[kMaxSeg];
-    if (L.seg_pref[1] == 0 || total > kValCap) {  // uniform
+    int total = 0, n_tasks = 0, any_own = 0, off = incl - cnt, toff = tincl - tcnt;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {  // uniform reads, in flight together
+        const int wt = L.wave_tot[w], tt = L.task_tot[w];
+        total += wt;
+        n_tasks += tt;
+        off += w < wave ? wt : 0;
+        toff += w < wave ? tt : 0;
+        any_own |= L.wave_own[w];
+    }
+    if (wave == 0) {  // lane w takes wave w's pair; L.mixed is read after barrier 2
+        const int64_t vz = ecc::wave_min_i64(lane < kWaves ? L.wave_min[lane] : INT64_MAX);
+        const int64_t cm = ecc::wave_max_i64(lane < kWaves ? L.wave_cmax[lane] : INT64_MIN);
+        if (lane == 0) L.mixed = cm > vz;
+    }
+    if (!any_own || total > kValCap + kWinPix) {  // uniform
         // no events in the tile: nothing to flag; too many values for the compact list: the
         // dense kernel takes it
-        if (total > kValCap && L.seg_pref[1] != 0 && tid == 0) over[atomicAdd(n_over, 1u)] = item;
+        if (any_own && tid == 0) over[atomicAdd(n_over, 1u)] = item;
         return;
     }
-    int pref[kMaxSeg + 1];
-#pragma unroll
-    for (int c = 0; c <= kMaxSeg; ++c) pref[c] = L.seg_pref[c];  // uniform
-    PairEntry ent[kSparseHold];
-    int ewp[kSparseHold];
-    const int slots = (total + kArcThreads - 1) / kArcThreads;  // uniform: the slots in use
-    // (measured slower: clamped unconditional entry loads behind a separate address pass, 15 us;
-    // every wave scanning the 13 segments itself so the loads issue before barrier 1, 10 us)
-#pragma unroll
-    for (int u = 0; u < kSparseHold; ++u) {
-        ewp[u] = -1;
-        if (u >= slots) continue;
-        const int i = u * kArcThreads + tid;
-        int r = 0;
-#pragma unroll
-        for (int c = 1; c < kMaxSeg; ++c) r += (i >= pref[c]) ? 1 : 0;
-        ent[u] = (i < total) ? entries[L.seg_lo[r] + (i - L.seg_pref[r])] : PairEntry{0u, 0u};
-        ewp[u] = (i < total) ? r : -1;
-    }
     if (win_lane) {
-        int off = incl - cnt;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) off += w < wave ? L.wave_tot[w] : 0;  // reads in flight together
-        int64_t vz = INT64_MAX;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
-        const uint32_t bcv = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
+        uint32_t bcv = 0u;  // clamp(B_g - L, 0, 2^27 - 1); above the range: the exact kernel
+        if (narrow && bq != INT64_MAX && bq > Lt) {
+            const int64_t d = bq - Lt;
+            if (d > (int64_t)kVMax) L.exact_only = 1;
+            bcv = d > (int64_t)kVMax ? kVMax : (uint32_t)d;
+        }
         reinterpret_cast<uint2 *>(L.pix)[wp] = make_uint2(mk_w, (uint32_t)off);
-        L.vals[off] = bcv;
+        uint32_t *dst = L.vals + off;
+        dst[0] = bcv;
+        if (p > 0) dst[1] = pre.rec.x;
+        if (p > 1) dst[2] = pre.rec.y;
+        if (p > 2) dst[3] = pre.rec.z;
+        if (p == kRecVals) {
+            dst[4] = pre.rec.w;
+        } else if (!ECC_ARC_XPF && p > kRecVals) {
+            overflow_values(overflow_base(ovf, pre.rec), kRecVals - 1, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
+        } else if (p > kRecVals) {  // v3 .. v6 from the prefetched line, the rest loaded now
+            dst[4] = xa.x;  // v_k goes to dst[1 + k] for k < p (here p >= 5)
+            dst[5] = xa.y;
+            if (p > 5) dst[6] = xa.z;
+            if (p > 6) dst[7] = xa.w;
+            if (ECC_ARC_XPF > 1) {
+                if (p > 7) dst[8] = xb.x;
+                if (p > 8) dst[9] = xb.y;
+                if (p > 9) dst[10] = xb.z;
+                if (p > 10) dst[11] = xb.w;
+            }
+            if (p > kRecVals + 4 * ECC_ARC_XPF - 1)
+                overflow_values(overflow_base(ovf, pre.rec), kRecVals + 4 * ECC_ARC_XPF - 1, p,
+                                [&](int k, uint32_t v) { dst[1 + k] = v; });
+        }
+        const int lp = oy * kTile + ox;
+        for (uint32_t m = tm; m; m &= m - 1u) L.tasks[toff++] = (uint16_t)((__ffs(m) - 1) * kTilePix + lp);
     }
     __syncthreads();  // 2
     ARC_MARK(1);  // B
@@ -1233,20 +1213,6 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
         return;
     }
-#pragma unroll
-    for (int u = 0; u < kSparseHold; ++u) {
-        if (u >= slots) break;
-        if (ewp[u] < 0) continue;
-        const int r = ewp[u];
-        const int lp = (int)(ent[u].meta & 255u), j = (int)(ent[u].meta >> 8);
-        const int e = window_segment_offset(r) + (lp / kTile) * kWin + lp % kTile;
-        if (r == 0 && (int64_t)grp * kGroup + j >= g.first_detect && !is_border(x0 + lp % kTile, y0 + lp / kTile, g))
-            L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)(j * kTilePix + lp);
-        const PixInfo pq = L.pix[e];
-        L.vals[pq.off + 1u + __popc(pq.mask & ((1u << j) - 1u))] = ent[u].v;
-    }
-    __syncthreads();  // 3
-    ARC_MARK(2);  // C
     // Tests through the compact lists, on clamped 32-bit keys only.  No exact int64 path and no
     // call: an item its keys cannot decide (a wide group, a value above t_last, a tie the clamping
     // may have merged) or whose circle-3 survivors overflow the queue goes whole to
@@ -1254,7 +1220,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
 #ifndef ECC_ARC_SKIP
 #define ECC_ARC_SKIP 0  // timing experiments only (wrong results): 1 = no circle 4, 2 = no tests
 #endif
-    const int n_tasks = ECC_ARC_SKIP >= 2 ? 0 : L.n_tasks;
+    if (ECC_ARC_SKIP >= 2) n_tasks = 0;
     const bool ties_exact = !L.mixed;
     for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
         const int pi = L.tasks[ti];
@@ -1273,7 +1239,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
             L.redo = 1;
         }
     }
-    __syncthreads();  // 4
+    __syncthreads();  // 3
     ARC_MARK(3);  // circle 3
     if (L.redo) {  // uniform
         if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
@@ -1300,7 +1266,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         if (r4 > 0) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
         else if (r4 < 0) L.redo = 1;
     }
-    __syncthreads();  // 5
+    __syncthreads();  // 4
     ARC_MARK(4);  // circle 4
 #if ECC_ARC_PROFILE
     if (tid == 0 && item < kProfItems) {
@@ -1319,17 +1285,16 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
 // runs on XCD b % 8, so XCD x takes the contiguous item range [x * per, (x + 1) * per) —
 // neighbouring tiles of one group share that XCD's L2.
 __global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)  // waves/SIMD: 8 = four 8-wave workgroups per CU
-arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const int64_t *__restrict__ item_base,
-           const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
-           const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res,
-           int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
+arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const uint32_t *__restrict__ ovf,
+           const uint4 *__restrict__ pv, const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask,
+           uint32_t *__restrict__ res, int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
     __shared__ SparseLds L;
     const int64_t per = gridDim.x / 8;
     const int64_t item = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
     if (item >= n_items) return;
     ArcPre pre;
-    arc_prefetch(pre, item, g, item_base, sub_end, gB, gmask);
-    arc_item(L, item, pre, t, g, item_base, entries, sub_end, gB, gmask, res, over, n_over);
+    arc_prefetch(pre, item, g, pv, gB, gmask);
+    arc_item(L, item, pre, t, g, ovf, res, over, n_over);
 }
 
 
@@ -1337,13 +1302,12 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const i
 // dense per-slice planes.
 __global__ void __launch_bounds__(kArcThreads, 4)  // 4 waves/SIMD: two 8-wave workgroups per CU
 arc_dense_kernel(const int64_t *__restrict__ t, CornerGeom g, const int64_t *__restrict__ over,
-                 const uint32_t *__restrict__ n_over, const int64_t *__restrict__ item_base,
-                 const PairEntry *__restrict__ entries, const int32_t *__restrict__ sub_end,
+                 const uint32_t *__restrict__ n_over, const uint32_t *__restrict__ ovf, const uint4 *__restrict__ pv,
                  const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res) {
     __shared__ ArcLds L;
     const uint32_t n = *n_over;
     for (uint32_t li = blockIdx.x; li < n; li += gridDim.x) {
-        arc_dense_item(L, over[li], t, g, item_base, entries, sub_end, gB, gmask, res);
+        arc_dense_item(L, over[li], t, g, ovf, pv, gB, gmask, res);
         __syncthreads();
     }
 }
@@ -1564,9 +1528,8 @@ struct GroupImages {
     uint32_t *mask;       // [n_groups][H*W] slices of the group that touched the pixel
     int64_t *B;           // [n_groups][H*W] last t of the group, then (in place) B_g
     uint32_t *res;        // [n_groups][32][n_tiles][kSegWords] corner (slice, pixel) pairs, slice-major
-    PairEntry *entries;   // [n] distinct (slice, pixel) pairs per item, at item_base[item]
-    int64_t *item_base;   // [n_items]
-    int32_t *sub_end;     // [n_items][kSub] sub-region ends inside each item's entries
+    uint4 *pv;            // [n_groups][H*W] value record of each (group, pixel) (pair_build)
+    uint32_t *ovf;        // [n] the values past a record's first three, in each item's part of the range
     int64_t *over;        // [n_items] items arc_kernel leaves to arc_dense_kernel (heavy or undecidable)
     uint32_t *n_over;     // [0]: their count
 };
@@ -1582,9 +1545,8 @@ Sorted carve_sorted(Carve &cv, const CornerGeom &g, int64_t n_items, int64_t n_g
     gi->mask = cv.take<uint32_t>(img);
     gi->B = cv.take<int64_t>(img);
     gi->res = cv.take<uint32_t>((size_t)n_groups * kGroup * g.seg_stride);
-    gi->entries = cv.take<PairEntry>((size_t)g.n);
-    gi->item_base = cv.take<int64_t>((size_t)n_items);
-    gi->sub_end = cv.take<int32_t>((size_t)n_items * kSub);
+    gi->pv = cv.take<uint4>(img);
+    gi->ovf = cv.take<uint32_t>((size_t)g.n + 4 * (size_t)n_items + 8);
     gi->over = cv.take<int64_t>((size_t)n_items);
     gi->n_over = cv.take<uint32_t>(64);
     return so;
@@ -1690,6 +1652,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     const int64_t n_groups = (g.n_slices + kGroup - 1) / kGroup;
     const int64_t n_items = n_groups * g.n_tiles;  // work items: (group, tile)
     if (n_items > (int64_t)INT32_MAX - 8) return ECC_ERR_INVALID;
+    if ((n + 4 * n_items) / 4 >= (int64_t)UINT32_MAX) return ECC_ERR_INVALID;  // 16-B overflow index in a u32
     int32_t *first_border = nullptr;
     GroupImages gi{};
     Carve measure{nullptr};
@@ -1719,8 +1682,8 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     }
     {
         ECC_TIMED(ctx, s, "pair_build_kernel");
-        hipLaunchKernelGGL(pair_build_kernel, dim3((unsigned)n_items), dim3(kThreads), 0, s, t, g, so, gi.entries,
-                           gi.item_base, gi.sub_end, gi.mask, gi.B);
+        hipLaunchKernelGGL(pair_build_kernel, dim3((unsigned)n_items), dim3(kThreads), 0, s, t, g, so, gi.ovf, gi.pv,
+                           gi.mask, gi.B);
     }
     if (local_last) {
         ECC_TIMED(ctx, s, "sae_local_last_kernel");
@@ -1751,15 +1714,14 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         {
             const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
             hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
-                               (const int64_t *)gi.item_base, (const PairEntry *)gi.entries, (const int32_t *)gi.sub_end,
-                               (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over);
+                               (const uint32_t *)gi.ovf, (const uint4 *)gi.pv, (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over);
         }
     }
     {
         ECC_TIMED(ctx, s, "arc_dense_kernel");  // the items arc_kernel left: dense planes, exact tests
         hipLaunchKernelGGL(arc_dense_kernel, dim3(512), dim3(kArcThreads), 0, s, t, g, (const int64_t *)gi.over,
-                           (const uint32_t *)gi.n_over, (const int64_t *)gi.item_base, (const PairEntry *)gi.entries,
-                           (const int32_t *)gi.sub_end, (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res);
+                           (const uint32_t *)gi.n_over, (const uint32_t *)gi.ovf, (const uint4 *)gi.pv,
+                           (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res);
     }
     {
         ECC_TIMED(ctx, s, "flags_kernel");

@@ -194,6 +194,9 @@ __device__ __forceinline__ int64_t wave_reduce_i64(int64_t v, int64_t identity, 
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
     return wave_reduce_i64(v, INT64_MAX, [](int64_t a, int64_t b) { return a < b ? a : b; });
 }
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+    return wave_reduce_i64(v, INT64_MIN, [](int64_t a, int64_t b) { return a > b ? a : b; });
+}
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
     return wave_reduce_i64(v, 0, [](int64_t a, int64_t b) { return a + b; });
 }

@@ -26,6 +26,6 @@ for rep in range(3):
     ctx.sync()
     prof(o, C.byref(tpu))
     items = max(o[7], 1)
-    names = ["A: loads + scans", "B: records + clamp", "C: tasks + scatter", "circle 3", "circle 4"]
+    names = ["A: loads + scans", "B: records + clamp", "C: (head: tasks + scatter)", "circle 3", "circle 4"]
     print(f"rep {rep}: {items} items, {o[5] / items:.1f} circle-3 / {o[6] / items:.1f} circle-4 tests/item; per item (us): " +
           ", ".join(f"{nm} {o[k] / tpu.value / items:.2f}" for k, nm in enumerate(names)), flush=True)
