@@ -1001,7 +1001,10 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
 // the pixel, so a lookup is one 8-B pixel read and one value read, no select.  ~34 KB of LDS
 // instead of the dense planes' ~80 KB: four 8-wave workgroups per CU.  Windows with more than
 // kValCap values go to the overflow list (arc_dense_kernel).
-constexpr int kValCap = 4096;
+#ifndef ECC_ARC_VALCAP
+#define ECC_ARC_VALCAP 4096
+#endif
+constexpr int kValCap = ECC_ARC_VALCAP;
 
 struct PixInfo {
     uint32_t mask;  // slices of the group that touched the pixel
