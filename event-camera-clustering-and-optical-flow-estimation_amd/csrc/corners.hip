@@ -1017,10 +1017,9 @@ struct SparseLds {
     uint32_t res[kPairWords];
     uint16_t tasks[kValCap];  // the tile's eligible pairs (j * 196 + pixel): at most the window's pairs
     uint16_t q4[kQ4Cap];
-    int64_t wave_min[kWaves];
-    int64_t wave_cmax[kWaves];  // the largest B_g at or below L (clamped to 0)
+    int64_t wave_c0[kWaves];    // the wave's first B_g at or below L (clamped to 0) ...
+    int32_t wave_cf[kWaves];    // ... bit 1: it has one, bit 0: another differs from it
     int32_t wave_tot[kWaves];
-    int32_t task_tot[kWaves];
     int32_t wave_own[kWaves];  // the wave's own-tile pixels have pairs
     int32_t exact_only, mixed, q4n, redo;
 };
@@ -1123,13 +1122,24 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     const int cnt = win_lane ? __popc(mk_w) + 1 : 0;  // the pixel's values + its B_g slot
     const int tcnt = __popc(tm);
     // wave scans and the wave minimum of B_g by DPP moves
-    const int incl = ecc::wave_incl_scan(cnt);
-    const int tincl = ecc::wave_incl_scan(tcnt);
+    // one scan of both counts, packed (task count << 16 | value count: a workgroup's sums stay
+    // below 2^16, at most 484 * 33 values and 196 * 32 tasks)
+    const int both = ecc::wave_incl_scan(tcnt << 16 | cnt);
+    const int incl = both & 0xffff, tincl = both >> 16;
     const uint64_t own_pairs = __ballot(own && mk_w != 0u);
-    // the clamped B_g values are not all equal ("mixed", so ties among them may be artefacts) iff
-    // the largest of them exceeds the window minimum: per-wave minimum and largest clamped value
-    const int64_t bmin = ecc::wave_min_i64(bq);
-    const int64_t cmax = ecc::wave_max_i64(bq <= Lt ? bq : INT64_MIN);  // bq: INT64_MAX outside
+    // the clamped B_g values (at or below L) are "mixed" when not all equal: ties among their keys
+    // may then be artefacts of the clamp.  Per wave: its first clamped value and whether another
+    // clamped value differs (ballots and two readlanes, no 64-bit reductions)
+    const bool clp = bq <= Lt;  // bq: INT64_MAX outside the sensor
+    const uint64_t cball = __ballot(clp);
+    int64_t c0 = 0;
+    int cf = 0;
+    if (cball) {  // uniform
+        const int f = __ffsll((unsigned long long)cball) - 1;
+        c0 = (int64_t)((uint64_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)bq >> 32), f) << 32 |
+                       (uint64_t)__builtin_amdgcn_readlane((uint32_t)bq, f));
+        cf = 2 | (__ballot(clp && bq != c0) != 0ull ? 1 : 0);
+    }
     // a pixel with more than 4 values: v3 .. v6 as one 16-B load, issued now (its address is in
     // the record) so that it flies during the scans and the barrier; the other lanes of the wave
     // load the first line of ovf (no per-lane branch around the load)
@@ -1143,13 +1153,10 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         xa = x4[0];
         if (ECC_ARC_XPF > 1) xb = x4[1];
     }
-    if (lane == 63) {
-        L.wave_tot[wave] = incl;
-        L.task_tot[wave] = tincl;
-    }
+    if (lane == 63) L.wave_tot[wave] = both;
     if (lane == 0) {
-        L.wave_min[wave] = bmin;
-        L.wave_cmax[wave] = cmax;
+        L.wave_c0[wave] = c0;
+        L.wave_cf[wave] = cf;
         L.wave_own[wave] = own_pairs != 0ull;
     }
     __syncthreads();  // 1
@@ -1157,17 +1164,25 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     int total = 0, n_tasks = 0, any_own = 0, off = incl - cnt, toff = tincl - tcnt;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) {  // uniform reads, in flight together
-        const int wt = L.wave_tot[w], tt = L.task_tot[w];
+        const int wb = L.wave_tot[w], wt = wb & 0xffff, tt = wb >> 16;
         total += wt;
         n_tasks += tt;
         off += w < wave ? wt : 0;
         toff += w < wave ? tt : 0;
         any_own |= L.wave_own[w];
     }
-    if (wave == 0) {  // lane w takes wave w's pair; L.mixed is read after barrier 2
-        const int64_t vz = ecc::wave_min_i64(lane < kWaves ? L.wave_min[lane] : INT64_MAX);
-        const int64_t cm = ecc::wave_max_i64(lane < kWaves ? L.wave_cmax[lane] : INT64_MIN);
-        if (lane == 0) L.mixed = cm > vz;
+    if (wave == 0) {  // lane w takes wave w's flags; L.mixed is read after barrier 2
+        const int wf = lane < kWaves ? L.wave_cf[lane] : 0;
+        const int64_t wv = lane < kWaves ? L.wave_c0[lane] : 0;
+        const uint64_t has = __ballot(wf & 2);
+        bool mixed = __ballot(wf & 1) != 0ull;
+        if (has) {  // uniform
+            const int f = __ffsll((unsigned long long)has) - 1;
+            const int64_t v0 = (int64_t)((uint64_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)wv >> 32), f) << 32 |
+                                         (uint64_t)__builtin_amdgcn_readlane((uint32_t)wv, f));
+            mixed = mixed || __ballot((wf & 2) && wv != v0) != 0ull;
+        }
+        if (lane == 0) L.mixed = mixed;
     }
     if (!any_own || total > kValCap + kWinPix) {  // uniform
         // no events in the tile: nothing to flag; too many values for the compact list: the
