@@ -336,7 +336,7 @@ __device__ __forceinline__ void tile_segs(const CornerGeom &g, const Sorted &so,
         len = row[tile + 1] - a;
     }
     const int incl = ecc::wave_incl_scan(len);         // DPP (wave 0: all 64 lanes)
-    const int64_t asum = ecc::wave_sum_i64((int64_t)a);
+    const int asum = ecc::wave_sum_i32(a);  // < 32 * S <= 2^24: a 32-bit sum
     if (tid < kGroup) {
         T.start[tid] = s * g.S + a;
         T.pref[tid + 1] = incl;
@@ -406,8 +406,8 @@ pair_build_kernel(const int64_t *__restrict__ t, CornerGeom g, Sorted so, uint32
     __shared__ TileSegs segs;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t item = blockIdx.x;
-    const int64_t grp = item / g.n_tiles;
-    const int tile = (int)(item % g.n_tiles);
+    const int64_t grp = (int)item / g.n_tiles;  // n_items < 2^31 (host check): 32-bit division
+    const int tile = (int)item % g.n_tiles;
     const int lp = tid < kTilePix ? tid : 0;  // this lane's tile pixel
     {
         uint4 *z = reinterpret_cast<uint4 *>(&tab[0][0]);
@@ -708,6 +708,7 @@ struct ArcLds {
     int32_t wave_own[kWaves];  // the wave's own-tile pixels have pairs
 };
 
+// arc_dense_kernel's clamp: v <= L maps to 0 (mixed_flag set when v is not the window minimum vz)
 __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, int32_t *exact_flag,
                                               int32_t *mixed_flag) {
     if (v <= L) {
@@ -716,6 +717,48 @@ __device__ __forceinline__ uint32_t clamp_rel(int64_t v, int64_t L, int64_t vz, 
     }
     const int64_t d = v - L;
     if (d > (int64_t)kVMax) { *exact_flag = 1; return kVMax; }
+    return (uint32_t)d;
+}
+
+// The clamped B_g values (at or below L) are "mixed" when not all equal: ties among their keys may
+// then be artefacts of the clamp.  Per wave: its first clamped value c0 and flags cf (bit 1: it has
+// one, bit 0: another differs), by ballots and readlanes (no 64-bit reductions); bq = INT64_MAX
+// outside the sensor.
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int l) {
+    return (int64_t)((uint64_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), l) << 32 |
+                     (uint64_t)__builtin_amdgcn_readlane((uint32_t)v, l));
+}
+__device__ __forceinline__ void clamp_wave_flags(int64_t bq, int64_t Lt, int64_t &c0, int &cf) {
+    const bool clp = bq <= Lt;
+    const uint64_t cball = __ballot(clp);
+    c0 = 0;
+    cf = 0;
+    if (cball) {  // uniform
+        c0 = readlane_i64(bq, __ffsll((unsigned long long)cball) - 1);
+        cf = 2 | (__ballot(clp && bq != c0) != 0ull ? 1 : 0);
+    }
+}
+// Wave 0 after the barrier: lane w takes wave w's (c0, cf); the window's "mixed" flag.
+template <int W>
+__device__ __forceinline__ bool clamp_mixed(const int64_t *wc0, const int32_t *wcf, int lane) {
+    const int wf = lane < W ? wcf[lane] : 0;
+    const int64_t wv = lane < W ? wc0[lane] : 0;
+    const uint64_t has = __ballot(wf & 2);
+    bool mixed = __ballot(wf & 1) != 0ull;
+    if (has) {  // uniform
+        const int64_t v0 = readlane_i64(wv, __ffsll((unsigned long long)has) - 1);
+        mixed = mixed || __ballot((wf & 2) && wv != v0) != 0ull;
+    }
+    return mixed;
+}
+// clamp(B_g - L, 0, 2^27 - 1); above the range the window goes to the exact test (*exact_flag)
+__device__ __forceinline__ uint32_t clamp_value(int64_t bq, int64_t Lt, bool narrow, int32_t *exact_flag) {
+    if (!narrow || bq == INT64_MAX || bq <= Lt) return 0u;
+    const int64_t d = bq - Lt;
+    if (d > (int64_t)kVMax) {
+        *exact_flag = 1;
+        return kVMax;
+    }
     return (uint32_t)d;
 }
 
@@ -827,8 +870,8 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
                                                const uint32_t *__restrict__ ovf, const uint4 *__restrict__ pv,
                                                const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask,
                                                uint32_t *__restrict__ res) {
-    const int64_t grp = item / g.n_tiles;
-    const int tile = (int)(item % g.n_tiles);
+    const int64_t grp = (int)item / g.n_tiles;  // n_items < 2^31 (host check): 32-bit division
+    const int tile = (int)item % g.n_tiles;
     if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #if ECC_ARC_PROFILE
@@ -1069,8 +1112,8 @@ __device__ __forceinline__ void arc_prefetch(ArcPre &p, int64_t item, const Corn
     p.mk = 0u;
     p.rec = make_uint4(0u, 0u, 0u, 0u);
     const int64_t HW = (int64_t)g.H * g.W;
-    const int64_t grp = item / g.n_tiles;
-    const int tile = (int)(item % g.n_tiles);
+    const int64_t grp = (int)item / g.n_tiles;  // n_items < 2^31 (host check): 32-bit division
+    const int tile = (int)item % g.n_tiles;
     const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
     const int wx = tx * kTile - kHalo + tid % kWin, wy = ty * kTile - kHalo + tid / kWin;
     if (tid < kWinPix && wx >= 0 && wy >= 0 && wx < g.W && wy < g.H) {
@@ -1092,8 +1135,8 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
                                          const int64_t *__restrict__ t, const CornerGeom &g,
                                          const uint32_t *__restrict__ ovf, uint32_t *__restrict__ res,
                                          int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
-    const int64_t grp = item / g.n_tiles;
-    const int tile = (int)(item % g.n_tiles);
+    const int64_t grp = (int)item / g.n_tiles;  // n_items < 2^31 (host check): 32-bit division
+    const int tile = (int)item % g.n_tiles;
     if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #if ECC_ARC_PROFILE
@@ -1127,19 +1170,9 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     const int both = ecc::wave_incl_scan(tcnt << 16 | cnt);
     const int incl = both & 0xffff, tincl = both >> 16;
     const uint64_t own_pairs = __ballot(own && mk_w != 0u);
-    // the clamped B_g values (at or below L) are "mixed" when not all equal: ties among their keys
-    // may then be artefacts of the clamp.  Per wave: its first clamped value and whether another
-    // clamped value differs (ballots and two readlanes, no 64-bit reductions)
-    const bool clp = bq <= Lt;  // bq: INT64_MAX outside the sensor
-    const uint64_t cball = __ballot(clp);
-    int64_t c0 = 0;
-    int cf = 0;
-    if (cball) {  // uniform
-        const int f = __ffsll((unsigned long long)cball) - 1;
-        c0 = (int64_t)((uint64_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)bq >> 32), f) << 32 |
-                       (uint64_t)__builtin_amdgcn_readlane((uint32_t)bq, f));
-        cf = 2 | (__ballot(clp && bq != c0) != 0ull ? 1 : 0);
-    }
+    int64_t c0;
+    int cf;
+    clamp_wave_flags(bq, Lt, c0, cf);  // the window's "mixed" clamp, per wave
     // a pixel with more than 4 values: v3 .. v6 as one 16-B load, issued now (its address is in
     // the record) so that it flies during the scans and the barrier; the other lanes of the wave
     // load the first line of ovf (no per-lane branch around the load)
@@ -1171,17 +1204,8 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         toff += w < wave ? tt : 0;
         any_own |= L.wave_own[w];
     }
-    if (wave == 0) {  // lane w takes wave w's flags; L.mixed is read after barrier 2
-        const int wf = lane < kWaves ? L.wave_cf[lane] : 0;
-        const int64_t wv = lane < kWaves ? L.wave_c0[lane] : 0;
-        const uint64_t has = __ballot(wf & 2);
-        bool mixed = __ballot(wf & 1) != 0ull;
-        if (has) {  // uniform
-            const int f = __ffsll((unsigned long long)has) - 1;
-            const int64_t v0 = (int64_t)((uint64_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)wv >> 32), f) << 32 |
-                                         (uint64_t)__builtin_amdgcn_readlane((uint32_t)wv, f));
-            mixed = mixed || __ballot((wf & 2) && wv != v0) != 0ull;
-        }
+    if (wave == 0) {  // L.mixed is read after barrier 2
+        const bool mixed = clamp_mixed<kWaves>(L.wave_c0, L.wave_cf, lane);
         if (lane == 0) L.mixed = mixed;
     }
     if (!any_own || total > kValCap + kWinPix) {  // uniform
@@ -1191,12 +1215,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         return;
     }
     if (win_lane) {
-        uint32_t bcv = 0u;  // clamp(B_g - L, 0, 2^27 - 1); above the range: the exact kernel
-        if (narrow && bq != INT64_MAX && bq > Lt) {
-            const int64_t d = bq - Lt;
-            if (d > (int64_t)kVMax) L.exact_only = 1;
-            bcv = d > (int64_t)kVMax ? kVMax : (uint32_t)d;
-        }
+        const uint32_t bcv = clamp_value(bq, Lt, narrow, &L.exact_only);  // above the range: the exact kernel
         reinterpret_cast<uint2 *>(L.pix)[wp] = make_uint2(mk_w, (uint32_t)off);
         uint32_t *dst = L.vals + off;
         dst[0] = bcv;
@@ -1307,8 +1326,8 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const u
            const uint4 *__restrict__ pv, const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask,
            uint32_t *__restrict__ res, int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
     __shared__ SparseLds L;
-    const int64_t per = gridDim.x / 8;
-    const int64_t item = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    const int per = (int)(gridDim.x / 8);
+    const int64_t item = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
     if (item >= n_items) return;
     ArcPre pre;
     arc_prefetch(pre, item, g, pv, gB, gmask);
