@@ -49,14 +49,18 @@ KMEANS_KERNELS = ("kmeans_count_kernel", "kmeans_count_sum_kernel", "kmeans_exte
 NMS_KERNELS = ("nms_compact_kernel", "nms_kernel")
 
 
-def parse():
+PRESET_SLICES = {"c4": 1221, "c5": 3052}  # 20 004 864 / 50 003 968 events per GPU
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--preset", choices=("c4", "c5"), default="c4",
+    ap.add_argument("--preset", choices=("c4", "c5"), default=None,
                     help="c4: 20.0 M events per GPU (1221 slices, BASELINE C4, the metric's config); "
-                         "c5: 50.0 M events per GPU (3052 slices; 8 GPUs = the 400 M-event stream of C5)")
+                         "c5: 50.0 M events per GPU (3052 slices; 8 GPUs = the 400 M-event stream of C5). "
+                         "Default: c4 on one GPU, c5 when --gpus > 1 (the multi-GPU line is BASELINE C5)")
     ap.add_argument("--events", type=int, default=None, help="events per GPU per step (overrides --preset)")
     ap.add_argument("--width", type=int, default=346)
     ap.add_argument("--height", type=int, default=260)
@@ -87,9 +91,13 @@ def parse():
     ap.add_argument("--overlap", action="store_true",
                     help="keep the two-stream sharded schedule under gloo too (correctness rehearsals; gloo "
                          "collectives block the host, so it is not a timing configuration)")
-    a = ap.parse_args()
+    ap.add_argument("--no-n1-rate", action="store_true",
+                    help="sharded runs: skip rank 0's single-GPU rate at the same per-GPU size (per_gpu_rate_n1)")
+    a = ap.parse_args(argv)
+    if a.preset is None:
+        a.preset = "c5" if a.gpus > 1 else "c4"
     if a.events is None:
-        a.events = {"c4": 1221, "c5": 3052}[a.preset] * SLICE
+        a.events = PRESET_SLICES[a.preset] * SLICE
     return a
 
 
@@ -229,7 +237,7 @@ def main():
     # single GPU: downsample -> k-means and the corner chain read the same resident batch and are
     # independent, so they run on two streams (fork/join with events) and overlap
     s2, ev_fork, ev_join = ecc.P(), ecc.P(), ecc.P()
-    if not dist:
+    if not dist or rank == 0:  # sharded: rank 0's single-GPU rate at the same size (per_gpu_rate_n1)
         # the k-means chain's stream (a priority or a CU split for it measured no faster: DESIGN §5)
         ecc.check(lib.ecc_stream_create(ecc.C.byref(s2)), "stream")
         ecc.check(lib.ecc_event_create(ecc.C.byref(ev_fork)), "event")
@@ -285,6 +293,10 @@ def main():
             # gloo collectives block the host, so its timing runs keep one stream (measured faster);
             # --overlap keeps the two-stream schedule for correctness rehearsals
             return step_sharded(nb, serial or (args.dist_backend != "nccl" and not args.overlap))
+        return step_single(serial, nb)
+
+    def step_single(serial=args.serial, nb=0):
+        """The single-GPU step: downsample -> k-means on the second stream beside detect + NMS."""
         ks = ctx.stream if serial else s2.value  # the k-means chain's stream
         ecc.check(lib.ecc_event_record(ev_fork, ctx.stream))
         ecc.check(lib.ecc_stream_wait_event(ks, ev_fork))
@@ -313,6 +325,28 @@ def main():
             raise RuntimeError("corner_nms reported a status error")
     if dist and lib.ecc_kmeans_counts_status(ctx.ctx, ctx.stream) != 0:
         raise RuntimeError("a representative lies outside the k-means count frame")
+
+    # sharded runs: rank 0's single-GPU rate at the same per-GPU size, measured in this job before
+    # the sharded timed region (the other ranks wait at the barrier), so that the line itself
+    # carries the N=1 reference of its scaling efficiency
+    per_gpu_rate_n1 = None
+    if dist and rank == 0 and not args.no_n1_rate:
+        for _ in range(max(1, args.warmup)):
+            step_single(args.serial)
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step_single(args.serial)
+        ctx.sync()
+        dt1 = time.perf_counter() - t0
+        if ctx.fast_detect_status() != 0 or ctx.corner_nms_status() != 0:
+            raise RuntimeError("single-GPU reference steps reported a status error")
+        per_gpu_rate_n1 = {"value": round(args.steps * n / dt1 / 1e6, 2), "unit": "Mevents/s",
+                           "ms_per_step": round(dt1 / args.steps * 1e3, 3), "events_per_gpu": n,
+                           "how": "rank 0, the single-GPU two-stream step (no collectives) over the same "
+                                  f"{n}-event shard, {args.steps} steps after warm-up, in this job"}
+    if dist:
+        dist.barrier()
     n_reps = int(uniq.numpy().sum())
     # --graph: the step's ~40 launches and memsets are captured once into a HIP graph
     # (ecc_graph_*) and replayed — the same kernels on the same buffers, without per-launch
@@ -407,11 +441,21 @@ def main():
             "bytes_note": "9 B/representative: 4 B read by the count pass, 4 B by the label pass, 1 B label",
             "gpoint_passes_s": round(n_reps * (I + 1) / (t_stage["kmeans"] * 1e-3) / 1e9, 2)}
     e2e_bytes = sum(bytes_stage.values())
+    # the bytes this pipeline must actually move: the count-image k-means never moves §8d's
+    # 8 B/point/pass, so its 9 B/representative replace them (downsample + k-means + corner)
+    pipe_bytes = bytes_stage["downsample"] + 9.0 * n_reps + bytes_stage["corner"]
     stages["nms"] = {"ms_per_step": round(stage_ms(NMS_KERNELS), 4), "bound": "latency"}
-    stages["e2e"] = {"ms_per_step": round(ms_step, 4), "algorithmic_bytes": e2e_bytes,
-                     "achieved_gbs": round(e2e_bytes / (ms_step * 1e-3) / 1e9, 1),
-                     "frac": round(e2e_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "note": "wall time of the whole step (both streams) over the three stages' §8d bytes"}
+    pipe_gbs = pipe_bytes / (ms_step * 1e-3) / 1e9
+    s8d_gbs = e2e_bytes / (ms_step * 1e-3) / 1e9
+    stages["e2e"] = {"ms_per_step": round(ms_step, 4),
+                     "pipeline_bytes": pipe_bytes, "achieved_gbs": round(pipe_gbs, 1),
+                     "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),
+                     "algorithmic_bytes_s8d": e2e_bytes, "achieved_gbs_s8d": round(s8d_gbs, 1),
+                     "frac_s8d": round(s8d_gbs / HBM_PEAK_GBS, 4),
+                     "note": "wall time of the whole step (both streams).  frac: over the bytes the pipeline "
+                             "moves (downsample 4 B/event + 4 B/rep + 8 B/window, k-means 9 B/rep, corner "
+                             "13 B/event); frac_s8d: over SURVEY §8d's stage bytes, whose k-means term "
+                             "(8 B/point/pass x 10 passes) the count-image form never moves"}
     # the dominant kernel carries its stage's §8d bytes (the corner stage's 13 B/event for the arc
     # kernel): what that stage must move at minimum, over this one kernel's launch time
     stage_of = {**{k: "corner" for k in CORNER_KERNELS}, **{k: "kmeans" for k in KMEANS_KERNELS},
@@ -431,13 +475,10 @@ def main():
             traffic_src = tfiles[-1].name
         except (ValueError, KeyError, TypeError):
             traffic = None
-    # the same kernel's average launch time from the newest committed rocprofv3 --stats summary
-    # (a one-stream `bench.py --serial` trace, scripts/gpu_evidence.sh); the line's frac is the
-    # rocprof one (the live HIP-event figure is reported beside it)
-    rp_ms, rp_src = rocprof_avg_ms(dominant)
-    achieved_live = achieved
-    if rp_ms:
-        achieved = bytes_per_launch / (rp_ms * 1e-3) / 1e9
+    # the line's frac is this run's own HIP-event figure.  Beside it: the same kernel's average
+    # from a committed rocprofv3 --stats summary, only when that trace was taken with THIS
+    # library (its meta file records the libecc sha256; scripts/gpu_evidence.sh writes it)
+    rp_ms, rp_src = rocprof_avg_ms(dominant, lib_sha256(ecc))
 
     # ---- tracker (sequential over slices, rank 0 of a 1-GPU run) ---------------------------------
     tracker = None
@@ -584,6 +625,13 @@ def main():
         c3_res = bench_c3(ecc, ctx, args, rep_xy, uniq, c0, K)
 
     value = world * args.steps * n / elapsed / 1e6
+    preset = next((k for k, v in PRESET_SLICES.items() if v * SLICE == n), None)
+    cname = {"c4": "BASELINE configs C2-C4", "c5": "BASELINE C5 per-GPU share"}.get(preset, "custom size")
+    if world > 1:
+        wl = (f"C5: {world}xMI355X time-window shards of a {world * n}-event stream ({n} events/GPU; "
+              f"{cname}); per shard: ")
+    else:
+        wl = ""
     if graph is not None:
         lib.ecc_graph_destroy(graph)
     result = {
@@ -602,10 +650,11 @@ def main():
         "dtype": "u16xy/i64t (int), fp32 k-means",
         "data": "synthetic (seeded splitmix64 event generator: moving polygons + Gaussian blobs + noise)",
         "config": {
-            "workload": f"e2e hash-downsample(8192-event windows) -> k-means k={K} ({I} iters) on reps -> "
-                        f"SAE+FAST arc corners (16384-event slices) -> 15x15 NMS; {W}x{H} sensor; "
-                        f"{n} events/GPU/step (BASELINE configs C2-C4{', C5 per-GPU share' if n == 3052 * SLICE else ''})",
-            "events_per_gpu": n, "reps_per_gpu": n_reps, "width": W, "height": H, "k": K,
+            "workload": wl + f"e2e hash-downsample(8192-event windows) -> k-means k={K} ({I} iters) on reps -> "
+                             f"SAE+FAST arc corners (16384-event slices) -> 15x15 NMS; {W}x{H} sensor; "
+                             f"{n} events/GPU/step ({cname})",
+            "events_per_gpu": n, "events_total": world * n, "preset": preset,
+            "reps_per_gpu": n_reps, "width": W, "height": H, "k": K,
             "kmeans_iters": I, "parallelism": f"time-window shards x{world}",
             "launch": "hipGraph replay of the captured step" if graph is not None else "eager launches",
             "streams": "two streams sharing all CUs" if not (dist or args.serial) else "see parallelism",
@@ -614,10 +663,9 @@ def main():
         "roofline": {
             "kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "avg_launch_ms": round(avg_ms, 5), "achieved_hip_events": round(achieved_live, 2),
+            "avg_launch_ms": round(avg_ms, 5), "frac_from": "HIP events (this run)",
             "rocprof_avg_launch_ms": round(rp_ms, 5) if rp_ms else None, "rocprof_source": rp_src,
-            "frac_from": "rocprof average" if rp_ms else "HIP events",
-            "frac_hip_events": round(achieved_live / HBM_PEAK_GBS, 5),
+            "frac_rocprof": round(bytes_per_launch / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if rp_ms else None,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "algorithmic_bytes": f"SURVEY §8d bytes of the kernel's stage ({dom_stage})",
             "traffic_source": traffic_src,
@@ -629,6 +677,7 @@ def main():
         "corner_items": detect_stats,
         "tracker": tracker,
         "track_merge": track_merge,
+        "per_gpu_rate_n1": per_gpu_rate_n1,
         "dist_parity": dist_parity,
         "ingest": ingest,
         "eps": eps_res,
@@ -646,13 +695,28 @@ def main():
         dist.destroy_process_group()
 
 
-def rocprof_avg_ms(kernel):
+def lib_sha256(ecc):
+    import hashlib
+    try:
+        return hashlib.sha256(Path(ecc.LIB_PATH).read_bytes()).hexdigest()
+    except OSError:
+        return None
+
+
+def rocprof_avg_ms(kernel, sha):
     """(average ms per launch, file) of `kernel` (libecc's timing name) in the newest
-    profiles/*_kernel_stats.csv that lists it, or (None, None)."""
+    profiles/*_kernel_stats.csv that lists it AND whose meta file
+    (<same stem>.meta.json, {"libecc_sha256": ...}) names the loaded library, or (None, None)."""
     import csv
     import re
     for f in sorted((ROOT / "profiles").glob("r*_kernel_stats.csv"), reverse=True):
         if "kmeans_f32" in f.name:
+            continue
+        try:
+            meta = json.loads(f.with_name(f.name[:-len(".csv")] + ".meta.json").read_text())
+        except (OSError, ValueError):
+            continue
+        if not sha or meta.get("libecc_sha256") != sha:
             continue
         try:
             for r in csv.DictReader(open(f)):

@@ -43,7 +43,9 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kBuildUnroll = 8;
-// ctx->flags[10]: unsorted-time verdict of the running call (flags[0]: the last finished call's)
+// ctx->flags[10]: the tag of the last sort phase that saw decreasing time (every sort phase gets
+// a fresh host-side tag, so a stale word never matches a later call); flags[0]: the verdict
+// sae_prefix_kernel published for the last finished call (pending word == its prepare's tag)
 constexpr int kSortPendingWord = 10;
 // the flag pass's dynamic LDS limit: 160 KiB less its static LDS (ctot[kFlagQuads][4], 128 B)
 constexpr size_t kFlagDynLdsMax = 160 * 1024 - 256;
@@ -185,7 +187,7 @@ __device__ __forceinline__ int block_excl_scan_inplace(int32_t *a, int n, int32_
 
 __global__ void __launch_bounds__(kSortThreads, 8)  // 8 waves/SIMD: two workgroups per CU
 slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t, CornerGeom g, Sorted so,
-                  int32_t *__restrict__ first_border, int32_t *__restrict__ err, int32_t *__restrict__ err_status,
+                  int32_t *__restrict__ first_border, int32_t *__restrict__ err, int32_t tag,
                   uint32_t *__restrict__ zero0, int32_t *__restrict__ zero1) {
     extern __shared__ int32_t hist[];  // [nb]: counts, then offsets, then (long slices) cursors;
                                        // then [kSortChunk] staging (single slices: the keys in
@@ -194,13 +196,11 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
     const int tid = threadIdx.x, lane = tid & 63;
     const int64_t s = blockIdx.x;
     // the call's counters that later kernels of the call start from (a 4-B memset each was a
-    // fill launch on the critical path): arc_kernel's overflow count, the NMS error word
-    // and the published sort verdict of the previous call (the pending word `err` is cleared by
-    // the previous call's sae_prefix_kernel, or is still set if that call stopped after prepare)
+    // fill launch on the critical path): arc_kernel's overflow count, the NMS error word.  The
+    // sort verdict needs no reset: a workgroup that sees decreasing time writes this call's tag.
     if (s == 0 && tid == 0) {
         if (zero0) *zero0 = 0u;
         if (zero1) *zero1 = 0;
-        *err_status = 0;
     }
     const int64_t lo = s * g.S;
     const int len = (int)((lo + g.S < g.n ? lo + g.S : g.n) - lo);
@@ -266,7 +266,7 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
             br[u] |= (uint32_t)atomicAdd(&hist[br[u] >> 16], 1) & 0xffffu;
         }
     }
-    if (__any(bad) && lane == 0 && !g.any_order) *err = 1;  // pending: published by sae_prefix_kernel
+    if (__any(bad) && lane == 0 && !g.any_order) *err = tag;  // pending: published by sae_prefix_kernel
     fb = ecc::wave_min_i32(fb);  // DPP
     if (lane == 0) wsum[tid >> 6] = fb;
     __syncthreads();
@@ -509,15 +509,18 @@ constexpr int kPrefixRound = kPrefixPer * (kThreads / 64);
 
 __global__ void __launch_bounds__(kThreads)
 sae_prefix_kernel(CornerGeom g, int64_t n_groups, const uint32_t *__restrict__ gmask, int64_t *__restrict__ gB,
-                  int64_t *__restrict__ sae, int32_t *__restrict__ err_status, int32_t *__restrict__ err_pending,
+                  int64_t *__restrict__ sae, int32_t *__restrict__ err_status,
+                  int32_t *__restrict__ err_pending, int32_t tag,
                   uint32_t *__restrict__ zero0, int32_t *__restrict__ zero1) {
-    // the call's sort verdict: slice_sort (all of it finished before this kernel) left it in the
-    // pending word; publish it and clear the pending word for the next call.  Both words live in
-    // device memory and are rewritten by every call, so a captured graph replays them correctly.
+    // the call's sort verdict: its sort phase (finished before this kernel, in this call or in
+    // the prepare it finishes) wrote its tag into the pending word iff it saw decreasing time;
+    // publish it and consume the pending word (a captured graph replays the same tag, so each
+    // replay must start from a clean word; a stale word from an abandoned prepare carries another
+    // tag and never matches).
     // A finish-only call also zeroes the counters of its later kernels here (the arc kernels'
     // overflow count, the NMS error word), as slice_sort does in a one-call detection.
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *err_status = *err_pending;
+        *err_status = *err_pending == tag ? 1 : 0;
         *err_pending = 0;
         if (zero0) *zero0 = 0u;
         if (zero1) *zero1 = 0;
@@ -1536,6 +1539,11 @@ struct CornerState {
     // diagnostics of the last detection (ecc_fast_detect_stats)
     const uint32_t *n_over = nullptr;
     int64_t n_items = 0, n_slices = 0, n_groups = 0;
+    // the unsorted-time verdict (ecc_fast_detect_status): every sort phase takes a fresh tag;
+    // status_src says what the last call left to report (0: nothing, an empty call -> OK;
+    // 1: a prepare-only call -> the pending word against prep_tag; 2: a finished call -> flags[0])
+    int32_t next_tag = 0, prep_tag = 0;
+    int status_src = 0;
 };
 
 std::mutex g_state_mu;
@@ -1681,7 +1689,12 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     hipStream_t s = ecc::as_stream(stream);
     ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
     CornerState *st = state_of(ctx);
+    if (phases & 1) {  // a fresh tag for this sort phase (never 0: the pending word starts at 0)
+        st->next_tag = st->next_tag == INT32_MAX ? 1 : st->next_tag + 1;
+        st->prep_tag = st->next_tag;
+    }
     if (n == 0) {
+        st->status_src = 0;  // an empty call reports OK, whatever earlier calls saw
         if (local_last) ECC_CHECK_HIP(ctx, hipMemsetAsync(local_last, 0, (size_t)g.W * g.H * 8, s), "memset(local)");
         return ECC_OK;
     }
@@ -1714,7 +1727,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         }
         ECC_TIMED(ctx, s, "slice_sort_kernel");
         hipLaunchKernelGGL(slice_sort_kernel, dim3((unsigned)g.n_slices), dim3(kSortThreads), lds, s, xy, t, g,
-                           so, first_border, ctx->flags + kSortPendingWord, ctx->flags,
+                           so, first_border, ctx->flags + kSortPendingWord, st->prep_tag,
                            (phases & 2) ? gi.n_over : nullptr, zero_nms_err);
     }
     {
@@ -1731,9 +1744,11 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     }
     }  // phase 1
     if (!(phases & 2)) {
+        st->status_src = 1;
         ECC_CHECK_LAUNCH(ctx, "fast_detect_prepare");
         return ECC_OK;
     }
+    st->status_src = 2;
     st->n_over = gi.n_over;
     st->n_items = n_items;
     st->n_slices = g.n_slices;
@@ -1744,7 +1759,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
         const unsigned blocks = (unsigned)((HW + kPrefixPix - 1) / kPrefixPix);
         hipLaunchKernelGGL(sae_prefix_kernel, dim3(blocks), dim3(kThreads), 0, s, g, n_groups,
                            (const uint32_t *)gi.mask, gi.B, sae, ctx->flags, ctx->flags + kSortPendingWord,
-                           (phases & 1) ? nullptr : gi.n_over, (phases & 1) ? nullptr : zero_nms_err);
+                           st->prep_tag, (phases & 1) ? nullptr : gi.n_over, (phases & 1) ? nullptr : zero_nms_err);
     }
     {
         ECC_TIMED(ctx, s, "arc_kernel");
@@ -1889,14 +1904,15 @@ ECC_API int ecc_fast_detect_finish(ecc_ctx *ctx, const uint32_t *xy, const int64
 
 ECC_API int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream) {
     if (!ctx) return ECC_ERR_INVALID;
-    // flags[0]: the last finished call's verdict; the pending word: a prepare-only call's
-    int32_t f = 0, pend = 0;
-    ECC_CHECK_HIP(ctx, hipMemcpyAsync(&f, ctx->flags, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)),
-                  "read err flag");
-    ECC_CHECK_HIP(ctx, hipMemcpyAsync(&pend, ctx->flags + kSortPendingWord, 4, hipMemcpyDeviceToHost,
-                                      ecc::as_stream(stream)), "read err flag");
+    // the verdict of the last call on this context (CornerState::status_src)
+    const CornerState *st = state_of(ctx);
+    if (st->status_src == 0) return ECC_OK;
+    int32_t w = 0;
+    const int32_t *src = st->status_src == 1 ? ctx->flags + kSortPendingWord : ctx->flags;
+    ECC_CHECK_HIP(ctx, hipMemcpyAsync(&w, src, 4, hipMemcpyDeviceToHost, ecc::as_stream(stream)), "read err flag");
     ECC_CHECK_HIP(ctx, hipStreamSynchronize(ecc::as_stream(stream)), "sync");
-    return (f != 0 || pend != 0) ? ECC_ERR_UNSORTED_TIME : ECC_OK;
+    const bool bad = st->status_src == 1 ? w == st->prep_tag : w != 0;
+    return bad ? ECC_ERR_UNSORTED_TIME : ECC_OK;
 }
 
 ECC_API int ecc_fast_detect_stats(ecc_ctx *ctx, int64_t *out, int32_t n_out, ecc_stream_t stream) {

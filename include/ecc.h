@@ -265,8 +265,16 @@ int ecc_fast_detect_prepare(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, 
 int ecc_fast_detect_finish(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t, int64_t n,
                            const ecc_corner_cfg *cfg, int64_t *sae, uint8_t *corner_flags,
                            ecc_stream_t stream);
-/* Synchronises `stream` and reports ECC_ERR_UNSORTED_TIME if the last ecc_fast_detect on
- * this context saw decreasing timestamps, else ECC_OK. */
+/* Synchronises `stream` and reports the verdict of the LAST detection call on this context:
+ * ECC_ERR_UNSORTED_TIME if its batch had decreasing timestamps, else ECC_OK.
+ *  - ecc_fast_detect / _nms: that call's batch.
+ *  - ecc_fast_detect_prepare: the prepared batch (known as soon as the sort phase ran).
+ *  - ecc_fast_detect_finish / _finish_nms: the batch of the prepare it finishes.
+ *  - a call with n == 0: ECC_OK.
+ * Every sort phase carries its own tag, so a verdict never leaks into a later call: a prepare
+ * that is abandoned (never finished) affects only itself; the next prepare or full call starts
+ * clean.  A finish reports (and consumes) the verdict of the most recent prepare on the
+ * context. */
 int ecc_fast_detect_status(ecc_ctx *ctx, ecc_stream_t stream);
 /* Diagnostics of the last ecc_fast_detect / _finish on this context (synchronises `stream`):
  * out[0] = (group of 32 slices, 14x14 tile) work items, out[1] = items tested by the dense-plane

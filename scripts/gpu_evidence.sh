@@ -15,6 +15,8 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 fault() { case "$1" in 0) return 0;; *) echo "rc=$1 at $2, stopping"; exit "$1";; esac; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv -- python3 "$REPO/bench.py" $ARGS > "$OUT/trace_bench.json" 2> "$OUT/trace.err"; fault $? trace
+python3 -c 'import hashlib, json, sys; print(json.dumps({"libecc_sha256": hashlib.sha256(open(sys.argv[1], "rb").read()).hexdigest(), "command": sys.argv[2]}))' \
+  "${ECC_LIB:-$REPO/event-camera-clustering-and-optical-flow-estimation_amd/lib/libecc.so}" "bench.py $ARGS" > "$OUT/kernel_stats.meta.json"
 echo "trace done"
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- python3 "$REPO/bench.py" $ARGS > /dev/null 2> "$OUT/fetch.err"; fault $? fetch
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- python3 "$REPO/bench.py" $ARGS > /dev/null 2> "$OUT/write.err"; fault $? write

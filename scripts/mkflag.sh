@@ -2,7 +2,7 @@
 # mkflag.sh <tag> <file.hip> <-Dflags...> : lib_<tag> = current objects with <file.hip> (working tree)
 # recompiled with the extra flags (A/B of build switches)
 set -e
-cd /root/repo/event-camera-clustering-and-optical-flow-estimation_amd
+cd "$(dirname "$0")/../event-camera-clustering-and-optical-flow-estimation_amd"
 T=$1; F=$2; shift 2
 rm -rf build_exp/f_$T lib_$T; mkdir -p build_exp/f_$T lib_$T
 cp build/*.o build_exp/f_$T/

@@ -1,7 +1,7 @@
 #!/bin/bash
 # mkvar.sh <tag> <file.hip>... : lib_<tag> = current objects with the listed files from HEAD
 set -e
-cd /root/repo/event-camera-clustering-and-optical-flow-estimation_amd
+cd "$(dirname "$0")/../event-camera-clustering-and-optical-flow-estimation_amd"
 T=$1; shift
 rm -rf build_exp/v_$T lib_$T; mkdir -p build_exp/v_$T/src lib_$T
 cp build/*.o build_exp/v_$T/

@@ -60,3 +60,20 @@ def test_launch_ranks_builds_child_command(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
     assert bench.launch_ranks(bench.parse()) is None
     assert len(calls) == 1
+
+
+def test_default_sizes_per_gpu_count():
+    """One GPU keeps the metric's C4 batch (1221 slices = 20 004 864 events); the multi-GPU line is
+    BASELINE C5 by default: 50 M events per GPU (3052 slices), 400 M at N = 8."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    assert bench.parse([]).events == 20_004_864
+    assert bench.parse(["--gpus", "1"]).preset == "c4"
+    a8 = bench.parse(["--gpus", "8"])
+    assert a8.preset == "c5" and a8.events == 3052 * 16384 == 50_003_968
+    assert 8 * a8.events >= 400_000_000
+    assert bench.parse(["--gpus", "2"]).events == 50_003_968
+    # explicit sizes win
+    assert bench.parse(["--gpus", "8", "--preset", "c4"]).events == 20_004_864
+    assert bench.parse(["--gpus", "8", "--events", "163840"]).events == 163840
+    assert bench.parse(["--preset", "c5"]).events == 50_003_968

@@ -60,6 +60,9 @@ def test_rccl_one_rank_sharded_step_matches_oracle():
     assert tm is not None and tm["ranks"] == 1 and tm["slices"] == 40 and tm["tracks_end"] > 0, tm
     assert tm["pipelined"]["mevents_s"] > 0 and tm["pipelined"]["steps"] >= 3, tm
     assert res["n_gpus"] == 1
+    # rank 0's single-GPU rate at the same per-GPU size, measured in the same job
+    n1 = res["per_gpu_rate_n1"]
+    assert n1 is not None and n1["value"] > 0 and n1["events_per_gpu"] == 16384 * 40, n1
 
 
 @pytest.mark.gpu
@@ -76,3 +79,5 @@ def test_gloo_two_ranks_overlapped_schedule_matches_oracle():
     tm = res["track_merge"]
     assert tm is not None and tm["ranks"] == 2 and tm["slices"] == 48 and tm["tracks_end"] > 0, tm
     assert tm["pipelined"]["mevents_s"] > 0, tm
+    assert res["config"]["events_total"] == 2 * 16384 * 24 and res["config"]["workload"].startswith("C5"), res["config"]
+    assert res["per_gpu_rate_n1"]["value"] > 0

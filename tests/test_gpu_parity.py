@@ -505,6 +505,59 @@ def test_fast_detect_rejects_decreasing_time(ecc, gpu):
     out, cnt = ecc.DeviceArray(ns * 64, ecc.CORNER_DTYPE), ecc.DeviceArray(ns, np.int32)
     gpu.fast_detect_nms(dev(ecc, xy), dev(ecc, t), len(xy), cfg, sae, flags, 15, 64, out, cnt)
     assert gpu.fast_detect_status() == ecc.ERR_UNSORTED_TIME
+    # unsorted -> empty call -> OK (the empty call launches nothing and still reports its own verdict)
+    gpu.fast_detect(dev(ecc, xy), dev(ecc, t), 0, cfg, sae, flags)
+    assert gpu.fast_detect_status() == 0
+
+
+def test_fast_detect_status_prepare_finish_verdicts(ecc, gpu):
+    """ecc_fast_detect_status over the two-call form (ecc.h): a prepare reports its own batch, a
+    finish the batch of its prepare, and an abandoned unsorted prepare leaks into no later call."""
+    xy, t, _ = ecc.gen_events(40000, seed=3)
+    bad = t.copy()
+    bad[30000] = bad[29999] - 7
+    cfg = ecc.corner_cfg(width=W_SMALL, height=H_SMALL, first_detect_slice=0)
+    n = len(xy)
+    d_xy, d_ok, d_bad = dev(ecc, xy), dev(ecc, t), dev(ecc, bad)
+    local = ecc.DeviceArray(W_SMALL * H_SMALL, np.int64)
+    sae = ecc.DeviceArray.zeros(W_SMALL * H_SMALL, np.int64)
+    flags = ecc.DeviceArray(n, np.uint8)
+    lib, C = ecc.lib, ecc.C
+
+    def prepare(tt, nn=n):
+        ecc.check(lib.ecc_fast_detect_prepare(gpu.ctx, d_xy.ptr, tt.ptr, nn, C.byref(cfg), local.ptr, gpu.stream))
+
+    def finish(tt, nn=n):
+        ecc.check(lib.ecc_fast_detect_finish(gpu.ctx, d_xy.ptr, tt.ptr, nn, C.byref(cfg), sae.ptr, flags.ptr,
+                                             gpu.stream))
+
+    # unsorted prepare -> its verdict at once; then abandoned, a sorted full call reports OK
+    prepare(d_bad)
+    assert gpu.fast_detect_status() == ecc.ERR_UNSORTED_TIME
+    gpu.fast_detect(d_xy, d_ok, n, cfg, sae, flags)
+    assert gpu.fast_detect_status() == 0
+    # unsorted prepare (abandoned) -> sorted prepare + finish: OK at both steps
+    prepare(d_bad)
+    prepare(d_ok)
+    assert gpu.fast_detect_status() == 0
+    finish(d_ok)
+    assert gpu.fast_detect_status() == 0
+    # unsorted prepare + finish: the finish reports its prepare's batch
+    prepare(d_bad)
+    finish(d_bad)
+    assert gpu.fast_detect_status() == ecc.ERR_UNSORTED_TIME
+    # sorted prepare after it, then an empty prepare: OK
+    prepare(d_ok)
+    assert gpu.fast_detect_status() == 0
+    prepare(d_bad)
+    prepare(d_ok, 0)
+    assert gpu.fast_detect_status() == 0
+    # unsorted prepare, then a sorted fused detect + NMS: OK
+    prepare(d_bad)
+    ns = -(-n // cfg.slice_events)
+    out, cnt = ecc.DeviceArray(ns * 64, ecc.CORNER_DTYPE), ecc.DeviceArray(ns, np.int32)
+    gpu.fast_detect_nms(d_xy, d_ok, n, cfg, sae, flags, 15, 64, out, cnt)
+    assert gpu.fast_detect_status() == 0
 
 
 def _any_order_times(kind, n, seed):
