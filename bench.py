@@ -91,6 +91,10 @@ def parse(argv=None):
     ap.add_argument("--overlap", action="store_true",
                     help="keep the two-stream sharded schedule under gloo too (correctness rehearsals; gloo "
                          "collectives block the host, so it is not a timing configuration)")
+    ap.add_argument("--dist-native", action="store_true",
+                    help="sharded runs: every device collective through libecc's own RCCL entry points "
+                         "(ecc_dist_*: count all-reduce, SAE hand-off, corner gather); torch.distributed (gloo, "
+                         "CPU) only carries the control plane (the RCCL unique id, barriers, the timing max)")
     ap.add_argument("--no-n1-rate", action="store_true",
                     help="sharded runs: skip rank 0's single-GPU rate at the same per-GPU size (per_gpu_rate_n1)")
     a = ap.parse_args(argv)
@@ -157,7 +161,9 @@ def main():
         if not args.same_device and local >= torch.cuda.device_count():
             raise SystemExit(f"bench.py: rank {rank} needs device {local}, only {torch.cuda.device_count()} visible")
         torch.cuda.set_device(local)
-        tdist.init_process_group(args.dist_backend)
+        # --dist-native: the process group is the control plane only (gloo); the data path is
+        # libecc's ecc_dist_* over RCCL
+        tdist.init_process_group("gloo" if args.dist_native else args.dist_backend)
         dist = tdist
         if dist.get_world_size() != world:
             raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
@@ -168,6 +174,11 @@ def main():
         raise SystemExit("--events must be a multiple of the 16384-event slice (global slice alignment)")
     # one stream for libecc and the collectives (torch's current stream) when sharded
     ctx = ecc.Context(local, stream=torch.cuda.current_stream().cuda_stream) if dist else ecc.Context(local)
+    native = None
+    if dist and args.dist_native:
+        uid = [ecc.Dist.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        native = ecc.Dist(ctx, uid[0], world, rank)
     xy_h, t_h, p_h = ecc.gen_events(n, first=rank * n, seed=1, width=W, height=H)
     d_xy, d_t = ecc.DeviceArray.from_numpy(xy_h, ctx.stream), ecc.DeviceArray.from_numpy(t_h, ctx.stream)
     hcfg = ecc.hash_cfg(window=WINDOW)  # reference bounds 0<=x<=1280, 0<=y<=720
@@ -197,6 +208,7 @@ def main():
     if dist:
         t_b = torch.cuda.Stream(device=f"cuda:{local}")  # the k-means chain's stream
         ev_f, ev_j = torch.cuda.Event(), torch.cuda.Event()
+        ev_cnt, ev_ar = torch.cuda.Event(), torch.cuda.Event()
 
     def step_sharded(nb=0, serial=args.serial):
         """Shard-local downsample/detection/NMS; global k-means from ONE all-reduce of the
@@ -213,6 +225,8 @@ def main():
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
                                           uniq.ptr, rep.ptr, B), "downsample")
         ecc.check(lib.ecc_kmeans_counts_xy16(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, W, H, t_counts.data_ptr(), B))
+        if native is not None:
+            return step_sharded_native(nb, serial, S, B, main)
         # prepare is enqueued before the collectives: a blocking backend (gloo) waits on the host
         ecc.check(lib.ecc_fast_detect_prepare(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), t_local.data_ptr(), S))
         if serial:
@@ -233,6 +247,44 @@ def main():
         ctx.corner_nms(d_xy, flags, n, SLICE, W, H, 15, cap, nms_out[nb], nms_cnt[nb])
         if not serial:
             main.wait_event(ev_j)
+
+    def step_sharded_native(nb, serial, S, B, main):
+        """The rest of the sharded step over libecc's RCCL entry points: both collectives on the
+        detection stream, in the same order on every rank (operations of one communicator must
+        not overlap), the k-means chain joining through events (as apps/ecc_sharded_step.cpp)."""
+        if not serial:
+            ev_cnt.record(t_b)
+        ecc.check(lib.ecc_fast_detect_prepare(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), t_local.data_ptr(), S))
+        if not serial:
+            main.wait_event(ev_cnt)
+        native.allreduce_counts(t_counts.data_ptr(), W * H, S)
+        if not serial:
+            ev_ar.record(main)
+        native.sae_handoff(t_local.data_ptr(), W * H, t_all.data_ptr(), sae.ptr, S)
+        if not serial:
+            t_b.wait_event(ev_ar)
+        ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, B))
+        ecc.check(lib.ecc_kmeans_run_counts(ctx.ctx, t_counts.data_ptr(), W, H, ecc.C.byref(kcfg), d_c.ptr, None, B))
+        ecc.check(lib.ecc_kmeans_labels_xy16(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, d_c.ptr, K,
+                                             kcfg.threshold, labels.ptr, B))
+        if not serial:
+            ev_j.record(t_b)
+        ecc.check(lib.ecc_fast_detect_finish(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), sae.ptr,
+                                             flags.ptr, S), "fast_detect_finish")
+        ctx.corner_nms(d_xy, flags, n, SLICE, W, H, 15, cap, nms_out[nb], nms_cnt[nb])
+        if not serial:
+            main.wait_event(ev_j)
+
+    def gather_lists(nb):
+        """Shard NMS lists -> every rank: (corners, starts, counts, n_slices, keep-alive)."""
+        ctx.corner_pack(nms_out[nb], nms_cnt[nb], ns, cap, packed.data_ptr(), offs.data_ptr())
+        if native is not None:
+            a, st_, ct_, nst = native.gather_corners(packed.data_ptr(), offs.data_ptr(), ns)
+            return a.ptr, st_.ptr, ct_.ptr, nst, (a, st_, ct_)
+        total_b = int(offs[-1].item())
+        ecc.check(lib.ecc_memcpy_d2d(cnt_t.data_ptr(), nms_cnt[nb].ptr, 4 * ns, ctx.stream))
+        pk_b, st_b, ct_b = edist.gather_corner_lists(comm, packed[:total_b], cnt_t)
+        return pk_b.data_ptr(), st_b.data_ptr(), ct_b.data_ptr(), int(st_b.numel()), (pk_b, st_b, ct_b)
 
     # single GPU: downsample -> k-means and the corner chain read the same resident batch and are
     # independent, so they run on two streams (fork/join with events) and overlap
@@ -534,28 +586,28 @@ def main():
         comm = edist.TorchComm(dist)
         packed = torch.zeros((ns * cap, 3), dtype=torch.int32, device=f"cuda:{local}")
         offs = torch.zeros(ns + 1, dtype=torch.int64, device=f"cuda:{local}")
+        cnt_t = torch.empty(ns, dtype=torch.int32, device=f"cuda:{local}")
         dist.barrier()
         ctx.sync()
         tm0 = time.perf_counter()
-        ctx.corner_pack(nms_out[0], nms_cnt[0], ns, cap, packed.data_ptr(), offs.data_ptr())
-        total = int(offs[-1].item())
-        cnt_t = torch.empty(ns, dtype=torch.int32, device=f"cuda:{local}")
-        ecc.check(lib.ecc_memcpy_d2d(cnt_t.data_ptr(), nms_cnt[0].ptr, 4 * ns, ctx.stream))
+        pk_p, st_p, ct_p, n_gs, keep = gather_lists(0)
         ctx.sync()
-        all_pk, starts, cnts = edist.gather_corner_lists(comm, packed[:total], cnt_t)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tm0) * 1e3
         if rank == 0:
             tr = ecc.Tracker(ctx)
             tmr = ecc.Timer(ctx.stream)
             tmr.start()
-            tr.update_lists(all_pk.data_ptr(), starts.data_ptr(), cnts.data_ptr(), int(starts.numel()))
+            tr.update_lists(pk_p, st_p, ct_p, n_gs)
             merge_ms = tmr.stop()
             if tr.status() != 0:
                 raise RuntimeError("merged tracker reported a status error")
-            track_merge = {"ranks": world, "slices": int(starts.numel()), "corners": int(cnts.sum().item()),
+            cts = keep[2].numpy() if native is not None else keep[2].cpu().numpy()
+            n_corners = int(cts[:n_gs].astype(np.int64).sum())
+            track_merge = {"ranks": world, "slices": n_gs, "corners": n_corners,
+                           "transport": "ecc_dist_* (libecc RCCL)" if native is not None else "torch.distributed",
                            "pack_gather_ms": round(gather_ms, 3), "tracker_ms": round(merge_ms, 3),
-                           "us_per_slice": round(merge_ms * 1e3 / int(starts.numel()), 2),
+                           "us_per_slice": round(merge_ms * 1e3 / n_gs, 2),
                            "tracks_end": len(tr.tracks())}
             merged_tracks = (tr.tracks(), tr.groups()[0])
             tr.close()
@@ -578,16 +630,12 @@ def main():
             if b >= 2 and rank == 0:  # the gathered lists of step b-2 are released after their tracker
                 ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_trk[nb]))
             step(nb=nb)
-            ctx.corner_pack(nms_out[nb], nms_cnt[nb], ns, cap, packed.data_ptr(), offs.data_ptr())
-            total_b = int(offs[-1].item())
-            ecc.check(lib.ecc_memcpy_d2d(cnt_t.data_ptr(), nms_cnt[nb].ptr, 4 * ns, ctx.stream))
-            held[nb] = edist.gather_corner_lists(comm, packed[:total_b], cnt_t)
+            held[nb] = gather_lists(nb)
             if rank == 0:
-                pk_b, st_b, ct_b = held[nb]
+                pk_p, st_p, ct_p, n_gs, _ = held[nb]
                 ecc.check(lib.ecc_event_record(ev_g[nb], ctx.stream))
                 ecc.check(lib.ecc_stream_wait_event(s3.value, ev_g[nb]))
-                ecc.check(lib.ecc_tracker_update_lists(trp.tr, pk_b.data_ptr(), st_b.data_ptr(), ct_b.data_ptr(),
-                                                       int(st_b.numel()), s3.value), "tracker lists")
+                ecc.check(lib.ecc_tracker_update_lists(trp.tr, pk_p, st_p, ct_p, n_gs, s3.value), "tracker lists")
                 ecc.check(lib.ecc_event_record(ev_trk[nb], s3.value))
         ecc.check(lib.ecc_stream_sync(s3.value))
         ctx.sync()
@@ -640,7 +688,8 @@ def main():
         "unit": "Mevents/s",
         "n_gpus": world,
         "dist_world": dist.get_world_size() if dist else None,
-        "dist_backend": args.dist_backend if dist else None,
+        "dist_backend": ("ecc_dist (libecc RCCL) + gloo control plane" if native is not None else args.dist_backend)
+                        if dist else None,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
@@ -692,6 +741,8 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
+        if native is not None:
+            native.close()
         dist.destroy_process_group()
 
 

@@ -194,7 +194,17 @@ _sigs = {
     "ecc_dbscan_status": (C.c_int, [P, P]),
     "ecc_device_sync": (C.c_int, []),
     "ecc_reslice_n_us": (C.c_int, [P, P, i64, i64, P, i64, P, P]),
+    "ecc_dist_available": (C.c_int, []),
+    "ecc_dist_get_unique_id": (C.c_int, [P]),
+    "ecc_dist_init": (C.c_int, [C.POINTER(P), P, P, i32, i32]),
+    "ecc_dist_destroy": (C.c_int, [P]),
+    "ecc_dist_rank": (C.c_int, [P, C.POINTER(i32), C.POINTER(i32)]),
+    "ecc_dist_allreduce_counts": (C.c_int, [P, P, i64, P]),
+    "ecc_dist_allreduce_f64_max": (C.c_int, [P, P, i64, P]),
+    "ecc_dist_sae_handoff": (C.c_int, [P, P, i64, P, P, P]),
+    "ecc_dist_gather_corners": (C.c_int, [P, P, P, i32, P, i64, P, P, i64, C.POINTER(i64), C.POINTER(i64), P]),
 }
+DIST_ID_BYTES = 128
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)  # every bound symbol must exist (fail loudly on a stale build)
     _f.restype = _res
@@ -712,3 +722,58 @@ def pack_xy(x, y) -> np.ndarray:
 def unpack_xy(xy):
     xy = np.asarray(xy, np.uint32)
     return (xy & 0xFFFF).astype(np.int32), (xy >> 16).astype(np.int32)
+
+
+class Dist:
+    """Native RCCL communicator of one rank (ecc_dist_*: librccl opened by libecc, collectives on
+    the caller's stream).  `uid` is the 128-byte id rank 0 made with unique_id(), shipped to the
+    other ranks over any channel."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * DIST_ID_BYTES)()
+        check(lib.ecc_dist_get_unique_id(buf), "ecc_dist_get_unique_id")
+        return bytes(buf)
+
+    def __init__(self, ctx: "Context", uid: bytes, n_ranks: int, rank: int):
+        self.ctx = ctx
+        self.d = P()
+        buf = (C.c_uint8 * DIST_ID_BYTES).from_buffer_copy(uid)
+        rc = lib.ecc_dist_init(C.byref(self.d), ctx.ctx, buf, n_ranks, rank)
+        if rc != OK:
+            raise EccError(rc, f"ecc_dist_init: {lib.ecc_ctx_last_error(ctx.ctx).decode()}")
+
+    def allreduce_counts(self, ptr: int, n: int, stream=None):
+        check(lib.ecc_dist_allreduce_counts(self.d, ptr, n, stream if stream is not None else self.ctx.stream),
+              "ecc_dist_allreduce_counts")
+
+    def allreduce_f64_max(self, ptr: int, n: int, stream=None):
+        check(lib.ecc_dist_allreduce_f64_max(self.d, ptr, n, stream if stream is not None else self.ctx.stream),
+              "ecc_dist_allreduce_f64_max")
+
+    def sae_handoff(self, local_ptr: int, hw: int, all_ptr: int, sae_ptr: int, stream=None):
+        check(lib.ecc_dist_sae_handoff(self.d, local_ptr, hw, all_ptr, sae_ptr,
+                                       stream if stream is not None else self.ctx.stream), "ecc_dist_sae_handoff")
+
+    def gather_corners(self, packed_ptr: int, offsets_ptr: int, n_slices: int, stream=None):
+        """-> (all DeviceArray[CORNER_DTYPE], starts DeviceArray[int64], counts DeviceArray[int32],
+        n_slices_total): the arguments of ecc_tracker_update_lists over every rank's lists."""
+        st = stream if stream is not None else self.ctx.stream
+        ns_tot, stride = i64(0), i64(0)
+        check(lib.ecc_dist_gather_corners(self.d, packed_ptr, offsets_ptr, n_slices, None, 0, None, None, 0,
+                                          C.byref(ns_tot), C.byref(stride), st), "ecc_dist_gather_corners(sizes)")
+        nr = i32(0)
+        check(lib.ecc_dist_rank(self.d, None, C.byref(nr)))
+        cap = nr.value * stride.value
+        all_ = DeviceArray(max(cap, 1), CORNER_DTYPE)
+        starts = DeviceArray(max(ns_tot.value, 1), np.int64)
+        counts = DeviceArray(max(ns_tot.value, 1), np.int32)
+        check(lib.ecc_dist_gather_corners(self.d, packed_ptr, offsets_ptr, n_slices, all_.ptr, cap, starts.ptr,
+                                          counts.ptr, ns_tot.value, C.byref(ns_tot), C.byref(stride), st),
+              "ecc_dist_gather_corners")
+        return all_, starts, counts, ns_tot.value
+
+    def close(self):
+        if self.d:
+            lib.ecc_dist_destroy(self.d)
+            self.d = P()

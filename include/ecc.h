@@ -626,6 +626,53 @@ int ecc_evt_status(ecc_ctx *ctx, ecc_stream_t stream);
 int ecc_reslice_n_us(ecc_ctx *ctx, const int64_t *t, int64_t n, int64_t period_us,
                      int64_t *bounds, int64_t max_slices, int64_t *n_slices, ecc_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------
+ * 9. Multi-GPU time-window shards over RCCL (xGMI) — SURVEY.md §8e, BASELINE config C5.
+ * Reference: none (the reference is single-device); the exchanges restate its sequential slice
+ *            loop FCT/…group_track.cpp:832-850 exactly.
+ * One process per GPU; rank r owns the r-th time window of the stream (windows are multiples
+ * of the 16384-event slice).  Rank 0 calls ecc_dist_get_unique_id and ships the 128 bytes to
+ * the other ranks over any channel (pipe, file, socket, MPI); every rank then calls
+ * ecc_dist_init with its own context (its GPU).  Collectives are enqueued on `stream` and
+ * ordered with libecc's kernels; only ecc_dist_gather_corners synchronises `stream` (one
+ * size exchange).  librccl is opened on first use (dlopen): ecc_dist_available() == 0 when it
+ * cannot be, and ecc_dist_init then returns ECC_ERR_NO_DEVICE.
+ * The sharded step (apps/ecc_sharded_step.cpp):
+ *   ecc_downsample_hash -> ecc_kmeans_counts_xy16 -> ecc_dist_allreduce_counts ->
+ *   ecc_kmeans_run_counts -> ecc_kmeans_labels_xy16            (global centroids, bit-exact)
+ *   ecc_fast_detect_prepare -> ecc_dist_sae_handoff -> ecc_fast_detect_finish_nms (exact SAE)
+ *   ecc_corner_pack -> ecc_dist_gather_corners -> (rank 0) ecc_tracker_update_lists
+ * ------------------------------------------------------------------------------------- */
+#define ECC_DIST_ID_BYTES 128
+typedef struct ecc_dist ecc_dist;
+int ecc_dist_available(void);
+int ecc_dist_get_unique_id(uint8_t *id /* [ECC_DIST_ID_BYTES] */);
+int ecc_dist_init(ecc_dist **out, ecc_ctx *ctx, const uint8_t *id, int32_t n_ranks, int32_t rank);
+int ecc_dist_destroy(ecc_dist *d);
+int ecc_dist_rank(const ecc_dist *d, int32_t *rank, int32_t *n_ranks);
+/* k-means: in-place SUM over ranks of the per-pixel count images (DEVICE uint32[n],
+ * ecc_kmeans_counts_xy16). */
+int ecc_dist_allreduce_counts(ecc_dist *d, uint32_t *counts, int64_t n, ecc_stream_t stream);
+/* In-place MAX over ranks of DEVICE doubles (e.g. per-rank step times). */
+int ecc_dist_allreduce_f64_max(ecc_dist *d, double *values, int64_t n, ecc_stream_t stream);
+/* SAE hand-off: all[n_ranks*hw] (DEVICE scratch) = every rank's local_last image
+ * (ecc_fast_detect_prepare), then sae[hw] = element-wise max over ranks < this rank (zeros on
+ * rank 0) = this shard's exact initial SAE for ecc_fast_detect_finish(_nms). */
+int ecc_dist_sae_handoff(ecc_dist *d, const int64_t *local_last, int64_t hw, int64_t *all,
+                         int64_t *sae, ecc_stream_t stream);
+/* Track-merge exchange: packed/offsets = this rank's ecc_corner_pack output (n_slices slices).
+ * On every rank: all[r * stride + i] = rank r's packed corner i (stride = the largest rank's
+ * corner count, *corners_stride), and slice k of the global order (ranks in order) is
+ * all[starts[k] .. starts[k] + counts[k]) (DEVICE int64 / int32 arrays, k < *n_slices_total)
+ * — exactly the arguments of ecc_tracker_update_lists.  ECC_ERR_CAPACITY (with
+ * *n_slices_total / *corners_stride set) if n_ranks * stride > all_cap or the slices exceed
+ * slices_cap.  With all, starts and counts all NULL it only returns the sizes (the size
+ * exchange is itself collective: every rank makes the same calls). */
+int ecc_dist_gather_corners(ecc_dist *d, const ecc_corner *packed, const int64_t *offsets,
+                            int32_t n_slices, ecc_corner *all, int64_t all_cap, int64_t *starts,
+                            int32_t *counts, int64_t slices_cap, int64_t *n_slices_total,
+                            int64_t *corners_stride, ecc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
