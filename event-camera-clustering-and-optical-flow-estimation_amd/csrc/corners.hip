@@ -833,20 +833,27 @@ __device__ __forceinline__ uint32_t eligible_slices(const CornerGeom &g, int64_t
     return j0 <= 0 ? 0xffffffffu : (j0 >= kGroup ? 0u : (0xffffffffu << (int)j0));
 }
 
-// Values k0 .. p-1 (p > 4, k0 >= 3) of a pixel whose record is r: v_k at ovf[4 r.w + k - 3],
-// four loads in flight at a time (clamped indices), handed to put(k, v).
-__device__ __forceinline__ const uint32_t *overflow_base(const uint32_t *__restrict__ ovf, const uint4 &r) {
-    return ovf + 4 * (int64_t)r.w - (kRecVals - 1);
-}
+// The values v3 .. v_{p-1} (p > 4) of a pixel whose record is r, from the overflow array:
+// the run starts 16-B aligned at line r.w, so line l holds
+// v_{3 + 4l} .. v_{6 + 4l}.  Lines l0 .. of the run, four lines (16 values) in flight per trip
+// (clamped to the last line, no load under a lane condition): a pixel with 32 values costs two
+// dependent round trips instead of seven 4-value ones.
 template <class Put>
-__device__ __forceinline__ void overflow_values(const uint32_t *__restrict__ xo, int k0, int p, Put put) {
-    for (; k0 < p; k0 += 4) {
-        uint32_t a[4];
+__device__ __forceinline__ void overflow_lines(const uint32_t *__restrict__ ovf, const uint4 &r, int l0, int p, Put put) {
+    const uint4 *__restrict__ x4 = reinterpret_cast<const uint4 *>(ovf) + r.w;
+    const int nl = (p - (kRecVals - 1) + 3) >> 2;
+    for (; l0 < nl; l0 += 4) {
+        uint4 a[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) a[u] = xo[min(k0 + u, p - 1)];
+        for (int u = 0; u < 4; ++u) a[u] = x4[min(l0 + u, nl - 1)];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (k0 + u < p) put(k0 + u, a[u]);
+        for (int u = 0; u < 4; ++u) {
+            const int k = (kRecVals - 1) + 4 * (l0 + u);
+            if (k < p) put(k, a[u].x);
+            if (k + 1 < p) put(k + 1, a[u].y);
+            if (k + 2 < p) put(k + 2, a[u].z);
+            if (k + 3 < p) put(k + 3, a[u].w);
+        }
     }
 }
 
@@ -930,7 +937,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         if (mm && p == kRecVals) {
             L.T[__ffs(mm) - 1][wp] = rec.w;
         } else if (mm) {  // v3.. from the overflow array, ascending j as the bits
-            overflow_values(overflow_base(ovf, rec), kRecVals - 1, p, [&](int, uint32_t v) {
+            overflow_lines(ovf, rec, 0, p, [&](int, uint32_t v) {
                 L.T[__ffs(mm) - 1][wp] = v;
                 mm &= mm - 1u;
             });
@@ -1228,7 +1235,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         if (p == kRecVals) {
             dst[4] = pre.rec.w;
         } else if (!ECC_ARC_XPF && p > kRecVals) {
-            overflow_values(overflow_base(ovf, pre.rec), kRecVals - 1, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
+            overflow_lines(ovf, pre.rec, 0, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
         } else if (p > kRecVals) {  // v3 .. v6 from the prefetched line, the rest loaded now
             dst[4] = xa.x;  // v_k goes to dst[1 + k] for k < p (here p >= 5)
             dst[5] = xa.y;
@@ -1241,8 +1248,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
                 if (p > 10) dst[11] = xb.w;
             }
             if (p > kRecVals + 4 * ECC_ARC_XPF - 1)
-                overflow_values(overflow_base(ovf, pre.rec), kRecVals + 4 * ECC_ARC_XPF - 1, p,
-                                [&](int k, uint32_t v) { dst[1 + k] = v; });
+                overflow_lines(ovf, pre.rec, ECC_ARC_XPF, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
         }
         const int lp = oy * kTile + ox;
         for (uint32_t m = tm; m; m &= m - 1u) L.tasks[toff++] = (uint16_t)((__ffs(m) - 1) * kTilePix + lp);
