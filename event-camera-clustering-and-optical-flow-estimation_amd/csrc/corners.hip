@@ -1088,6 +1088,12 @@ __device__ __forceinline__ uint32_t sparse_value(const SparseLds &L, int wp, uin
 #ifndef ECC_ARC_WAVES
 #define ECC_ARC_WAVES 8
 #endif
+#ifndef ECC_ARC_PF_AT
+#define ECC_ARC_PF_AT 2  // the resident kernel issues the next item's loads before barrier 2 (3: after it)
+#endif
+#ifndef ECC_ARC_RESIDENT
+#define ECC_ARC_RESIDENT 0  // 1: arc_kernel_resident (persistent, next item's loads prefetched)
+#endif
 
 #if ECC_ARC_PROFILE
 // profiling builds: per-workgroup wall-clock of arc_kernel's phases, summed (thread 0); [7] = items
@@ -1141,13 +1147,20 @@ __device__ __forceinline__ void arc_prefetch(ArcPre &p, int64_t item, const Corn
 // Every lane knows its own pixel's values, so the list offsets, the task offsets and the window
 // minimum of B_g are all wave scans before the first barrier, and each lane writes its pixel's
 // list and tasks itself (no scatter, no LDS atomics).
-__device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPre &pre,
+// Persistent form (next >= 0): once this item's values are in LDS (phase B), `pre` is refilled
+// with item `next`'s loads, which then fly during this item's tests; next < 0: nothing to load.
+__device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, ArcPre &pre,
                                          const int64_t *__restrict__ t, const CornerGeom &g,
                                          const uint32_t *__restrict__ ovf, uint32_t *__restrict__ res,
-                                         int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
+                                         int64_t *__restrict__ over, uint32_t *__restrict__ n_over,
+                                         int64_t next, const uint4 *__restrict__ pv, const int64_t *__restrict__ gB,
+                                         const uint32_t *__restrict__ gmask) {
     const int64_t grp = (int)item / g.n_tiles;  // n_items < 2^31 (host check): 32-bit division
     const int tile = (int)item % g.n_tiles;
-    if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
+    if ((grp + 1) * kGroup <= g.first_detect) {  // every slice of the group precedes detection
+        if (next >= 0) arc_prefetch(pre, next, g, pv, gB, gmask);
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #if ECC_ARC_PROFILE
     unsigned long long arc_t_ = wall_clock64(), arc_ph_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1222,6 +1235,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         // no events in the tile: nothing to flag; too many values for the compact list: the
         // dense kernel takes it
         if (any_own && tid == 0) over[atomicAdd(n_over, 1u)] = item;
+        if (next >= 0) arc_prefetch(pre, next, g, pv, gB, gmask);
         return;
     }
     if (win_lane) {
@@ -1253,8 +1267,10 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         const int lp = oy * kTile + ox;
         for (uint32_t m = tm; m; m &= m - 1u) L.tasks[toff++] = (uint16_t)((__ffs(m) - 1) * kTilePix + lp);
     }
+    if (ECC_ARC_PF_AT == 2 && next >= 0) arc_prefetch(pre, next, g, pv, gB, gmask);  // this item's records are dead
     __syncthreads();  // 2
     ARC_MARK(1);  // B
+    if (ECC_ARC_PF_AT == 3 && next >= 0) arc_prefetch(pre, next, g, pv, gB, gmask);
     if (L.exact_only) {  // uniform: a wide group or a value above t_last — the exact kernel takes it
         if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
         return;
@@ -1340,7 +1356,31 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const u
     if (item >= n_items) return;
     ArcPre pre;
     arc_prefetch(pre, item, g, pv, gB, gmask);
-    arc_item(L, item, pre, t, g, ovf, res, over, n_over);
+    arc_item(L, item, pre, t, g, ovf, res, over, n_over, -1, pv, gB, gmask);
+}
+
+// Persistent form: gridDim.x = 8 * k workgroups (k per XCD, the resident slots); workgroup b
+// (XCD b % 8) walks the XCD's contiguous item range with stride k, and the next item's record
+// loads fly during the current item's tests (arc_item's `next`).
+__global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)
+arc_kernel_resident(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const uint32_t *__restrict__ ovf,
+                    const uint4 *__restrict__ pv, const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask,
+                    uint32_t *__restrict__ res, int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
+    __shared__ SparseLds L;
+    const int k = (int)(gridDim.x / 8), xcd = (int)(blockIdx.x % 8);
+    const int per = (int)((n_items + 7) / 8);
+    const int hi = min((xcd + 1) * per, (int)n_items);
+    int item = xcd * per + (int)(blockIdx.x / 8);
+    if (item >= hi) return;
+    ArcPre pre;
+    arc_prefetch(pre, item, g, pv, gB, gmask);
+    for (;;) {
+        const int next = item + k < hi ? item + k : -1;
+        arc_item(L, item, pre, t, g, ovf, res, over, n_over, next, pv, gB, gmask);
+        if (next < 0) break;
+        item = next;
+        __syncthreads();  // the item's LDS (res, counters) is reused
+    }
 }
 
 
@@ -1769,7 +1809,12 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     }
     {
         ECC_TIMED(ctx, s, "arc_kernel");
-        {
+        if (ECC_ARC_RESIDENT) {  // four resident workgroups per CU, next item's loads in flight
+            const int per_cu = ECC_ARC_WAVES / 2;  // 8-wave workgroups resident per CU
+            const unsigned grid = (unsigned)(8 * std::min<int64_t>((n_items + 7) / 8, (int64_t)ctx->n_cu * per_cu / 8));
+            hipLaunchKernelGGL(arc_kernel_resident, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
+                               (const uint32_t *)gi.ovf, (const uint4 *)gi.pv, (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over);
+        } else {
             const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
             hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
                                (const uint32_t *)gi.ovf, (const uint4 *)gi.pv, (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over);
