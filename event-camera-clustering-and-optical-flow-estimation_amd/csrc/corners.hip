@@ -648,7 +648,7 @@ __device__ __forceinline__ void sort_desc(uint32_t (&k)[N]) {
 template <int N, int NP, int IB, int SMIN, int SMAX>
 __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
     sort_desc<NP>(k);
-    if (!ties_exact && (k[SMAX] >> IB) == 0u) return -1;
+    const bool undecided = !ties_exact && (k[SMAX] >> IB) == 0u;  // a select, not a branch
     constexpr uint32_t full = (1u << N) - 1u;
     uint32_t m = 0;
     bool ok = false;
@@ -661,7 +661,7 @@ __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
             ok |= sep && (__popc(m & ~rot) == 1);
         }
     }
-    return ok ? 1 : 0;
+    return undecided ? -1 : (ok ? 1 : 0);
 }
 
 // Staged neighbourhood of one (group, tile) item.  T[j][wp] holds the value set at window pixel
@@ -1065,7 +1065,8 @@ struct PixInfo {
 };
 
 struct SparseLds {
-    uint32_t vals[kValCap + kWinPix];   // 17.9 KiB: the pairs + one B_g slot per window pixel
+    uint32_t vals[kValCap + kWinPix + kArcThreads];  // 19.9 KiB: the pairs + one B_g slot per window
+                                                      // pixel + one sink word per lane (phase B)
     PixInfo pix[kWinPix];               // 3.8 KiB
     uint32_t res[kPairWords];
     uint16_t tasks[kValCap];  // the tile's eligible pairs (j * 196 + pixel): at most the window's pairs
@@ -1087,12 +1088,6 @@ __device__ __forceinline__ uint32_t sparse_value(const SparseLds &L, int wp, uin
 
 #ifndef ECC_ARC_WAVES
 #define ECC_ARC_WAVES 8
-#endif
-#ifndef ECC_ARC_PF_AT
-#define ECC_ARC_PF_AT 2  // the resident kernel issues the next item's loads before barrier 2 (3: after it)
-#endif
-#ifndef ECC_ARC_RESIDENT
-#define ECC_ARC_RESIDENT 0  // 1: arc_kernel_resident (persistent, next item's loads prefetched)
 #endif
 
 #if ECC_ARC_PROFILE
@@ -1147,20 +1142,13 @@ __device__ __forceinline__ void arc_prefetch(ArcPre &p, int64_t item, const Corn
 // Every lane knows its own pixel's values, so the list offsets, the task offsets and the window
 // minimum of B_g are all wave scans before the first barrier, and each lane writes its pixel's
 // list and tasks itself (no scatter, no LDS atomics).
-// Persistent form (next >= 0): once this item's values are in LDS (phase B), `pre` is refilled
-// with item `next`'s loads, which then fly during this item's tests; next < 0: nothing to load.
-__device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, ArcPre &pre,
+__device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPre &pre,
                                          const int64_t *__restrict__ t, const CornerGeom &g,
                                          const uint32_t *__restrict__ ovf, uint32_t *__restrict__ res,
-                                         int64_t *__restrict__ over, uint32_t *__restrict__ n_over,
-                                         int64_t next, const uint4 *__restrict__ pv, const int64_t *__restrict__ gB,
-                                         const uint32_t *__restrict__ gmask) {
+                                         int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
     const int64_t grp = (int)item / g.n_tiles;  // n_items < 2^31 (host check): 32-bit division
     const int tile = (int)item % g.n_tiles;
-    if ((grp + 1) * kGroup <= g.first_detect) {  // every slice of the group precedes detection
-        if (next >= 0) arc_prefetch(pre, next, g, pv, gB, gmask);
-        return;
-    }
+    if ((grp + 1) * kGroup <= g.first_detect) return;  // every slice of the group precedes detection
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #if ECC_ARC_PROFILE
     unsigned long long arc_t_ = wall_clock64(), arc_ph_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1200,14 +1188,10 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, ArcPre &pre
     // the record) so that it flies during the scans and the barrier; the other lanes of the wave
     // load the first line of ovf (no per-lane branch around the load)
     const int p = cnt - 1;
-    uint4 xa = make_uint4(0u, 0u, 0u, 0u), xb = xa;
-#ifndef ECC_ARC_XPF
-#define ECC_ARC_XPF 1  // 16-B overflow lines loaded before barrier 1 (0: none, after it)
-#endif
-    if (ECC_ARC_XPF && __ballot(p > kRecVals)) {  // uniform
+    uint4 xa = make_uint4(0u, 0u, 0u, 0u);
+    if (__ballot(p > kRecVals)) {  // uniform (measured: no line 171 us, one 166.6, two 166.0)
         const uint4 *x4 = reinterpret_cast<const uint4 *>(ovf) + (p > kRecVals ? pre.rec.w : 0u);
         xa = x4[0];
-        if (ECC_ARC_XPF > 1) xb = x4[1];
     }
     if (lane == 63) L.wave_tot[wave] = both;
     if (lane == 0) {
@@ -1235,42 +1219,26 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, ArcPre &pre
         // no events in the tile: nothing to flag; too many values for the compact list: the
         // dense kernel takes it
         if (any_own && tid == 0) over[atomicAdd(n_over, 1u)] = item;
-        if (next >= 0) arc_prefetch(pre, next, g, pv, gB, gmask);
         return;
     }
     if (win_lane) {
         const uint32_t bcv = clamp_value(bq, Lt, narrow, &L.exact_only);  // above the range: the exact kernel
         reinterpret_cast<uint2 *>(L.pix)[wp] = make_uint2(mk_w, (uint32_t)off);
-        uint32_t *dst = L.vals + off;
-        dst[0] = bcv;
-        if (p > 0) dst[1] = pre.rec.x;
-        if (p > 1) dst[2] = pre.rec.y;
-        if (p > 2) dst[3] = pre.rec.z;
-        if (p == kRecVals) {
-            dst[4] = pre.rec.w;
-        } else if (!ECC_ARC_XPF && p > kRecVals) {
-            overflow_lines(ovf, pre.rec, 0, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
-        } else if (p > kRecVals) {  // v3 .. v6 from the prefetched line, the rest loaded now
-            dst[4] = xa.x;  // v_k goes to dst[1 + k] for k < p (here p >= 5)
-            dst[5] = xa.y;
-            if (p > 5) dst[6] = xa.z;
-            if (p > 6) dst[7] = xa.w;
-            if (ECC_ARC_XPF > 1) {
-                if (p > 7) dst[8] = xb.x;
-                if (p > 8) dst[9] = xb.y;
-                if (p > 9) dst[10] = xb.z;
-                if (p > 10) dst[11] = xb.w;
-            }
-            if (p > kRecVals + 4 * ECC_ARC_XPF - 1)
-                overflow_lines(ovf, pre.rec, ECC_ARC_XPF, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
-        }
+        // the B_g slot and values v0 .. v6 (the record's three or four, then the prefetched
+        // line), every write unconditional: a slot past the pixel's values goes to the lane's
+        // sink word (a branch per write cost the scalar unit and serialised the LDS stores)
+        const uint32_t sink = kValCap + kWinPix + tid;
+        const uint32_t v3 = p == kRecVals ? pre.rec.w : xa.x;
+        const uint32_t wv[kRecVals + 4] = {bcv, pre.rec.x, pre.rec.y, pre.rec.z, v3, xa.y, xa.z, xa.w};
+#pragma unroll
+        for (int k = 0; k < kRecVals + 4; ++k) L.vals[k <= p ? (uint32_t)off + k : sink] = wv[k];
+        if (p > kRecVals + 3)  // v7 .. from the overflow array
+            overflow_lines(ovf, pre.rec, 1, p, [&](int k, uint32_t v) { L.vals[off + 1 + k] = v; });
         const int lp = oy * kTile + ox;
         for (uint32_t m = tm; m; m &= m - 1u) L.tasks[toff++] = (uint16_t)((__ffs(m) - 1) * kTilePix + lp);
     }
-    if (ECC_ARC_PF_AT == 2 && next >= 0) arc_prefetch(pre, next, g, pv, gB, gmask);  // this item's records are dead
     __syncthreads();  // 2
     ARC_MARK(1);  // B
-    if (ECC_ARC_PF_AT == 3 && next >= 0) arc_prefetch(pre, next, g, pv, gB, gmask);
     if (L.exact_only) {  // uniform: a wide group or a value above t_last — the exact kernel takes it
         if (tid == 0) over[atomicAdd(n_over, 1u)] = item;
         return;
@@ -1356,31 +1324,7 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const u
     if (item >= n_items) return;
     ArcPre pre;
     arc_prefetch(pre, item, g, pv, gB, gmask);
-    arc_item(L, item, pre, t, g, ovf, res, over, n_over, -1, pv, gB, gmask);
-}
-
-// Persistent form: gridDim.x = 8 * k workgroups (k per XCD, the resident slots); workgroup b
-// (XCD b % 8) walks the XCD's contiguous item range with stride k, and the next item's record
-// loads fly during the current item's tests (arc_item's `next`).
-__global__ void __launch_bounds__(kArcThreads, ECC_ARC_WAVES)
-arc_kernel_resident(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const uint32_t *__restrict__ ovf,
-                    const uint4 *__restrict__ pv, const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask,
-                    uint32_t *__restrict__ res, int64_t *__restrict__ over, uint32_t *__restrict__ n_over) {
-    __shared__ SparseLds L;
-    const int k = (int)(gridDim.x / 8), xcd = (int)(blockIdx.x % 8);
-    const int per = (int)((n_items + 7) / 8);
-    const int hi = min((xcd + 1) * per, (int)n_items);
-    int item = xcd * per + (int)(blockIdx.x / 8);
-    if (item >= hi) return;
-    ArcPre pre;
-    arc_prefetch(pre, item, g, pv, gB, gmask);
-    for (;;) {
-        const int next = item + k < hi ? item + k : -1;
-        arc_item(L, item, pre, t, g, ovf, res, over, n_over, next, pv, gB, gmask);
-        if (next < 0) break;
-        item = next;
-        __syncthreads();  // the item's LDS (res, counters) is reused
-    }
+    arc_item(L, item, pre, t, g, ovf, res, over, n_over);
 }
 
 
@@ -1809,12 +1753,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     }
     {
         ECC_TIMED(ctx, s, "arc_kernel");
-        if (ECC_ARC_RESIDENT) {  // four resident workgroups per CU, next item's loads in flight
-            const int per_cu = ECC_ARC_WAVES / 2;  // 8-wave workgroups resident per CU
-            const unsigned grid = (unsigned)(8 * std::min<int64_t>((n_items + 7) / 8, (int64_t)ctx->n_cu * per_cu / 8));
-            hipLaunchKernelGGL(arc_kernel_resident, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
-                               (const uint32_t *)gi.ovf, (const uint4 *)gi.pv, (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over);
-        } else {
+        {
             const unsigned grid = (unsigned)(8 * ((n_items + 7) / 8));  // multiple of 8 (XCD-aware order)
             hipLaunchKernelGGL(arc_kernel, dim3(grid), dim3(kArcThreads), 0, s, t, g, n_items,
                                (const uint32_t *)gi.ovf, (const uint4 *)gi.pv, (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res, gi.over, gi.n_over);
