@@ -157,6 +157,10 @@ constexpr int kSortWaves = kSortThreads / 64;
 // bitmap (the staging area, not yet in use).  Events of one round at one pixel all stay (no
 // ordering inside a round), so the maximum always survives.  ~46 % of the events remain on the
 // bench's stream (40 % are distinct (slice, pixel) pairs), and pair_build reads only those.
+#ifndef ECC_SORT_DEDUP_STEP
+#define ECC_SORT_DEDUP_STEP 1  // event slots per dedup round (a divisor of kSortEPT)
+#endif
+constexpr int kSortDedupStep = ECC_SORT_DEDUP_STEP;
 #ifndef ECC_SORT_DEDUP
 #define ECC_SORT_DEDUP 1
 #endif
@@ -245,19 +249,29 @@ slice_sort_kernel(const uint32_t *__restrict__ xy, const int64_t *__restrict__ t
             if (ok && is_border(ecc::xy_x(v), ecc::xy_y(v), g)) fb = min(fb, i);
         }
         if (dedup && !__syncthreads_or(bad)) {  // uniform (single slices: one pass of this loop)
+            // rounds of kSortDedupStep event slots, latest first: an event is dropped when a later
+            // round already holds its (slice, pixel); events of one round are not compared with
+            // each other (pair_build's atomicMax keeps the last of what remains)
 #pragma unroll
-            for (int u = kSortEPT - 1; u >= 0; --u) {
-                const uint32_t b = br[u] >> 16;  // 0xffff: no event; n_tiles: outside the sensor (kept)
-                const bool cand = b < (uint32_t)g.n_tiles;
-                const uint32_t tp = b * kTilePix + (stage[u * kSortThreads + tid] & 255u);  // own key
-                bool drop = false;
-                if (u < kSortEPT - 1) {
-                    drop = cand && ((bm[tp >> 5] >> (tp & 31u)) & 1u);
-                    __syncthreads();  // every check of round u before its bits are set
+            for (int u0 = kSortEPT - 1; u0 >= 0; u0 -= kSortDedupStep) {
+                bool drop[kSortDedupStep];
+                uint32_t tp[kSortDedupStep];
+                bool cand[kSortDedupStep];
+#pragma unroll
+                for (int d = 0; d < kSortDedupStep; ++d) {
+                    const int u = u0 - d;
+                    const uint32_t b = br[u] >> 16;  // 0xffff: no event; n_tiles: outside the sensor (kept)
+                    cand[d] = b < (uint32_t)g.n_tiles;
+                    tp[d] = b * kTilePix + (stage[u * kSortThreads + tid] & 255u);  // own key
+                    drop[d] = u0 < kSortEPT - 1 && cand[d] && ((bm[tp[d] >> 5] >> (tp[d] & 31u)) & 1u);
                 }
-                if (drop) br[u] = 0xffffffffu;
-                else if (cand) atomicOr(&bm[tp >> 5], 1u << (tp & 31u));
-                if (u > 0) __syncthreads();  // round u's bits before round u-1's checks
+                if (u0 < kSortEPT - 1) __syncthreads();  // every check of the round before its bits are set
+#pragma unroll
+                for (int d = 0; d < kSortDedupStep; ++d) {
+                    if (drop[d]) br[u0 - d] = 0xffffffffu;
+                    else if (cand[d]) atomicOr(&bm[tp[d] >> 5], 1u << (tp[d] & 31u));
+                }
+                if (u0 - kSortDedupStep >= 0) __syncthreads();  // the round's bits before the next checks
             }
         }
 #pragma unroll
@@ -648,7 +662,7 @@ __device__ __forceinline__ void sort_desc(uint32_t (&k)[N]) {
 template <int N, int NP, int IB, int SMIN, int SMAX>
 __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
     sort_desc<NP>(k);
-    const bool undecided = !ties_exact && (k[SMAX] >> IB) == 0u;  // a select, not a branch
+    if (!ties_exact && (k[SMAX] >> IB) == 0u) return -1;
     constexpr uint32_t full = (1u << N) - 1u;
     uint32_t m = 0;
     bool ok = false;
@@ -661,7 +675,7 @@ __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
             ok |= sep && (__popc(m & ~rot) == 1);
         }
     }
-    return undecided ? -1 : (ok ? 1 : 0);
+    return ok ? 1 : 0;
 }
 
 // Staged neighbourhood of one (group, tile) item.  T[j][wp] holds the value set at window pixel
@@ -1065,8 +1079,7 @@ struct PixInfo {
 };
 
 struct SparseLds {
-    uint32_t vals[kValCap + kWinPix + kArcThreads];  // 19.9 KiB: the pairs + one B_g slot per window
-                                                      // pixel + one sink word per lane (phase B)
+    uint32_t vals[kValCap + kWinPix];   // 17.9 KiB: the pairs + one B_g slot per window pixel
     PixInfo pix[kWinPix];               // 3.8 KiB
     uint32_t res[kPairWords];
     uint16_t tasks[kValCap];  // the tile's eligible pairs (j * 196 + pixel): at most the window's pairs
@@ -1188,10 +1201,14 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     // the record) so that it flies during the scans and the barrier; the other lanes of the wave
     // load the first line of ovf (no per-lane branch around the load)
     const int p = cnt - 1;
-    uint4 xa = make_uint4(0u, 0u, 0u, 0u);
-    if (__ballot(p > kRecVals)) {  // uniform (measured: no line 171 us, one 166.6, two 166.0)
+    uint4 xa = make_uint4(0u, 0u, 0u, 0u), xb = xa;
+#ifndef ECC_ARC_XPF
+#define ECC_ARC_XPF 1  // 16-B overflow lines loaded before barrier 1 (0: none, after it)
+#endif
+    if (ECC_ARC_XPF && __ballot(p > kRecVals)) {  // uniform
         const uint4 *x4 = reinterpret_cast<const uint4 *>(ovf) + (p > kRecVals ? pre.rec.w : 0u);
         xa = x4[0];
+        if (ECC_ARC_XPF > 1) xb = x4[1];
     }
     if (lane == 63) L.wave_tot[wave] = both;
     if (lane == 0) {
@@ -1224,16 +1241,29 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     if (win_lane) {
         const uint32_t bcv = clamp_value(bq, Lt, narrow, &L.exact_only);  // above the range: the exact kernel
         reinterpret_cast<uint2 *>(L.pix)[wp] = make_uint2(mk_w, (uint32_t)off);
-        // the B_g slot and values v0 .. v6 (the record's three or four, then the prefetched
-        // line), every write unconditional: a slot past the pixel's values goes to the lane's
-        // sink word (a branch per write cost the scalar unit and serialised the LDS stores)
-        const uint32_t sink = kValCap + kWinPix + tid;
-        const uint32_t v3 = p == kRecVals ? pre.rec.w : xa.x;
-        const uint32_t wv[kRecVals + 4] = {bcv, pre.rec.x, pre.rec.y, pre.rec.z, v3, xa.y, xa.z, xa.w};
-#pragma unroll
-        for (int k = 0; k < kRecVals + 4; ++k) L.vals[k <= p ? (uint32_t)off + k : sink] = wv[k];
-        if (p > kRecVals + 3)  // v7 .. from the overflow array
-            overflow_lines(ovf, pre.rec, 1, p, [&](int k, uint32_t v) { L.vals[off + 1 + k] = v; });
+        uint32_t *dst = L.vals + off;
+        dst[0] = bcv;
+        if (p > 0) dst[1] = pre.rec.x;
+        if (p > 1) dst[2] = pre.rec.y;
+        if (p > 2) dst[3] = pre.rec.z;
+        if (p == kRecVals) {
+            dst[4] = pre.rec.w;
+        } else if (!ECC_ARC_XPF && p > kRecVals) {
+            overflow_lines(ovf, pre.rec, 0, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
+        } else if (p > kRecVals) {  // v3 .. v6 from the prefetched line, the rest loaded now
+            dst[4] = xa.x;  // v_k goes to dst[1 + k] for k < p (here p >= 5)
+            dst[5] = xa.y;
+            if (p > 5) dst[6] = xa.z;
+            if (p > 6) dst[7] = xa.w;
+            if (ECC_ARC_XPF > 1) {
+                if (p > 7) dst[8] = xb.x;
+                if (p > 8) dst[9] = xb.y;
+                if (p > 9) dst[10] = xb.z;
+                if (p > 10) dst[11] = xb.w;
+            }
+            if (p > kRecVals + 4 * ECC_ARC_XPF - 1)
+                overflow_lines(ovf, pre.rec, ECC_ARC_XPF, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
+        }
         const int lp = oy * kTile + ox;
         for (uint32_t m = tm; m; m &= m - 1u) L.tasks[toff++] = (uint16_t)((__ffs(m) - 1) * kTilePix + lp);
     }
