@@ -1724,6 +1724,53 @@ def test_kmeans_count_images_sum_over_shards(ecc, orc, gpu):
     assert lib.ecc_kmeans_counts_status(gpu.ctx, gpu.stream) == ecc.ERR_INVALID
 
 
+@pytest.mark.parametrize("force32", [False, True])
+@pytest.mark.parametrize("case", ["hot", "chunks", "segments"])
+def test_kmeans_count_images_packed_exact(ecc, gpu, monkeypatch, case, force32):
+    """The packed counts (16-bit halves, u16 partials) against np.bincount, where they are
+    hardest: parts of more than 2^16 points (two u32 passes per chunk) with one pixel holding
+    more than 2^16 of them (the partial's high bits spill to the excess image, cleared for the
+    next call: the call is made twice), frames of several 64 K-pixel chunks with pixels at the
+    chunk edges and the frame's corners, and ragged segments; ECC_KM_COUNT32 = the u32 chunks."""
+    if force32:
+        monkeypatch.setenv("ECC_KM_COUNT32", "1")
+    rng = np.random.default_rng(7)
+    if case == "hot":
+        W, H = 346, 260
+        n = 300_000
+        x = np.where(rng.random(n) < 0.8, 5, rng.integers(0, W, n))
+        y = np.where(x == 5, 7, rng.integers(0, H, n))
+        segs, stride, counts = 1, n, None
+    elif case == "chunks":
+        W, H = 1280, 720  # 14 chunks of 65536 pixels
+        n = 200_000
+        idx = np.concatenate([rng.integers(0, W * H, n - 8), [0, W * H - 1, 65535, 65536, 131071, 131072, W - 1,
+                                                               (H - 1) * W]])
+        x, y = idx % W, idx // W
+        segs, stride, counts = 1, n, None
+    else:
+        W, H = 346, 260
+        segs, stride = 97, 4096
+        counts = rng.integers(0, stride + 1, segs).astype(np.int32)
+        n = segs * stride
+        x, y = rng.integers(0, W, n), rng.integers(0, H, n)
+    pts = ecc.pack_xy(x.astype(np.uint32), y.astype(np.uint32)).astype(np.uint32)
+    if counts is None:
+        ref = np.bincount(y.astype(np.int64) * W + x, minlength=W * H)
+    else:
+        valid = (np.arange(stride)[None, :] < counts[:, None]).ravel()
+        ref = np.bincount((y.astype(np.int64) * W + x)[valid], minlength=W * H)
+    d_pts = dev(ecc, pts)
+    d_cnt = None if counts is None else dev(ecc, counts)
+    lib = ecc.lib
+    for _ in range(2):
+        cnt = ecc.DeviceArray(W * H, np.uint32)
+        ecc.check(lib.ecc_kmeans_counts_xy16(gpu.ctx, d_pts.ptr, segs, stride, None if d_cnt is None else d_cnt.ptr,
+                                             W, H, cnt.ptr, gpu.stream))
+        assert lib.ecc_kmeans_counts_status(gpu.ctx, gpu.stream) == 0
+        assert (cnt.numpy() == ref).all(), np.nonzero(cnt.numpy() != ref)[0][:8]
+
+
 # ------------------------------------------------------------------------------ fp64 radius / OPTICS
 def _brute_ball(pts, i, eps2):
     """square_distance (kdTree.hpp:180-192) in the same operation order, vectorised."""
