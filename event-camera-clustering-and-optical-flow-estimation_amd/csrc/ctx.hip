@@ -156,7 +156,6 @@ ECC_API int ecc_ctx_destroy(ecc_ctx *ctx) {
     ecc::nms_state_release(ctx);
     if (ctx->ws) hipFree(ctx->ws);
     if (ctx->flags) hipFree(ctx->flags);
-    if (ctx->km_excess) hipFree(ctx->km_excess);
     delete ctx;
     return ECC_OK;
 }

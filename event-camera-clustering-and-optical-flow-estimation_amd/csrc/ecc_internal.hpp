@@ -37,10 +37,6 @@ struct ecc_ctx {
     size_t ws_bytes = 0;
     // Small pinned-free device words: [0] unsorted-time flag of the last fast_detect.
     int32_t *flags = nullptr;
-    // k-means packed counts: per-pixel spill of partial counts above 0xffff (kmeans.hip), zero
-    // between calls (the sum kernel clears what it reads); grown on demand, zeroed on allocation
-    uint32_t *km_excess = nullptr;
-    int64_t km_excess_cells = 0;
 };
 
 namespace ecc {

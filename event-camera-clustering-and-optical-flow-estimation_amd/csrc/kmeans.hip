@@ -1721,215 +1721,6 @@ kmeans_count_sum_kernel(const uint32_t *__restrict__ partial, int parts, const u
     }
 }
 
-// Packed per-pixel counts for a caller-given frame (the bench step's and the multi-GPU count
-// images): two pixels per LDS word (16-bit halves), so one 128 KiB chunk covers 65536 pixels —
-// 346x260 (90 K pixels) takes two chunk slots instead of three, so every point is read twice
-// instead of three times — and each part's partial image is u16 (half the bytes written by this
-// kernel and read by the sum).  Exact for any input: a part with fewer than 2^16 points cannot
-// overflow a 16-bit half; a larger part counts each chunk as two 32768-pixel u32 halves (two
-// passes over its points).  A partial count above 0xffff (possible only then) stores its low 16
-// bits and adds the rest to `excess` (device-scope atomic, rare), which the sum kernel adds back
-// and clears for the next call.
-constexpr int kHist16Chunk = 65536;                // pixels per packed LDS chunk (128 KiB)
-constexpr int64_t kHist16Budget = 32 << 20;        // u16 partial entries (64 MiB)
-constexpr int64_t kCount16MaxCells = (int64_t)kImgSide * kImgSide;  // frames up to the label image
-
-__host__ __device__ inline int parts16_used(int parts, int64_t cells) {
-    const int64_t p = cells > 0 ? kHist16Budget / cells : parts;
-    return (int)(p < 1 ? 1 : (p < parts ? p : parts));
-}
-
-inline void count16_layout(int64_t n_segs, int64_t cells, int &parts, int &slots) {
-    const int64_t ch = (cells + kHist16Chunk - 1) / kHist16Chunk;
-    slots = (int)(ch < 1 ? 1 : (ch < kCountSlots ? ch : kCountSlots));
-    parts = (int)std::min<int64_t>(ECC_KM_COUNT_MUL * (32 / slots), std::max<int64_t>(n_segs, 1));
-}
-
-__global__ void __launch_bounds__(kHistThreads)
-kmeans_count16_kernel(const uint32_t *__restrict__ xy, Segs segs, int parts, int slots, uint16_t *__restrict__ partial,
-                      uint32_t *__restrict__ excess, uint32_t *__restrict__ wh, uint32_t *__restrict__ outside,
-                      uint32_t *__restrict__ n_outside, uint32_t w, uint32_t h, int32_t *__restrict__ err) {
-    extern __shared__ uint32_t hist[];  // [kHist16Chunk / 2]: packed pairs, or one u32 half-chunk
-    __shared__ int64_t s_tot[kHistThreads / 64];
-    const int xcd = (int)(blockIdx.x % 8), i8 = (int)(blockIdx.x / 8);
-    const int m = (i8 / slots) * 8 + xcd, slot = i8 % slots, tid = threadIdx.x;
-    const int64_t cells = (int64_t)w * h;
-    if (blockIdx.x == 0 && tid == 0) {
-        wh[0] = w;
-        wh[1] = h;
-    }
-    parts = parts16_used(parts, cells);
-    if (m >= parts) return;
-    const int64_t s0 = segs.n_segs * m / parts, s1 = segs.n_segs * (m + 1) / parts;
-    // the part's points (uniform): below 2^16 no 16-bit half can overflow
-    int64_t tot = 0;
-    for (int64_t sg = s0 + tid; sg < s1; sg += kHistThreads) {
-        const int64_t c = segs.count(sg);
-        tot += c > 0 ? c : 0;
-    }
-    tot = ecc::wave_sum_i64(tot);
-    if ((tid & 63) == 0) s_tot[tid >> 6] = tot;
-    __syncthreads();
-    tot = 0;
-#pragma unroll
-    for (int wv = 0; wv < kHistThreads / 64; ++wv) tot += s_tot[wv];
-    const bool packed = tot < 65536;
-    constexpr int kHalf = kHist16Chunk / 2;  // pixels per u32 pass
-    const int64_t n_chunks = (cells + kHist16Chunk - 1) / kHist16Chunk;
-    for (int64_t c = slot; c < n_chunks; c += slots) {
-        const int64_t lo = c * kHist16Chunk;
-        const int n_loc = (int)((cells - lo) < kHist16Chunk ? (cells - lo) : kHist16Chunk);
-        for (int half = 0; half < (packed ? 1 : 2); ++half) {
-            const int64_t plo = packed ? lo : lo + (int64_t)half * kHalf;  // first pixel of this pass
-            const int p_n = packed ? n_loc : min(max(n_loc - half * kHalf, 0), kHalf);
-            if (p_n <= 0) continue;  // uniform
-            for (int i = tid; i < kHalf; i += kHistThreads) hist[i] = 0u;
-            __syncthreads();
-            for (int64_t sg = s0; sg < s1; sg += kHistSegs) {
-                int64_t cnt[kHistSegs], base[kHistSegs], cmax = 0;
-                int32_t cl[kHistSegs];
-                if (segs.counts) {
-#pragma unroll
-                    for (int i = 0; i < kHistSegs; ++i) cl[i] = segs.counts[sg + i < s1 ? sg + i : s1 - 1];
-                } else {
-#pragma unroll
-                    for (int i = 0; i < kHistSegs; ++i) cl[i] = (int32_t)segs.count(sg + i);
-                }
-#pragma unroll
-                for (int i = 0; i < kHistSegs; ++i) {
-                    cnt[i] = sg + i < s1 ? cl[i] : 0;
-                    base[i] = (sg + i) * segs.stride;
-                    cmax = cnt[i] > cmax ? cnt[i] : cmax;
-                }
-                __amdgpu_buffer_rsrc_t vs[kHistSegs];
-#pragma unroll
-                for (int i = 0; i < kHistSegs; ++i) vs[i] = ecc::buffer_view(xy + base[i], (uint32_t)cnt[i] * 4u);
-                for (int64_t j0 = 0; j0 < cmax; j0 += kHistUnroll * kHistThreads) {
-                    uint32_t v[kHistSegs][kHistUnroll];
-#pragma unroll
-                    for (int i = 0; i < kHistSegs; ++i)
-#pragma unroll
-                        for (int u = 0; u < kHistUnroll; ++u)
-                            v[i][u] = ecc::buffer_load_u32(vs[i], (uint32_t)tid * 4u, (uint32_t)(j0 + u * kHistThreads) * 4u);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int i = 0; i < kHistSegs; ++i)
-#pragma unroll
-                        for (int u = 0; u < kHistUnroll; ++u) {
-                            if (j0 + u * kHistThreads + tid >= cnt[i]) continue;
-                            const uint32_t x = v[i][u] & 0xffffu, y = v[i][u] >> 16;
-                            if (x < w && y < h) {
-                                const int64_t idx = (int64_t)y * w + x - plo;
-                                if (idx >= 0 && idx < p_n) {
-                                    if (packed) atomicAdd(&hist[idx >> 1], 1u << ((idx & 1) << 4));
-                                    else atomicAdd(&hist[idx], 1u);
-                                }
-                            } else if (c == 0 && half == 0) {
-                                if (err) *err = 1;
-                                else outside[atomicAdd(n_outside, 1u)] = v[i][u];
-                            }
-                        }
-                }
-            }
-            __syncthreads();
-            uint16_t *out = partial + (int64_t)m * cells + plo;
-            for (int i = tid; i < p_n; i += kHistThreads) {
-                const uint32_t n = packed ? (hist[i >> 1] >> ((i & 1) << 4)) & 0xffffu : hist[i];
-                out[i] = (uint16_t)n;
-                if (n > 0xffffu) atomicAdd(&excess[plo + i], n & 0xffff0000u);
-            }
-            __syncthreads();
-        }
-    }
-}
-
-__global__ void __launch_bounds__(kThreads)
-kmeans_count_sum16_kernel(const uint16_t *__restrict__ partial, int parts, const uint32_t *__restrict__ wh,
-                          uint32_t *__restrict__ excess, uint32_t *__restrict__ cnt) {
-    const int64_t cells = (int64_t)wh[0] * wh[1];
-    parts = parts16_used(parts, cells);
-    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < cells; i += (int64_t)gridDim.x * kThreads) {
-        uint32_t t = excess[i];
-        if (t) excess[i] = 0u;  // zero for the next call
-        int m = 0;
-        for (; m + 8 <= parts; m += 8) {  // eight independent loads in flight
-            uint32_t v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = partial[(int64_t)(m + u) * cells + i];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) t += v[u];
-        }
-        for (; m < parts; ++m) t += partial[(int64_t)m * cells + i];
-        cnt[i] = t;
-    }
-}
-
-// The packed counts need the per-context excess image (zeroed once at allocation).
-int km_excess_reserve(ecc_ctx *ctx, int64_t cells) {
-    if (ctx->km_excess_cells >= cells) return ECC_OK;
-    if (ctx->km_excess) hipFree(ctx->km_excess);
-    ctx->km_excess = nullptr;
-    ctx->km_excess_cells = 0;
-    ECC_CHECK_HIP(ctx, hipMalloc(&ctx->km_excess, (size_t)cells * 4), "hipMalloc(kmeans excess)");
-    ECC_CHECK_HIP(ctx, hipMemset(ctx->km_excess, 0, (size_t)cells * 4), "memset(kmeans excess)");
-    ctx->km_excess_cells = cells;
-    return ECC_OK;
-}
-
-// Counts of a fixed frame (w x h) into cnt: the packed kernels when the frame is at most the label
-// image, else the u32 chunks.  partial: the workspace's partial-count area (kHistBudget * 4 bytes).
-int count_frame(ecc_ctx *ctx, hipStream_t s, const uint32_t *xy, const Segs &segs, uint32_t w, uint32_t h,
-                void *partial, uint32_t *wh, uint32_t *outside, uint32_t *n_out, int32_t *err, uint32_t *cnt) {
-    const int64_t cells = (int64_t)w * h;
-    const char *force32 = std::getenv("ECC_KM_COUNT32");  // A/B switch: the u32 chunks
-    if (cells <= kCount16MaxCells && !(force32 && *force32 && *force32 != '0')) {
-        int rc = km_excess_reserve(ctx, cells);
-        if (rc) return rc;
-        int parts, slots;
-        count16_layout(segs.n_segs, cells, parts, slots);
-        static bool lds16_ok = false;
-        if (!lds16_ok) {
-            ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&kmeans_count16_kernel),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kHist16Chunk * 2),
-                          "kmeans_count16 LDS");
-            lds16_ok = true;
-        }
-        {
-            ECC_TIMED(ctx, s, "kmeans_count_kernel");
-            hipLaunchKernelGGL(kmeans_count16_kernel, dim3(count_grid(parts, slots)), dim3(kHistThreads),
-                               kHist16Chunk * 2, s, xy, segs, parts, slots, (uint16_t *)partial, ctx->km_excess, wh,
-                               outside, n_out, w, h, err);
-        }
-        {
-            ECC_TIMED(ctx, s, "kmeans_count_sum_kernel");
-            hipLaunchKernelGGL(kmeans_count_sum16_kernel, dim3(1024), dim3(kThreads), 0, s,
-                               (const uint16_t *)partial, parts, (const uint32_t *)wh, ctx->km_excess, cnt);
-        }
-        return ECC_OK;
-    }
-    int parts, slots;
-    count_layout(segs.n_segs, cells, parts, slots);
-    static bool lds_ok = false;
-    if (!lds_ok) {
-        ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&kmeans_count_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, kHistChunk * 4),
-                      "kmeans_count LDS");
-        lds_ok = true;
-    }
-    {
-        ECC_TIMED(ctx, s, "kmeans_count_kernel");
-        hipLaunchKernelGGL(kmeans_count_kernel, dim3(count_grid(parts, slots)), dim3(kHistThreads), kHistChunk * 4, s,
-                           xy, segs, (const uint32_t *)nullptr, 0, parts, slots, (uint32_t *)partial, wh, outside, n_out,
-                           w, h, err);
-    }
-    {
-        ECC_TIMED(ctx, s, "kmeans_count_sum_kernel");
-        hipLaunchKernelGGL(kmeans_count_sum_kernel, dim3(1024), dim3(kThreads), 0, s, (const uint32_t *)partial, parts,
-                           (const uint32_t *)wh, cnt);
-    }
-    return ECC_OK;
-}
-
 // One kmeans_step_kernel per Lloyd pass replaces "update, then label image": every workgroup
 // re-derives the centroid update from the previous pass's accumulator replicas (a few hundred
 // L2 reads), so no second launch and no grid-wide hand-off is needed.  Buffers alternate by pass:
@@ -2222,12 +2013,8 @@ static int kmeans_run_xy16_impl(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
         if (frame_w == 0) {  // no frame given: the points' bounding box
             ECC_TIMED(ctx, s, "kmeans_extent_kernel");
             hipLaunchKernelGGL(kmeans_extent_kernel, dim3(grid), dim3(kThreads), 0, s, xy, segs, ext);
-        } else {  // the caller's frame: the packed counts
-            rc = count_frame(ctx, s, xy, segs, (uint32_t)frame_w, (uint32_t)frame_h, partial, wh, outside, n_out,
-                             nullptr, cnt);
-            if (rc) return rc;
         }
-        if (frame_w == 0) {
+        {
             ECC_TIMED(ctx, s, "kmeans_count_kernel");
             static bool lds_ok = false;
             if (!lds_ok) {
@@ -2240,7 +2027,7 @@ static int kmeans_run_xy16_impl(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs
                                s, xy, segs, ext, grid, parts, slots, partial, wh, outside, n_out, (uint32_t)frame_w,
                                (uint32_t)frame_h, (int32_t *)nullptr);
         }
-        if (frame_w == 0) {
+        {
             ECC_TIMED(ctx, s, "kmeans_count_sum_kernel");
             hipLaunchKernelGGL(kmeans_count_sum_kernel, dim3(1024), dim3(kThreads), 0, s, partial, parts, wh, cnt);
         }
@@ -2575,9 +2362,24 @@ ECC_API int ecc_kmeans_counts_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_s
     char *ws = static_cast<char *>(ctx->ws);
     auto *wh = reinterpret_cast<uint32_t *>(ws);
     auto *partial = reinterpret_cast<uint32_t *>(ws + off_part);
-    rc = count_frame(ctx, s, xy, segs, (uint32_t)frame_w, (uint32_t)frame_h, partial, wh, nullptr, nullptr,
-                     ctx->flags + kKmFlagWord, counts);
-    if (rc) return rc;
+    static bool lds_ok = false;
+    if (!lds_ok) {
+        ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&kmeans_count_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kHistChunk * 4),
+                      "kmeans_count LDS");
+        lds_ok = true;
+    }
+    {
+        ECC_TIMED(ctx, s, "kmeans_count_kernel");
+        hipLaunchKernelGGL(kmeans_count_kernel, dim3(count_grid(parts, slots)), dim3(kHistThreads), kHistChunk * 4, s,
+                           xy, segs, (const uint32_t *)nullptr, 0, parts, slots, partial, wh, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                           (uint32_t)frame_w, (uint32_t)frame_h, ctx->flags + kKmFlagWord);
+    }
+    {
+        ECC_TIMED(ctx, s, "kmeans_count_sum_kernel");
+        hipLaunchKernelGGL(kmeans_count_sum_kernel, dim3(1024), dim3(kThreads), 0, s, (const uint32_t *)partial, parts,
+                           (const uint32_t *)wh, counts);
+    }
     ECC_CHECK_LAUNCH(ctx, "kmeans counts");
     return ECC_OK;
 }

@@ -1724,16 +1724,12 @@ def test_kmeans_count_images_sum_over_shards(ecc, orc, gpu):
     assert lib.ecc_kmeans_counts_status(gpu.ctx, gpu.stream) == ecc.ERR_INVALID
 
 
-@pytest.mark.parametrize("force32", [False, True])
 @pytest.mark.parametrize("case", ["hot", "chunks", "segments"])
-def test_kmeans_count_images_packed_exact(ecc, gpu, monkeypatch, case, force32):
-    """The packed counts (16-bit halves, u16 partials) against np.bincount, where they are
-    hardest: parts of more than 2^16 points (two u32 passes per chunk) with one pixel holding
-    more than 2^16 of them (the partial's high bits spill to the excess image, cleared for the
-    next call: the call is made twice), frames of several 64 K-pixel chunks with pixels at the
-    chunk edges and the frame's corners, and ragged segments; ECC_KM_COUNT32 = the u32 chunks."""
-    if force32:
-        monkeypatch.setenv("ECC_KM_COUNT32", "1")
+def test_kmeans_count_images_exact(ecc, gpu, case):
+    """Per-pixel count images against np.bincount where the chunked LDS counts are hardest: one
+    pixel holding more than 2^16 points of one part, frames of many 32 K-pixel chunks with points
+    at the chunk edges and the frame's corners, and ragged segments (each call made twice: no
+    state leaks between calls)."""
     rng = np.random.default_rng(7)
     if case == "hot":
         W, H = 346, 260
