@@ -716,13 +716,13 @@ struct ArcLds {
     uint32_t res[kPairWords];         // corner (slice, pixel) pairs of the tile
     uint16_t tasks[kGroup * kTilePix]; // the tile's eligible pairs (j * 196 + pixel)
     uint16_t q4[kQ4Cap];               // circle-3 survivors (beyond the cap: tested inline)
-    int64_t wave_min[kWaves];
+    int64_t wave_min[16];  // per wave (up to 16 waves: arc_dense_kernel's workgroup size is a switch)
     int32_t exact_only;  // a value above t_last: clamped keys unusable
     int32_t mixed;       // clamped values not all equal to the window minimum of B
     int32_t n_tasks;
     int32_t q4n;
     int32_t n_exact;      // some task needs the exact int64 test
-    int32_t wave_own[kWaves];  // the wave's own-tile pixels have pairs
+    int32_t wave_own[16];  // the wave's own-tile pixels have pairs
 };
 
 // arc_dense_kernel's clamp: v <= L maps to 0 (mixed_flag set when v is not the window minimum vz)
@@ -890,6 +890,7 @@ __device__ unsigned long long g_dense_prof[8];
 #define DENSE_MARK(k) do { } while (0)
 #endif
 
+template <int NT>
 __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const int64_t *__restrict__ t, const CornerGeom &g,
                                                const uint32_t *__restrict__ ovf, const uint4 *__restrict__ pv,
                                                const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask,
@@ -915,7 +916,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     //     flight together; its values go to the dense planes T[j][wp], the own tile's eligible
     //     pairs (slice and pixel; the per-event cut of border mode 1 is applied when flagging)
     //     are the test tasks
-    static_assert(kArcThreads >= kWinPix, "one lane per window pixel");
+    static_assert(NT >= kWinPix, "one lane per window pixel");
     const int wp = tid;
     const bool win_lane = wp < kWinPix;
     const int ox = wp % kWin - kHalo, oy = wp / kWin - kHalo;  // pixel relative to the tile origin
@@ -930,7 +931,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         mk = gmask[q];
         rec = pv[q];
     }
-    for (int w = tid; w < kPairWords; w += kArcThreads) L.res[w] = 0u;
+    for (int w = tid; w < kPairWords; w += NT) L.res[w] = 0u;
     if (tid == 0) {
         L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
         L.mixed = 0;
@@ -969,7 +970,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     {
         int any = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) any |= L.wave_own[w];
+        for (int w = 0; w < NT / 64; ++w) any |= L.wave_own[w];
         if (!any) return;  // uniform: no events in the tile, nothing to flag
     }
     DENSE_MARK(1);
@@ -978,7 +979,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     if (win_lane) {
         int64_t vz = INT64_MAX;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
+        for (int w = 0; w < NT / 64; ++w) vz = L.wave_min[w] < vz ? L.wave_min[w] : vz;
         L.mb[wp].bc = (!narrow || bq == INT64_MAX) ? 0u : clamp_rel(bq, Lt, vz, &L.exact_only, &L.mixed);
     }
     __syncthreads();
@@ -995,7 +996,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     const bool ties_exact = !L.mixed;
     constexpr uint16_t kOpen3 = 0x4000, kOpen4 = 0x8000;
     if (fast) {
-        for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+        for (int ti = tid; ti < n_tasks; ti += NT) {
             const int pi = L.tasks[ti];
             const int j = pi / kTilePix, lp = pi % kTilePix;
             const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
@@ -1017,7 +1018,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     __syncthreads();
     DENSE_MARK(3);  // circle 3
     const int n4 = min(L.q4n, kQ4Cap);
-    for (int qi = tid; qi < n4; qi += kArcThreads) {
+    for (int qi = tid; qi < n4; qi += NT) {
         const int ti = L.q4[qi];
         const int pi = L.tasks[ti];
         const int j = pi / kTilePix, lp = pi % kTilePix;
@@ -1039,7 +1040,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     __syncthreads();
     DENSE_MARK(4);  // circle 4
     if (!fast || L.n_exact) {  // uniform; rare: the exact int64 tests
-        for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
+        for (int ti = tid; ti < n_tasks; ti += NT) {
             const int e = L.tasks[ti], pi = e & 0x3fff;
             if (fast && !(e & (kOpen3 | kOpen4))) continue;
             const int j = pi / kTilePix, lp = pi % kTilePix;
@@ -1360,14 +1361,18 @@ arc_kernel(const int64_t *__restrict__ t, CornerGeom g, int64_t n_items, const u
 
 // The windows above the compact list's capacity (arc_kernel's overflow list), each with the
 // dense per-slice planes.
-__global__ void __launch_bounds__(kArcThreads, 4)  // 4 waves/SIMD: two 8-wave workgroups per CU
+#ifndef ECC_DENSE_THREADS
+#define ECC_DENSE_THREADS 512  // arc_dense_kernel's workgroup: 512 = two per CU, 1024 = one per CU
+#endif
+constexpr int kDenseThreads = ECC_DENSE_THREADS;
+__global__ void __launch_bounds__(kDenseThreads, 4)  // 4 waves/SIMD (128 VGPRs)
 arc_dense_kernel(const int64_t *__restrict__ t, CornerGeom g, const int64_t *__restrict__ over,
                  const uint32_t *__restrict__ n_over, const uint32_t *__restrict__ ovf, const uint4 *__restrict__ pv,
                  const int64_t *__restrict__ gB, const uint32_t *__restrict__ gmask, uint32_t *__restrict__ res) {
     __shared__ ArcLds L;
     const uint32_t n = *n_over;
     for (uint32_t li = blockIdx.x; li < n; li += gridDim.x) {
-        arc_dense_item(L, over[li], t, g, ovf, pv, gB, gmask, res);
+        arc_dense_item<kDenseThreads>(L, over[li], t, g, ovf, pv, gB, gmask, res);
         __syncthreads();
     }
 }
@@ -1791,7 +1796,7 @@ static int fast_detect_phases(ecc_ctx *ctx, const uint32_t *xy, const int64_t *t
     }
     {
         ECC_TIMED(ctx, s, "arc_dense_kernel");  // the items arc_kernel left: dense planes, exact tests
-        hipLaunchKernelGGL(arc_dense_kernel, dim3(512), dim3(kArcThreads), 0, s, t, g, (const int64_t *)gi.over,
+        hipLaunchKernelGGL(arc_dense_kernel, dim3(kDenseThreads == 512 ? 512 : ctx->n_cu), dim3(kDenseThreads), 0, s, t, g, (const int64_t *)gi.over,
                            (const uint32_t *)gi.n_over, (const uint32_t *)gi.ovf, (const uint4 *)gi.pv,
                            (const int64_t *)gi.B, (const uint32_t *)gi.mask, gi.res);
     }
