@@ -68,8 +68,59 @@ def two(side):
     ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_join))
 
 
+ev_gate = ecc.C.c_void_p()
+ecc.check(lib.ecc_event_create(ecc.C.byref(ev_gate)))
+
+
+def corner_nms_fused():
+    ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
+    ctx.fast_detect_nms(d_xy, d_t, n, ccfg, sae, flags, 15, cap, nms_out, nms_cnt)
+
+
+def prepare():
+    ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
+    ecc.check(lib.ecc_fast_detect_prepare(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), None, ctx.stream))
+
+
+def finish():
+    ecc.check(lib.ecc_fast_detect_finish_nms(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), sae.ptr, flags.ptr, 15,
+                                             cap, nms_out.ptr, nms_cnt.ptr, ctx.stream))
+
+
+def gated(first_at, rest_at, join):
+    """The corner chain split at prepare | finish; the side chain's downsample starts at
+    `first_at` and its k-means at `rest_at` ("start" or "prepared": after the step's sort phase);
+    join=False: no per-step join, so step i's side chain may overlap step i+1's corner chain."""
+    ks = s2.value
+
+    def gate():
+        ecc.check(lib.ecc_event_record(ev_gate, ctx.stream))
+        ecc.check(lib.ecc_stream_wait_event(ks, ev_gate))
+    if first_at == "start":
+        gate()
+        ds(ks)
+    prepare()
+    if first_at == "prepared":
+        gate()
+        ds(ks)
+    elif rest_at == "prepared":
+        gate()
+    km(ks)
+    finish()
+    if join:
+        ecc.check(lib.ecc_event_record(ev_join, ks))
+        ecc.check(lib.ecc_stream_wait_event(ctx.stream, ev_join))
+
+
 variants = {
     "corner chain alone": corner,
+    "corner (fused detect+nms) alone": corner_nms_fused,
+    "split | side at start, joined": lambda: gated("start", "start", True),
+    "split | side after sort, joined": lambda: gated("prepared", "prepared", True),
+    "split | ds at start, km after sort, joined": lambda: gated("start", "prepared", True),
+    "split | side at start, not joined": lambda: gated("start", "start", False),
+    "split | side after sort, not joined": lambda: gated("prepared", "prepared", False),
+    "split | ds at start, km after sort, not joined": lambda: gated("start", "prepared", False),
     "downsample+kmeans alone": lambda: (ds(ctx.stream), km(ctx.stream)),
     "corner | downsample": lambda: two(ds),
     "corner | downsample+kmeans (bench step)": lambda: two(lambda ks: (ds(ks), km(ks))),
@@ -79,8 +130,10 @@ for name, fn in variants.items():
     for _ in range(3):
         fn()
     ctx.sync()
+    ecc.check(lib.ecc_stream_sync(s2.value))
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
     ctx.sync()
+    ecc.check(lib.ecc_stream_sync(s2.value))
     print(f"{name:42s} {(time.perf_counter() - t0) * 1e3 / steps:.3f} ms/step", flush=True)
