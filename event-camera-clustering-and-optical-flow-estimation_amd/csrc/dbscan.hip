@@ -627,9 +627,6 @@ constexpr int kDrHw = 512;      // disk half-width table: eps < 512
 constexpr int kDrPer = kGridMaxPts / kThreads;
 constexpr int kDrNarrow = 32;  // eps up to which a chord (2 eps + 1 pixels) spans at most 3 words
 constexpr int kDrRows = 4;     // chord rows per union batch
-#ifndef ECC_DB_UNION2
-#define ECC_DB_UNION2 0
-#endif
 
 __global__ void __launch_bounds__(kThreads)
 dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stride, const int32_t *__restrict__ seg_counts,
@@ -854,10 +851,6 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         // Chords of at most 3 words (eps <= kDrNarrow) go kDrRows rows at a time: their core
         // words, ranks, indices and roots are loaded for all rows of the batch together (one
         // dependent LDS round trip per step instead of one per row and step).
-        // ECC_DB_UNION2: the row links of every point first, then the trees flattened (every
-        // core point's parent -> its root), then the chords below: their root walks start from
-        // flat row chains instead of the trees the concurrent links are still building
-        auto union_pass = [&](const bool right, const bool below) {
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
             const int j = u * kThreads + tid;
@@ -876,14 +869,13 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                 uf_union(parent, j, q);  // lost a race: the general loop
                 ra = uf_find(parent, j);
             };
-            if (right && x + 1 < Wb && e_int > 0) {
+            if (x + 1 < Wb && e_int > 0) {
                 const int c = first_core(y * WW, x + 1, min(x + e_int, Wb - 1));
                 if (c >= 0) {
                     const int q = rk2idx[rank_at(c, y)];
                     unite_root(q, uf_find(parent, q));
                 }
             }
-            if (!below) continue;
             if (e_int <= kDrNarrow) {  // uniform
                 for (int a0 = 1; a0 <= amax && y + a0 < H; a0 += kDrRows) {
                     int cand[2 * kDrRows];
@@ -910,23 +902,6 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                     }
                 }
             }
-        }
-        };
-        if (ECC_DB_UNION2) {
-            union_pass(true, false);
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < kDrPer; ++u) {
-                const int j = u * kThreads + tid;
-                if (j < m && parent[j] != -1) {
-                    const int r = uf_root(parent, j);
-                    if (r != parent[j]) parent[j] = r;
-                }
-            }
-            __syncthreads();
-            union_pass(false, true);
-        } else {
-            union_pass(true, true);
         }
         __syncthreads();
         DB_MARK(1);  // unions

@@ -949,11 +949,7 @@ template <int kCtrl>
 __device__ __forceinline__ float qperm_f(float v) { return __int_as_float(qperm<kCtrl>(__float_as_int(v))); }
 
 constexpr int kFT = 256;    // the largest T + C of a slice handled here (LDS arrays)
-#ifndef ECC_TRK_FTHREADS
-#define ECC_TRK_FTHREADS 512
-#endif
-constexpr int kFThreads = ECC_TRK_FTHREADS;  // 8 waves: the round-0 scan runs 2-4 lanes per track
-static_assert(kFThreads >= kFT, "a thread per track and per detection");
+constexpr int kFThreads = 512;  // 8 waves: the round-0 scan runs 2-4 lanes per track
 constexpr int kFW = kFThreads / 64;
 constexpr int kFList = 8;   // in-range detections a track keeps in registers (more: it rescans)
 constexpr int kFTagTop = (1 << 23) - 1;  // round tags: ((kFTagTop - round) << 8) | track
@@ -1156,7 +1152,7 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
         // order, is the minimum of (dist, index) over its lanes; its in-range detections are
         // merged into one list (order irrelevant) for the later rounds.
         {
-            const int lsh = T * 4 <= kFThreads ? 2 : (T * 2 <= kFThreads ? 1 : 0);  // uniform: L = 1 << lsh, T * L <= kFThreads
+            const int lsh = T <= 128 ? 2 : 1;  // uniform: L = 1 << lsh, T * L <= kFThreads
             const int L = 1 << lsh;
             const int ti = tid >> lsh, tj = tid & (L - 1);
             const bool act = ti < T && f_st[ti] == -3;
@@ -1232,13 +1228,11 @@ tracker_fast_kernel(DevTrack *buf0, DevTrack *buf1, int max_tracks, DevGroup *__
                 const int u2 = qperm<0x44>(incl);             // lane - 2
                 incl += tj >= 2 ? u2 : 0;
                 total = qperm<0xFF>(incl);                   // lane 3 of the quad
-            } else if (L == 2) {
+            } else {
                 take(qperm_f<0xB1>(bd), qperm<0xB1>(bi));  // lane ^ 1
                 const int u1 = qperm<0xA0>(incl);             // lane - 1 within the pair
                 incl += tj >= 1 ? u1 : 0;
                 total = qperm<0xF5>(incl);                   // lane 1 of the pair
-            } else {
-                total = incl;  // one lane per track
             }
             if (act && total <= kFList) {
                 const int off = incl - cnt;
