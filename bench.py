@@ -76,6 +76,9 @@ def parse(argv=None):
                          "and streams (the multi-GPU SAE hand-off inside the device)")
     ap.add_argument("--serial", action="store_true",
                     help="one stream for the whole step (isolated per-kernel times for profiling)")
+    ap.add_argument("--joined", action="store_true",
+                    help="one GPU: join the k-means stream at the end of every step (default: steps pipelined — "
+                         "step i's k-means chain may still run beside step i+1's detection; r06k: 0.520 -> 0.50 ms)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the single-GPU step as a captured HIP graph (measured equal to eager)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPUs; gloo for rehearsal")
@@ -288,12 +291,18 @@ def main():
 
     # single GPU: downsample -> k-means and the corner chain read the same resident batch and are
     # independent, so they run on two streams (fork/join with events) and overlap
-    s2, ev_fork, ev_join = ecc.P(), ecc.P(), ecc.P()
+    s2, ev_fork, ev_join, ev_gate = ecc.P(), ecc.P(), ecc.P(), ecc.P()
     if not dist or rank == 0:  # sharded: rank 0's single-GPU rate at the same size (per_gpu_rate_n1)
         # the k-means chain's stream (a priority or a CU split for it measured no faster: DESIGN §5)
         ecc.check(lib.ecc_stream_create(ecc.C.byref(s2)), "stream")
-        ecc.check(lib.ecc_event_create(ecc.C.byref(ev_fork)), "event")
-        ecc.check(lib.ecc_event_create(ecc.C.byref(ev_join)), "event")
+        for e in (ev_fork, ev_join, ev_gate):
+            ecc.check(lib.ecc_event_create(ecc.C.byref(e)), "event")
+
+    def sync_all():
+        """Both streams idle (a pipelined step may leave its k-means chain running)."""
+        ctx.sync()
+        if s2.value:
+            ecc.check(lib.ecc_stream_sync(s2.value), "stream sync")
 
     # --corner-shards P (one GPU): the corner chain as P time-window shards of the batch on P
     # contexts and streams — the multi-GPU SAE hand-off inside one device (prepare every shard,
@@ -347,11 +356,33 @@ def main():
             return step_sharded(nb, serial or (args.dist_backend != "nccl" and not args.overlap))
         return step_single(serial, nb)
 
+    pipelined = not (args.joined or args.graph or P > 1)
+
     def step_single(serial=args.serial, nb=0):
-        """The single-GPU step: downsample -> k-means on the second stream beside detect + NMS."""
+        """The single-GPU step: downsample -> k-means on the second stream beside detect + NMS.
+        Pipelined (default): the detection is split at its sort phase (prepare | finish + NMS),
+        the k-means passes wait for that point, and the step does not wait for the k-means
+        stream, so step i's k-means chain overlaps step i+1's detection (a stream of batches as a
+        host would feed it); every step still runs every stage on its own batch, and the timed
+        region ends only when both streams are idle.  --joined: the per-step fork/join."""
         ks = ctx.stream if serial else s2.value  # the k-means chain's stream
         ecc.check(lib.ecc_event_record(ev_fork, ctx.stream))
         ecc.check(lib.ecc_stream_wait_event(ks, ev_fork))
+        if pipelined and not serial:
+            ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
+                                              uniq.ptr, rep.ptr, ks), "downsample")
+            ecc.check(lib.ecc_memset_async(sae.ptr, 0, sae.nbytes, ctx.stream))
+            ecc.check(lib.ecc_fast_detect_prepare(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), None, ctx.stream),
+                      "fast_detect_prepare")
+            ecc.check(lib.ecc_event_record(ev_gate, ctx.stream))  # the sort phase is enqueued
+            ecc.check(lib.ecc_stream_wait_event(ks, ev_gate))
+            ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, ks))
+            ecc.check(lib.ecc_kmeans_run_xy16_frame(ctx.ctx, rep_xy.ptr, n_win, WINDOW, uniq.ptr, W, H,
+                                                    ecc.C.byref(kcfg), d_c.ptr, labels.ptr, None, ks), "kmeans")
+            ecc.check(lib.ecc_fast_detect_finish_nms(ctx.ctx, d_xy.ptr, d_t.ptr, n, ecc.C.byref(ccfg), sae.ptr,
+                                                     flags.ptr, 15, cap, nms_out[nb].ptr, nms_cnt[nb].ptr,
+                                                     ctx.stream), "fast_detect_finish_nms")
+            return
         ecc.check(lib.ecc_downsample_hash(ctx.ctx, d_xy.ptr, n, ecc.C.byref(hcfg), rep_xy.ptr, None,
                                           uniq.ptr, rep.ptr, ks), "downsample")
         ecc.check(lib.ecc_memcpy_d2d(d_c.ptr, d_c0.ptr, 8 * K, ks))
@@ -368,7 +399,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    ctx.sync()
+    sync_all()
     for cx in [ctx] + [c["ctx"] for c in cshards[1:]]:
         cx.sync()
         if cx.fast_detect_status() != 0:
@@ -385,11 +416,11 @@ def main():
     if dist and rank == 0 and not args.no_n1_rate:
         for _ in range(max(1, args.warmup)):
             step_single(args.serial)
-        ctx.sync()
+        sync_all()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step_single(args.serial)
-        ctx.sync()
+        sync_all()
         dt1 = time.perf_counter() - t0
         if ctx.fast_detect_status() != 0 or ctx.corner_nms_status() != 0:
             raise RuntimeError("single-GPU reference steps reported a status error")
@@ -412,7 +443,7 @@ def main():
         ecc.check(lib.ecc_graph_end(ctx.stream, ecc.C.byref(gp)), "ecc_graph_end")
         graph = gp.value
         ecc.check(lib.ecc_graph_launch(graph, ctx.stream), "ecc_graph_launch")  # one untimed replay
-        ctx.sync()
+        sync_all()
 
     def timed_step():
         if graph is not None:
@@ -424,11 +455,11 @@ def main():
     #    drains the queue between kernels and costs ~0.6 ms/step here)
     if dist:
         dist.barrier()
-    ctx.sync()
+    sync_all()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         timed_step()
-    ctx.sync()
+    sync_all()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -443,11 +474,11 @@ def main():
     #    ONE stream, so that a kernel's time is its own (not queueing behind the other chain).
     lib.ecc_ctx_set_timing(ctx.ctx, 1)
     lib.ecc_ctx_timing_reset(ctx.ctx)
-    ctx.sync()
+    sync_all()
     t1 = time.perf_counter()
     for _ in range(args.steps):
         step(serial=True)
-    ctx.sync()
+    sync_all()
     instrumented = time.perf_counter() - t1
     lib.ecc_ctx_set_timing(ctx.ctx, 0)
     stats = ctx.timing_report()
@@ -555,7 +586,7 @@ def main():
             ecc.check(lib.ecc_event_create(ecc.C.byref(e)), "event")
         trp = ecc.Tracker(ctx)
         kp = max(3, min(args.steps, 6))
-        ctx.sync()
+        sync_all()
         tp0 = time.perf_counter()
         for b in range(kp):
             nb = b % 2
@@ -567,7 +598,7 @@ def main():
             ecc.check(lib.ecc_tracker_update(trp.tr, nms_out[nb].ptr, nms_cnt[nb].ptr, ns, cap, s3.value))
             ecc.check(lib.ecc_event_record(ev_trk[nb], s3.value))
         ecc.check(lib.ecc_stream_sync(s3.value))
-        ctx.sync()
+        sync_all()
         tp = time.perf_counter() - tp0
         trp.close()
         tracker = {
@@ -588,10 +619,10 @@ def main():
         offs = torch.zeros(ns + 1, dtype=torch.int64, device=f"cuda:{local}")
         cnt_t = torch.empty(ns, dtype=torch.int32, device=f"cuda:{local}")
         dist.barrier()
-        ctx.sync()
+        sync_all()
         tm0 = time.perf_counter()
         pk_p, st_p, ct_p, n_gs, keep = gather_lists(0)
-        ctx.sync()
+        sync_all()
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tm0) * 1e3
         if rank == 0:
@@ -623,7 +654,7 @@ def main():
         held = [None, None]
         kp = max(3, min(args.steps, 6))
         dist.barrier()
-        ctx.sync()
+        sync_all()
         tp0 = time.perf_counter()
         for b in range(kp):
             nb = b % 2
@@ -638,7 +669,7 @@ def main():
                 ecc.check(lib.ecc_tracker_update_lists(trp.tr, pk_p, st_p, ct_p, n_gs, s3.value), "tracker lists")
                 ecc.check(lib.ecc_event_record(ev_trk[nb], s3.value))
         ecc.check(lib.ecc_stream_sync(s3.value))
-        ctx.sync()
+        sync_all()
         dist.barrier()
         tp = time.perf_counter() - tp0
         if rank == 0:
@@ -707,6 +738,9 @@ def main():
             "kmeans_iters": I, "parallelism": f"time-window shards x{world}",
             "launch": "hipGraph replay of the captured step" if graph is not None else "eager launches",
             "streams": "two streams sharing all CUs" if not (dist or args.serial) else "see parallelism",
+            "schedule": ("pipelined: the k-means passes of step i start after its sort phase and may overlap step "
+                         "i+1's detection; the timed region ends when both streams are idle")
+                        if (pipelined and not dist and not args.serial) else "joined (per-step fork/join)",
             "corner_shards": P,
         },
         "roofline": {
