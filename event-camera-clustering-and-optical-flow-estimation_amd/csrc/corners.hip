@@ -668,9 +668,10 @@ __device__ __forceinline__ int arc_keys(uint32_t (&k)[NP], bool ties_exact) {
     bool ok = false;
 #pragma unroll
     for (int s = 1; s <= SMAX; ++s) {
-        m |= 1u << (k[s - 1] & ((1u << IB) - 1u));
+        m |= 1u << (k[s - 1] & ((1u << IB) - 1u));  // IB = 5: the shift's own 5-bit mask, no AND
         if (s >= SMIN) {
-            const bool sep = (k[s - 1] >> IB) > (k[s] >> IB);
+            // (a >> IB) > (b >> IB)  <=>  a > (b | low IB bits): one OR, one compare
+            const bool sep = k[s - 1] > (k[s] | ((1u << IB) - 1u));
             const uint32_t rot = ((m << 1) | (m >> (N - 1))) & full;
             ok |= sep && (__popc(m & ~rot) == 1);
         }
@@ -779,7 +780,8 @@ __device__ __forceinline__ uint32_t clamp_value(int64_t bq, int64_t Lt, bool nar
     return (uint32_t)d;
 }
 
-__device__ __forceinline__ uint32_t below_mask(int j) { return (j == 31) ? 0xffffffffu : ((2u << j) - 1u); }
+// slices 0 .. j (j <= 31: 2u << 31 is 0 in 32 bits, so j = 31 gives all ones without a select)
+__device__ __forceinline__ uint32_t below_mask(int j) { return (2u << j) - 1u; }
 
 // Clamped value at window pixel wp for slice j (fast path).
 __device__ __forceinline__ uint32_t win_value(const ArcLds &L, int wp, uint32_t below) {
@@ -1265,8 +1267,9 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
             if (p > kRecVals + 4 * ECC_ARC_XPF - 1)
                 overflow_lines(ovf, pre.rec, ECC_ARC_XPF, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
         }
-        const int lp = oy * kTile + ox;
-        for (uint32_t m = tm; m; m &= m - 1u) L.tasks[toff++] = (uint16_t)((__ffs(m) - 1) * kTilePix + lp);
+        // a task is (slice j, window pixel) as j << 9 | wp: the tests decode it with a shift and
+        // a mask (no division by the tile and window widths)
+        for (uint32_t m = tm; m; m &= m - 1u) L.tasks[toff++] = (uint16_t)((__ffs(m) - 1) << 9 | wp);
     }
     __syncthreads();  // 2
     ARC_MARK(1);  // B
@@ -1284,14 +1287,13 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     if (ECC_ARC_SKIP >= 2) n_tasks = 0;
     const bool ties_exact = !L.mixed;
     for (int ti = tid; ti < n_tasks; ti += kArcThreads) {
-        const int pi = L.tasks[ti];
-        const int j = pi / kTilePix, lp = pi % kTilePix;
-        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-        const uint32_t below = below_mask(j);
+        const int pi = L.tasks[ti];  // j << 9 | window pixel
+        const int wp0 = pi & 511;
+        const uint32_t below = below_mask(pi >> 9);
         uint32_t k3[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) k3[k] = (sparse_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
-        const int r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+        for (int k = 0; k < 16; ++k) k3[k] = (sparse_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 5) | k;
+        const int r3 = arc_keys<16, 16, 5, 3, 6>(k3, ties_exact);
         if (r3 > 0) {
             const int qi = atomicAdd(&L.q4n, 1);
             if (qi < kQ4Cap) L.q4[qi] = (uint16_t)pi;
@@ -1314,9 +1316,8 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     }
 #endif
     for (int qi = tid; qi < n4; qi += kArcThreads) {
-        const int pi = L.q4[qi];
-        const int j = pi / kTilePix, lp = pi % kTilePix;
-        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        const int pt = L.q4[qi];  // j << 9 | window pixel
+        const int j = pt >> 9, wp0 = pt & 511;
         const uint32_t below = below_mask(j);
         uint32_t k4[32];
 #pragma unroll
@@ -1324,8 +1325,12 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
 #pragma unroll
         for (int k = 20; k < 32; ++k) k4[k] = 0u;
         const int r4 = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
-        if (r4 > 0) atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
-        else if (r4 < 0) L.redo = 1;
+        if (r4 > 0) {  // the pair's bit: slice j, tile pixel (wp0's row and column less the halo)
+            const int pi = j * kTilePix + (wp0 / kWin - kHalo) * kTile + (wp0 % kWin - kHalo);
+            atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
+        } else if (r4 < 0) {
+            L.redo = 1;
+        }
     }
     __syncthreads();  // 4
     ARC_MARK(4);  // circle 4
