@@ -1075,9 +1075,6 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
 #define ECC_ARC_VALCAP 4096
 #endif
 constexpr int kValCap = ECC_ARC_VALCAP;
-#ifndef ECC_ARC_TASK_SINK
-#define ECC_ARC_TASK_SINK 0  // 1: arc_kernel writes its task list four entries per trip (sink slots)
-#endif
 
 struct PixInfo {
     uint32_t mask;  // slices of the group that touched the pixel
@@ -1088,9 +1085,7 @@ struct SparseLds {
     uint32_t vals[kValCap + kWinPix];   // 17.9 KiB: the pairs + one B_g slot per window pixel
     PixInfo pix[kWinPix];               // 3.8 KiB
     uint32_t res[kPairWords];
-    uint16_t tasks[kValCap + ECC_ARC_TASK_SINK * kArcThreads];  // the tile's eligible pairs (j << 9 | window
-                                                                 // pixel): at most the window's pairs
-                                                                 // (+ a sink slot per lane)
+    uint16_t tasks[kValCap];  // the tile's eligible pairs (j << 9 | window pixel): at most the window's pairs
     uint16_t q4[kQ4Cap];
     int64_t wave_c0[kWaves];    // the wave's first B_g at or below L (clamped to 0) ...
     int32_t wave_cf[kWaves];    // ... bit 1: it has one, bit 0: another differs from it
@@ -1274,22 +1269,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         }
         // a task is (slice j, window pixel) as j << 9 | wp: the tests decode it with a shift and
         // a mask (no division by the tile and window widths)
-        if (ECC_ARC_TASK_SINK) {
-            // four tasks per trip, every write unconditional (past the pixel's tasks: the lane's
-            // sink slot), so the wave's trip count is a quarter of its largest task count
-            const int sink = kValCap + tid;
-            for (uint32_t m = tm; m;) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const bool has = m != 0u;
-                    L.tasks[has ? toff : sink] = (uint16_t)((__ffs(m) - 1) << 9 | wp);
-                    toff += has ? 1 : 0;
-                    m &= m - 1u;
-                }
-            }
-        } else {
-            for (uint32_t m = tm; m; m &= m - 1u) L.tasks[toff++] = (uint16_t)((__ffs(m) - 1) << 9 | wp);
-        }
+        for (uint32_t m = tm; m; m &= m - 1u) L.tasks[toff++] = (uint16_t)((__ffs(m) - 1) << 9 | wp);
     }
     __syncthreads();  // 2
     ARC_MARK(1);  // B
