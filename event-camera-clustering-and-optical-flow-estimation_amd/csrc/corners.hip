@@ -1102,6 +1102,9 @@ __device__ __forceinline__ uint32_t sparse_value(const SparseLds &L, int wp, uin
     return L.vals[p.y + __popc(p.x & below)];
 }
 
+#ifndef ECC_ARC_SKIP_OVF
+#define ECC_ARC_SKIP_OVF 0  // timing experiments only (wrong results): 1 = no overflow loads past the first line
+#endif
 #ifndef ECC_ARC_WAVES
 #define ECC_ARC_WAVES 8
 #endif
@@ -1264,7 +1267,7 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
                 if (p > 9) dst[10] = xb.z;
                 if (p > 10) dst[11] = xb.w;
             }
-            if (p > kRecVals + 4 * ECC_ARC_XPF - 1)
+            if (!ECC_ARC_SKIP_OVF && p > kRecVals + 4 * ECC_ARC_XPF - 1)
                 overflow_lines(ovf, pre.rec, ECC_ARC_XPF, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
         }
         // a task is (slice j, window pixel) as j << 9 | wp: the tests decode it with a shift and
