@@ -1207,14 +1207,19 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
     // the record) so that it flies during the scans and the barrier; the other lanes of the wave
     // load the first line of ovf (no per-lane branch around the load)
     const int p = cnt - 1;
-    uint4 xa = make_uint4(0u, 0u, 0u, 0u), xb = xa;
 #ifndef ECC_ARC_XPF
 #define ECC_ARC_XPF 1  // 16-B overflow lines loaded before barrier 1 (0: none, after it)
 #endif
+    constexpr int kXpf = ECC_ARC_XPF > 0 ? ECC_ARC_XPF : 1;
+    uint4 xs[kXpf];
+#pragma unroll
+    for (int u = 0; u < kXpf; ++u) xs[u] = make_uint4(0u, 0u, 0u, 0u);
     if (ECC_ARC_XPF && __ballot(p > kRecVals)) {  // uniform
-        const uint4 *x4 = reinterpret_cast<const uint4 *>(ovf) + (p > kRecVals ? pre.rec.w : 0u);
-        xa = x4[0];
-        if (ECC_ARC_XPF > 1) xb = x4[1];
+        const bool o = p > kRecVals;
+        const uint4 *x4 = reinterpret_cast<const uint4 *>(ovf) + (o ? pre.rec.w : 0u);
+        const int nl = o ? (p - (kRecVals - 1) + 3) >> 2 : 1;  // lines of the lane's run
+#pragma unroll
+        for (int u = 0; u < kXpf; ++u) xs[u] = x4[min(u, nl - 1)];  // no load past the run
     }
     if (lane == 63) L.wave_tot[wave] = both;
     if (lane == 0) {
@@ -1257,15 +1262,14 @@ __device__ __forceinline__ void arc_item(SparseLds &L, int64_t item, const ArcPr
         } else if (!ECC_ARC_XPF && p > kRecVals) {
             overflow_lines(ovf, pre.rec, 0, p, [&](int k, uint32_t v) { dst[1 + k] = v; });
         } else if (p > kRecVals) {  // v3 .. v6 from the prefetched line, the rest loaded now
-            dst[4] = xa.x;  // v_k goes to dst[1 + k] for k < p (here p >= 5)
-            dst[5] = xa.y;
-            if (p > 5) dst[6] = xa.z;
-            if (p > 6) dst[7] = xa.w;
-            if (ECC_ARC_XPF > 1) {
-                if (p > 7) dst[8] = xb.x;
-                if (p > 8) dst[9] = xb.y;
-                if (p > 9) dst[10] = xb.z;
-                if (p > 10) dst[11] = xb.w;
+            // v_k goes to dst[1 + k] for k < p (here p >= 5); line u holds v_{3+4u} .. v_{6+4u}
+#pragma unroll
+            for (int u = 0; u < kXpf; ++u) {
+                const int k = (kRecVals - 1) + 4 * u;
+                if (k < p) dst[1 + k] = xs[u].x;
+                if (k + 1 < p) dst[2 + k] = xs[u].y;
+                if (k + 2 < p) dst[3 + k] = xs[u].z;
+                if (k + 3 < p) dst[4 + k] = xs[u].w;
             }
             if (!ECC_ARC_SKIP_OVF && p > kRecVals + 4 * ECC_ARC_XPF - 1)
                 overflow_lines(ovf, pre.rec, ECC_ARC_XPF, p, [&](int k, uint32_t v) { dst[1 + k] = v; });

@@ -608,8 +608,8 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
 // ---- row-run DBSCAN (distinct-pixel segments: downsample windows) -------------------------------
 // A downsample window's representatives are distinct pixels, so the segment is an occupancy
 // bitmap over its bounding box (eps.hip's row-run form): word w of row y holds 32 pixels and the
-// number of points in the words before it, so a pixel's raster rank is one word read + popc, and
-// rk2idx[rank] is its segment index.  A second bitmap marks the core points.
+// number of points in the words before it, so a pixel's raster rank is one word read + popc (the
+// point's id in the union-find below).  A second bitmap marks the core points.
 //   counts:  the disk's rows as prefix differences (eps_run_counts_kernel's count, self included);
 //   unions:  the core points within eps of core point p in a row are a chord [x - w, x + w] of
 //            that row.  Consecutive core points of one row within eps of each other (gap <= e)
@@ -621,28 +621,36 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
 //   members: a non-core point walks the core bits of its disk's chords (fewer than min_pts);
 // the rest (component ids in seed order, sizes, output order, labels, duplicate memberships) is
 // dbscan_grid_kernel's closed form.  Segments that repeat a pixel, whose bitmap exceeds kDrWords,
-// or with eps >= kDrHw are marked (n_clusters[s] = -1, counted in *left) for dbscan_grid_kernel.
-constexpr int kDrWords = 4864;  // (bits, prefix) pairs: 346x260 needs 2860
+// with more than kDrComp components or with eps >= kDrHw are marked (n_clusters[s] = -1, counted in *left) for dbscan_grid_kernel.
+constexpr int kDrWords = 2880;  // (bits, prefix) pairs: 346x260 needs 2860 (LDS < 80 KiB in all)
 constexpr int kDrHw = 512;      // disk half-width table: eps < 512
 constexpr int kDrPer = kGridMaxPts / kThreads;
 constexpr int kDrNarrow = 32;  // eps up to which a chord (2 eps + 1 pixels) spans at most 3 words
 constexpr int kDrRows = 4;     // chord rows per union batch
+constexpr int kDrComp = 1024;  // components per segment (more: dbscan_grid_kernel takes the segment)
+constexpr int kDrJWords = kGridMaxPts / 32;  // one bit per segment index
 
-__global__ void __launch_bounds__(kThreads)
+// The union-find lives in raster-rank space (parent[rank]: a chord's core bit is its own id, no
+// rank -> index table), and the roots (the smallest rank of each component) are renumbered in
+// the seed order dbscan_grid_kernel uses — ascending smallest core index — through a bitmap over
+// the segment's indices.  LDS < 80 KiB and 64 VGPRs: two 16-wave workgroups per CU.
+__global__ void __launch_bounds__(kThreads, 8)
 dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stride, const int32_t *__restrict__ seg_counts,
                   int e_int, uint32_t r2i, int min_pts, int min_size, int max_size, int32_t *__restrict__ labels,
                   int32_t *__restrict__ n_clusters, int64_t *__restrict__ dups, int64_t dup_cap,
                   unsigned long long *n_dups, int32_t *err, int32_t *left) {
     __shared__ uint2 wd[kDrWords + 1];     // occupancy bits | points before the word; [kDrWords] = 0
     __shared__ uint32_t cw[kDrWords + 1];  // core bits
-    __shared__ uint16_t rk2idx[kGridMaxPts];
-    __shared__ int parent[kGridMaxPts];
-    __shared__ int c_size[kMaxComp], c_front[kMaxComp];
-    __shared__ int16_t c_rank[kMaxComp];
+    __shared__ int parent[kGridMaxPts];  // by raster rank: -1 non-core, >= 0 core (a parent), <= -2 root
+    __shared__ int c_size[kDrComp], c_front[kDrComp];
+    __shared__ int16_t c_rank[kDrComp];
     __shared__ uint16_t hwt[kDrHw];
+    __shared__ uint32_t jb[kDrJWords];    // bit j: index j is the first core point of its component
+    __shared__ uint32_t sb[kDrJWords];    // the same points by rank
+    __shared__ uint16_t jpre[kDrJWords];  // set bits of jb before word w
     __shared__ int box[kThreads / 64][4];
     __shared__ int wsum[kThreads / 64];
-    __shared__ int s_dup, s_kept;
+    __shared__ int s_dup, s_kept, s_nc;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kW = kThreads / 64;
     if (tid == 0) {
@@ -698,6 +706,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             wd[w] = make_uint2(0u, 0u);
             cw[w] = 0u;
         }
+        for (int w = tid; w < kDrJWords; w += kThreads) jb[w] = sb[w] = 0u;
         __syncthreads();
         if (!leftover) {
 #pragma unroll
@@ -740,13 +749,17 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             return (int)q.y + __popc(q.x & ((1u << (x & 31)) - 1u));
         };
         const int amax = min(e_int, H - 1);
-        // counts -> core flags and bits; rank -> index
+        // the point of lane tid's slot u, re-read (an L2 hit) in the phases after the counts: its
+        // register copy would not fit the 64 VGPRs beside the union batches
+        auto pt = [&](int u) -> uint32_t {
+            return __hip_atomic_load(xy + base + u * kThreads + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+        // counts -> core flags and bits
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
             const int j = u * kThreads + tid;
             if (j >= m) break;
             const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
-            rk2idx[rank_at(x, y)] = (uint16_t)j;
             int cnt = 0;
 #pragma unroll 4
             for (int a = 0; a <= amax; ++a) {  // (unrolled: four rows' word loads in flight)
@@ -765,7 +778,8 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                 }
             }
             const bool core = cnt >= min_pts;
-            parent[j] = core ? j : -1;
+            const int r = rank_at(x, y);
+            parent[r] = core ? r : -1;
             if (core) atomicOr(&cw[y * WW + (x >> 5)], 1u << (x & 31));
         }
         __syncthreads();
@@ -789,31 +803,29 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             }
             return -1;
         };
-        // Rows y + s*a0 .. y + s*(a0 + kDrRows - 1) (s = +1 or -1; rows past amax or the box give
-        // -1): per row, the segment indices of the first and last core point of the point's chord
-        // there (eps <= kDrNarrow: a chord spans at most 3 words), -1 if none or the same point.
-        auto chord_ends_batch = [&](int a0, int x, int y, int sgn, int (&cand)[2 * kDrRows]) {
-            int pos[2 * kDrRows], row[kDrRows];
-            uint32_t b[kDrRows][3];
-            int lo[kDrRows], hi[kDrRows];
+        // Rows y + a0 .. y + a0 + kDrRows - 1: per row, the ranks of the first and last core point
+        // of the point's chord there (eps <= kDrNarrow: a chord spans at most 3 words), -1 if none
+        // or the same point.  A row past amax or the box reads the zero word cw[kDrWords]: -1.
+        auto chord_ends_batch = [&](int a0, int x, int y, int (&cand)[2 * kDrRows]) {
+            uint32_t b[kDrRows][3], lh[kDrRows];  // lh: lo | hi << 16
 #pragma unroll
             for (int r = 0; r < kDrRows; ++r) {
-                const int a = a0 + r, yy = y + sgn * a;
-                const bool ok = a <= amax && (unsigned)yy < (unsigned)H;
+                const int a = a0 + r, yy = y + a;
+                const bool ok = a <= amax && yy < H;
                 const int hw = hwt[ok ? a : 0];
-                lo[r] = max(x - hw, 0);
-                hi[r] = min(x + hw, Wb - 1);
-                row[r] = ok ? yy : -1;
-                const int w0 = lo[r] >> 5, w1 = hi[r] >> 5, rb = yy * WW;
+                const int lo = max(x - hw, 0), hi = min(x + hw, Wb - 1);
+                lh[r] = (uint32_t)lo | (uint32_t)hi << 16;
+                const int w0 = lo >> 5, w1 = hi >> 5, rb = yy * WW;
                 b[r][0] = cw[ok ? rb + w0 : kDrWords];
                 b[r][1] = cw[ok && w1 > w0 ? rb + w0 + 1 : kDrWords];
                 b[r][2] = cw[ok && w1 > w0 + 1 ? rb + w0 + 2 : kDrWords];
             }
 #pragma unroll
             for (int r = 0; r < kDrRows; ++r) {
-                const int w0 = lo[r] >> 5, nw = (hi[r] >> 5) - w0;  // last word: 0..2
-                const uint32_t hm = (hi[r] & 31) == 31 ? 0xffffffffu : ((2u << (hi[r] & 31)) - 1u);
-                uint32_t b0 = b[r][0] & ~((1u << (lo[r] & 31)) - 1u), b1 = b[r][1], b2 = b[r][2];
+                const int lo = (int)(lh[r] & 0xffffu), hi = (int)(lh[r] >> 16);
+                const int w0 = lo >> 5, nw = (hi >> 5) - w0;  // last word: 0..2
+                const uint32_t hm = (hi & 31) == 31 ? 0xffffffffu : ((2u << (hi & 31)) - 1u);
+                uint32_t b0 = b[r][0] & ~((1u << (lo & 31)) - 1u), b1 = b[r][1], b2 = b[r][2];
                 if (nw == 0) b0 &= hm;
                 else if (nw == 1) b1 &= hm;
                 else b2 &= hm;
@@ -821,16 +833,12 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                 const int base = w0 << 5;
                 const int cl = lw ? base + __builtin_ctzll(lw) : (b2 ? base + 64 + __builtin_ctz(b2) : -1);
                 const int cr = b2 ? base + 95 - __builtin_clz(b2) : (lw ? base + 63 - __builtin_clzll(lw) : -1);
-                pos[2 * r] = row[r] >= 0 && cl >= 0 ? rank_at(cl, row[r]) : -1;
-                pos[2 * r + 1] = row[r] >= 0 && cr > cl ? rank_at(cr, row[r]) : -1;
+                cand[2 * r] = cl >= 0 ? rank_at(cl, y + a0 + r) : -1;
+                cand[2 * r + 1] = cr > cl ? rank_at(cr, y + a0 + r) : -1;
             }
-#pragma unroll
-            for (int k = 0; k < 2 * kDrRows; ++k) cand[k] = pos[k] >= 0 ? (int)rk2idx[pos[k]] : -1;
         };
-        // the roots of cand[] (-1 stays -1), the chains walked in lockstep
-        auto roots_batch = [&](const int (&cand)[2 * kDrRows], int (&rt)[2 * kDrRows]) {
-#pragma unroll
-            for (int k = 0; k < 2 * kDrRows; ++k) rt[k] = cand[k];
+        // rt[] -> the roots of rt[] (-1 stays -1), the chains walked in lockstep
+        auto roots_batch = [&](int (&rt)[2 * kDrRows]) {
             for (;;) {
                 int nxt[2 * kDrRows];
                 bool more = false;
@@ -851,12 +859,12 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         // Chords of at most 3 words (eps <= kDrNarrow) go kDrRows rows at a time: their core
         // words, ranks, indices and roots are loaded for all rows of the batch together (one
         // dependent LDS round trip per step instead of one per row and step).
-#pragma unroll
+#pragma unroll 1
         for (int u = 0; u < kDrPer; ++u) {
-            const int j = u * kThreads + tid;
-            if (j >= m) break;
+            if (u * kThreads + tid >= m) break;
+            const int x = ecc::xy_x(pt(u)) - xmn, y = ecc::xy_y(pt(u)) - ymn;
+            const int j = rank_at(x, y);  // the point's id in the union-find
             if (parent[j] == -1) continue;
-            const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
             int ra = uf_find(parent, j);
             auto unite_root = [&](int q, int rb) {  // rb: q's root when looked up (may be stale)
                 if (rb == ra) return;
@@ -872,19 +880,18 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             if (x + 1 < Wb && e_int > 0) {
                 const int c = first_core(y * WW, x + 1, min(x + e_int, Wb - 1));
                 if (c >= 0) {
-                    const int q = rk2idx[rank_at(c, y)];
+                    const int q = rank_at(c, y);
                     unite_root(q, uf_find(parent, q));
                 }
             }
             if (e_int <= kDrNarrow) {  // uniform
                 for (int a0 = 1; a0 <= amax && y + a0 < H; a0 += kDrRows) {
-                    int cand[2 * kDrRows];
-                    chord_ends_batch(a0, x, y, +1, cand);
                     int rt[2 * kDrRows];
-                    roots_batch(cand, rt);
+                    chord_ends_batch(a0, x, y, rt);
+                    roots_batch(rt);
 #pragma unroll
-                    for (int k = 0; k < 2 * kDrRows; ++k)
-                        if (cand[k] >= 0) unite_root(cand[k], rt[k]);
+                    for (int k = 0; k < 2 * kDrRows; ++k)  // a root stands for its chord point
+                        if (rt[k] >= 0) unite_root(rt[k], rt[k]);
                 }
             } else {
                 for (int a = 1; a <= amax && y + a < H; ++a) {
@@ -893,11 +900,11 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                     const int rb = (y + a) * WW;
                     const int cl = first_core(rb, lo, hi);
                     if (cl < 0) continue;
-                    int q = rk2idx[rank_at(cl, y + a)];
+                    int q = rank_at(cl, y + a);
                     unite_root(q, uf_find(parent, q));
                     const int cr = last_core(rb, cl, hi);
                     if (cr > cl) {
-                        q = rk2idx[rank_at(cr, y + a)];
+                        q = rank_at(cr, y + a);
                         unite_root(q, uf_find(parent, q));
                     }
                 }
@@ -905,48 +912,77 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         }
         __syncthreads();
         DB_MARK(1);  // unions
-        // compress; roots -> component ids in ascending root (= seed) order
-        int roots[kGridPer], nr = 0;
-        const int j0 = tid * kGridPer;
+        // compress (ranks r0 .. r0 + 7 per lane); each root then keeps the smallest index of its
+        // component's core points (the seed), and the seeds' order gives the component ids
+        uint32_t rootm = 0u;
+        const int r0 = tid * kGridPer;
 #pragma unroll
         for (int u = 0; u < kGridPer; ++u) {
-            const int j = j0 + u;
-            roots[u] = 0;
-            if (j < m && parent[j] != -1) {
-                const int r = uf_find(parent, j);
-                roots[u] = r == j;
-                nr += roots[u];
+            const int r = r0 + u;
+            if (r < m && parent[r] != -1 && uf_find(parent, r) == r) rootm |= 1u << u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u) {
+            const int r = r0 + u;
+            if (r < m && parent[r] != -1 && !((rootm >> u) & 1u)) parent[r] = uf_root(parent, r);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u)
+            if ((rootm >> u) & 1u) parent[r0 + u] = -2 - kGridMaxPts;  // no index yet
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kDrPer; ++u) {
+            const int j = u * kThreads + tid;
+            if (j >= m) break;
+            const int r = rank_at(ecc::xy_x(pt(u)) - xmn, ecc::xy_y(pt(u)) - ymn);
+            const int pr = parent[r];
+            if (pr != -1) atomicMax(&parent[pr >= 0 ? pr : r], -2 - j);  // -2 - j: larger = earlier
+        }
+        __syncthreads();
+        // the seeds: index j in jb, rank in sb (the memberships' "neighbour is a seed" test)
+#pragma unroll
+        for (int u = 0; u < kDrPer; ++u) {
+            const int j = u * kThreads + tid;
+            if (j >= m) break;
+            const int r = rank_at(ecc::xy_x(pt(u)) - xmn, ecc::xy_y(pt(u)) - ymn);
+            const int pr = parent[r];
+            if (pr == -1 || -2 - parent[pr >= 0 ? pr : r] != j) continue;
+            atomicOr(&jb[j >> 5], 1u << (j & 31));
+            atomicOr(&sb[r >> 5], 1u << (r & 31));
+        }
+        __syncthreads();
+        if (wave == 0) {  // seeds before each word of jb
+            static_assert(kDrJWords == 4 * 64, "four jb words per lane");
+            int c4[4], loc = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) loc += (c4[k] = __popc(jb[4 * lane + k]));
+            const int inc = ecc::wave_incl_scan(loc);
+            int off = inc - loc;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                jpre[4 * lane + k] = (uint16_t)off;
+                off += c4[k];
             }
+            if (lane == 63) s_nc = inc;
         }
         __syncthreads();
-#pragma unroll
-        for (int u = 0; u < kGridPer; ++u) {
-            const int j = j0 + u;
-            if (j < m && parent[j] != -1 && !roots[u]) parent[j] = uf_root(parent, j);
-        }
-        const int xs = ecc::wave_incl_scan(nr);  // DPP
-        if (lane == 63) wsum[wave] = xs;
-        __syncthreads();
-        int pre = 0, nc = 0;
-        for (int w = 0; w < kW; ++w) {
-            if (w < wave) pre += wsum[w];
-            nc += wsum[w];
-        }
-        int cid = pre + xs - nr;
-        if (nc <= kMaxComp) {
-#pragma unroll
-            for (int u = 0; u < kGridPer; ++u)
-                if (roots[u]) parent[j0 + u] = -(cid++) - 2;
-        }
-        __syncthreads();
-        if (nc > kMaxComp) {  // too many components for the LDS tables
+        const int nc = s_nc;
+        if (nc > kDrComp) {  // uniform: too many components for the tables, the grid kernel redoes it
             if (tid == 0) {
-                atomicOr(err, 2);
-                n_clusters[s] = 0;
+                n_clusters[s] = -1;
+                atomicAdd(left, 1);
             }
-            for (int j = tid; j < m; j += kThreads) labels[base + j] = -1;
             __syncthreads();
             continue;
+        }
+#pragma unroll
+        for (int u = 0; u < kGridPer; ++u) {
+            if (!((rootm >> u) & 1u)) continue;
+            const int j = -2 - parent[r0 + u];
+            const int id = jpre[j >> 5] + __popc(jb[j >> 5] & ((1u << (j & 31)) - 1u));
+            parent[r0 + u] = -id - 2;
         }
         for (int c = tid; c < nc; c += kThreads) {
             c_size[c] = 0;
@@ -972,46 +1008,51 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                     while (b) {
                         const int bit = __ffs(b) - 1;
                         b &= b - 1u;
-                        f((int)rk2idx[q.y + __popc(q.x & ((1u << bit) - 1u))]);
+                        f((int)q.y + __popc(q.x & ((1u << bit) - 1u)));  // the core point's rank
                     }
                 }
             }
         };
         // memberships -> sizes and first members (first claim + later seeds, as the grid kernel)
-        int claim[kDrPer];
+        uint32_t claim2[kDrPer / 2];  // claim + 1 of points u (low half) and u + 1 (high half)
         uint32_t more = 0u;
+#pragma unroll
+        for (int u = 0; u < kDrPer / 2; ++u) claim2[u] = 0u;
+        auto set_claim = [&](int u, int c) { claim2[u >> 1] |= (uint32_t)(c + 1) << ((u & 1) * 16); };
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
             const int j = u * kThreads + tid;
-            claim[u] = -1;
             if (j >= m) continue;
-            const int cj = comp_of(parent, j);
+            const int x = ecc::xy_x(pt(u)) - xmn, y = ecc::xy_y(pt(u)) - ymn;
+            const int cj = comp_of(parent, rank_at(x, y));
             if (cj >= 0) {
-                claim[u] = cj;
+                set_claim(u, cj);
                 atomicAdd(&c_size[cj], 1);
                 atomicMin(&c_front[cj], j);
                 continue;
             }
-            const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
             int first = 0x7fffffff, n_seed = 0, seed_c = -1;
             for_core_nbrs(x, y, [&](int q) {
                 const int pv = parent[q];
                 const int c = pv <= -2 ? -pv - 2 : -parent[pv] - 2;
+                const bool seed = (sb[q >> 5] >> (q & 31)) & 1u;
                 first = c < first ? c : first;
-                n_seed += pv <= -2 ? 1 : 0;
-                seed_c = pv <= -2 ? c : seed_c;
+                n_seed += seed ? 1 : 0;
+                seed_c = seed ? c : seed_c;
             });
             if (first == 0x7fffffff) continue;  // noise
-            claim[u] = first;
+            set_claim(u, first);
             atomicAdd(&c_size[first], 1);
             atomicMin(&c_front[first], j);
             if (n_seed == 0 || (n_seed == 1 && seed_c == first)) continue;
             more |= 1u << u;
             for_core_nbrs(x, y, [&](int q) {  // later clusters seeded by a neighbour
+                if (!((sb[q >> 5] >> (q & 31)) & 1u)) return;
                 const int pv = parent[q];
-                if (pv <= -2 && -pv - 2 != first) {
-                    atomicAdd(&c_size[-pv - 2], 1);
-                    atomicMin(&c_front[-pv - 2], j);
+                const int c = pv <= -2 ? -pv - 2 : -parent[pv] - 2;
+                if (c != first) {
+                    atomicAdd(&c_size[c], 1);
+                    atomicMin(&c_front[c], j);
                 }
             });
         }
@@ -1043,17 +1084,19 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         for (int u = 0; u < kDrPer; ++u) {
             const int j = u * kThreads + tid;
             if (j >= m) break;
-            labels[base + j] = claim[u] >= 0 ? c_rank[claim[u]] : -1;
+            const int first = (int)((claim2[u >> 1] >> ((u & 1) * 16)) & 0xffffu) - 1;
+            labels[base + j] = first >= 0 ? c_rank[first] : -1;
             if (!((more >> u) & 1u)) continue;
-            const int first = claim[u];
-            const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
+            const int x = ecc::xy_x(pt(u)) - xmn, y = ecc::xy_y(pt(u)) - ymn;
             for_core_nbrs(x, y, [&](int q) {
+                if (!((sb[q >> 5] >> (q & 31)) & 1u)) return;
                 const int pv = parent[q];
-                if (pv <= -2 && -pv - 2 != first && c_rank[-pv - 2] >= 0) {
+                const int c = pv <= -2 ? -pv - 2 : -parent[pv] - 2;
+                if (c != first && c_rank[c] >= 0) {
                     const unsigned long long at = atomicAdd(n_dups, 1ull);
                     if ((int64_t)at < dup_cap) {
                         dups[2 * at] = base + j;
-                        dups[2 * at + 1] = c_rank[-pv - 2];
+                        dups[2 * at + 1] = c_rank[c];
                     } else {
                         atomicOr(err, 2);
                     }

@@ -1450,6 +1450,33 @@ def test_dbscan_grid_distinct_pixel_segments(ecc, orc, gpu, monkeypatch, eps, mi
             assert np.array_equal(a, b), s
 
 
+@pytest.mark.parametrize("n_comp", [1023, 1024, 1025, 2000])
+def test_dbscan_grid_many_components(ecc, orc, gpu, n_comp):
+    """Distinct-pixel segments with about kDrComp (1 024) components: isolated lattice points at
+    min_pts 1 (every point a core point and its own cluster) plus a few two-point clusters.  Up to
+    1 024 the row-run kernel keeps the segment; above, it leaves it to the cell-grid kernel, whose
+    tables hold 4 096 — the output must be the oracle's either way."""
+    rng = np.random.default_rng(n_comp)
+    stride = 4096
+    segs = []
+    for k in range(3):
+        g = rng.permutation(170 * 130)[:n_comp]
+        pts = np.stack([(g % 170) * 2, (g // 170) * 2], 1)  # spacing 2 > eps: isolated
+        if k == 1:  # some pairs: a neighbour at distance 1 joins a lattice point's cluster
+            pts = np.concatenate([pts, pts[:50] + [1, 0]])
+        segs.append(pts[rng.permutation(len(pts))].astype(np.int64))
+    counts = np.array([len(p) for p in segs], np.int32)
+    xy = np.zeros(len(segs) * stride, np.uint32)
+    for s, p in enumerate(segs):
+        xy[s * stride: s * stride + len(p)] = ecc.pack_xy(p[:, 0], p[:, 1])
+    got = _dbscan_gpu(ecc, gpu, xy, len(segs), stride, counts, 1.0, 1, 1, 1 << 30, True)
+    for s, p in enumerate(segs):
+        ref = orc.dbscan_lists(p.reshape(-1, 2), 1.0, 1)
+        assert len(got[s]) == len(ref), (s, len(got[s]), len(ref))
+        for a, b in zip(got[s], ref):
+            assert np.array_equal(a, b), s
+
+
 def test_dbscan_extract_rejects_short_lists(ecc, gpu):
     """offsets that run past nbr_len: the segment is rejected (status CAPACITY), never read."""
     n = 64
