@@ -626,7 +626,10 @@ constexpr int kDrWords = 2880;  // (bits, prefix) pairs: 346x260 needs 2860 (LDS
 constexpr int kDrHw = 512;      // disk half-width table: eps < 512
 constexpr int kDrPer = kGridMaxPts / kThreads;
 constexpr int kDrNarrow = 32;  // eps up to which a chord (2 eps + 1 pixels) spans at most 3 words
-constexpr int kDrRows = 4;     // chord rows per union batch
+#ifndef ECC_DR_ROWS
+#define ECC_DR_ROWS 4
+#endif
+constexpr int kDrRows = ECC_DR_ROWS;  // chord rows per union batch
 constexpr int kDrComp = 1024;  // components per segment (more: dbscan_grid_kernel takes the segment)
 constexpr int kDrJWords = kGridMaxPts / 32;  // one bit per segment index
 
@@ -650,7 +653,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
     __shared__ uint16_t jpre[kDrJWords];  // set bits of jb before word w
     __shared__ int box[kThreads / 64][4];
     __shared__ int wsum[kThreads / 64];
-    __shared__ int s_dup, s_kept, s_nc;
+    __shared__ int s_dup, s_kept, s_nc, s_nl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kW = kThreads / 64;
     if (tid == 0) {
@@ -1013,48 +1016,80 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                 }
             }
         };
-        // memberships -> sizes and first members (first claim + later seeds, as the grid kernel)
-        uint32_t claim2[kDrPer / 2];  // claim + 1 of points u (low half) and u + 1 (high half)
-        uint32_t more = 0u;
-#pragma unroll
-        for (int u = 0; u < kDrPer / 2; ++u) claim2[u] = 0u;
-        auto set_claim = [&](int u, int c) { claim2[u >> 1] |= (uint32_t)(c + 1) << ((u & 1) * 16); };
+        // memberships -> sizes and first members (first claim + later seeds, as the grid kernel).
+        // Core points by their lane; the non-core points' disk walks are first listed workgroup-
+        // wide (c_rank's 1 024 slots, unused until the ranks) and then walked one per lane, so a
+        // wave does about one walk instead of one per slot u.  A walked point's claim goes to
+        // labels[] (first | more << 16, -1 noise) until the labels pass translates it.
+        uint32_t ncm = 0u;  // bit u: slot u holds a non-core point
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
             const int j = u * kThreads + tid;
             if (j >= m) continue;
-            const int x = ecc::xy_x(pt(u)) - xmn, y = ecc::xy_y(pt(u)) - ymn;
-            const int cj = comp_of(parent, rank_at(x, y));
+            const int cj = comp_of(parent, rank_at(ecc::xy_x(pt(u)) - xmn, ecc::xy_y(pt(u)) - ymn));
             if (cj >= 0) {
-                set_claim(u, cj);
                 atomicAdd(&c_size[cj], 1);
                 atomicMin(&c_front[cj], j);
-                continue;
+            } else {
+                ncm |= 1u << u;
             }
-            int first = 0x7fffffff, n_seed = 0, seed_c = -1;
-            for_core_nbrs(x, y, [&](int q) {
-                const int pv = parent[q];
-                const int c = pv <= -2 ? -pv - 2 : -parent[pv] - 2;
-                const bool seed = (sb[q >> 5] >> (q & 31)) & 1u;
-                first = c < first ? c : first;
-                n_seed += seed ? 1 : 0;
-                seed_c = seed ? c : seed_c;
-            });
-            if (first == 0x7fffffff) continue;  // noise
-            set_claim(u, first);
-            atomicAdd(&c_size[first], 1);
-            atomicMin(&c_front[first], j);
-            if (n_seed == 0 || (n_seed == 1 && seed_c == first)) continue;
-            more |= 1u << u;
-            for_core_nbrs(x, y, [&](int q) {  // later clusters seeded by a neighbour
-                if (!((sb[q >> 5] >> (q & 31)) & 1u)) return;
-                const int pv = parent[q];
-                const int c = pv <= -2 ? -pv - 2 : -parent[pv] - 2;
-                if (c != first) {
-                    atomicAdd(&c_size[c], 1);
-                    atomicMin(&c_front[c], j);
+        }
+        uint16_t *const walk = reinterpret_cast<uint16_t *>(c_rank);  // [kDrComp] non-core indices
+        const uint32_t ncm0 = ncm;
+        for (;;) {
+            if (tid == 0) s_nl = 0;
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < kDrPer; ++u) {  // append (wave-aggregated), while there is room
+                const bool nc_u = (ncm >> u) & 1u;
+                const uint64_t bal = __ballot(nc_u);
+                if (!bal) continue;  // uniform
+                const int leader = __ffsll((unsigned long long)bal) - 1;
+                int b = 0;
+                if (lane == leader) b = atomicAdd(&s_nl, __popcll(bal));
+                b = __shfl(b, leader);
+                const int pos = b + __popcll(bal & ((1ull << lane) - 1ull));
+                if (nc_u && pos < kDrComp) {
+                    walk[pos] = (uint16_t)(u * kThreads + tid);
+                    ncm &= ~(1u << u);
                 }
-            });
+            }
+            __syncthreads();
+            const int n_walk = min(s_nl, kDrComp);
+            if (tid < n_walk) {
+                const int j = walk[tid];
+                const uint32_t p = xy[base + j];
+                const int x = ecc::xy_x(p) - xmn, y = ecc::xy_y(p) - ymn;
+                int first = 0x7fffffff, n_seed = 0, seed_c = -1;
+                for_core_nbrs(x, y, [&](int q) {
+                    const int pv = parent[q];
+                    const int c = pv <= -2 ? -pv - 2 : -parent[pv] - 2;
+                    const bool seed = (sb[q >> 5] >> (q & 31)) & 1u;
+                    first = c < first ? c : first;
+                    n_seed += seed ? 1 : 0;
+                    seed_c = seed ? c : seed_c;
+                });
+                int claim = -1;
+                if (first != 0x7fffffff) {  // else noise
+                    atomicAdd(&c_size[first], 1);
+                    atomicMin(&c_front[first], j);
+                    const bool more = !(n_seed == 0 || (n_seed == 1 && seed_c == first));
+                    claim = first | (more ? 1 << 16 : 0);
+                    if (more) {
+                        for_core_nbrs(x, y, [&](int q) {  // later clusters seeded by a neighbour
+                            if (!((sb[q >> 5] >> (q & 31)) & 1u)) return;
+                            const int pv = parent[q];
+                            const int c = pv <= -2 ? -pv - 2 : -parent[pv] - 2;
+                            if (c != first) {
+                                atomicAdd(&c_size[c], 1);
+                                atomicMin(&c_front[c], j);
+                            }
+                        });
+                    }
+                }
+                labels[base + j] = claim;
+            }
+            if (!__syncthreads_or(ncm != 0u)) break;  // also: the list is read before the next appends
         }
         __syncthreads();
         DB_MARK(3);  // memberships
@@ -1079,15 +1114,22 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         if (tid == 0) n_clusters[s] = s_kept;
         DB_MARK(4);  // ranks
         // labels (first claim, coalesced: lane tid holds j = u * kThreads + tid) and the further
-        // memberships
+        // memberships; a non-core point's claim is read back from labels[] (written by the lane
+        // that walked it, before the barriers since)
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
             const int j = u * kThreads + tid;
             if (j >= m) break;
-            const int first = (int)((claim2[u >> 1] >> ((u & 1) * 16)) & 0xffffu) - 1;
-            labels[base + j] = first >= 0 ? c_rank[first] : -1;
-            if (!((more >> u) & 1u)) continue;
             const int x = ecc::xy_x(pt(u)) - xmn, y = ecc::xy_y(pt(u)) - ymn;
+            if (!((ncm0 >> u) & 1u)) {
+                labels[base + j] = c_rank[comp_of(parent, rank_at(x, y))];
+                continue;
+            }
+            const int claim = __hip_atomic_load(labels + base + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (claim < 0) continue;  // noise: -1 already
+            const int first = claim & 0xffff;
+            labels[base + j] = c_rank[first];
+            if (!(claim >> 16)) continue;
             for_core_nbrs(x, y, [&](int q) {
                 if (!((sb[q >> 5] >> (q & 31)) & 1u)) return;
                 const int pv = parent[q];
