@@ -399,7 +399,7 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
             const int ra = rep[c];
             if (ra == 0x7fffffff || !self_clique) continue;
             const int cx = c % g.gx, cy = c / g.gx;
-#pragma unroll 1
+#pragma unroll  // g.kx[r] stays in registers (a dynamic index would put it in scratch)
             for (int r = 0; r <= 2 * ecc::epsg::kMaxR; ++r) {
                 const int dyc = r - ecc::epsg::kMaxR, kx = g.kx[r], ry = cy + dyc;
                 if (kx < 0 || dyc < 0 || ry >= g.gy) continue;
@@ -432,7 +432,7 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
                 }
             };
             if (!self_clique) pair_test(alo, ahi, true);
-#pragma unroll 1
+#pragma unroll  // g.kx[r] stays in registers (a dynamic index would put it in scratch)
             for (int r = 0; r <= 2 * ecc::epsg::kMaxR; ++r) {
                 const int dyc = r - ecc::epsg::kMaxR, kx = g.kx[r], ry = cy + dyc;
                 if (kx < 0 || dyc < 0 || ry >= g.gy) continue;
@@ -451,23 +451,19 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
         __syncthreads();
         DB_MARK(1);  // unions
         // 3. compress; roots -> component ids in ascending root order (block scan over j)
-        int roots[kGridPer], nr = 0;
+        uint32_t rootm = 0u;  // bit u: j0 + u is a root
         const int j0 = tid * kGridPer;
 #pragma unroll
         for (int u = 0; u < kGridPer; ++u) {
             const int j = j0 + u;
-            roots[u] = 0;
-            if (j < m && parent[j] != -1) {
-                const int r = uf_find(parent, j);
-                roots[u] = r == j;
-                nr += roots[u];
-            }
+            if (j < m && parent[j] != -1 && uf_find(parent, j) == j) rootm |= 1u << u;
         }
+        const int nr = __popc(rootm);
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kGridPer; ++u) {
             const int j = j0 + u;
-            if (j < m && parent[j] != -1 && !roots[u]) parent[j] = uf_root(parent, j);
+            if (j < m && parent[j] != -1 && !((rootm >> u) & 1u)) parent[j] = uf_root(parent, j);
         }
         const int x = ecc::wave_incl_scan(nr);  // DPP
         if (lane == 63) wsum[wave] = x;
@@ -481,7 +477,7 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
         if (nc <= kMaxComp) {
 #pragma unroll
             for (int u = 0; u < kGridPer; ++u)
-                if (roots[u]) parent[j0 + u] = -(cid++) - 2;
+                if ((rootm >> u) & 1u) parent[j0 + u] = -(cid++) - 2;
         }
         __syncthreads();
         if (nc > kMaxComp) {  // too many components for the LDS tables
@@ -502,18 +498,26 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
         // 4. memberships -> sizes and first members.  A non-core point's first claim (the
         //    first-created cluster with a core neighbour) and whether a LATER cluster's seed is
         //    its neighbour come from one walk over its cells; the claim stays in registers for
-        //    the labels, the (rare) further memberships are walked again in phase 6.
-        int claim[kGridPer];
+        //    the labels (16 bits each, two per register), the (rare) further memberships are
+        //    walked again in phase 6.
+        uint32_t claim2[kGridPer / 2];  // claim + 1 of query u in bits 16 (u & 1) of word u / 2
         uint32_t more = 0u;  // bit u: query u has further memberships
+#pragma unroll
+        for (int u = 0; u < kGridPer / 2; ++u) claim2[u] = 0u;
+        auto get16 = [&](int u) { return (int)((claim2[u >> 1] >> ((u & 1) * 16)) & 0xffffu) - 1; };
+        auto set16 = [&](int u, int v) {  // v >= -1
+            const int sh = (u & 1) * 16;
+            claim2[u >> 1] = (claim2[u >> 1] & ~(0xffffu << sh)) | (uint32_t)(v + 1) << sh;
+        };
+        static_assert(kMaxComp < 0xffff, "claims in 16 bits");
 #pragma unroll
         for (int u = 0; u < kGridPer; ++u) {
             const int q = u * kThreads + tid;
-            claim[u] = -1;
             if (q >= m) continue;
             const int i = sidx[q];
             const int ci = comp_of(parent, i);
             if (ci >= 0) {
-                claim[u] = ci;
+                set16(u, ci);
                 atomicAdd(&c_size[ci], 1);
                 atomicMin(&c_front[ci], i);
                 continue;
@@ -530,7 +534,7 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
                 seed_c = pv <= -2 ? c : seed_c;
             });
             if (first == 0x7fffffff) continue;  // noise
-            claim[u] = first;
+            set16(u, first);
             atomicAdd(&c_size[first], 1);
             atomicMin(&c_front[first], i);
             if (n_seed == 0 || (n_seed == 1 && seed_c == first)) continue;
@@ -567,15 +571,15 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
         if (tid == 0) n_clusters[s] = s_kept;
         DB_MARK(4);  // ranks
         // 6. labels (the first claim, staged over parent[] by segment index for a coalesced
-        //    write) and the further memberships
-        int lab[kGridPer], lidx[kGridPer];
+        //    write; the label replaces the claim in its register half) and the further memberships
 #pragma unroll
         for (int u = 0; u < kGridPer; ++u) {
             const int q = u * kThreads + tid;
-            lidx[u] = q < m ? (int)sidx[q] : -1;
-            lab[u] = claim[u] >= 0 ? c_rank[claim[u]] : -1;
+            if (q >= m) break;
+            const int first = get16(u);
+            set16(u, first >= 0 ? c_rank[first] : -1);
             if (!((more >> u) & 1u)) continue;
-            const int i = lidx[u], first = claim[u];
+            const int i = sidx[q];
             const uint32_t v = spt[q];
             ecc::epsg::for_candidates(g, cend, spt, v, [&](int a, uint32_t w, bool ok) {
                 if (!(eps_in(g, v, w, e_int, r2i) & ok)) return;
@@ -593,8 +597,10 @@ dbscan_grid_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t stri
         }
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < kGridPer; ++u)
-            if (lidx[u] >= 0) parent[lidx[u]] = lab[u];
+        for (int u = 0; u < kGridPer; ++u) {
+            const int q = u * kThreads + tid;
+            if (q < m) parent[sidx[q]] = get16(u);
+        }
         __syncthreads();
         for (int j = tid; j < m; j += kThreads) labels[base + j] = parent[j];
         __syncthreads();
