@@ -632,6 +632,14 @@ constexpr int kDrWords = 2880;  // (bits, prefix) pairs: 346x260 needs 2860 (LDS
 constexpr int kDrHw = 512;      // disk half-width table: eps < 512
 constexpr int kDrPer = kGridMaxPts / kThreads;
 constexpr int kDrNarrow = 32;  // eps up to which a chord (2 eps + 1 pixels) spans at most 3 words
+// A lane index the compiler cannot hoist or reuse across the kernel's phases: values derived
+// from it are born in the phase that uses them (hoisted to the top and kept, they were spilled to
+// scratch around the unions: one scratch round trip per value and segment).
+__device__ __forceinline__ int opaque_lane(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 #ifndef ECC_DR_ROWS
 #define ECC_DR_ROWS 4
 #endif
@@ -711,11 +719,11 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         const int64_t words64 = (int64_t)H * WW;
         bool leftover = words64 > kDrWords || e_int >= kDrHw;  // uniform
         const int words = leftover ? 0 : (int)words64;
-        for (int w = tid; w < words; w += kThreads) {
+        for (int w = opaque_lane(tid); w < words; w += kThreads) {
             wd[w] = make_uint2(0u, 0u);
             cw[w] = 0u;
         }
-        for (int w = tid; w < kDrJWords; w += kThreads) jb[w] = sb[w] = 0u;
+        for (int w = opaque_lane(tid); w < kDrJWords; w += kThreads) jb[w] = sb[w] = 0u;
         __syncthreads();
         if (!leftover) {
 #pragma unroll
@@ -738,14 +746,14 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         }
         {  // points before each word (thread t: words [t * per, t * per + per))
             const int per = (words + kThreads - 1) / kThreads;
-            const int w0 = tid * per, w1 = min(w0 + per, words);
+            const int w0 = opaque_lane(tid) * per, w1 = min(w0 + per, words);
             int loc = 0;
             for (int w = w0; w < w1; ++w) loc += __popc(wd[w].x);
             const int inc = ecc::wave_incl_scan(loc);
-            if (lane == 63) wsum[wave] = inc;
+            if (lane == 63) wsum[opaque_lane(wave)] = inc;
             __syncthreads();
             int off = inc - loc;
-            for (int w = 0; w < wave; ++w) off += wsum[w];
+            for (int w = 0; w < opaque_lane(wave); ++w) off += wsum[w];
             for (int w = w0; w < w1; ++w) {
                 wd[w].y = (uint32_t)off;
                 off += __popc(wd[w].x);
@@ -761,12 +769,12 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         // the point of lane tid's slot u, re-read (an L2 hit) in the phases after the counts: its
         // register copy would not fit the 64 VGPRs beside the union batches
         auto pt = [&](int u) -> uint32_t {
-            return __hip_atomic_load(xy + base + u * kThreads + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return __hip_atomic_load(xy + base + u * kThreads + opaque_lane(tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         };
         // counts -> core flags and bits
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
-            const int j = u * kThreads + tid;
+            const int j = u * kThreads + opaque_lane(tid);
             if (j >= m) break;
             const int x = ecc::xy_x(v[u]) - xmn, y = ecc::xy_y(v[u]) - ymn;
             int cnt = 0;
@@ -870,7 +878,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         // dependent LDS round trip per step instead of one per row and step).
 #pragma unroll 1
         for (int u = 0; u < kDrPer; ++u) {
-            if (u * kThreads + tid >= m) break;
+            if (u * kThreads + opaque_lane(tid) >= m) break;
             const int x = ecc::xy_x(pt(u)) - xmn, y = ecc::xy_y(pt(u)) - ymn;
             const int j = rank_at(x, y);  // the point's id in the union-find
             if (parent[j] == -1) continue;
@@ -924,7 +932,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         // compress (ranks r0 .. r0 + 7 per lane); each root then keeps the smallest index of its
         // component's core points (the seed), and the seeds' order gives the component ids
         uint32_t rootm = 0u;
-        const int r0 = tid * kGridPer;
+        const int r0 = opaque_lane(tid) * kGridPer;
 #pragma unroll
         for (int u = 0; u < kGridPer; ++u) {
             const int r = r0 + u;
@@ -943,7 +951,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
-            const int j = u * kThreads + tid;
+            const int j = u * kThreads + opaque_lane(tid);
             if (j >= m) break;
             const int r = rank_at(ecc::xy_x(pt(u)) - xmn, ecc::xy_y(pt(u)) - ymn);
             const int pr = parent[r];
@@ -953,7 +961,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         // the seeds: index j in jb, rank in sb (the memberships' "neighbour is a seed" test)
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
-            const int j = u * kThreads + tid;
+            const int j = u * kThreads + opaque_lane(tid);
             if (j >= m) break;
             const int r = rank_at(ecc::xy_x(pt(u)) - xmn, ecc::xy_y(pt(u)) - ymn);
             const int pr = parent[r];
@@ -966,7 +974,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             static_assert(kDrJWords == 4 * 64, "four jb words per lane");
             int c4[4], loc = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) loc += (c4[k] = __popc(jb[4 * lane + k]));
+            for (int k = 0; k < 4; ++k) loc += (c4[k] = __popc(jb[4 * opaque_lane(lane) + k]));
             const int inc = ecc::wave_incl_scan(loc);
             int off = inc - loc;
 #pragma unroll
@@ -993,7 +1001,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
             const int id = jpre[j >> 5] + __popc(jb[j >> 5] & ((1u << (j & 31)) - 1u));
             parent[r0 + u] = -id - 2;
         }
-        for (int c = tid; c < nc; c += kThreads) {
+        for (int c = opaque_lane(tid); c < nc; c += kThreads) {
             c_size[c] = 0;
             c_front[c] = 0x7fffffff;
         }
@@ -1030,7 +1038,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         uint32_t ncm = 0u;  // bit u: slot u holds a non-core point
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
-            const int j = u * kThreads + tid;
+            const int j = u * kThreads + opaque_lane(tid);
             if (j >= m) continue;
             const int cj = comp_of(parent, rank_at(ecc::xy_x(pt(u)) - xmn, ecc::xy_y(pt(u)) - ymn));
             if (cj >= 0) {
@@ -1054,16 +1062,16 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
                 int b = 0;
                 if (lane == leader) b = atomicAdd(&s_nl, __popcll(bal));
                 b = __shfl(b, leader);
-                const int pos = b + __popcll(bal & ((1ull << lane) - 1ull));
+                const int pos = b + __popcll(bal & ((1ull << opaque_lane(lane)) - 1ull));
                 if (nc_u && pos < kDrComp) {
-                    walk[pos] = (uint16_t)(u * kThreads + tid);
+                    walk[pos] = (uint16_t)(u * kThreads + opaque_lane(tid));
                     ncm &= ~(1u << u);
                 }
             }
             __syncthreads();
             const int n_walk = min(s_nl, kDrComp);
             if (tid < n_walk) {
-                const int j = walk[tid];
+                const int j = walk[opaque_lane(tid)];
                 const uint32_t p = xy[base + j];
                 const int x = ecc::xy_x(p) - xmn, y = ecc::xy_y(p) - ymn;
                 int first = 0x7fffffff, n_seed = 0, seed_c = -1;
@@ -1102,7 +1110,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         // output order: kept clusters by (size desc, front asc, creation asc)
         if (tid == 0) s_kept = 0;
         __syncthreads();
-        for (int c = tid; c < nc; c += kThreads) {
+        for (int c = opaque_lane(tid); c < nc; c += kThreads) {
             const int sz = c_size[c], fr = c_front[c];
             int r = -1;
             if (sz >= min_size && sz <= max_size) {
@@ -1124,7 +1132,7 @@ dbscan_run_kernel(const uint32_t *__restrict__ xy, int64_t n_segs, int64_t strid
         // that walked it, before the barriers since)
 #pragma unroll
         for (int u = 0; u < kDrPer; ++u) {
-            const int j = u * kThreads + tid;
+            const int j = u * kThreads + opaque_lane(tid);
             if (j >= m) break;
             const int x = ecc::xy_x(pt(u)) - xmn, y = ecc::xy_y(pt(u)) - ymn;
             if (!((ncm0 >> u) & 1u)) {
