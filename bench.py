@@ -55,8 +55,8 @@ PRESET_SLICES = {"c4": 1221, "c5": 3052}  # 20 004 864 / 50 003 968 events per G
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--preset", choices=("c4", "c5"), default=None,
                     help="c4: 20.0 M events per GPU (1221 slices, BASELINE C4, the metric's config); "
                          "c5: 50.0 M events per GPU (3052 slices; 8 GPUs = the 400 M-event stream of C5). "
