@@ -720,10 +720,10 @@ struct ArcLds {
     int64_t wave_min[16];  // per wave (up to 16 waves: arc_dense_kernel's workgroup size is a switch)
     int32_t exact_only;  // a value above t_last: clamped keys unusable
     int32_t mixed;       // clamped values not all equal to the window minimum of B
-    int32_t n_tasks;
     int32_t q4n;
     int32_t n_exact;      // some task needs the exact int64 test
     int32_t wave_own[16];  // the wave's own-tile pixels have pairs
+    int32_t wave_tasks[16];  // the wave's eligible pairs (task-list offsets by a scan)
 };
 
 // arc_dense_kernel's clamp: v <= L maps to 0 (mixed_flag set when v is not the window minimum vz)
@@ -937,14 +937,19 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     if (tid == 0) {
         L.exact_only = narrow ? 0 : 1;  // wide groups: every test exact
         L.mixed = 0;
-        L.n_tasks = 0;
         L.q4n = 0;
         L.n_exact = 0;
     }
     const bool own = win_lane && ox >= 0 && oy >= 0 && ox < kTile && oy < kTile;
     const uint64_t own_pairs = __ballot(own && mk != 0u);
     if (lane == 0) L.wave_own[wave] = own_pairs != 0ull;
-    __syncthreads();  // the task counter is zeroed
+    // the own tile's eligible pairs, placed by a scan (one returning LDS atomic per pair on one
+    // counter serialised a heavy item's ~3 000 tasks)
+    const uint32_t tm0 = (own && !is_border(wx, wy, g)) ? (mk & eligible_slices(g, grp)) : 0u;
+    const int tcnt = __popc(tm0);
+    const int tincl = ecc::wave_incl_scan(tcnt);  // DPP
+    if (lane == 63) L.wave_tasks[wave] = tincl;
+    __syncthreads();
     if (win_lane) {
         L.mb[wp].mask = mk;
         const int p = __popc(mk);
@@ -959,11 +964,17 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
                 mm &= mm - 1u;
             });
         }
-        if (own && !is_border(wx, wy, g)) {
-            const int lp = oy * kTile + ox;
-            for (uint32_t tm = mk & eligible_slices(g, grp); tm; tm &= tm - 1u)
-                L.tasks[atomicAdd(&L.n_tasks, 1)] = (uint16_t)((__ffs(tm) - 1) * kTilePix + lp);
-        }
+    }
+    int toff = tincl - tcnt, n_tasks = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        const int c = L.wave_tasks[w];
+        toff += w < wave ? c : 0;
+        n_tasks += c;
+    }
+    {
+        const int lp = oy * kTile + ox;
+        for (uint32_t tm = tm0; tm; tm &= tm - 1u) L.tasks[toff++] = (uint16_t)((__ffs(tm) - 1) * kTilePix + lp);
     }
     const int64_t bmin = ecc::wave_min_i64(bq);  // DPP
     if (lane == 0) L.wave_min[wave] = bmin;
@@ -993,7 +1004,6 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     //     exact int64 tests of whatever the keys could not decide, marked in the task list
     //     itself (bit 14: circle 3 undecided; bit 15: circle 3 passed, circle 4 still open).
     //     Wide groups and values above t_last (exact_only) take every task exactly.
-    const int n_tasks = L.n_tasks;
     const bool fast = !L.exact_only;
     const bool ties_exact = !L.mixed;
     constexpr uint16_t kOpen3 = 0x4000, kOpen4 = 0x8000;
