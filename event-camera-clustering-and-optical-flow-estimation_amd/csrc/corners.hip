@@ -715,7 +715,7 @@ struct ArcLds {
     uint32_t T[kGroup][kWinPix];      // 60.5 KiB
     MaskB mb[kWinPix];
     uint32_t res[kPairWords];         // corner (slice, pixel) pairs of the tile
-    uint16_t tasks[kGroup * kTilePix]; // the tile's eligible pairs (j * 196 + pixel)
+    uint16_t tasks[kGroup * kTilePix]; // the tile's eligible pairs (j << 9 | window pixel)
     uint16_t q4[kQ4Cap];               // circle-3 survivors (beyond the cap: tested inline)
     int64_t wave_min[16];  // per wave (up to 16 waves: arc_dense_kernel's workgroup size is a switch)
     int32_t exact_only;  // a value above t_last: clamped keys unusable
@@ -972,10 +972,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         toff += w < wave ? c : 0;
         n_tasks += c;
     }
-    {
-        const int lp = oy * kTile + ox;
-        for (uint32_t tm = tm0; tm; tm &= tm - 1u) L.tasks[toff++] = (uint16_t)((__ffs(tm) - 1) * kTilePix + lp);
-    }
+    for (uint32_t tm = tm0; tm; tm &= tm - 1u) L.tasks[toff++] = (uint16_t)((__ffs(tm) - 1) << 9 | wp);  // j << 9 | window pixel
     const int64_t bmin = ecc::wave_min_i64(bq);  // DPP
     if (lane == 0) L.wave_min[wave] = bmin;
     __syncthreads();
@@ -1009,14 +1006,13 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     constexpr uint16_t kOpen3 = 0x4000, kOpen4 = 0x8000;
     if (fast) {
         for (int ti = tid; ti < n_tasks; ti += NT) {
-            const int pi = L.tasks[ti];
-            const int j = pi / kTilePix, lp = pi % kTilePix;
-            const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-            const uint32_t below = below_mask(j);
+            const int pi = L.tasks[ti];  // j << 9 | window pixel
+            const int wp0 = pi & 511;
+            const uint32_t below = below_mask(pi >> 9);
             uint32_t k3[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) k3[k] = (win_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 4) | k;
-            const int r3 = arc_keys<16, 16, 4, 3, 6>(k3, ties_exact);
+            for (int k = 0; k < 16; ++k) k3[k] = (win_value(L, wp0 + c3dy[k] * kWin + c3dx[k], below) << 5) | k;
+            const int r3 = arc_keys<16, 16, 5, 3, 6>(k3, ties_exact);
             if (r3 > 0) {
                 const int qi = atomicAdd(&L.q4n, 1);
                 if (qi < kQ4Cap) L.q4[qi] = (uint16_t)ti;
@@ -1033,8 +1029,7 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
     for (int qi = tid; qi < n4; qi += NT) {
         const int ti = L.q4[qi];
         const int pi = L.tasks[ti];
-        const int j = pi / kTilePix, lp = pi % kTilePix;
-        const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
+        const int j = pi >> 9, wp0 = pi & 511;
         const uint32_t below = below_mask(j);
         uint32_t k4[32];
 #pragma unroll
@@ -1042,8 +1037,9 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
 #pragma unroll
         for (int k = 20; k < 32; ++k) k4[k] = 0u;
         const int r4 = arc_keys<20, 32, 5, 4, 8>(k4, ties_exact);
-        if (r4 > 0) {
-            atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
+        if (r4 > 0) {  // the pair's bit: slice j, tile pixel (wp0's row and column less the halo)
+            const int rb = j * kTilePix + (wp0 / kWin - kHalo) * kTile + (wp0 % kWin - kHalo);
+            atomicOr(&L.res[rb >> 5], 1u << (rb & 31));
         } else if (r4 < 0) {
             L.tasks[ti] = (uint16_t)(pi | kOpen4);
             L.n_exact = 1;
@@ -1055,12 +1051,14 @@ __device__ __forceinline__ void arc_dense_item(ArcLds &L, int64_t item, const in
         for (int ti = tid; ti < n_tasks; ti += NT) {
             const int e = L.tasks[ti], pi = e & 0x3fff;
             if (fast && !(e & (kOpen3 | kOpen4))) continue;
-            const int j = pi / kTilePix, lp = pi % kTilePix;
-            const int wp0 = (lp / kTile + kHalo) * kWin + (lp % kTile + kHalo);
-            const int64_t q0 = (int64_t)(y0 + lp / kTile) * g.W + (x0 + lp % kTile);
+            const int j = pi >> 9, wp0 = pi & 511;
+            const int ly = wp0 / kWin - kHalo, lx = wp0 % kWin - kHalo;
+            const int64_t q0 = (int64_t)(y0 + ly) * g.W + (x0 + lx);
             const uint32_t below = below_mask(j);
-            if (exact_pair_test(&L, wp0, q0, below, (e & kOpen4) != 0, Bg, t, grp_first, Lt, g.W, narrow))
-                atomicOr(&L.res[pi >> 5], 1u << (pi & 31));
+            if (exact_pair_test(&L, wp0, q0, below, (e & kOpen4) != 0, Bg, t, grp_first, Lt, g.W, narrow)) {
+                const int rb = j * kTilePix + ly * kTile + lx;
+                atomicOr(&L.res[rb >> 5], 1u << (rb & 31));
+            }
         }
         __syncthreads();
     }
