@@ -2326,6 +2326,173 @@ ECC_API int ecc_kmeans_labels_xy16(ecc_ctx *ctx, const uint32_t *xy, int64_t n_s
     return ECC_OK;
 }
 
+// ---- "ref_compat" k-means loop ----------------------------------------
+// The reference's host loop KM/assign_to_centers2.c:184-548 over its three kernels, with its
+// quirks: 8 centres; assign_to_centers (:10-27 of the .cl) labels a point, assign_data_cluster
+// appends it to its cluster's bin of 2048 slots (x in [0, 2048), y in [2048, 4096) of the bin's
+// 4096 floats; a point past the 2048th is counted but not stored); the bins are zeroed once
+// (:133-137) and never cleared, so a bin keeps the previous passes' values past its count (Q8);
+// reduction_scalar sums each 1024-float chunk as a pairwise tree; the update reads the chunk sums
+// as ss[j], ss[j+1] (x) and ss[j+2], ss[j+3] (y) for j = 2c (:509-512, Q7), divides by the bin
+// count (0: inf / NaN), and replaces coordinate j only while |new - old| — C's int abs of the
+// float — exceeds the running maximum (:525-532, Q9); the loop restarts while that maximum is
+// > 10 (:545-548).  The reference appends in atomic order; here a bin is filled in point-index
+// order (oracle/oracle.cpp orc_kmeans_refcompat, pinned pass by pass against the reference kernels
+// run on the box: tests/test_ref_opencl.py).  ONE workgroup: the 128 KB of bins live in LDS for
+// the whole loop, the points are taken in 16 rounds of 1024 (a bin slot is the point's rank in
+// its cluster by ballots and per-wave counts), and wave w sums chunks w and w + 16 with each lane
+// holding the chunk's elements lane + 64 i (the tree's first four levels inside a lane, the last
+// six by shuffles).
+constexpr int kRcThreads = 1024;
+constexpr int kRcPer = 16;                         // points per thread
+constexpr int kRcMaxPts = kRcThreads * kRcPer;     // 16384 = 8 bins of 2048
+constexpr int kRcBinFloats = 8 * 4096;
+
+// C's int abs of a float (the reference's `abs` on float, :526-527): truncation to int; an
+// out-of-range or NaN value converts to INT_MIN on the reference's x86-64 (cvttss2si), whose abs
+// stays INT_MIN (the oracle's ref_int_abs)
+__device__ __forceinline__ float ref_int_abs_dev(float d) {
+    if (!(d > -2147483648.f && d < 2147483648.f)) return -2147483648.f;
+    const int i = __float2int_rz(d);
+    return __int2float_rn(i < 0 ? -i : i);
+}
+
+__global__ void __launch_bounds__(kRcThreads)
+kmeans_refcompat_kernel(const float *__restrict__ xy, int n, float *__restrict__ cent16, int max_passes,
+                        int32_t *__restrict__ passes_out, int32_t *__restrict__ bin_counts_out,
+                        float *__restrict__ sums_out) {
+    extern __shared__ float bins[];  // [8][4096]
+    __shared__ float2 s_c[8];
+    __shared__ float s_ss[32];
+    __shared__ int s_wc[kRcThreads / 64][8];  // a round's cluster counts per wave
+    __shared__ int s_run[8];                  // the pass's cluster counts so far (cluster_index)
+    __shared__ int s_again;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int i = tid; i < kRcBinFloats; i += kRcThreads) bins[i] = 0.f;  // :133-137, once
+    if (tid < 8) s_c[tid] = make_float2(cent16[2 * tid], cent16[2 * tid + 1]);
+    int passes = 0;
+    for (;;) {
+        if (tid < 8) s_run[tid] = 0;
+        __syncthreads();
+        // assign_to_centers, then assign_data_cluster in point-index order: round u takes points
+        // u * 1024 + thread, so a point's slot is its cluster's count over the earlier rounds,
+        // the earlier waves of its round and the earlier lanes of its wave
+        for (int u = 0; u < kRcPer; ++u) {
+            const int g = u * kRcThreads + tid;
+            float x = 0.f, y = 0.f;
+            uint32_t c = 127u;
+            if (g < n) {
+                x = xy[2 * g];
+                y = xy[2 * g + 1];
+                const uint32_t a = assign_point(x, y, s_c, 8, 50.f);
+                c = a == 255u ? 127u : a;  // (2c)/2 of the reference's label: 255/2 = 127, no bin
+            }
+            int rank = 0;
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) {
+                const uint64_t m = __ballot(c == (uint32_t)cc);
+                if (c == (uint32_t)cc) rank = __popcll(m & lt);
+                if (lane == 0) s_wc[wave][cc] = __popcll(m);
+            }
+            __syncthreads();
+            if (c < 8u) {
+                int idx = s_run[c] + rank;
+                for (int w = 0; w < wave; ++w) idx += s_wc[w][c];
+                if (idx < 2048) {  // counted but not stored past the bin (no check in the kernel)
+                    bins[c * 4096 + idx] = x;
+                    bins[c * 4096 + 2048 + idx] = y;
+                }
+            }
+            __syncthreads();
+            if (tid < 8) {
+                int tot = 0;
+#pragma unroll
+                for (int w = 0; w < kRcThreads / 64; ++w) tot += s_wc[w][tid];
+                s_run[tid] += tot;
+            }
+        }
+        __syncthreads();
+        // reduction_scalar: chunk sums, buf[l] += buf[l + s] for s = 512 .. 1
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int chunk = wave + 16 * h;
+            float v[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = bins[chunk * 1024 + lane + 64 * i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = __fadd_rn(v[i], v[i + 8]);  // s = 512
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(v[i], v[i + 4]);  // 256
+            v[0] = __fadd_rn(v[0], v[2]);                                   // 128
+            v[1] = __fadd_rn(v[1], v[3]);
+            v[0] = __fadd_rn(v[0], v[1]);                                   // 64
+#pragma unroll
+            for (int sft = 32; sft > 0; sft >>= 1) {                        // 32 .. 1
+                const float o = __shfl_down(v[0], sft);
+                if (lane < sft) v[0] = __fadd_rn(v[0], o);
+            }
+            if (lane == 0) s_ss[chunk] = v[0];
+        }
+        __syncthreads();
+        if (tid == 0) {  // the update (:509-532) and the restart test (:545-548)
+            float nc[16], c16[16];
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) {
+                const float cn = __int2float_rn(s_run[j / 2]);
+                nc[j] = __fdiv_rn(__fadd_rn(s_ss[j], s_ss[j + 1]), cn);
+                nc[j + 1] = __fdiv_rn(__fadd_rn(s_ss[j + 2], s_ss[j + 3]), cn);
+                c16[j] = s_c[j / 2].x;
+                c16[j + 1] = s_c[j / 2].y;
+            }
+            float error_max = 0.f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float a = ref_int_abs_dev(__fsub_rn(nc[j], c16[j]));
+                if (a > error_max) {
+                    error_max = a;
+                    c16[j] = nc[j];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 8; ++c) s_c[c] = make_float2(c16[2 * c], c16[2 * c + 1]);
+            s_again = error_max > 10.f && passes + 1 < max_passes;
+        }
+        ++passes;
+        __syncthreads();
+        if (!s_again) break;  // uniform
+    }
+    if (tid < 8) {
+        cent16[2 * tid] = s_c[tid].x;
+        cent16[2 * tid + 1] = s_c[tid].y;
+        if (bin_counts_out) bin_counts_out[tid] = s_run[tid];
+    }
+    if (sums_out && tid < 32) sums_out[tid] = s_ss[tid];
+    if (passes_out && tid == 0) *passes_out = passes;
+}
+
+ECC_API int ecc_kmeans_refcompat_f32(ecc_ctx *ctx, const float *xy, int64_t n, float *centroids16, int32_t max_passes,
+                                     int32_t *passes_out, int32_t *bin_counts_out, float *partial_sums_out,
+                                     ecc_stream_t stream) {
+    if (!ctx || !centroids16 || n < 0 || n > kRcMaxPts || max_passes < 1 || (n > 0 && !xy)) return ECC_ERR_INVALID;
+    ECC_CHECK_HIP(ctx, hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t s = ecc::as_stream(stream);
+    static bool lds_ok = false;
+    if (!lds_ok) {
+        ECC_CHECK_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&kmeans_refcompat_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kRcBinFloats * 4),
+                      "kmeans_refcompat LDS");
+        lds_ok = true;
+    }
+    {
+        ECC_TIMED(ctx, s, "kmeans_refcompat_kernel");
+        hipLaunchKernelGGL(kmeans_refcompat_kernel, dim3(1), dim3(kRcThreads), kRcBinFloats * 4, s, xy, (int)n,
+                           centroids16, max_passes, passes_out, bin_counts_out, partial_sums_out);
+    }
+    ECC_CHECK_LAUNCH(ctx, "kmeans_refcompat");
+    return ECC_OK;
+}
+
 // ---- count images (multi-GPU k-means: one all-reduce of the counts instead of one per pass) ----
 // A shard's representatives counted per pixel of a caller-given frame (counts[y * w + x], u32).
 // Counts are additive over shards, and a Lloyd pass over a count image adds exactly the integer

@@ -135,6 +135,7 @@ _sigs = {
     "ecc_kmeans_run_xy16": (C.c_int, [P, P, i64, i64, P, C.POINTER(KmeansCfg), P, P, P, P]),
     "ecc_kmeans_run_f32": (C.c_int, [P, P, i64, C.POINTER(KmeansCfg), P, P, P, P]),
     "ecc_kmeans_run_xy16_frame": (C.c_int, [P, P, i64, i64, P, i32, i32, C.POINTER(KmeansCfg), P, P, P, P]),
+    "ecc_kmeans_refcompat_f32": (C.c_int, [P, P, i64, P, i32, P, P, P, P]),
     "ecc_kmeans_run_f32_engine": (C.c_int, [P, P, i64, C.POINTER(KmeansCfg), i32, P, P, P, P]),
     "ecc_kmeans_assign_f32": (C.c_int, [P, P, i64, P, i32, C.c_float, P, P]),
     "ecc_kmeans_accumulate_xy16": (C.c_int, [P, P, i64, i64, P, P, i32, C.c_float, P, P, P]),

@@ -371,6 +371,23 @@ std::vector<uint8_t> KMeans::fit(const std::vector<std::array<float, 2>> &points
     return labels;
 }
 
+int KMeans::fit_ref_compat(Context &ctx, const std::vector<std::array<float, 2>> &points,
+                           std::array<float, 16> &centroids, int max_passes, std::array<int32_t, 8> *bin_counts) {
+    const int64_t n = (int64_t)points.size();
+    DeviceBuffer d_p(std::max<int64_t>(n * 8, 8)), d_c(64), d_n(4), d_b(32);
+    if (n) d_p.upload(points.data(), n * 8, ctx.stream());
+    d_c.upload(centroids.data(), 64, ctx.stream());
+    check(ecc_kmeans_refcompat_f32(ctx.get(), d_p.as<float>(), n, d_c.as<float>(), max_passes, d_n.as<int32_t>(),
+                                   d_b.as<int32_t>(), nullptr, ctx.stream()),
+          "ecc_kmeans_refcompat_f32");
+    int32_t passes = 0;
+    d_c.download(centroids.data(), 64, ctx.stream());
+    d_n.download(&passes, 4, ctx.stream());
+    if (bin_counts) d_b.download(bin_counts->data(), 32, ctx.stream());
+    ctx.sync();
+    return passes;
+}
+
 // ------------------------------------------------------------------------------ eps lists
 void eps_neighbour_lists(Context &ctx, const std::vector<std::array<int, 2>> &points, double eps,
                          std::vector<int64_t> &offsets, std::vector<int32_t> &nbr, int min_pts,

@@ -191,6 +191,22 @@ int ecc_kmeans_run_xy16_frame(ecc_ctx *ctx, const uint32_t *xy, int64_t n_segs, 
 int ecc_kmeans_run_f32_engine(ecc_ctx *ctx, const float *xy, int64_t n_points, const ecc_kmeans_cfg *cfg,
                               int32_t engine, float *centroids, uint8_t *labels, int32_t *iters_out,
                               ecc_stream_t stream);
+/* The reference's k-means host loop in "ref_compat" mode (KM/assign_to_centers2.c:184-548 over
+ * KM/assign_to_centers.cl): 8 centres, n <= 16384 float (x, y)
+ * points in 8 bins of 2048 (a point past its bin's 2048th is counted, not stored); the bins are
+ * zeroed once and never cleared (Q8: a bin keeps earlier passes' values past its count; filled
+ * here in point-index order, where the reference's kernel appends in atomic order); each
+ * 1024-float chunk summed as reduction_scalar's pairwise tree; the update's partial-sum indexing
+ * ss[j], ss[j+1] / ss[j+2], ss[j+3] for j = 2c (Q7), C's int abs of the float shift with the
+ * running-maximum selective update, and the restart while that maximum is > 10 (Q9), at most
+ * max_passes passes.  centroids16: DEVICE float[16] (x0, y0, .., x7, y7) in/out; passes_out
+ * DEVICE int32[1], bin_counts_out DEVICE int32[8] (cluster_index) and partial_sums_out DEVICE
+ * float[32] (the chunk sums) of the last pass, each may be NULL.  Bit-exact vs the oracle's
+ * orc_kmeans_refcompat, whose passes are pinned against the reference's kernels.  The product's
+ * default is the "fixed" loop above (ecc_kmeans_run_*). */
+int ecc_kmeans_refcompat_f32(ecc_ctx *ctx, const float *xy, int64_t n, float *centroids16, int32_t max_passes,
+                             int32_t *passes_out, int32_t *bin_counts_out, float *partial_sums_out,
+                             ecc_stream_t stream);
 /* Split form of one Lloyd iteration, for multi-GPU: each rank accumulates its shard's exact
  * integer partial sums into acc (DEVICE uint64[3k]: count, sum x, sum y per centre; added to,
  * so zero it first), the ranks all-reduce acc (SUM), then every rank applies the identical

@@ -256,6 +256,11 @@ class KMeans {  // assign_to_centers + host loop, "fixed" mode (Appendix A Q7-Q1
     std::vector<uint8_t> fit(const std::vector<std::array<float, 2>> &points,
                              std::vector<std::array<float, 2>> &centroids, int *iters = nullptr);
     const ecc_kmeans_cfg &config() const { return cfg_; }
+    // the reference's own loop ("ref_compat", Appendix A Q7-Q9: 8 centres, <= 16384 points, bins of
+    // 2048 never cleared, the ss[j+1] index quirk, the int-abs restart test); returns the passes
+    static int fit_ref_compat(Context &ctx, const std::vector<std::array<float, 2>> &points,
+                              std::array<float, 16> &centroids, int max_passes = 50,
+                              std::array<int32_t, 8> *bin_counts = nullptr);
 
   private:
     Context &ctx_;

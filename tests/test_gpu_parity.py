@@ -1229,6 +1229,51 @@ def test_kmeans_frame_segments_match_oracle(ecc, orc, gpu, wh, frame, k):
     assert (g_dense == o_lab).all()
 
 
+@pytest.mark.parametrize("case", ["demo", "ints_full_bins", "floats", "empty_cluster", "one_pass", "few"])
+def test_kmeans_refcompat_matches_oracle(ecc, orc, gpu, case):
+    """ecc_kmeans_refcompat_f32 (the reference's own loop, Q7-Q9) against orc_kmeans_refcompat,
+    whose passes tests/test_ref_opencl.py pins against the reference kernels: the pass count, the
+    centroids, the last pass's bin counts and chunk sums, bit for bit.  Cases: the reference's demo
+    data and centres (KM/assign_to_centers2.c), 16 384 integer points (bins past 2 048: counted,
+    not stored), non-integer floats (the chunk sums' tree order matters), a centre no point reaches
+    (0/0 in the update: C's int abs of NaN), one pass, three points."""
+    rng = np.random.default_rng(5)
+    c0 = np.array([1, 1, 10, 10, 20, 20, 30, 30, 50, 50, 60, 60, 70, 70, 80, 80], np.float32)
+    max_passes = 50
+    if case == "demo":
+        pts = (np.arange(4096) % 100).astype(np.float32)
+    elif case == "ints_full_bins":
+        pts = rng.integers(0, 100, 2 * 16384).astype(np.float32)
+    elif case == "floats":
+        pts = (rng.random(2 * 5000) * 90).astype(np.float32)
+    elif case == "empty_cluster":
+        pts = (rng.random(2 * 3000) * 40).astype(np.float32)
+        c0 = c0.copy()
+        c0[14:] = 1000.0  # unreachable centre (threshold 50)
+    elif case == "one_pass":
+        pts = rng.integers(0, 100, 2 * 4000).astype(np.float32)
+        max_passes = 1
+    else:
+        pts = np.array([3, 4, 55, 56, 81, 79], np.float32)
+    n = len(pts) // 2
+    o_c, o_cnt, o_ss = c0.copy(), np.zeros(8, np.int32), np.zeros(32, np.float32)
+    o_p = orc.lib.orc_kmeans_refcompat(pts.ctypes.data, n, o_c.ctypes.data, max_passes, o_cnt.ctypes.data,
+                                       o_ss.ctypes.data)
+    d_c, d_p, d_cnt, d_ss = dev(ecc, c0), ecc.DeviceArray(1, np.int32), ecc.DeviceArray(8, np.int32), ecc.DeviceArray(32, np.float32)
+    ecc.check(ecc.lib.ecc_kmeans_refcompat_f32(gpu.ctx, dev(ecc, pts).ptr, n, d_c.ptr, max_passes, d_p.ptr, d_cnt.ptr,
+                                               d_ss.ptr, gpu.stream))
+    gpu.sync()
+    assert int(d_p.numpy()[0]) == o_p, (d_p.numpy(), o_p)
+    assert np.array_equal(d_c.numpy().view(np.uint32), o_c.view(np.uint32)), (d_c.numpy(), o_c)
+    assert np.array_equal(d_cnt.numpy(), o_cnt), (d_cnt.numpy(), o_cnt)
+    assert np.array_equal(d_ss.numpy().view(np.uint32), o_ss.view(np.uint32)), (d_ss.numpy(), o_ss)
+    if case == "ints_full_bins":
+        assert o_cnt.max() > 2048  # the case really overflows a bin
+    if case == "empty_cluster":
+        assert o_cnt[7] == 0
+    assert ecc.lib.ecc_kmeans_refcompat_f32(gpu.ctx, None, 16385, d_c.ptr, 5, None, None, None, gpu.stream) == ecc.ERR_INVALID
+
+
 @pytest.mark.parametrize("engine", [1, 2, 3])
 def test_kmeans_c3_f32_50m(ecc, gpu, c3_points, engine):
     pts, c0, o_c, o_lab, o_it = c3_points
